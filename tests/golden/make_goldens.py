@@ -1,0 +1,517 @@
+"""Capture golden vectors from the reference (andrpac/alphazero-gnn) on CPU.
+
+Run ONLY in the build container, where the read-only reference is mounted:
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only NAME ...]
+
+The reference is imported from /root/reference (nothing is written there) and exercised
+through its own public entry points; intermediates are taken with forward hooks, never by
+re-deriving them.  Only data (inputs + outputs) is written to tests/golden/.  Nothing in
+tests/, bench.py or __graft_entry__.py reads /root/reference at run time.
+
+Fixtures:
+  G1 c4_net.npz          Connect4Net torch-default weights (seed 0), 256 boards, predict + batched fwd
+  G2 c4_gnn.npz          Connect4 GNN (synthetic PCG64 weights, seed 1234): predict_with_gnn on 64
+                         boards + one 64-row star forward (alpha, agg, row-0 per layer, heads)
+  G3 synth_gnn.npz       PolicyValueGNN(64): per-destination 32x32 grid forward + literal star N=4096
+  G4 ttt3.npz            TicTacToe 3x3 CNN+GNN weights (seed 0), predict/predict_with_gnn on every
+                         reachable canonical position
+  G5 train_ttt3.npz      one TicTacToeGNNWrapper.train (2 epochs) -> params after Adam
+     train_c4.npz        one Connect4GNNWrapper.train (dropout 0, 2 epochs) -> CNN params + GNN checksums
+  G6 mcts_c4.npz/json    Connect4 self-play episodes (sims 25, no GNN): per-move root counts/pi/choices,
+                         every NN output the search requested, the examples
+     mcts_ttt3.npz/json  TicTacToe 3x3 GNN self-play episodes with expand_tree
+  G7 coach_ttt3.json     one full TicTacToe 3x3 GNN Coach iteration (seeds 0): counts, arena W/L/D
+"""
+import argparse
+import importlib.util
+import json
+import os
+import random
+import shutil
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+sys.dont_write_bytecode = True
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REF)
+
+from gnn_utils import PolicyValueGNN  # noqa: E402
+from connect4.Connect4Game import Connect4Game  # noqa: E402
+from connect4.Connect4Net import Connect4NNetWrapper  # noqa: E402
+from connect4.Connect4GNN import Connect4GNNWrapper  # noqa: E402
+from tictactoe.TicTacToeGame import TicTacToeGame  # noqa: E402
+from tictactoe.TicTacToeGNN import TicTacToeGNNWrapper  # noqa: E402
+import MCTS as ref_mcts  # noqa: E402
+import Coach as ref_coach  # noqa: E402
+import Arena as ref_arena  # noqa: E402
+
+_spec = importlib.util.spec_from_file_location(
+    "az_weights", os.path.join(REPO, "alphazero-gnn_amd", "azhip", "weights.py"))
+W = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(W)
+
+torch.set_num_threads(8)
+
+
+class dotdict(dict):
+    """Same semantics as main.py:18-23."""
+    def __getattr__(self, name):
+        return self[name]
+
+    def __setattr__(self, name, value):
+        self[name] = value
+
+
+def base_args(**kw):
+    a = dotdict(lr=0.001, dropout=0.3, epochs=20, batch_size=64, use_gnn=False, gnn_layers=2,
+                numIters=1, numEps=20, tempThreshold=15, updateThreshold=0.6,
+                maxlenOfQueue=200000, numItersForTrainExamplesHistory=5,
+                numMCTSSims=10, cpuct=1.0, expand_by=5, arenaCompare=100)
+    a.update(kw)
+    return a
+
+
+def sd_np(module):
+    return {k: v.detach().cpu().numpy().copy() for k, v in module.state_dict().items()}
+
+
+def out(name):
+    return os.path.join(HERE, name)
+
+
+def random_play_boards(game, n, rng, max_moves=48):
+    """Canonical boards reached by uniformly random legal play (seeded)."""
+    boards = []
+    while len(boards) < n:
+        b = game.getInitBoard()
+        p = 1
+        steps = int(rng.integers(0, max_moves))
+        for _ in range(steps):
+            if game.getGameEnded(b, p) != 0:
+                break
+            v = game.getValidMoves(game.getCanonicalForm(b, p), 1)
+            a = int(rng.choice(np.flatnonzero(v)))
+            b, p = game.getNextState(b, p, a)
+        boards.append(game.getCanonicalForm(b, p).astype(np.int8))
+    return np.stack(boards)
+
+
+# ----------------------------------------------------------------------------------- G1
+def g1():
+    torch.manual_seed(0)
+    np.random.seed(0)
+    game = Connect4Game(7)
+    net = Connect4NNetWrapper(game, base_args())
+    sd = sd_np(net.nnet)
+    rng0 = np.random.default_rng(0)
+    rnd = rng0.integers(-1, 2, size=(128, 7, 7)).astype(np.int8)
+    play = random_play_boards(game, 128, np.random.default_rng(1))
+    boards = np.concatenate([rnd, play])
+    pis, vs = [], []
+    for b in boards:
+        pi, v = net.predict(b.astype(np.int64))
+        pis.append(pi)
+        vs.append(v)
+    net.nnet.eval()
+    with torch.no_grad():
+        lp, vb = net.nnet(torch.FloatTensor(boards.astype(np.float64)))
+    np.savez(out("c4_net.npz"), boards=boards, pi_b1=np.stack(pis).astype(np.float32),
+             v_b1=np.array(vs, np.float32), logp_batch=lp.numpy(), v_batch=vb.numpy()[:, 0],
+             **{"w/" + k: v for k, v in sd.items()})
+    return net, boards
+
+
+# ----------------------------------------------------------------------------------- G2
+GNN_C4_SEED = 1234
+
+
+def g2(c4net_sd, boards):
+    game = Connect4Game(7)
+    torch.manual_seed(0)
+    g = Connect4GNNWrapper(game, base_args(use_gnn=True))
+    g.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in c4net_sd.items()})
+    t0 = time.time()
+    gsd = W.synthetic_state_dict(W.gnn_spec(3136, 2), GNN_C4_SEED)
+    g.gnn.load_state_dict({k: torch.from_numpy(v) for k, v in gsd.items()})
+    del gsd
+    print(f"  G2 weights generated+loaded in {time.time() - t0:.1f}s")
+    sel = boards[::4][:64]
+    pis, vs = [], []
+    for b in sel:
+        pi, v = g.predict_with_gnn(b.astype(np.int64))
+        pis.append(pi)
+        vs.append(v)
+    # one 64-row star forward (the training-time shape, Connect4GNN.py:178-184) in eval mode
+    g.nnet.eval()
+    g.gnn.eval()
+    rec = {"attn": [[], []], "comb": [None, None], "row0": [None, None]}
+    hooks = []
+    for li, layer in enumerate(g.gnn.layers):
+        hooks.append(layer.attention.register_forward_hook(
+            lambda m, i, o, li=li: rec["attn"][li].append(torch.sigmoid(o).item())))
+        hooks.append(layer.gate.register_forward_hook(
+            lambda m, i, o, li=li: rec["comb"].__setitem__(li, i[0].detach().clone())))
+        hooks.append(layer.register_forward_hook(
+            lambda m, i, o, li=li: rec["row0"].__setitem__(li, o[0].detach().clone())))
+    with torch.no_grad():
+        feats = g.extract_features(torch.FloatTensor(sel.astype(np.float64)))
+        enh = g.gnn(feats)
+        lp, v = g.apply_policy_value_heads(enh)
+    for h in hooks:
+        h.remove()
+    F = 3136
+    np.savez(out("c4_gnn.npz"), seed=np.int64(GNN_C4_SEED), boards=sel,
+             pi_gnn_b1=np.stack(pis).astype(np.float32), v_gnn_b1=np.array(vs, np.float32),
+             star_alpha_raw=np.array(rec["attn"], np.float32),
+             star_agg=np.stack([c[0, F:].numpy() for c in rec["comb"]]),
+             star_row0=np.stack([r.numpy() for r in rec["row0"]]),
+             star_enh_row0=enh[0].numpy(), star_enh_rowsum=enh.sum(1).numpy(),
+             star_logp=lp.numpy(), star_v=v.numpy()[:, 0])
+    return g
+
+
+# ----------------------------------------------------------------------------------- G3
+SYN_SEED_W, SYN_SEED_X, SYN_SEED_STAR = 64, 0, 5
+
+
+def grid_csr(h, w):
+    """4-neighbour grid, CSR by destination, sources ascending."""
+    rowptr = [0]
+    col = []
+    for r in range(h):
+        for c in range(w):
+            nb = []
+            for dr, dc in ((-1, 0), (0, -1), (0, 1), (1, 0)):
+                rr, cc = r + dr, c + dc
+                if 0 <= rr < h and 0 <= cc < w:
+                    nb.append(rr * w + cc)
+            col += sorted(nb)
+            rowptr.append(len(col))
+    return np.array(rowptr, np.int32), np.array(col, np.int32)
+
+
+def g3():
+    gnn = PolicyValueGNN(64, 2)
+    sd = W.synthetic_state_dict(W.gnn_spec(64, 2), SYN_SEED_W)
+    gnn.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    gnn.eval()
+    rowptr, col = grid_csr(32, 32)
+    rng = np.random.Generator(np.random.PCG64(SYN_SEED_X))
+    x0 = (rng.random((1024, 64), dtype=np.float32) * np.float32(2) - np.float32(1))
+    xs = [torch.from_numpy(x0)]
+    with torch.no_grad():
+        for layer in gnn.layers:
+            cur = xs[-1]
+            nxt = torch.empty_like(cur)
+            for d in range(1024):
+                nb = col[rowptr[d]:rowptr[d + 1]]
+                feats = torch.cat([cur[d:d + 1], cur[torch.from_numpy(nb.astype(np.int64))]])
+                nxt[d] = layer(feats)[0]
+            xs.append(nxt)
+        grid_out = gnn.output_transform(xs[-1])
+        rng2 = np.random.Generator(np.random.PCG64(SYN_SEED_STAR))
+        star_x = rng2.random((4096, 64), dtype=np.float32) * np.float32(2) - np.float32(1)
+        star_out = gnn(torch.from_numpy(star_x))
+    np.savez(out("synth_gnn.npz"), seed_w=np.int64(SYN_SEED_W), seed_x=np.int64(SYN_SEED_X),
+             seed_star=np.int64(SYN_SEED_STAR), rowptr=rowptr, col=col,
+             grid_x1=xs[1].numpy(), grid_x2=xs[2].numpy(), grid_out=grid_out.numpy(),
+             star_out_head=star_out[:65].numpy(), star_out_rowsum=star_out.sum(1).numpy())
+
+
+# ----------------------------------------------------------------------------------- G4
+def reachable_ttt(game):
+    """Every distinct canonical board reachable from the empty board (BFS)."""
+    seen = {}
+    frontier = [(game.getInitBoard(), 1)]
+    while frontier:
+        nxt = []
+        for b, p in frontier:
+            c = game.getCanonicalForm(b, p)
+            key = c.tobytes()
+            if key in seen:
+                continue
+            seen[key] = c
+            if game.getGameEnded(b, p) != 0:
+                continue
+            v = game.getValidMoves(c, 1)
+            for a in np.flatnonzero(v):
+                nb, np_ = game.getNextState(b, p, int(a))
+                nxt.append((nb, np_))
+        frontier = nxt
+    return np.stack([seen[k] for k in sorted(seen)]).astype(np.int8)
+
+
+def g4():
+    torch.manual_seed(0)
+    game = TicTacToeGame(3)
+    net = TicTacToeGNNWrapper(game, base_args(use_gnn=True))
+    sd = sd_np(net.nnet)
+    gsd = sd_np(net.gnn)
+    boards = reachable_ttt(game)
+    pis, vs, gpis, gvs = [], [], [], []
+    for b in boards:
+        pi, v = net.predict(b.astype(np.int64))
+        gpi, gv = net.predict_with_gnn(b.astype(np.int64))
+        pis.append(pi)
+        vs.append(v)
+        gpis.append(gpi)
+        gvs.append(gv)
+    np.savez(out("ttt3.npz"), boards=boards, pi=np.stack(pis), v=np.array(vs, np.float32),
+             pi_gnn=np.stack(gpis), v_gnn=np.array(gvs, np.float32),
+             **{"w/" + k: v for k, v in sd.items()}, **{"g/" + k: v for k, v in gsd.items()})
+    return net, boards
+
+
+# ----------------------------------------------------------------------------------- G5
+def make_examples(boards, action_size, n, ngnn, rng):
+    idx = rng.integers(0, len(boards), n)
+    pis = rng.dirichlet(np.ones(action_size), n).astype(np.float64)
+    zs = rng.choice([-1, 1, 1e-4], n)
+    ex = [(boards[i].astype(np.int64), pis[j], zs[j]) for j, i in enumerate(idx)]
+    gidx = rng.integers(0, len(boards), ngnn)
+    gex = []
+    for j, i in enumerate(gidx):
+        ipi = rng.dirichlet(np.ones(action_size)).astype(np.float64)
+        epi = rng.dirichlet(np.ones(action_size)).astype(np.float64)
+        gex.append((boards[i].astype(np.int64), 1, ipi, np.float32(rng.uniform(-1, 1)), epi,
+                    np.float32(rng.uniform(-1, 1)), 1))
+    return ex, gex
+
+
+def pack_examples(ex, gex):
+    return dict(ex_boards=np.stack([e[0] for e in ex]).astype(np.int8),
+                ex_pis=np.stack([e[1] for e in ex]), ex_z=np.array([e[2] for e in ex], np.float64),
+                gex_boards=np.stack([e[0] for e in gex]).astype(np.int8),
+                gex_epis=np.stack([e[4] for e in gex]),
+                gex_ev=np.array([e[5] for e in gex], np.float32))
+
+
+CHECK_IDX = 97  # fixed flat indices for GNN param spot checks: PCG64(CHECK_IDX)
+
+
+def g5(ttt_boards, c4net_sd, c4_boards):
+    # --- TicTacToe 3x3: deterministic (no dropout anywhere, TicTacToeNet.py:28-48)
+    torch.manual_seed(0)
+    game = TicTacToeGame(3)
+    net = TicTacToeGNNWrapper(game, base_args(use_gnn=True, epochs=2))
+    ex, gex = make_examples(ttt_boards, 10, 200, 100, np.random.default_rng(11))
+    np.random.seed(7)
+    net.train(ex, gex)
+    np.savez(out("train_ttt3.npz"), np_seed=np.int64(7), epochs=np.int64(2),
+             **pack_examples(ex, gex),
+             **{"w/" + k: v for k, v in sd_np(net.nnet).items()},
+             **{"g/" + k: v for k, v in sd_np(net.gnn).items()})
+    # --- Connect4 with dropout 0 (Connect4Net.py:28): CNN params in full, GNN by checksums
+    game = Connect4Game(7)
+    g = Connect4GNNWrapper(game, base_args(use_gnn=True, epochs=2, dropout=0.0))
+    g.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in c4net_sd.items()})
+    gsd = W.synthetic_state_dict(W.gnn_spec(3136, 2), GNN_C4_SEED)
+    g.gnn.load_state_dict({k: torch.from_numpy(v) for k, v in gsd.items()})
+    del gsd
+    ex, gex = make_examples(c4_boards, 8, 100, 64, np.random.default_rng(12))
+    np.random.seed(9)
+    t0 = time.time()
+    g.train(ex, gex)
+    print(f"  G5 c4 train {time.time() - t0:.1f}s")
+    rng = np.random.Generator(np.random.PCG64(CHECK_IDX))
+    chk = {}
+    for k, v in g.gnn.state_dict().items():
+        a = v.numpy().ravel()
+        ii = rng.integers(0, a.size, 64)
+        chk["gsum/" + k] = np.float64(a.astype(np.float64).sum())
+        chk["gabs/" + k] = np.float64(np.abs(a.astype(np.float64)).sum())
+        chk["gidx/" + k] = ii
+        chk["gval/" + k] = a[ii]
+    np.savez(out("train_c4.npz"), np_seed=np.int64(9), epochs=np.int64(2),
+             gnn_seed=np.int64(GNN_C4_SEED), check_seed=np.int64(CHECK_IDX),
+             **pack_examples(ex, gex), **{"w/" + k: v for k, v in sd_np(g.nnet).items()}, **chk)
+
+
+# ----------------------------------------------------------------------------------- G6
+class Recorder:
+    """Transparent proxy that records every NN output the search requests."""
+
+    def __init__(self, net):
+        self.net = net
+        self.std = {}
+        self.gnn = {}
+
+    def predict(self, board):
+        pi, v = self.net.predict(board)
+        self.std[board.tobytes()] = (board.astype(np.int8).copy(), np.array(pi), np.float32(v))
+        return pi, v
+
+    def predict_with_gnn(self, board):
+        pi, v = self.net.predict_with_gnn(board)
+        self.gnn[board.tobytes()] = (board.astype(np.int8).copy(), np.array(pi), np.float32(v))
+        return pi, v
+
+
+def _tag(x):
+    if isinstance(x, np.floating):
+        return "np." + x.dtype.name
+    return type(x).__name__
+
+
+def run_episodes(game, net, args, episodes, name, n):
+    coach = ref_coach.Coach.__new__(ref_coach.Coach)  # skip pnet construction (Coach.py:21)
+    coach.game, coach.args = game, args
+    rec = Recorder(net)
+    coach.nnet = rec
+    moves = []
+    orig_choice = np.random.choice
+    choices = []
+
+    def rec_choice(*a, **k):
+        r = orig_choice(*a, **k)
+        choices.append(int(r))
+        return r
+
+    results = []
+    np.random.choice = rec_choice
+    try:
+        for e in episodes:
+            np.random.seed(e)
+            coach.mcts = ref_mcts.MCTS(game, rec, args)
+            mc = coach.mcts
+            orig_gap = mc.getActionProb
+            ep_moves = []
+
+            def gap(board, temp=1, mc=mc, orig=orig_gap, ep_moves=ep_moves):
+                c0 = len(choices)
+                pi = orig(board, temp=temp)
+                s = game.stringRepresentation(board)
+                A = game.getActionSize()
+                ep_moves.append(dict(
+                    board=board.astype(np.int8).tolist(), temp=temp,
+                    counts=[int(mc.Nsa.get((s, a), 0)) for a in range(A)],
+                    q=[float(mc.Qsa[(s, a)]) if (s, a) in mc.Qsa else None for a in range(A)],
+                    qtype=[_tag(mc.Qsa[(s, a)]) if (s, a) in mc.Qsa else None for a in range(A)],
+                    pi=[float(x) for x in pi], choices_before=c0))
+                return pi
+
+            mc.getActionProb = gap
+            c_start = len(choices)
+            std_ex, gnn_ex = coach.executeEpisode()
+            moves.append(ep_moves)
+            results.append(dict(
+                episode=e, choices=choices[c_start:],
+                n_nodes=len(mc.Ns), nsa_total=int(sum(mc.Nsa.values())),
+                std_examples=[(np.asarray(b).astype(int).tolist(), [float(x) for x in p], float(z))
+                              for b, p, z in std_ex],
+                gnn_examples=[(np.asarray(x[0]).astype(int).tolist(), int(x[1]),
+                               [float(t) for t in x[2]], float(x[3]), [float(t) for t in x[4]],
+                               float(x[5]), float(x[6]))
+                              for x in gnn_ex]))
+    finally:
+        np.random.choice = orig_choice
+    with open(out(name + ".json"), "w") as f:
+        json.dump(dict(args=dict(args), moves=moves, episodes=results), f)
+    std = list(rec.std.values())
+    gnn = list(rec.gnn.values())
+    np.savez(out(name + ".npz"),
+             std_boards=np.stack([s[0] for s in std]).reshape(-1, n, n),
+             std_pi=np.stack([s[1] for s in std]).astype(np.float32),
+             std_v=np.array([s[2] for s in std], np.float32),
+             gnn_boards=(np.stack([s[0] for s in gnn]).reshape(-1, n, n) if gnn
+                         else np.zeros((0, n, n), np.int8)),
+             gnn_pi=(np.stack([s[1] for s in gnn]).astype(np.float32) if gnn
+                     else np.zeros((0, game.getActionSize()), np.float32)),
+             gnn_v=np.array([s[2] for s in gnn], np.float32))
+
+
+def g6(c4net, tttnet):
+    run_episodes(Connect4Game(7), c4net, base_args(numMCTSSims=25), [0, 1], "mcts_c4", 7)
+    run_episodes(TicTacToeGame(3), tttnet, base_args(numMCTSSims=10, use_gnn=True),
+                 [0, 1, 2], "mcts_ttt3", 3)
+
+
+# ----------------------------------------------------------------------------------- G7
+def g7():
+    """main.py:158-285 wiring for: --game tictactoe --board_size 3 --use_gnn --numIters 1."""
+    import yaml
+    with open(os.path.join(REF, "tictactoe", "config.yaml")) as f:
+        config = yaml.safe_load(f)
+    args = dotdict({})
+    for section in config:                       # main.py:30-43
+        for k, v in config[section].items():
+            args[k] = v
+    args.checkpoint = args.checkpoint_path
+    args.board_size = 3
+    args.numIters = 1
+    args.use_gnn = True
+    args.gnn_layers = 2
+    args.game = "tictactoe"
+    args.load_model = False
+    tmp = tempfile.mkdtemp(prefix="az_g7_")
+    folder = os.path.join(tmp, "tictactoe")
+    os.makedirs(folder)
+    args.checkpoint = folder
+    args.load_folder_file = (folder, "best_gnn.pth.tar")
+    random.seed(0)
+    np.random.seed(0)
+    torch.manual_seed(0)
+    game = TicTacToeGame(n=3)
+    nnet = TicTacToeGNNWrapper(game, args)
+    coach = ref_coach.Coach(game, nnet, args)
+    arena_res = []
+    orig = ref_arena.Arena.playGames
+
+    def pg(self, num, verbose=False):
+        r = orig(self, num, verbose)
+        arena_res.append([int(x) for x in r])
+        return r
+
+    ref_arena.Arena.playGames = pg
+    try:
+        t0 = time.time()
+        coach.learn()
+        dt = time.time() - t0
+    finally:
+        ref_arena.Arena.playGames = orig
+    std_ex, gnn_ex = coach.trainExamplesHistory[0]
+    res = dict(n_std=len(std_ex), n_gnn=len(gnn_ex), arena_pwins_nwins_draws=arena_res[0],
+               files=sorted(os.listdir(folder)), seconds=dt)
+    shutil.rmtree(tmp)
+    with open(out("coach_ttt3.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print("  G7", res)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None)
+    a = ap.parse_args()
+    want = set(a.only) if a.only else {"g1", "g2", "g3", "g4", "g5", "g6", "g7"}
+    t0 = time.time()
+    c4net, c4b = g1()
+    print(f"G1 done {time.time() - t0:.1f}s")
+    c4sd = sd_np(c4net.nnet)
+    if "g2" in want:
+        g2(c4sd, c4b)
+        print(f"G2 done {time.time() - t0:.1f}s")
+    if "g3" in want:
+        g3()
+        print(f"G3 done {time.time() - t0:.1f}s")
+    tnet, tb = g4()
+    print(f"G4 done {time.time() - t0:.1f}s")
+    if "g5" in want:
+        g5(tb, c4sd, c4b)
+        print(f"G5 done {time.time() - t0:.1f}s")
+    if "g6" in want:
+        g6(c4net, tnet)
+        print(f"G6 done {time.time() - t0:.1f}s")
+    if "g7" in want:
+        g7()
+        print(f"G7 done {time.time() - t0:.1f}s")
+
+
+if __name__ == "__main__":
+    main()
