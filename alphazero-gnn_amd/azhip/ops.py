@@ -1,0 +1,223 @@
+"""Tensor-level wrappers over the C-ABI.  Tensors are torch CUDA(HIP) tensors used purely as
+device memory; every FLOP runs in libaz_hip.so on the current torch stream."""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, GemmDesc, Graph, LayerW  # noqa: F401
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _need(t, dtype=torch.float32, name="tensor"):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise ValueError(f"{name} must live on the GPU (got {t.device})")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype} (got {t.dtype})")
+
+
+def gemm(desc):
+    L = _lib.lib()
+    _lib.check(L.az_gemm_f32(ctypes.byref(desc), _stream()), "az_gemm_f32")
+
+
+def linear(x, w, b=None, act=ACT_NONE, out=None, x2=None, a_rows=None, R=None, G=None,
+           c_rows=None, beta=0.0, M=None):
+    """out = act(cat(x, x2) @ w.T + b) (optionally gated residual R + G*(...)), nn.Linear layout.
+    x: [M, K1] (row stride taken from the tensor), x2: [M, K2] or None, w: [N, K1+K2]."""
+    _need(x, name="x")
+    _need(w, name="w")
+    K1 = x.shape[1]
+    K = K1 + (x2.shape[1] if x2 is not None else 0)
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError(f"linear: w {tuple(w.shape)} vs K={K}")
+    if M is None:
+        M = a_rows.numel() if a_rows is not None else x.shape[0]
+    if out is None:
+        out = torch.empty((M, N), device=x.device, dtype=torch.float32)
+    d = GemmDesc()
+    d.M, d.N, d.K = M, N, K
+    d.A, d.lda, d.a_kmajor = x.data_ptr(), x.stride(0), 1
+    if x2 is not None:
+        d.A2, d.lda2, d.K0 = x2.data_ptr(), x2.stride(0), K1
+    d.a_rows = a_rows.data_ptr() if a_rows is not None else None
+    d.B, d.ldb, d.b_kmajor = w.data_ptr(), w.stride(0), 1
+    d.bias = b.data_ptr() if b is not None else None
+    d.act = act
+    if R is not None:
+        d.R, d.ldr = R.data_ptr(), R.stride(0)
+    if G is not None:
+        d.G, d.ldg = G.data_ptr(), G.stride(0)
+    d.beta = beta
+    d.C, d.ldc = out.data_ptr(), out.stride(0)
+    d.c_rows = c_rows.data_ptr() if c_rows is not None else None
+    gemm(d)
+    return out
+
+
+def matmul_tn(a, b, out, M, N, K, beta=0.0, lda=None, ldb=None):
+    """out[M,N] (+)= a^T b with a stored [K][M] and b stored [K][N] (weight gradients)."""
+    d = GemmDesc()
+    d.M, d.N, d.K = M, N, K
+    d.A, d.lda, d.a_kmajor = a.data_ptr(), lda or a.stride(0), 0
+    d.B, d.ldb, d.b_kmajor = b.data_ptr(), ldb or b.stride(0), 0
+    d.beta = beta
+    d.C, d.ldc = out.data_ptr(), out.stride(0)
+    gemm(d)
+    return out
+
+
+def matmul_nn(a, b, out, M, N, K, beta=0.0):
+    """out[M,N] (+)= a[M,K] @ b[K,N] (input gradients: dX = dY @ W)."""
+    d = GemmDesc()
+    d.M, d.N, d.K = M, N, K
+    d.A, d.lda, d.a_kmajor = a.data_ptr(), a.stride(0), 1
+    d.B, d.ldb, d.b_kmajor = b.data_ptr(), b.stride(0), 0
+    d.beta = beta
+    d.C, d.ldc = out.data_ptr(), out.stride(0)
+    gemm(d)
+    return out
+
+
+def c4_trunk(boards_i8, W, out=None):
+    """Connect4Net trunk (Connect4Net.py:42-49) on int8 boards [B,7,7] -> features [B,3136]."""
+    _need(boards_i8, torch.int8, "boards")
+    B = boards_i8.shape[0]
+    if out is None:
+        out = torch.empty((B, 3136), device=boards_i8.device, dtype=torch.float32)
+    L = _lib.lib()
+    _lib.check(L.az_c4_trunk_fwd(_p(boards_i8), B, _p(W["conv1.weight"]), _p(W["conv1.bias"]),
+                                 _p(W["conv2.weight"]), _p(W["conv2.bias"]), _p(out), _stream()),
+               "az_c4_trunk_fwd")
+    return out
+
+
+def conv3x3_relu(x, w, b, pad, out=None):
+    """x: int8 [B,H,W] (Cin=1) or fp32 [B,Cin,H,W] -> fp32 [B,Cout,Ho,Wo]."""
+    is_i8 = x.dtype == torch.int8
+    if is_i8:
+        B, H, Wd = x.shape
+        Cin = 1
+    else:
+        _need(x, name="x")
+        B, Cin, H, Wd = x.shape
+    Cout = w.shape[0]
+    Ho, Wo = H + 2 * pad - 2, Wd + 2 * pad - 2
+    if out is None:
+        out = torch.empty((B, Cout, Ho, Wo), device=x.device, dtype=torch.float32)
+    L = _lib.lib()
+    _lib.check(L.az_conv3x3_relu_fwd(_p(x), int(is_i8), B, Cin, H, Wd, _p(w), _p(b), Cout, pad,
+                                     _p(out), _stream()), "az_conv3x3_relu_fwd")
+    return out
+
+
+def heads(hp, wp, bp, wv, bv, hv=None, want_pi=True, logp=None, pi=None, v=None):
+    """logp = log_softmax(hp wp^T + bp); v = tanh(hv wv^T + bv) (hv defaults to hp)."""
+    hv = hp if hv is None else hv
+    B, K = hp.shape
+    A = wp.shape[0]
+    dev = hp.device
+    logp = torch.empty((B, A), device=dev) if logp is None else logp
+    pi = (torch.empty((B, A), device=dev) if pi is None else pi) if want_pi else None
+    v = torch.empty((B,), device=dev) if v is None else v
+    L = _lib.lib()
+    _lib.check(L.az_heads_fwd(_p(hp), hp.stride(0), _p(hv), hv.stride(0), B, K, _p(wp), _p(bp), A,
+                              _p(wv), _p(bv), _p(logp), _p(pi), _p(v), _stream()), "az_heads_fwd")
+    return logp, pi, v
+
+
+class DeviceGraph:
+    """A destination-sorted CSR graph resident in HBM (+ its edge->dst map and the list of
+    destinations with at least one in-edge)."""
+
+    def __init__(self, rowptr, col, device="cuda"):
+        import numpy as np
+        rowptr = np.asarray(rowptr, np.int64)
+        col = np.asarray(col, np.int64)
+        V = len(rowptr) - 1
+        deg = np.diff(rowptr)
+        self.V, self.E = V, int(rowptr[-1])
+        dst = np.repeat(np.arange(V), deg)
+        rows = np.flatnonzero(deg > 0)
+        self.D = len(rows)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.int32)).to(device)  # noqa: E731
+        self.rowptr, self.col, self.edge_dst, self.dst_rows = t(rowptr), t(col), t(dst), t(rows)
+        self.c = Graph(V, self.E, self.rowptr.data_ptr(), self.col.data_ptr(),
+                       self.edge_dst.data_ptr(), self.D, self.dst_rows.data_ptr())
+
+    @staticmethod
+    def star(n, device="cuda"):
+        """The reference's implicit graph: row 0 <- rows 1..n-1 (gnn_utils.py:38-43)."""
+        import numpy as np
+        rowptr = np.full(n + 1, max(n - 1, 0), np.int64)
+        rowptr[0] = 0
+        return DeviceGraph(rowptr, np.arange(1, n), device)
+
+
+def attn_score(g, P, H, b1, w2, b2, alpha=None):
+    alpha = torch.empty((g.E,), device=P.device) if alpha is None else alpha
+    L = _lib.lib()
+    _lib.check(L.az_gnn_attn_score_fwd(ctypes.byref(g.c), _p(P), P.stride(0), H, _p(b1), _p(w2),
+                                       _p(b2), _p(alpha), _stream()), "az_gnn_attn_score_fwd")
+    return alpha
+
+
+def aggregate(g, x, alpha, agg=None):
+    F = x.shape[1]
+    agg = torch.zeros_like(x) if agg is None else agg
+    L = _lib.lib()
+    _lib.check(L.az_gnn_aggregate_fwd(ctypes.byref(g.c), _p(x), x.stride(0), F, _p(alpha),
+                                      _p(agg), agg.stride(0), _stream()), "az_gnn_aggregate_fwd")
+    return agg
+
+
+def layer_weights(Wl):
+    """LayerW from a dict with GNNLayer state_dict suffixes."""
+    return LayerW(*[Wl[k].data_ptr() for k in (
+        "attention.0.weight", "attention.0.bias", "attention.2.weight", "attention.2.bias",
+        "update_net.0.weight", "update_net.0.bias", "update_net.2.weight", "update_net.2.bias",
+        "gate.0.weight", "gate.0.bias")])
+
+
+def layer_ws_bytes(g, F, H=128):
+    return int(_lib.load().az_gnn_layer_ws_bytes(g.V, g.E, g.D, F, H))
+
+
+def gnn_layer(g, x, Wl, out=None, ws=None, H=128):
+    F = x.shape[1]
+    out = torch.empty_like(x) if out is None else out
+    nbytes = layer_ws_bytes(g, F, H)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty((nbytes,), dtype=torch.uint8, device=x.device)
+    lw = layer_weights(Wl)
+    L = _lib.lib()
+    _lib.check(L.az_gnn_layer_fwd(ctypes.byref(g.c), _p(x), F, H, ctypes.byref(lw), _p(out),
+                                  _p(ws), ctypes.c_size_t(ws.numel()), _stream()),
+               "az_gnn_layer_fwd")
+    return out, ws
+
+
+def mlp2(x, w0, b0, w2, b2, hidden=None, out=None):
+    M, F = x.shape
+    hidden = torch.empty_like(x) if hidden is None else hidden
+    out = torch.empty_like(x) if out is None else out
+    L = _lib.lib()
+    _lib.check(L.az_mlp2_fwd(_p(x), M, F, _p(w0), _p(b0), _p(w2), _p(b2), _p(hidden), _p(out),
+                             _stream()), "az_mlp2_fwd")
+    return out, hidden
+
+
+def adam(p, g, m, v, lr, step, beta1=0.9, beta2=0.999, eps=1e-8):
+    L = _lib.lib()
+    _lib.check(L.az_adam_f32(_p(p), _p(g), _p(m), _p(v), p.numel(), lr, beta1, beta2, eps, step,
+                             _stream()), "az_adam_f32")

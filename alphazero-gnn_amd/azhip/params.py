@@ -1,0 +1,88 @@
+"""Flat parameter storage: one contiguous fp32 HBM buffer per network (+ grad / Adam moments),
+with a named view per tensor in the reference's state_dict order.  One buffer means one Adam
+launch and one all-reduce bucket per network; every tensor starts on a 16-byte boundary so
+the kernels can read it with 16-byte loads."""
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+
+def _align4(n):
+    return (n + 3) & ~3
+
+
+class FlatParams:
+    def __init__(self, spec, device, init=None):
+        self.spec = list(spec)
+        self.device = torch.device(device)
+        self.offsets = OrderedDict()
+        off = 0
+        for name, shape in self.spec:
+            n = int(np.prod(shape))
+            self.offsets[name] = (off, n, tuple(shape))
+            off = _align4(off + n)
+        self.numel = off
+        self.flat = torch.zeros(off, dtype=torch.float32, device=self.device)
+        self.views = self._views(self.flat)
+        self._grad = None
+        self.m = None
+        self.v = None
+        if init is not None:
+            self.load_state_dict(init)
+
+    def _views(self, buf):
+        return OrderedDict((k, buf[o:o + n].view(s)) for k, (o, n, s) in self.offsets.items())
+
+    def __getitem__(self, k):
+        return self.views[k]
+
+    def keys(self):
+        return self.views.keys()
+
+    # -- state_dict compatibility (torch.nn.Module semantics the reference relies on) --------
+    def state_dict(self):
+        return OrderedDict((k, v.detach()) for k, v in self.views.items())
+
+    def cpu_state_dict(self):
+        return OrderedDict((k, v.detach().cpu().clone()) for k, v in self.views.items())
+
+    def load_state_dict(self, sd, strict=True):
+        missing = [k for k in self.views if k not in sd]
+        unexpected = [k for k in sd if k not in self.views]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"Error(s) in loading state_dict: missing keys {missing}, "
+                               f"unexpected keys {unexpected}")
+        for k, dst in self.views.items():
+            if k not in sd:
+                continue
+            src = sd[k]
+            if isinstance(src, np.ndarray):
+                src = torch.from_numpy(np.ascontiguousarray(src))
+            if tuple(src.shape) != tuple(dst.shape):
+                raise RuntimeError(f"size mismatch for {k}: copying a param with shape "
+                                   f"{tuple(src.shape)}, the shape in current model is "
+                                   f"{tuple(dst.shape)}")
+            dst.copy_(src.to(torch.float32), non_blocking=False)
+
+    # -- training buffers -------------------------------------------------------------------
+    @property
+    def grad_flat(self):
+        if self._grad is None:
+            self._grad = torch.zeros_like(self.flat)
+            self.grads = self._views(self._grad)
+        return self._grad
+
+    def zero_grad(self):
+        self.grad_flat.zero_()
+
+    def reset_adam(self):
+        """A fresh torch.optim.Adam (the reference builds one per train() call,
+        Connect4GNN.py:132-133): zero moments, step count 0."""
+        if self.m is None:
+            self.m = torch.zeros_like(self.flat)
+            self.v = torch.zeros_like(self.flat)
+        else:
+            self.m.zero_()
+            self.v.zero_()
+        self.step = 0

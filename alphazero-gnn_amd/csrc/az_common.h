@@ -1,0 +1,60 @@
+// Shared helpers for the gfx950 kernels of libaz_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/az_hip.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace az {
+
+// Error reporting: every entry point returns AZ_OK or an AZ_E* code and leaves a message
+// retrievable with az_last_error() (thread-local).
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+enum Act { ACT_NONE = AZ_ACT_NONE, ACT_RELU = AZ_ACT_RELU, ACT_SIGMOID = AZ_ACT_SIGMOID,
+           ACT_TANH = AZ_ACT_TANH };
+
+__device__ __forceinline__ float sigmoidf_ref(float x) {
+  // torch.sigmoid on fp32: 1 / (1 + exp(-x))
+  return 1.0f / (1.0f + expf(-x));
+}
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_SIGMOID: return sigmoidf_ref(v);
+    case ACT_TANH: return tanhf(v);
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace az
+
+#define AZ_REQUIRE(cond, code, ...)      \
+  do {                                   \
+    if (!(cond)) {                       \
+      az::set_error(__VA_ARGS__);        \
+      return (code);                     \
+    }                                    \
+  } while (0)

@@ -1,0 +1,242 @@
+// GNN message passing of gnn_utils.py:5-74 on a destination-sorted CSR graph.
+//
+//   P      = x . W1'^T            one MFMA GEMM, W1 [H][2F] read as [2H][F] (row stride F), so
+//                                 P[v][2q] = W1[q,:F].x_v (target part), P[v][2q+1] = W1[q,F:].x_v
+//   alpha  = sigmoid(w2 . relu(P[d][2q] + P[s][2q+1] + b1) + b2)      attn_score_kernel
+//   agg[d] = sum_e (alpha_e / sum alpha) x[src_e]                      aggregate kernels (HBM-bound)
+//   x'[d]  = x_d + sigmoid(Wg[x_d;agg_d]+bg) * (Wu2 relu(Wu1[x_d;agg_d]+bu1)+bu2)   3 GEMMs,
+//            the concatenation [x_d;agg_d] is never materialised (A/A2 K-split + row gather),
+//            the gated residual is the last GEMM's epilogue.
+#include "az_common.h"
+
+namespace az {
+int gemm_f32(const az_gemm_desc* d, hipStream_t s);
+
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  // give every XCD (blocks b, b+8, ...) one contiguous run of destinations so the
+  // neighbour rows a destination gathers are mostly resident in that XCD's L2
+  return (n & 7) == 0 ? (b & 7) * (n >> 3) + (b >> 3) : b;
+}
+
+// 16 lanes per edge.  P rows interleave (target, source) projections per hidden unit q.
+__global__ __launch_bounds__(256) void attn_score_kernel(int E, const int* __restrict__ edge_dst,
+                                                        const int* __restrict__ col,
+                                                        const float* __restrict__ P, int ldp,
+                                                        int H, const float* __restrict__ b1,
+                                                        const float* __restrict__ w2,
+                                                        const float* __restrict__ b2,
+                                                        float* __restrict__ alpha) {
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int e = (blk * 256 + threadIdx.x) >> 4;
+  const int l = threadIdx.x & 15;
+  if (e >= E) return;  // whole 16-lane groups exit together
+  const int d = edge_dst[e], s = col[e];
+  const float* pd = P + (size_t)d * ldp;
+  const float* ps = P + (size_t)s * ldp;
+  float acc = 0.f;
+  for (int m = l; m < H / 2; m += 16) {
+    const f32x4 t = *reinterpret_cast<const f32x4*>(pd + 4 * m);
+    const f32x4 u = *reinterpret_cast<const f32x4*>(ps + 4 * m);
+    float h0 = t[0] + u[1] + b1[2 * m];
+    float h1 = t[2] + u[3] + b1[2 * m + 1];
+    h0 = h0 > 0.f ? h0 : 0.f;
+    h1 = h1 > 0.f ? h1 : 0.f;
+    acc = fmaf(h0, w2[2 * m], acc);
+    acc = fmaf(h1, w2[2 * m + 1], acc);
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
+  if (l == 0) alpha[e] = sigmoidf_ref(acc + b2[0]);
+}
+
+// LPR lanes per destination row (F <= 4*LPR*k, loop over the row in LPR*4-float strides).
+template <int LPR>
+__global__ __launch_bounds__(256) void aggregate_lanes_kernel(
+    int D, int identity, const int* __restrict__ dst_rows, const int* __restrict__ rowptr,
+    const int* __restrict__ col, const float* __restrict__ alpha, const float* __restrict__ x,
+    int ldx, int F, float* __restrict__ agg, int ldagg) {
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int i = (blk * 256 + threadIdx.x) / LPR;
+  const int l = threadIdx.x % LPR;
+  if (i >= D) return;
+  const int d = identity ? i : dst_rows[i];
+  const int e0 = rowptr[d], e1 = rowptr[d + 1];
+  float S = 0.f;
+  for (int e = e0; e < e1; ++e) S += alpha[e];
+  const bool norm = S > 0.f;
+  for (int f = l * 4; f < F; f += LPR * 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int e = e0;
+    for (; e + 4 <= e1; e += 4) {
+      int s[4];
+      float w[4];
+      f32x4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[j] = col[e + j];
+        w[j] = norm ? alpha[e + j] / S : alpha[e + j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const f32x4*>(x + (size_t)s[j] * ldx + f);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = fmaf(w[j], v[j][c], acc[c]);
+    }
+    for (; e < e1; ++e) {
+      const float w = norm ? alpha[e] / S : alpha[e];
+      const f32x4 v = *reinterpret_cast<const f32x4*>(x + (size_t)col[e] * ldx + f);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = fmaf(w, v[c], acc[c]);
+    }
+    *reinterpret_cast<f32x4*>(agg + (size_t)d * ldagg + f) = acc;
+  }
+}
+
+int aggregate(const az_graph* g, const float* x, int ldx, int F, const float* alpha, float* agg,
+              int ldagg, hipStream_t s) {
+  const int identity = (g->D == g->V) ? 1 : 0;
+  int lpr = 64;
+  if (F <= 64) lpr = 16;
+  else if (F <= 128) lpr = 32;
+  const long threads = (long)g->D * lpr;
+  const int blocks = (int)((threads + 255) / 256);
+  if (blocks == 0) return AZ_OK;
+  if (lpr == 16)
+    hipLaunchKernelGGL(aggregate_lanes_kernel<16>, dim3(blocks), dim3(256), 0, s, g->D, identity,
+                       g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg, ldagg);
+  else if (lpr == 32)
+    hipLaunchKernelGGL(aggregate_lanes_kernel<32>, dim3(blocks), dim3(256), 0, s, g->D, identity,
+                       g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg, ldagg);
+  else
+    hipLaunchKernelGGL(aggregate_lanes_kernel<64>, dim3(blocks), dim3(256), 0, s, g->D, identity,
+                       g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg, ldagg);
+  return check_launch("aggregate_lanes_kernel");
+}
+
+int attn_score(const az_graph* g, const float* P, int ldp, int H, const float* b1,
+               const float* w2, const float* b2, float* alpha, hipStream_t s) {
+  if (g->E == 0) return AZ_OK;
+  const int blocks = (int)(((long)g->E * 16 + 255) / 256);
+  hipLaunchKernelGGL(attn_score_kernel, dim3(blocks), dim3(256), 0, s, g->E, g->edge_dst, g->col,
+                     P, ldp, H, b1, w2, b2, alpha);
+  return check_launch("attn_score_kernel");
+}
+
+static int check_graph(const az_graph* g) {
+  AZ_REQUIRE(g && g->V >= 0 && g->E >= 0 && g->D >= 0 && g->D <= g->V, AZ_EINVAL,
+             "az_graph: bad sizes");
+  AZ_REQUIRE(g->rowptr && (g->E == 0 || (g->col && g->edge_dst)) && (g->D == 0 || g->dst_rows),
+             AZ_EINVAL, "az_graph: null arrays");
+  return AZ_OK;
+}
+
+static size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
+struct LayerWs {
+  float *P, *alpha, *agg, *gate, *u1;
+};
+
+static LayerWs carve(void* ws, int V, int E, int D, int F, int H) {
+  char* p = static_cast<char*>(ws);
+  LayerWs w;
+  w.P = reinterpret_cast<float*>(p); p += align256((size_t)V * 2 * H * 4);
+  w.alpha = reinterpret_cast<float*>(p); p += align256((size_t)E * 4);
+  w.agg = reinterpret_cast<float*>(p); p += align256((size_t)V * F * 4);
+  w.gate = reinterpret_cast<float*>(p); p += align256((size_t)D * F * 4);
+  w.u1 = reinterpret_cast<float*>(p);
+  return w;
+}
+
+}  // namespace az
+
+using namespace az;
+
+extern "C" int az_gnn_attn_score_fwd(const az_graph* g, const float* P, int ldp, int H,
+                                     const float* b1, const float* w2, const float* b2,
+                                     float* alpha, void* stream) {
+  int rc = check_graph(g);
+  if (rc) return rc;
+  AZ_REQUIRE(H > 0 && H % 2 == 0 && ldp % 4 == 0 && ldp >= 2 * H && aligned16(P), AZ_EINVAL,
+             "az_gnn_attn_score_fwd: P needs [V][>=2H] rows, 16B aligned");
+  AZ_REQUIRE(b1 && w2 && b2 && alpha, AZ_EINVAL, "az_gnn_attn_score_fwd: null");
+  return attn_score(g, P, ldp, H, b1, w2, b2, alpha, as_stream(stream));
+}
+
+extern "C" int az_gnn_aggregate_fwd(const az_graph* g, const float* x, int ldx, int F,
+                                    const float* alpha, float* agg, int ldagg, void* stream) {
+  int rc = check_graph(g);
+  if (rc) return rc;
+  AZ_REQUIRE(F > 0 && F % 4 == 0 && ldx % 4 == 0 && ldagg % 4 == 0 && aligned16(x) &&
+                 aligned16(agg),
+             AZ_EINVAL, "az_gnn_aggregate_fwd: F, strides %%4 and 16B alignment required");
+  AZ_REQUIRE(alpha || g->E == 0, AZ_EINVAL, "az_gnn_aggregate_fwd: null alpha");
+  return aggregate(g, x, ldx, F, alpha, agg, ldagg, as_stream(stream));
+}
+
+extern "C" size_t az_gnn_layer_ws_bytes(int V, int E, int D, int F, int H) {
+  return align256((size_t)V * 2 * H * 4) + align256((size_t)E * 4) + align256((size_t)V * F * 4) +
+         align256((size_t)D * F * 4) + align256((size_t)D * F * 4);
+}
+
+extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
+                                const az_gnn_layer_w* w, float* x_out, void* ws, size_t ws_bytes,
+                                void* stream) {
+  int rc = check_graph(g);
+  if (rc) return rc;
+  AZ_REQUIRE(x && x_out && w && ws && x != x_out, AZ_EINVAL, "az_gnn_layer_fwd: bad pointers");
+  AZ_REQUIRE(F % 16 == 0 && H % 4 == 0, AZ_EINVAL, "az_gnn_layer_fwd: F%%16, H%%4 required");
+  AZ_REQUIRE(ws_bytes >= az_gnn_layer_ws_bytes(g->V, g->E, g->D, F, H), AZ_EINVAL,
+             "az_gnn_layer_fwd: workspace too small");
+  hipStream_t s = as_stream(stream);
+  LayerWs L = carve(ws, g->V, g->E, g->D, F, H);
+  if (g->D < g->V) {
+    if (hipMemcpyAsync(x_out, x, (size_t)g->V * F * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return check_launch("hipMemcpyAsync");
+  }
+  if (g->D == 0) return AZ_OK;
+  // 1. attention projections for every node: P = x . W1'^T (W1 read as [2H][F])
+  az_gemm_desc d = {};
+  d.M = g->V; d.N = 2 * H; d.K = F;
+  d.A = x; d.lda = F; d.a_kmajor = 1;
+  d.B = w->att_w1; d.ldb = F; d.b_kmajor = 1;
+  d.C = L.P; d.ldc = 2 * H;
+  if ((rc = gemm_f32(&d, s))) return rc;
+  // 2. per-edge attention weights, 3. normalised aggregation
+  if ((rc = attn_score(g, L.P, 2 * H, H, w->att_b1, w->att_w2, w->att_b2, L.alpha, s))) return rc;
+  if ((rc = aggregate(g, x, F, F, L.alpha, L.agg, F, s))) return rc;
+  // 4. gate = sigmoid(Wg [x_d; agg_d] + bg), u1 = relu(Wu1 [x_d; agg_d] + bu1)
+  az_gemm_desc c = {};
+  c.M = g->D; c.N = F; c.K = 2 * F;
+  c.A = x; c.lda = F; c.a_kmajor = 1; c.A2 = L.agg; c.lda2 = F; c.K0 = F;
+  c.a_rows = (g->D == g->V) ? nullptr : g->dst_rows;
+  c.b_kmajor = 1; c.ldb = 2 * F; c.ldc = F;
+  c.B = w->gate_w; c.bias = w->gate_b; c.act = AZ_ACT_SIGMOID; c.C = L.gate;
+  if ((rc = gemm_f32(&c, s))) return rc;
+  c.B = w->upd_w1; c.bias = w->upd_b1; c.act = AZ_ACT_RELU; c.C = L.u1;
+  if ((rc = gemm_f32(&c, s))) return rc;
+  // 5. x_out[d] = x[d] + gate * (Wu2 u1 + bu2)
+  az_gemm_desc o = {};
+  o.M = g->D; o.N = F; o.K = F;
+  o.A = L.u1; o.lda = F; o.a_kmajor = 1;
+  o.B = w->upd_w2; o.ldb = F; o.b_kmajor = 1; o.bias = w->upd_b2;
+  o.R = x; o.ldr = F; o.G = L.gate; o.ldg = F;
+  o.C = x_out; o.ldc = F; o.c_rows = (g->D == g->V) ? nullptr : g->dst_rows;
+  return gemm_f32(&o, s);
+}
+
+extern "C" int az_mlp2_fwd(const float* x, int M, int F, const float* w0, const float* b0,
+                           const float* w2, const float* b2, float* hidden, float* y,
+                           void* stream) {
+  AZ_REQUIRE(x && w0 && b0 && w2 && b2 && hidden && y, AZ_EINVAL, "az_mlp2_fwd: null");
+  hipStream_t s = as_stream(stream);
+  az_gemm_desc d = {};
+  d.M = M; d.N = F; d.K = F;
+  d.A = x; d.lda = F; d.a_kmajor = 1;
+  d.B = w0; d.ldb = F; d.b_kmajor = 1; d.bias = b0; d.act = AZ_ACT_RELU;
+  d.C = hidden; d.ldc = F;
+  int rc = gemm_f32(&d, s);
+  if (rc) return rc;
+  d.A = hidden; d.B = w2; d.bias = b2; d.act = AZ_ACT_NONE; d.C = y;
+  return gemm_f32(&d, s);
+}

@@ -1,0 +1,260 @@
+// Board trunks and policy/value heads.
+//
+// c4_trunk: Connect4Net conv1 -> ReLU -> conv2 -> ReLU -> flatten (connect4/Connect4Net.py:42-49)
+// fused in one launch.  A 512-thread workgroup takes NB boards:
+//   1. boards (int8) -> zero-padded 9x9 fp32 tiles in LDS
+//   2. conv1 (1->32, 9 MACs/output) on the VALU into a zero-padded [NB][32][9][9] LDS image
+//   3. conv2 as an implicit GEMM on MFMA 16x16x4 f32:  rows = (board, position) flattened
+//      (NB*49), cols = 64 output channels, K = 288 ordered (tap, ci) so that every A-fragment
+//      read is ONE ds_read_b32 at lane-base + compile-time offset.  Each wave owns a 16-channel
+//      column tile and keeps its 72 weight fragments in VGPRs for the whole launch.
+//   4. bias + ReLU epilogue straight to the NCHW-flattened feature rows in HBM.
+#include <algorithm>
+#include "az_common.h"
+
+namespace az {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+template <int NB>
+__global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict__ boards, int B,
+                                                      const float* __restrict__ w1,
+                                                      const float* __restrict__ b1,
+                                                      const float* __restrict__ w2,
+                                                      const float* __restrict__ b2,
+                                                      float* __restrict__ feat) {
+  constexpr int P = 49, PP = 81, CI = 32;
+  constexpr int ROWS = NB * P;
+  constexpr int MT = (ROWS + 15) / 16;
+  __shared__ float bd[NB * PP];
+  __shared__ float c1[NB * CI * PP];
+  const int tid = threadIdx.x;
+  const int b0 = blockIdx.x * NB;
+  const int nb = min(NB, B - b0);
+
+  for (int i = tid; i < NB * PP; i += 512) {
+    const int b = i / PP, pp = i % PP, px = pp / 9, py = pp % 9;
+    float v = 0.f;
+    if (b < nb && px >= 1 && px <= 7 && py >= 1 && py <= 7)
+      v = (float)boards[(size_t)(b0 + b) * P + (px - 1) * 7 + (py - 1)];
+    bd[i] = v;
+  }
+  __syncthreads();
+  for (int i = tid; i < NB * CI * PP; i += 512) {
+    const int b = i / (CI * PP), rem = i % (CI * PP), ci = rem / PP, pp = rem % PP;
+    const int px = pp / 9, py = pp % 9;
+    float v = 0.f;
+    if (px >= 1 && px <= 7 && py >= 1 && py <= 7) {
+      float s = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+          s = fmaf(w1[ci * 9 + kh * 3 + kw], bd[b * PP + (px - 1 + kh) * 9 + (py - 1 + kw)], s);
+      s += b1[ci];
+      v = s > 0.f ? s : 0.f;
+    }
+    c1[i] = v;
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int nt = wave & 3, mh = wave >> 2;
+  const int h = lane >> 4, c16 = lane & 15;
+  const int co = nt * 16 + c16;
+  float breg[72];
+#pragma unroll
+  for (int s = 0; s < 72; ++s) {
+    const int tap = s >> 3, ci = 4 * (s & 7) + h;
+    breg[s] = w2[co * 288 + ci * 9 + (tap / 3) * 3 + (tap % 3)];
+  }
+  const float bias = b2[co];
+  for (int mt = mh; mt < MT; mt += 2) {
+    const int i = mt * 16 + c16;
+    int base = 0;
+    if (i < ROWS) {
+      const int b = i / P, p = i % P;
+      base = b * CI * PP + h * PP + (p / 7) * 9 + (p % 7);
+    }
+    const float* a_ptr = c1 + base;
+    f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 72; ++s) {
+      const int tap = s >> 3;
+      const int off = 4 * (s & 7) * PP + (tap / 3) * 9 + (tap % 3);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a_ptr[off], breg[s], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = mt * 16 + h * 4 + r;
+      if (row < nb * P) {
+        const int b = row / P, p = row % P;
+        const float v = acc[r] + bias;
+        feat[(size_t)(b0 + b) * 3136 + co * P + p] = v > 0.f ? v : 0.f;
+      }
+    }
+  }
+}
+
+// Generic 3x3 conv + ReLU, one thread per output (TicTacToe trunks: tiny, latency-bound).
+template <bool IN_I8>
+__global__ __launch_bounds__(256) void conv3x3_relu_kernel(const void* __restrict__ in_, int B,
+                                                          int Cin, int H, int W,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ b, int Cout,
+                                                          int pad, float* __restrict__ out) {
+  const int Ho = H + 2 * pad - 2, Wo = W + 2 * pad - 2;
+  const long total = (long)B * Cout * Ho * Wo;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int xo = idx % Wo, yo = (idx / Wo) % Ho, co = (idx / ((long)Wo * Ho)) % Cout;
+    const long bi = idx / ((long)Wo * Ho * Cout);
+    float s = 0.f;
+    for (int ci = 0; ci < Cin; ++ci) {
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int yi = yo + kh - pad;
+        if (yi < 0 || yi >= H) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int xi = xo + kw - pad;
+          if (xi < 0 || xi >= W) continue;
+          const long ii = ((bi * Cin + ci) * H + yi) * W + xi;
+          const float iv = IN_I8 ? (float)static_cast<const int8_t*>(in_)[ii]
+                                 : static_cast<const float*>(in_)[ii];
+          s = fmaf(w[((co * Cin + ci) * 3 + kh) * 3 + kw], iv, s);
+        }
+      }
+    }
+    s += b[co];
+    out[idx] = s > 0.f ? s : 0.f;
+  }
+}
+
+// Heads: one wave per board row.  Policy logits + log_softmax (+ exp), value + tanh.
+template <int AMAX>
+__global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ hp, int ldhp,
+                                                   const float* __restrict__ hv, int ldhv, int B,
+                                                   int K, const float* __restrict__ wp,
+                                                   const float* __restrict__ bp, int A,
+                                                   const float* __restrict__ wv,
+                                                   const float* __restrict__ bv,
+                                                   float* __restrict__ logp,
+                                                   float* __restrict__ pi,
+                                                   float* __restrict__ v) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  float acc[AMAX];
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) acc[a] = 0.f;
+  float accv = 0.f;
+  const bool same = (hp == hv && ldhp == ldhv);
+  for (int k = lane * 4; k < K; k += 256) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + k);
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) {
+      if (a < A) {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(wp + (size_t)a * K + k);
+        acc[a] = fmaf(x[3], w[3], fmaf(x[2], w[2], fmaf(x[1], w[1], fmaf(x[0], w[0], acc[a]))));
+      }
+    }
+    const f32x4 y = same ? x : *reinterpret_cast<const f32x4*>(hv + (size_t)row * ldhv + k);
+    const f32x4 wvv = *reinterpret_cast<const f32x4*>(wv + k);
+    accv = fmaf(y[3], wvv[3], fmaf(y[2], wvv[2], fmaf(y[1], wvv[1], fmaf(y[0], wvv[0], accv))));
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) {
+    if (a < A) {
+      acc[a] = wave_sum(acc[a]) + bp[a];
+      mx = fmaxf(mx, acc[a]);
+    }
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a)
+    if (a < A) se += expf(acc[a] - mx);
+  const float lse = logf(se);
+  accv = wave_sum(accv);
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) {
+    if (a < A && lane == a) {
+      const float l = (acc[a] - mx) - lse;
+      logp[(size_t)row * A + a] = l;
+      if (pi) pi[(size_t)row * A + a] = expf(l);
+    }
+  }
+  if (lane == 0) v[row] = tanhf(accv + bv[0]);
+}
+
+}  // namespace az
+
+using namespace az;
+
+extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w,
+                               const float* conv1_b, const float* conv2_w, const float* conv2_b,
+                               float* feat, void* stream) {
+  AZ_REQUIRE(B >= 0, AZ_EINVAL, "az_c4_trunk_fwd: B=%d", B);
+  if (B == 0) return AZ_OK;
+  AZ_REQUIRE(boards && conv1_w && conv1_b && conv2_w && conv2_b && feat, AZ_EINVAL,
+             "az_c4_trunk_fwd: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (B >= 4096) {
+    hipLaunchKernelGGL(c4_trunk_kernel<8>, dim3((B + 7) / 8), dim3(512), 0, s, boards, B,
+                       conv1_w, conv1_b, conv2_w, conv2_b, feat);
+  } else if (B >= 2048) {
+    hipLaunchKernelGGL(c4_trunk_kernel<4>, dim3((B + 3) / 4), dim3(512), 0, s, boards, B,
+                       conv1_w, conv1_b, conv2_w, conv2_b, feat);
+  } else if (B >= 256) {
+    hipLaunchKernelGGL(c4_trunk_kernel<2>, dim3((B + 1) / 2), dim3(512), 0, s, boards, B,
+                       conv1_w, conv1_b, conv2_w, conv2_b, feat);
+  } else {
+    hipLaunchKernelGGL(c4_trunk_kernel<1>, dim3(B), dim3(512), 0, s, boards, B, conv1_w,
+                       conv1_b, conv2_w, conv2_b, feat);
+  }
+  return check_launch("c4_trunk_kernel");
+}
+
+extern "C" int az_conv3x3_relu_fwd(const void* in, int in_int8, int B, int Cin, int H, int W,
+                                   const float* w, const float* b, int Cout, int pad, float* out,
+                                   void* stream) {
+  AZ_REQUIRE(B >= 0 && Cin > 0 && Cout > 0 && H >= 3 - 2 * pad && W >= 3 - 2 * pad &&
+                 (pad == 0 || pad == 1),
+             AZ_EINVAL, "az_conv3x3_relu_fwd: bad shape");
+  if (B == 0) return AZ_OK;
+  AZ_REQUIRE(in && w && b && out, AZ_EINVAL, "az_conv3x3_relu_fwd: null pointer");
+  AZ_REQUIRE(!in_int8 || Cin == 1, AZ_EINVAL, "az_conv3x3_relu_fwd: int8 input needs Cin=1");
+  const long total = (long)B * Cout * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+  hipStream_t s = as_stream(stream);
+  if (in_int8)
+    hipLaunchKernelGGL(conv3x3_relu_kernel<true>, dim3(blocks), dim3(256), 0, s, in, B, Cin, H, W,
+                       w, b, Cout, pad, out);
+  else
+    hipLaunchKernelGGL(conv3x3_relu_kernel<false>, dim3(blocks), dim3(256), 0, s, in, B, Cin, H,
+                       W, w, b, Cout, pad, out);
+  return check_launch("conv3x3_relu_kernel");
+}
+
+extern "C" int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv, int B, int K,
+                            const float* wp, const float* bp, int A, const float* wv,
+                            const float* bv, float* logp, float* pi, float* v, void* stream) {
+  AZ_REQUIRE(B >= 0 && K > 0 && K % 4 == 0 && A > 0 && A <= 64, AZ_EINVAL,
+             "az_heads_fwd: bad shape B=%d K=%d A=%d", B, K, A);
+  if (B == 0) return AZ_OK;
+  AZ_REQUIRE(hp && hv && wp && bp && wv && bv && logp && v, AZ_EINVAL, "az_heads_fwd: null");
+  AZ_REQUIRE(aligned16(hp) && aligned16(hv) && aligned16(wp) && aligned16(wv) && ldhp % 4 == 0 &&
+                 ldhv % 4 == 0,
+             AZ_EINVAL, "az_heads_fwd: operands need 16B alignment");
+  hipStream_t s = as_stream(stream);
+  dim3 g((B + 3) / 4), blk(256);
+  if (A <= 8)
+    hipLaunchKernelGGL(heads_kernel<8>, g, blk, 0, s, hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v);
+  else if (A <= 16)
+    hipLaunchKernelGGL(heads_kernel<16>, g, blk, 0, s, hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v);
+  else if (A <= 32)
+    hipLaunchKernelGGL(heads_kernel<32>, g, blk, 0, s, hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v);
+  else
+    hipLaunchKernelGGL(heads_kernel<64>, g, blk, 0, s, hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v);
+  return check_launch("heads_kernel");
+}

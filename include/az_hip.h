@@ -1,0 +1,175 @@
+/* libaz_hip.so — C-ABI of the MI355X (gfx950) board-evaluation hot path of
+ * andrpac/alphazero-gnn: the Connect4/TicTacToe conv trunk + policy/value heads,
+ * the GNN message-passing layers of gnn_utils.py, their backward pass and Adam.
+ *
+ * Conventions
+ *   - Every pointer except the ones documented as host pointers is a DEVICE pointer
+ *     (HBM), caller-allocated.  No entry point allocates, frees or synchronises, so a
+ *     caller may capture them into a hipGraph.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the legacy default stream).
+ *   - All arithmetic is fp32 (the reference runs torch fp32: SURVEY.md §0.8); GEMM-shaped
+ *     work runs on v_mfma_f32_32x32x2_f32, everything else on the VALU.
+ *   - Return value: AZ_OK (0) or a negative AZ_E* code; az_last_error() explains it.
+ *   - Layouts are the reference's: nn.Linear weights [out][in] row-major, conv weights
+ *     [Cout][Cin][3][3], features the NCHW flatten c*n*n + x*n + y
+ *     (connect4/Connect4Net.py:42-49).
+ *
+ * Each entry point names the reference interface it replaces (path:line in the
+ * reference tree).  The Python binding (ctypes) is alphazero-gnn_amd/azhip/_lib.py;
+ * INTEGRATION.md shows the reference-side binding.
+ */
+#ifndef AZ_HIP_H
+#define AZ_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AZ_ABI_VERSION 1
+
+#define AZ_OK 0
+#define AZ_EINVAL (-1)     /* bad shape / null pointer / misaligned buffer */
+#define AZ_ELAUNCH (-2)    /* a kernel launch failed (hipGetLastError) */
+#define AZ_EDEVICE (-3)    /* no gfx950 device / HIP runtime error */
+
+#define AZ_ACT_NONE 0
+#define AZ_ACT_RELU 1
+#define AZ_ACT_SIGMOID 2
+#define AZ_ACT_TANH 3
+
+int az_abi_version(void);
+const char* az_last_error(void);
+/* Checks that the current HIP device is a gfx950 (MI355X); returns AZ_OK or AZ_EDEVICE. */
+int az_check_device(void);
+
+/* ---------------------------------------------------------------------------------
+ * Dense fp32 GEMM with fused epilogue:  C = epi(op(A) . op(B))     (MFMA 32x32x2 f32;
+ * M <= 8 with a K-major B dispatches to a weight-streaming GEMV kernel).
+ * Replaces every nn.Linear of the path (gnn_utils.py:11-28,101-105, Connect4Net.py:21-25,
+ * TicTacToeNet.py:21-26) and, with the transposed layouts, their weight/input gradients.
+ *   A(i,k) = a_kmajor ? A[r(i)*lda + k] : A[k*lda + i]      r(i) = a_rows ? a_rows[i] : i
+ *            (k >= K0 reads A2[r(i)*lda2 + k-K0] when A2 != NULL: concatenation [A | A2]
+ *             along K, i.e. torch.cat([t, agg], dim=1) of gnn_utils.py:31,68)
+ *   B(k,j) = b_kmajor ? B[j*ldb + k] : B[k*ldb + j]          (b_kmajor = nn.Linear weight)
+ *   v      = act(sum_k A(i,k) B(k,j) + bias[j])
+ *   v      = R ? R[c(i)*ldr + j] + (G ? G[i*ldg + j] : 1) * v : v   (gated residual,
+ *            gnn_utils.py:71)
+ *   C[c(i)*ldc + j] = v + beta * C[c(i)*ldc + j]             c(i) = c_rows ? c_rows[i] : i
+ * Requirements: K % 4 == 0; lda, lda2, ldb % 4 == 0 and 16-byte aligned A/A2/B when the
+ * corresponding operand is read along its contiguous dimension; K0 % 16 == 0; a_rows only
+ * with a_kmajor; M % 4 == 0 when !a_kmajor; N % 4 == 0 when !b_kmajor.
+ * --------------------------------------------------------------------------------- */
+typedef struct az_gemm_desc {
+  int M, N, K;
+  const float* A; int lda; int a_kmajor;
+  const float* A2; int lda2; int K0;
+  const int* a_rows;
+  const float* B; int ldb; int b_kmajor;
+  const float* bias;
+  int act;
+  const float* R; int ldr;
+  const float* G; int ldg;
+  float beta;
+  float* C; int ldc;
+  const int* c_rows;
+} az_gemm_desc;
+
+int az_gemm_f32(const az_gemm_desc* d, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Connect4Net trunk, connect4/Connect4Net.py:42-49 (== Connect4GNNWrapper.extract_features,
+ * connect4/Connect4GNN.py:31-46 in eval mode): conv1 3x3 p1 + ReLU -> conv2 3x3 p1 + ReLU ->
+ * NCHW flatten, fused in one kernel (conv1 in LDS, conv2 as an implicit GEMM on MFMA 16x16x4).
+ *   boards  int8 [B][7][7] in {-1,0,1} (axis 0 = column x, axis 1 = row y)
+ *   feat    fp32 [B][3136]
+ * --------------------------------------------------------------------------------- */
+int az_c4_trunk_fwd(const int8_t* boards, int B,
+                    const float* conv1_w, const float* conv1_b,
+                    const float* conv2_w, const float* conv2_b,
+                    float* feat, void* stream);
+
+/* 3x3 conv (stride 1, padding `pad` in {0,1}) + ReLU on NCHW input; `in` is int8 boards
+ * [B][H][W] (Cin must be 1) when in_int8 != 0, else fp32 [B][Cin][H][W].
+ * TicTacToeNet conv1..conv3, tictactoe/TicTacToeNet.py:33-35. */
+int az_conv3x3_relu_fwd(const void* in, int in_int8, int B, int Cin, int H, int W,
+                        const float* w, const float* b, int Cout, int pad,
+                        float* out, void* stream);
+
+/* Policy/value heads: logits = hp . wp^T + bp  -> log_softmax;  v = tanh(hv . wv^T + bv).
+ * Connect4GNN.py:48-57 (hp = hv = features, K = 3136) and the last layers of
+ * TicTacToeGNN.py:36-45 (hp = relu(fc1), hv = relu(fc2), K = 512).  A <= 64.
+ *   logp [B][A], pi [B][A] = exp(logp) (may be NULL), v [B]. */
+int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv, int B, int K,
+                 const float* wp, const float* bp, int A, const float* wv, const float* bv,
+                 float* logp, float* pi, float* v, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * GNN message passing (gnn_utils.py:5-74) over a destination-sorted CSR graph.
+ * The reference's star (row 0 = destination, rows 1..N-1 = sources) is the CSR with
+ * rowptr = [0, N-1, N-1, ...], col = [1..N-1]; the synthetic grid has one segment per node.
+ * --------------------------------------------------------------------------------- */
+typedef struct az_graph {
+  int V, E;
+  const int* rowptr;    /* [V+1] */
+  const int* col;       /* [E] source node of edge e (sorted by destination) */
+  const int* edge_dst;  /* [E] destination node of edge e */
+  int D;                /* number of destinations with >= 1 in-edge */
+  const int* dst_rows;  /* [D] those destinations (ascending) */
+} az_graph;
+
+typedef struct az_gnn_layer_w {     /* GNNLayer parameters, state_dict order */
+  const float* att_w1; const float* att_b1;   /* attention.0  [H][2F], [H] */
+  const float* att_w2; const float* att_b2;   /* attention.2  [1][H],  [1] */
+  const float* upd_w1; const float* upd_b1;   /* update_net.0 [F][2F], [F] */
+  const float* upd_w2; const float* upd_b2;   /* update_net.2 [F][F],  [F] */
+  const float* gate_w; const float* gate_b;   /* gate.0       [F][2F], [F] */
+} az_gnn_layer_w;
+
+/* alpha[e] = sigmoid(w2 . relu(P[dst(e)][2q] + P[col(e)][2q+1] + b1) + b2)
+ * the factored attention MLP of GNNLayer.compute_attention (gnn_utils.py:30-32,48-55):
+ * W1 [t; x] = W1[:, :F] t + W1[:, F:] x, so both halves are projected once per NODE.
+ * P [V][2H] (row stride ldp) interleaves them: P[v][2q] = W1[q, :F].x_v,
+ * P[v][2q+1] = W1[q, F:].x_v, which is exactly the GEMM x . W1'^T with W1 [H][2F] read as
+ * [2H][F] (row stride F).  H % 2 == 0. */
+int az_gnn_attn_score_fwd(const az_graph* g, const float* P, int ldp, int H,
+                          const float* b1, const float* w2, const float* b2,
+                          float* alpha, void* stream);
+
+/* agg[d] = sum_{e in seg(d)} a'_e x[col(e)],  a' = a / sum(a) when sum(a) > 0
+ * (gnn_utils.py:57-65), for the D destinations g->dst_rows (D == V means every row);
+ * other rows of agg are not written.  Edges are summed in CSR order (deterministic).
+ * x, agg: [V][F] with row strides ldx, ldagg; F % 4 == 0. */
+int az_gnn_aggregate_fwd(const az_graph* g, const float* x, int ldx, int F,
+                         const float* alpha, float* agg, int ldagg, void* stream);
+
+/* One full GNNLayer.forward (gnn_utils.py:34-74) generalised per destination:
+ * x_out[d] = x[d] + sigmoid(Wg[x_d;agg_d]+bg) * (Wu2 relu(Wu1[x_d;agg_d]+bu1)+bu2) for the D
+ * destinations, x_out[v] = x[v] for every other row (a 1-row GNNLayer input is returned
+ * unchanged, gnn_utils.py:35-36).  x_out may not alias x.  `ws` is a device workspace of
+ * az_gnn_layer_ws_bytes() bytes; when `save` is non-NULL the activations the backward
+ * pass needs are kept in it (see az_gnn_layer_bwd). */
+size_t az_gnn_layer_ws_bytes(int V, int E, int D, int F, int H);
+int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H, const az_gnn_layer_w* w,
+                     float* x_out, void* ws, size_t ws_bytes, void* stream);
+
+/* output_transform, gnn_utils.py:101-105,115: y = W2 relu(W0 x + b0) + b2 on M rows.
+ * hidden: [M][F] scratch (kept for the backward pass). */
+int az_mlp2_fwd(const float* x, int M, int F, const float* w0, const float* b0,
+                const float* w2, const float* b2, float* hidden, float* y, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * torch.optim.Adam step (defaults of Connect4GNN.py:132-133: betas (0.9,0.999), eps 1e-8,
+ * no weight decay, no amsgrad) over one flat fp32 parameter buffer:
+ *   m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2;
+ *   p -= (lr / (1-b1^t)) m / (sqrt(v) / sqrt(1-b2^t) + eps)          (t = step >= 1)
+ * --------------------------------------------------------------------------------- */
+int az_adam_f32(float* p, const float* g, float* m, float* v, int64_t n,
+                double lr, double beta1, double beta2, double eps, int step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AZ_HIP_H */

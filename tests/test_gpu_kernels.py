@@ -1,0 +1,255 @@
+"""Kernel-level parity on the MI355X: every C-ABI entry point against the oracle (numpy
+float64 restatement of the reference) or, for plain GEMM shapes, a torch fp32 reference."""
+import numpy as np
+import pytest
+
+from conftest import golden, split_weights
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from azhip import ops as _ops
+    from azhip import _lib
+    _lib.lib()
+    return _ops
+
+
+def cu(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 3136, 3136), (3, 37, 64), (8, 128, 6272), (64, 128, 3136),
+                                   (512, 3136, 3136), (130, 70, 48), (4096, 256, 64)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_linear_vs_torch(ops, M, N, K, act):
+    g = torch.Generator().manual_seed(M * 7 + N + K + act)
+    x = torch.rand((M, K), generator=g) * 2 - 1
+    w = (torch.rand((N, K), generator=g) * 2 - 1) / K ** 0.5
+    b = torch.rand((N,), generator=g) - 0.5
+    ref = x.double() @ w.double().T + b.double()
+    ref = [lambda t: t, torch.relu, torch.sigmoid][act](ref)
+    y = ops.linear(x.cuda(), w.cuda(), b.cuda(), act=act).cpu()
+    assert rel_err(y.numpy(), ref.numpy()) < 2e-6
+
+
+def test_linear_split_gather_gated(ops):
+    g = torch.Generator().manual_seed(3)
+    V, F = 40, 64
+    x = torch.rand((V, F), generator=g) - 0.5
+    agg = torch.rand((V, F), generator=g) - 0.5
+    w = torch.rand((F, 2 * F), generator=g) - 0.5
+    b = torch.rand((F,), generator=g)
+    rows = torch.tensor([0, 5, 7, 39], dtype=torch.int32)
+    Gt = torch.rand((4, F), generator=g)
+    R = torch.rand((V, F), generator=g)
+    out = torch.zeros((V, F))
+    c = torch.cat([x, agg], 1)[rows.long()].double()
+    ref = R.double()[rows.long()] + Gt.double() * (c @ w.double().T + b.double())
+    for M in (4,):
+        o = out.cuda()
+        ops.linear(x.cuda(), w.cuda(), b.cuda(), x2=agg.cuda(), a_rows=rows.cuda(), R=R.cuda(),
+                   G=Gt.cuda(), c_rows=rows.cuda(), out=o, M=M)
+        got = o.cpu()[rows.long()]
+        assert rel_err(got.numpy(), ref.numpy()) < 2e-6
+        untouched = np.setdiff1d(np.arange(V), rows.numpy())
+        assert np.all(o.cpu().numpy()[untouched] == 0)
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 3136, 64), (128, 256, 4096), (36, 20, 64)])
+def test_matmul_tn_nn(ops, M, N, K):
+    g = torch.Generator().manual_seed(11)
+    a = torch.rand((K, M), generator=g) - 0.5      # a^T is [M, K]
+    b = torch.rand((K, N), generator=g) - 0.5
+    out = torch.ones((M, N)).cuda()
+    ops.matmul_tn(a.cuda(), b.cuda(), out, M, N, K, beta=1.0)
+    ref = a.double().T @ b.double() + 1
+    assert rel_err(out.cpu().numpy(), ref.numpy()) < 2e-6
+    a2 = torch.rand((M, K), generator=g) - 0.5
+    out2 = torch.empty((M, N)).cuda()
+    ops.matmul_nn(a2.cuda(), b.cuda(), out2, M, N, K)
+    assert rel_err(out2.cpu().numpy(), (a2.double() @ b.double()).numpy()) < 2e-6
+
+
+def test_c4_trunk_and_heads_vs_oracle(ops):
+    from oracle import nets as O
+    z = golden("c4_net.npz")
+    W = split_weights(z, "w/")
+    Wd = {k: cu(v) for k, v in W.items()}
+    for B in (1, 3, 256):
+        boards = np.concatenate([z["boards"]] * 2)[:B]
+        feat = ops.c4_trunk(cu(boards), Wd)
+        ref = O.c4_features(boards, W)
+        np.testing.assert_allclose(feat.cpu().numpy(), ref, atol=1e-5, rtol=1e-5)
+        logp, pi, v = ops.heads(feat, Wd["fc_policy.weight"], Wd["fc_policy.bias"],
+                                Wd["fc_value.weight"], Wd["fc_value.bias"])
+        rlp, rv = O.c4_heads(ref, W)
+        np.testing.assert_allclose(logp.cpu().numpy(), rlp, atol=1e-5)
+        np.testing.assert_allclose(v.cpu().numpy(), rv, atol=1e-5)
+        np.testing.assert_allclose(pi.cpu().numpy(), np.exp(rlp), atol=1e-5)
+    # golden reference outputs directly (batch-1 predict of the reference)
+    np.testing.assert_allclose(pi.cpu().numpy()[:256], z["pi_b1"], atol=1e-5)
+    np.testing.assert_allclose(v.cpu().numpy()[:256], z["v_b1"], atol=1e-5)
+
+
+def test_c4_trunk_large_batches(ops):
+    """NB = 2/4/8 boards-per-workgroup variants and ragged tails."""
+    from oracle import nets as O
+    z = golden("c4_net.npz")
+    W = split_weights(z, "w/")
+    Wd = {k: cu(v) for k, v in W.items()}
+    rng = np.random.default_rng(5)
+    for B in (2047, 4100):
+        boards = rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int8)
+        feat = ops.c4_trunk(cu(boards), Wd).cpu().numpy()
+        sel = np.r_[0:8, B - 9:B]
+        np.testing.assert_allclose(feat[sel], O.c4_features(boards[sel], W), atol=1e-5, rtol=1e-5)
+
+
+def test_ttt_trunk_heads_vs_golden(ops):
+    from oracle import nets as O
+    z = golden("ttt3.npz")
+    W, G = split_weights(z, "w/"), split_weights(z, "g/")
+    Wd = {k: cu(v) for k, v in W.items()}
+    Gd = {k: cu(v) for k, v in G.items()}
+    b = cu(z["boards"])
+    s = ops.conv3x3_relu(b, Wd["conv1.weight"], Wd["conv1.bias"], 1)
+    s = ops.conv3x3_relu(s, Wd["conv2.weight"], Wd["conv2.bias"], 1)
+    s = ops.conv3x3_relu(s, Wd["conv3.weight"], Wd["conv3.bias"], 0)
+    feat = s.reshape(s.shape[0], -1)
+    np.testing.assert_allclose(feat.cpu().numpy(), O.ttt_features(z["boards"], W), atol=1e-5)
+
+    def heads(f):
+        h1 = ops.linear(f, Wd["fc1.weight"], Wd["fc1.bias"], act=ops.ACT_RELU)
+        h2 = ops.linear(f, Wd["fc2.weight"], Wd["fc2.bias"], act=ops.ACT_RELU)
+        return ops.heads(h1, Wd["fc_policy.weight"], Wd["fc_policy.bias"], Wd["fc_value.weight"],
+                         Wd["fc_value.bias"], hv=h2)
+    _, pi, v = heads(feat)
+    np.testing.assert_allclose(pi.cpu().numpy(), z["pi"], atol=1e-5)
+    np.testing.assert_allclose(v.cpu().numpy(), z["v"], atol=1e-5)
+    enh, _ = ops.mlp2(feat, Gd["output_transform.0.weight"], Gd["output_transform.0.bias"],
+                      Gd["output_transform.2.weight"], Gd["output_transform.2.bias"])
+    _, pi, v = heads(enh)
+    np.testing.assert_allclose(pi.cpu().numpy(), z["pi_gnn"], atol=1e-5)
+    np.testing.assert_allclose(v.cpu().numpy(), z["v_gnn"], atol=1e-5)
+
+
+def _synth():
+    from azhip.weights import gnn_spec, synthetic_state_dict
+    z = golden("synth_gnn.npz")
+    G = synthetic_state_dict(gnn_spec(64, 2), int(z["seed_w"]))
+    rng = np.random.Generator(np.random.PCG64(int(z["seed_x"])))
+    x0 = rng.random((1024, 64), dtype=np.float32) * np.float32(2) - np.float32(1)
+    return z, G, x0
+
+
+def test_grid_attention_and_aggregate_vs_oracle(ops):
+    from oracle import nets as O
+    z, G, x0 = _synth()
+    g = ops.DeviceGraph(z["rowptr"], z["col"])
+    Gd = {k: cu(v) for k, v in G.items()}
+    x = cu(x0)
+    w1 = Gd["layers.0.attention.0.weight"]
+    P = ops.linear(x, w1.view(256, 64))
+    alpha = ops.attn_score(g, P, 128, Gd["layers.0.attention.0.bias"],
+                           Gd["layers.0.attention.2.weight"], Gd["layers.0.attention.2.bias"])
+    L = {k[len("layers.0."):]: v.astype(np.float64) for k, v in G.items() if k.startswith("layers.0.")}
+    deg = np.diff(z["rowptr"])
+    dst = np.repeat(np.arange(1024), deg)
+    ref_a = O.attention_scores_pairs(x0[dst].astype(np.float64), x0[z["col"]].astype(np.float64), L)
+    np.testing.assert_allclose(alpha.cpu().numpy(), ref_a, atol=2e-6)
+    agg = ops.aggregate(g, x, alpha).cpu().numpy()
+    s = np.zeros(1024)
+    np.add.at(s, dst, ref_a)
+    ref_agg = np.zeros((1024, 64))
+    np.add.at(ref_agg, dst, x0[z["col"]] * (ref_a / s[dst])[:, None])
+    np.testing.assert_allclose(agg, ref_agg, atol=2e-6)
+
+
+def test_grid_layers_vs_golden(ops):
+    z, G, x0 = _synth()
+    g = ops.DeviceGraph(z["rowptr"], z["col"])
+    Gd = {k: cu(v) for k, v in G.items()}
+    x = cu(x0)
+    outs = []
+    for i in range(2):
+        Wl = {k[len(f"layers.{i}."):]: v for k, v in Gd.items() if k.startswith(f"layers.{i}.")}
+        x, _ = ops.gnn_layer(g, x, Wl)
+        outs.append(x.cpu().numpy())
+    np.testing.assert_allclose(outs[0], z["grid_x1"], atol=1e-5)
+    np.testing.assert_allclose(outs[1], z["grid_x2"], atol=1e-5)
+    y, _ = ops.mlp2(x, Gd["output_transform.0.weight"], Gd["output_transform.0.bias"],
+                    Gd["output_transform.2.weight"], Gd["output_transform.2.bias"])
+    np.testing.assert_allclose(y.cpu().numpy(), z["grid_out"], atol=1e-5)
+
+
+def test_star_literal_n4096(ops):
+    z, G, _ = _synth()
+    Gd = {k: cu(v) for k, v in G.items()}
+    rng = np.random.Generator(np.random.PCG64(int(z["seed_star"])))
+    sx = rng.random((4096, 64), dtype=np.float32) * np.float32(2) - np.float32(1)
+    g = ops.DeviceGraph.star(4096)
+    x = cu(sx)
+    for i in range(2):
+        Wl = {k[len(f"layers.{i}."):]: v for k, v in Gd.items() if k.startswith(f"layers.{i}.")}
+        x, _ = ops.gnn_layer(g, x, Wl)
+    y, _ = ops.mlp2(x, Gd["output_transform.0.weight"], Gd["output_transform.0.bias"],
+                    Gd["output_transform.2.weight"], Gd["output_transform.2.bias"])
+    y = y.cpu().numpy()
+    np.testing.assert_allclose(y[:65], z["star_out_head"], atol=1e-5)
+    np.testing.assert_allclose(y.sum(1), z["star_out_rowsum"], atol=1e-4)
+
+
+def test_c4_star_forward_vs_golden(ops, c4_gnn_weights):
+    z = golden("c4_gnn.npz")
+    W = split_weights(golden("c4_net.npz"), "w/")
+    Wd = {k: cu(v) for k, v in W.items()}
+    Gd = {k: cu(v) for k, v in c4_gnn_weights.items()}
+    feat = ops.c4_trunk(cu(z["boards"]), Wd)
+    g = ops.DeviceGraph.star(64)
+    x = feat
+    for i in range(2):
+        Wl = {k[len(f"layers.{i}."):]: v for k, v in Gd.items() if k.startswith(f"layers.{i}.")}
+        x, _ = ops.gnn_layer(g, x, Wl)
+        np.testing.assert_allclose(x[0].cpu().numpy(), z["star_row0"][i], atol=1e-5)
+        np.testing.assert_array_equal(x[1:].cpu().numpy(), feat[1:].cpu().numpy())
+    y, _ = ops.mlp2(x, Gd["output_transform.0.weight"], Gd["output_transform.0.bias"],
+                    Gd["output_transform.2.weight"], Gd["output_transform.2.bias"])
+    logp, pi, v = ops.heads(y, Wd["fc_policy.weight"], Wd["fc_policy.bias"],
+                            Wd["fc_value.weight"], Wd["fc_value.bias"])
+    np.testing.assert_allclose(logp.cpu().numpy(), z["star_logp"], atol=1e-5)
+    np.testing.assert_allclose(v.cpu().numpy(), z["star_v"], atol=1e-5)
+    # per-row semantics (predict_with_gnn): layers are the identity on a 1-row input
+    y1, _ = ops.mlp2(feat, Gd["output_transform.0.weight"], Gd["output_transform.0.bias"],
+                     Gd["output_transform.2.weight"], Gd["output_transform.2.bias"])
+    _, pi, v = ops.heads(y1, Wd["fc_policy.weight"], Wd["fc_policy.bias"],
+                         Wd["fc_value.weight"], Wd["fc_value.bias"])
+    np.testing.assert_allclose(pi.cpu().numpy(), z["pi_gnn_b1"], atol=1e-5)
+    np.testing.assert_allclose(v.cpu().numpy(), z["v_gnn_b1"], atol=1e-5)
+
+
+def test_adam_vs_oracle(ops):
+    from oracle.nets import Adam
+    rng = np.random.default_rng(0)
+    n = 10007
+    p = rng.standard_normal(n).astype(np.float32)
+    P = {"p": p.astype(np.float64)}
+    opt = Adam(P, lr=1e-3)
+    pd, md, vd = cu(p), torch.zeros(n).cuda(), torch.zeros(n).cuda()
+    for step in range(1, 4):
+        g = (rng.standard_normal(n) * 10.0 ** rng.integers(-6, 1, n)).astype(np.float32)
+        ops.adam(pd, cu(g), md, vd, 1e-3, step)
+        P = opt.step(P, {"p": g.astype(np.float64)})
+    np.testing.assert_allclose(pd.cpu().numpy(), P["p"], atol=1e-6)
