@@ -1,0 +1,224 @@
+"""Headline benchmark: Connect4 GNN board evaluation (BASELINE.json configs[1]).
+
+A step = one predict_with_gnn pass (per-board semantics, Connect4GNN.py:86-120 applied to a
+batch) over 512 synthetic random Connect4 boards already resident in HBM:
+    fused conv trunk -> output_transform GEMM1 (+ReLU) -> GEMM2 -> policy/value heads.
+Weights are random-init (PCG64) with the reference's shapes (no checkpoint download).
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N     (one rank/GPU)
+
+Each rank evaluates its own batch (rows are independent, no collective on the data path):
+value = N * B * K / max-over-ranks(time).  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "alphazero-gnn_amd"))
+
+METRIC = "board-state evals/sec (GNN fwd) + self-play games/sec, Connect4, 1/2/4/8 GPU"
+F = 3136
+A = 8
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="bounded CPU-baseline sample (rank 0, N=1 only)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-aggregate", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(W, G, seconds, B):
+    """The oracle (numpy restatement, fp32, BLAS threads) on the same workload: per-board GNN
+    forward of 512-board batches, repeated for ~`seconds`."""
+    from oracle import nets as O
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        threads = os.cpu_count()
+    rng = np.random.default_rng(1)
+    boards = rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int8)
+    W32 = {k: np.asarray(v, np.float32) for k, v in W.items()}
+    G32 = {k: np.asarray(v, np.float32) for k, v in G.items() if k.startswith("output_transform")}
+    f = np.float32
+    O.c4_heads(O.policy_value_gnn_per_row(O.c4_features(boards, W32, f), G32, f), W32, f)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        O.c4_heads(O.policy_value_gnn_per_row(O.c4_features(boards, W32, f), G32, f), W32, f)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n * B / dt, "unit": "board evals/s", "cores": int(threads), "kind": "port",
+            "sample": f"{n} batches x {B} random boards (numpy fp32 oracle: c4_features -> "
+                      f"output_transform -> heads, BLAS threads={threads}), {dt:.1f} s"}
+
+
+def aggregate_roofline(torch, ops, device, graphs=512):
+    """Config 5 per-GPU shard (4096 grids / 8 GPUs): 32x32 4-neighbour grids, F=64, CSR by
+    destination.  Times the scatter-aggregate kernel alone (HIP events)."""
+    h = w = 32
+    rp, cl = [0], []
+    for r in range(h):
+        for c in range(w):
+            nb = sorted(rr * w + cc for rr, cc in ((r - 1, c), (r, c - 1), (r, c + 1), (r + 1, c))
+                        if 0 <= rr < h and 0 <= cc < w)
+            cl += nb
+            rp.append(len(cl))
+    rp, cl = np.array(rp, np.int64), np.array(cl, np.int64)
+    V1, E1 = h * w, len(cl)
+    rowptr = np.concatenate([rp[:-1] + g * E1 for g in range(graphs)] + [[graphs * E1]])
+    col = np.concatenate([cl + g * V1 for g in range(graphs)])
+    g = ops.DeviceGraph(rowptr, col, device)
+    V, E, Fd = g.V, g.E, 64
+    gen = torch.Generator(device=device).manual_seed(0)
+    x = torch.rand((V, Fd), device=device, generator=gen) * 2 - 1
+    alpha = torch.rand((E,), device=device, generator=gen)
+    agg = torch.empty_like(x)
+    for _ in range(3):
+        ops.aggregate(g, x, alpha, agg)
+    reps = 20
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+    for i in range(reps):
+        ev[2 * i].record()
+        ops.aggregate(g, x, alpha, agg)
+        ev[2 * i + 1].record()
+    torch.cuda.synchronize()
+    ms = float(np.mean([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps)]))
+    nbytes = V * Fd * 4 + E * 4 + E * 4 + (V + 1) * 4 + V * Fd * 4
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"kernel": "aggregate_lanes_kernel<16>", "bound": "hbm", "achieved": round(gbs, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "traffic": None, "avg_launch_us": round(ms * 1e3, 2),
+            "workload": f"{graphs} 32x32 grids, V={V}, E={E}, F=64 (config-5 shard per GPU)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
+    from azhip import ops
+    from azhip.nets import C4Evaluator
+    from azhip.weights import connect4_net_spec, gnn_spec, synthetic_state_dict
+
+    W = synthetic_state_dict(connect4_net_spec(7), 1)
+    G = synthetic_state_dict(gnn_spec(F, 2), 2)
+    ev = C4Evaluator(W, G, device=device)
+    B = args.batch
+    rng = np.random.default_rng(1000 + rank)
+    boards = torch.from_numpy(rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int8)).to(device)
+    Wn, Gn = ev.nnet.params, ev.gnn.params
+    h = torch.empty((B, F), device=device)
+    y = torch.empty((B, F), device=device)
+    logp = torch.empty((B, A), device=device)
+    pi = torch.empty((B, A), device=device)
+    v = torch.empty((B,), device=device)
+
+    def step(events=None):
+        feat = ev.nnet.features(boards)
+        if events is not None:
+            events[0].record()
+        ops.linear(feat, Gn["output_transform.0.weight"], Gn["output_transform.0.bias"],
+                   act=ops.ACT_RELU, out=h)
+        if events is not None:
+            events[1].record()
+        ops.linear(h, Gn["output_transform.2.weight"], Gn["output_transform.2.bias"], out=y)
+        if events is not None:
+            events[2].record()
+        ops.heads(y, Wn["fc_policy.weight"], Wn["fc_policy.bias"], Wn["fc_value.weight"],
+                  Wn["fc_value.bias"], logp=logp, pi=pi, v=v)
+
+    # correctness guard: the bench path equals the evaluator's predict_with_gnn path
+    step()
+    _, pi_ref, v_ref = ev.evaluate(boards, gnn=True)
+    torch.cuda.synchronize()
+    assert torch.allclose(pi, pi_ref) and torch.allclose(v, v_ref)
+
+    for _ in range(args.warmup):
+        step()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    gemm_ms = [e[0].elapsed_time(e[1]) for e in evs] + [e[1].elapsed_time(e[2]) for e in evs]
+    avg_gemm_s = float(np.mean(gemm_ms)) * 1e-3
+    flop = 2.0 * B * F * F
+    achieved = flop / avg_gemm_s / 1e12
+
+    agg = None
+    if not args.no_aggregate:
+        agg = aggregate_roofline(torch, ops, device)
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "gemm_pmc.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(W, G, args.cpu_seconds, B)
+
+    if rank == 0:
+        value = world * B * args.steps / elapsed
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "board evals/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (uniform random {-1,0,1} 7x7 boards; PCG64 random-init weights "
+                    "of the reference shapes)",
+            "config": {"workload": "Connect4 (reference 7x7+pass board) Connect4GNN "
+                                   "predict_with_gnn per-board fwd: trunk -> output_transform "
+                                   "-> heads, batch of random boards per GPU",
+                       "global_batch": B * world, "batch_per_gpu": B, "feature_dim": F,
+                       "parallelism": f"dp{world} (independent shards, no collective)"},
+            "roofline": {"kernel": "gemm_f32_mfma (output_transform Linear 3136x3136)",
+                         "bound": "mfma", "achieved": round(achieved, 2),
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "avg_launch_us": round(avg_gemm_s * 1e6, 2),
+                         "flop_per_launch": flop},
+            "aggregate_roofline": agg,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
