@@ -15,7 +15,7 @@ c_int, c_float, c_double, c_void_p, c_int64, c_size_t = (
     ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_void_p, ctypes.c_int64, ctypes.c_size_t)
 c_char_p = ctypes.c_char_p
 
-ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH = 0, 1, 2, 3
+ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_DRELU = 0, 1, 2, 3, 4
 
 
 class GemmDesc(ctypes.Structure):
@@ -25,6 +25,7 @@ class GemmDesc(ctypes.Structure):
         ("A2", c_void_p), ("lda2", c_int), ("K0", c_int),
         ("a_rows", c_void_p),
         ("B", c_void_p), ("ldb", c_int), ("b_kmajor", c_int),
+        ("b_rows", c_void_p),
         ("bias", c_void_p),
         ("act", c_int),
         ("R", c_void_p), ("ldr", c_int),
@@ -32,6 +33,8 @@ class GemmDesc(ctypes.Structure):
         ("beta", c_float),
         ("C", c_void_p), ("ldc", c_int),
         ("c_rows", c_void_p),
+        ("C2", c_void_p), ("ldc2", c_int),
+        ("ws", c_void_p), ("ws_bytes", c_size_t),
     ]
 
 
@@ -56,9 +59,10 @@ SIGNATURES = {
                                 c_void_p, c_void_p]),
     "az_conv3x3_relu_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "az_heads_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
     "az_heads_fwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p,
                              c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                             c_void_p]),
+                             c_void_p, c_size_t, c_void_p]),
     "az_gnn_attn_score_fwd": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_void_p]),
     "az_gnn_aggregate_fwd": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int, c_void_p,
@@ -67,7 +71,7 @@ SIGNATURES = {
     "az_gnn_layer_fwd": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int,
                                  ctypes.POINTER(LayerW), c_void_p, c_void_p, c_size_t, c_void_p]),
     "az_mlp2_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                            c_void_p, c_void_p, c_void_p]),
+                            c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "az_adam_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_double, c_double,
                             c_double, c_double, c_int, c_void_p]),
 }

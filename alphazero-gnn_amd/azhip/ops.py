@@ -25,8 +25,23 @@ def _need(t, dtype=torch.float32, name="tensor"):
         raise ValueError(f"{name} must be {dtype} (got {t.dtype})")
 
 
-def gemm(desc):
+_WS = {}
+
+
+def workspace(device, nbytes=64 << 20):
+    """Per-device split-K workspace (kept for the process lifetime; grows on demand)."""
+    key = str(device)
+    t = _WS.get(key)
+    if t is None or t.numel() < nbytes:
+        t = _WS[key] = torch.empty((nbytes,), dtype=torch.uint8, device=device)
+    return t
+
+
+def gemm(desc, device=None):
     L = _lib.lib()
+    if device is not None and not desc.ws:
+        ws = workspace(device)
+        desc.ws, desc.ws_bytes = ws.data_ptr(), ws.numel()
     _lib.check(L.az_gemm_f32(ctypes.byref(desc), _stream()), "az_gemm_f32")
 
 
@@ -61,7 +76,7 @@ def linear(x, w, b=None, act=ACT_NONE, out=None, x2=None, a_rows=None, R=None, G
     d.beta = beta
     d.C, d.ldc = out.data_ptr(), out.stride(0)
     d.c_rows = c_rows.data_ptr() if c_rows is not None else None
-    gemm(d)
+    gemm(d, x.device)
     return out
 
 
@@ -73,7 +88,7 @@ def matmul_tn(a, b, out, M, N, K, beta=0.0, lda=None, ldb=None):
     d.B, d.ldb, d.b_kmajor = b.data_ptr(), ldb or b.stride(0), 0
     d.beta = beta
     d.C, d.ldc = out.data_ptr(), out.stride(0)
-    gemm(d)
+    gemm(d, out.device)
     return out
 
 
@@ -85,7 +100,7 @@ def matmul_nn(a, b, out, M, N, K, beta=0.0):
     d.B, d.ldb, d.b_kmajor = b.data_ptr(), b.stride(0), 0
     d.beta = beta
     d.C, d.ldc = out.data_ptr(), out.stride(0)
-    gemm(d)
+    gemm(d, out.device)
     return out
 
 
@@ -131,8 +146,11 @@ def heads(hp, wp, bp, wv, bv, hv=None, want_pi=True, logp=None, pi=None, v=None)
     pi = (torch.empty((B, A), device=dev) if pi is None else pi) if want_pi else None
     v = torch.empty((B,), device=dev) if v is None else v
     L = _lib.lib()
+    nbytes = int(L.az_heads_ws_bytes(B, K, A))
+    ws = workspace(dev, max(nbytes, 64 << 20))
     _lib.check(L.az_heads_fwd(_p(hp), hp.stride(0), _p(hv), hv.stride(0), B, K, _p(wp), _p(bp), A,
-                              _p(wv), _p(bv), _p(logp), _p(pi), _p(v), _stream()), "az_heads_fwd")
+                              _p(wv), _p(bv), _p(logp), _p(pi), _p(v), _p(ws),
+                              ctypes.c_size_t(ws.numel()), _stream()), "az_heads_fwd")
     return logp, pi, v
 
 
@@ -212,8 +230,9 @@ def mlp2(x, w0, b0, w2, b2, hidden=None, out=None):
     hidden = torch.empty_like(x) if hidden is None else hidden
     out = torch.empty_like(x) if out is None else out
     L = _lib.lib()
+    ws = workspace(x.device)
     _lib.check(L.az_mlp2_fwd(_p(x), M, F, _p(w0), _p(b0), _p(w2), _p(b2), _p(hidden), _p(out),
-                             _stream()), "az_mlp2_fwd")
+                             _p(ws), ctypes.c_size_t(ws.numel()), _stream()), "az_mlp2_fwd")
     return out, hidden
 
 

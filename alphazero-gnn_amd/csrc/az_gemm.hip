@@ -1,12 +1,16 @@
 // fp32 GEMM on gfx950 MFMA (v_mfma_f32_32x32x2_f32) with fused epilogues, plus a
 // weight-streaming GEMV for M <= 8 (batch-1 predict, the star's row-0 update).
 //
-// Tile kernel: 256 threads = 4 waves as 2x2, BM x BN block tile, BK = 16, register-staged
-// double-buffered LDS.  Both operands are kept K-contiguous in LDS ([row][k], stride 20
-// floats: conflict-free ds_read_b128 for 16-lane groups) so each lane fetches 4 k-values
+// Tile kernel: 256 threads = 4 waves as 2x2, BM x BN block tile (128x128 or 64x64), BK = 32,
+// register-staged double-buffered LDS, optional split-K with a deterministic slab reduce when
+// the tile grid alone cannot fill the 256 CUs.  Both operands are kept K-contiguous in LDS
+// ([row][k], stride 36 floats: conflict-free ds_read_b128 for the 16-lane groups) so each lane
+// fetches 4 k-values
 // of its A row / B column with one ds_read_b128 and feeds 4 MFMAs; the k order inside an
 // 8-k group is permuted (lane half h owns k = 4h..4h+3, MFMA t sums k = t and 4+t), which
 // changes only the fp32 summation order.
+#include <algorithm>
+
 #include "az_common.h"
 
 namespace az {
@@ -17,21 +21,30 @@ struct GemmArgs {
   const float* A2; int lda2; int K0;
   const int* a_rows;
   const float* B; int ldb;
+  const int* b_rows;
   const float* bias; int act;
   const float* R; int ldr;
   const float* G; int ldg;
   float beta;
   float* C; int ldc;
   const int* c_rows;
+  float* C2; int ldc2;
+  // split-K: block (tile, s) covers k in [s*kc, min(K, (s+1)*kc)) and writes raw partial sums
+  // to slab[s][M][N]; splitk_reduce_kernel sums the slabs in s order (deterministic) and runs
+  // the epilogue.
+  int splits, kc;
+  float* slab;
 };
-
-constexpr int BK = 16;
-constexpr int LDK = BK + 4;
 
 __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int col, float acc) {
   if (row >= p.M || col >= p.N) return;
   float v = acc + (p.bias ? p.bias[col] : 0.f);
-  v = apply_act(v, p.act);
+  if (p.act == AZ_ACT_DRELU) {
+    v = p.G[(size_t)row * p.ldg + col] > 0.f ? v : 0.f;
+  } else {
+    v = apply_act(v, p.act);
+  }
+  if (p.C2) p.C2[(size_t)row * p.ldc2 + col] = v;
   const int cr = p.c_rows ? p.c_rows[row] : row;
   if (p.R) v = p.R[(size_t)cr * p.ldr + col] + (p.G ? p.G[(size_t)row * p.ldg + col] : 1.f) * v;
   float* dst = p.C + (size_t)cr * p.ldc + col;
@@ -39,18 +52,19 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int c
   *dst = v;
 }
 
-// Load one BK-deep slice of a K-major operand (rows x BK, row-major along k) as float4s.
-template <int ROWS, bool IS_A>
-__device__ __forceinline__ void load_kmajor(const GemmArgs& p, int r0, int k0, int nrows,
+// One BK-deep slice of a K-major operand (rows x BK, contiguous along k) as float4s.
+template <int ROWS, int BK, bool IS_A>
+__device__ __forceinline__ void load_kmajor(const GemmArgs& p, int r0, int k0, int kend, int nrows,
                                             f32x4 (&reg)[ROWS * BK / 4 / 256]) {
   constexpr int NF4 = ROWS * BK / 4 / 256;
+  constexpr int F4_PER_ROW = BK / 4;
 #pragma unroll
   for (int q = 0; q < NF4; ++q) {
     const int idx = threadIdx.x + q * 256;
-    const int row = idx >> 2, kq = idx & 3;
+    const int row = idx / F4_PER_ROW, kq = idx % F4_PER_ROW;
     const int gr = r0 + row, k = k0 + kq * 4;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (gr < nrows && k < p.K) {
+    if (gr < nrows && k < kend) {
       if (IS_A) {
         const int ar = p.a_rows ? p.a_rows[gr] : gr;
         const float* src = (p.A2 && k >= p.K0) ? p.A2 + (size_t)ar * p.lda2 + (k - p.K0)
@@ -64,21 +78,24 @@ __device__ __forceinline__ void load_kmajor(const GemmArgs& p, int r0, int k0, i
   }
 }
 
-template <int ROWS>
+template <int ROWS, int BK, int LDK>
 __device__ __forceinline__ void store_kmajor(float* lds, const f32x4 (&reg)[ROWS * BK / 4 / 256]) {
   constexpr int NF4 = ROWS * BK / 4 / 256;
+  constexpr int F4_PER_ROW = BK / 4;
 #pragma unroll
   for (int q = 0; q < NF4; ++q) {
     const int idx = threadIdx.x + q * 256;
-    const int row = idx >> 2, kq = idx & 3;
+    const int row = idx / F4_PER_ROW, kq = idx % F4_PER_ROW;
     *reinterpret_cast<f32x4*>(lds + row * LDK + kq * 4) = reg[q];
   }
 }
 
-// Operand stored contiguous along its M/N dimension: element (k, i) at base[k*ld + i].
-template <int ROWS>
-__device__ __forceinline__ void load_mnmajor(const float* base, int ld, int r0, int k0, int nrows,
-                                             int K, f32x4 (&reg)[ROWS * BK / 4 / 256]) {
+// Operand contiguous along its M/N dimension: element (k, i) at base[row(k)*ld + i] with
+// row(k) = rows ? rows[k] : k (row gather for weight gradients of gathered destinations).
+template <int ROWS, int BK>
+__device__ __forceinline__ void load_mnmajor(const float* base, int ld, const int* rows, int r0,
+                                             int k0, int kend, int nrows,
+                                             f32x4 (&reg)[ROWS * BK / 4 / 256]) {
   constexpr int NF4 = ROWS * BK / 4 / 256;
   constexpr int PER_K = ROWS / 4;
 #pragma unroll
@@ -87,12 +104,15 @@ __device__ __forceinline__ void load_mnmajor(const float* base, int ld, int r0, 
     const int kr = idx / PER_K, mq = idx % PER_K;
     const int gr = r0 + mq * 4, k = k0 + kr;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (k < K && gr < nrows) v = *reinterpret_cast<const f32x4*>(base + (size_t)k * ld + gr);
+    if (k < kend && gr < nrows) {
+      const int rk = rows ? rows[k] : k;
+      v = *reinterpret_cast<const f32x4*>(base + (size_t)rk * ld + gr);
+    }
     reg[q] = v;
   }
 }
 
-template <int ROWS>
+template <int ROWS, int BK, int LDK>
 __device__ __forceinline__ void store_mnmajor(float* lds, const f32x4 (&reg)[ROWS * BK / 4 / 256]) {
   constexpr int NF4 = ROWS * BK / 4 / 256;
   constexpr int PER_K = ROWS / 4;
@@ -105,8 +125,9 @@ __device__ __forceinline__ void store_mnmajor(float* lds, const f32x4 (&reg)[ROW
   }
 }
 
-template <int BM, int BN, bool A_KM, bool B_KM>
+template <int BM, int BN, int BK, bool A_KM, bool B_KM>
 __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs p) {
+  constexpr int LDK = BK + 4;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TI = WM / 32, TJ = WN / 32;
   constexpr int AF4 = BM * BK / 4 / 256, BF4 = BN * BK / 4 / 256;
@@ -114,13 +135,14 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
 
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
-  const int nwg = mt_n * nt_n;
+  const int nwg = mt_n * nt_n * p.splits;
   int bid = blockIdx.x;
-  // XCD-aware remap (blocks b, b+8 share an XCD): give each XCD a contiguous run of tile ids,
-  // consecutive ids share the B (weight) panel -> weight panel re-reads hit that XCD's L2.
+  // XCD-aware remap (blocks b, b+8 share an XCD): each XCD gets a contiguous run of ids;
+  // consecutive ids share (split, B panel) -> the weight slice is re-read from that XCD's L2.
   if ((nwg & 7) == 0) bid = (bid & 7) * (nwg >> 3) + (bid >> 3);
-  const int mt = bid % mt_n, nt = bid / mt_n;
+  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
   const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -135,25 +157,29 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs p) {
 
   f32x4 ra[AF4], rb[BF4];
   auto load = [&](int k0) {
-    if constexpr (A_KM) load_kmajor<BM, true>(p, m0, k0, p.M, ra);
-    else load_mnmajor<BM>(p.A, p.lda, m0, k0, p.M, p.K, ra);
-    if constexpr (B_KM) load_kmajor<BN, false>(p, n0, k0, p.N, rb);
-    else load_mnmajor<BN>(p.B, p.ldb, n0, k0, p.N, p.K, rb);
+    if constexpr (A_KM) load_kmajor<BM, BK, true>(p, m0, k0, kend, p.M, ra);
+    else load_mnmajor<BM, BK>(p.A, p.lda, nullptr, m0, k0, kend, p.M, ra);
+    if constexpr (B_KM) load_kmajor<BN, BK, false>(p, n0, k0, kend, p.N, rb);
+    else load_mnmajor<BN, BK>(p.B, p.ldb, p.b_rows, n0, k0, kend, p.N, rb);
   };
   auto store = [&](int buf) {
-    if constexpr (A_KM) store_kmajor<BM>(As[buf], ra); else store_mnmajor<BM>(As[buf], ra);
-    if constexpr (B_KM) store_kmajor<BN>(Bs[buf], rb); else store_mnmajor<BN>(Bs[buf], rb);
+    if constexpr (A_KM) store_kmajor<BM, BK, LDK>(As[buf], ra);
+    else store_mnmajor<BM, BK, LDK>(As[buf], ra);
+    if constexpr (B_KM) store_kmajor<BN, BK, LDK>(Bs[buf], rb);
+    else store_mnmajor<BN, BK, LDK>(Bs[buf], rb);
   };
 
-  const int nk = (p.K + BK - 1) / BK;
-  load(0);
-  store(0);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    load(kbeg);
+    store(0);
+  }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load((kt + 1) * BK);
+    if (kt + 1 < nk) load(kbeg + (kt + 1) * BK);
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < BK / 8; ++g) {
       f32x4 a[TI], b[TJ];
 #pragma unroll
       for (int i = 0; i < TI; ++i)
@@ -175,6 +201,7 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs p) {
     __syncthreads();
   }
 
+  float* slab = p.splits > 1 ? p.slab + (size_t)sp * p.M * p.N : nullptr;
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -183,8 +210,22 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs p) {
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int col = n0 + wn * WN + j * 32 + (lane & 31);
-        epilogue_store(p, row, col, acc[i][j][r]);
+        if (slab) {
+          if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][r];
+        } else {
+          epilogue_store(p, row, col, acc[i][j][r]);
+        }
       }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
+  const long total = (long)p.M * p.N;
+  const size_t plane = (size_t)p.M * p.N;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int k = 0; k < p.splits; ++k) s += p.slab[k * plane + idx];
+    epilogue_store(p, (int)(idx / p.N), (int)(idx % p.N), s);
+  }
 }
 
 // ------------------------------------------------------------------------------ GEMV
@@ -261,13 +302,13 @@ __global__ __launch_bounds__(256) void gemv_f32(GemmArgs p) {
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int BK>
 static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
-  const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  if (akm && bkm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, true, true>), dim3(nwg), dim3(256), 0, s, a);
-  else if (akm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, true, false>), dim3(nwg), dim3(256), 0, s, a);
-  else if (bkm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, false, true>), dim3(nwg), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, false, false>), dim3(nwg), dim3(256), 0, s, a);
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
+  if (akm && bkm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, true, true>), dim3(nwg), dim3(256), 0, s, a);
+  else if (akm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, true, false>), dim3(nwg), dim3(256), 0, s, a);
+  else if (bkm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, false, true>), dim3(nwg), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, false, false>), dim3(nwg), dim3(256), 0, s, a);
 }
 
 static void launch_gemv(const GemmArgs& a, hipStream_t s) {
@@ -280,40 +321,73 @@ static void launch_gemv(const GemmArgs& a, hipStream_t s) {
   }
 }
 
+// Pick the block tile and the split-K factor: aim for ~2 blocks per CU (512) on the 256 CUs,
+// keep >= 4 BK steps per split, and only split when the caller's workspace holds the slabs.
+static void plan(GemmArgs& a, int bm, int bn, int bk, size_t ws_bytes) {
+  const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+  int S = 1;
+  if (tiles < 256 && a.slab) {
+    S = (int)std::min<long>((512 + tiles - 1) / tiles, a.K / (bk * 4));
+    while (S > 1 && (size_t)S * a.M * a.N * 4 > ws_bytes) --S;
+    if (S < 1) S = 1;
+  }
+  a.splits = S;
+  a.kc = S > 1 ? ((a.K + S - 1) / S + bk - 1) / bk * bk : a.K;
+  if (S > 1) a.splits = (a.K + a.kc - 1) / a.kc;
+}
+
 int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
   AZ_REQUIRE(d != nullptr, AZ_EINVAL, "az_gemm_f32: null descriptor");
   AZ_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, AZ_EINVAL, "az_gemm_f32: negative size");
   if (d->M == 0 || d->N == 0) return AZ_OK;
   AZ_REQUIRE(d->A && d->B && d->C, AZ_EINVAL, "az_gemm_f32: null A/B/C");
-  AZ_REQUIRE(d->K % 4 == 0, AZ_EINVAL, "az_gemm_f32: K=%d must be a multiple of 4", d->K);
   const bool akm = d->a_kmajor != 0, bkm = d->b_kmajor != 0;
+  AZ_REQUIRE(!(akm || bkm) || d->K % 4 == 0, AZ_EINVAL,
+             "az_gemm_f32: K=%d must be a multiple of 4 for a K-major operand", d->K);
   AZ_REQUIRE(d->lda % 4 == 0 && aligned16(d->A), AZ_EINVAL, "az_gemm_f32: A needs lda%%4==0, 16B alignment");
   AZ_REQUIRE(d->ldb % 4 == 0 && aligned16(d->B), AZ_EINVAL, "az_gemm_f32: B needs ldb%%4==0, 16B alignment");
   if (d->A2) {
     AZ_REQUIRE(akm, AZ_EINVAL, "az_gemm_f32: A2 needs a K-major A");
-    AZ_REQUIRE(d->K0 % 16 == 0 && d->K0 > 0 && d->K0 < d->K, AZ_EINVAL, "az_gemm_f32: K0 must be a multiple of 16 inside (0,K)");
+    AZ_REQUIRE(d->K0 % 4 == 0 && d->K0 > 0 && d->K0 < d->K, AZ_EINVAL,
+               "az_gemm_f32: K0 must be a multiple of 4 inside (0,K)");
     AZ_REQUIRE(d->lda2 % 4 == 0 && aligned16(d->A2), AZ_EINVAL, "az_gemm_f32: A2 needs lda2%%4==0, 16B alignment");
   }
   AZ_REQUIRE(!d->a_rows || akm, AZ_EINVAL, "az_gemm_f32: a_rows needs a K-major A");
+  AZ_REQUIRE(!d->b_rows || !bkm, AZ_EINVAL, "az_gemm_f32: b_rows needs an N-major B");
   AZ_REQUIRE(akm || d->M % 4 == 0, AZ_EINVAL, "az_gemm_f32: M-major A needs M%%4==0");
   AZ_REQUIRE(bkm || d->N % 4 == 0, AZ_EINVAL, "az_gemm_f32: N-major B needs N%%4==0");
-  AZ_REQUIRE(d->act >= 0 && d->act <= 3, AZ_EINVAL, "az_gemm_f32: bad act %d", d->act);
+  AZ_REQUIRE(d->act >= 0 && d->act <= AZ_ACT_DRELU, AZ_EINVAL, "az_gemm_f32: bad act %d", d->act);
+  AZ_REQUIRE(d->act != AZ_ACT_DRELU || d->G, AZ_EINVAL, "az_gemm_f32: DRELU needs G");
+  AZ_REQUIRE(!(d->act == AZ_ACT_DRELU && d->R), AZ_EINVAL, "az_gemm_f32: DRELU excludes R");
 
-  GemmArgs a;
+  GemmArgs a = {};
   a.M = d->M; a.N = d->N; a.K = d->K;
   a.A = d->A; a.lda = d->lda; a.A2 = d->A2; a.lda2 = d->lda2; a.K0 = d->A2 ? d->K0 : d->K;
-  a.a_rows = d->a_rows; a.B = d->B; a.ldb = d->ldb;
+  a.a_rows = d->a_rows; a.B = d->B; a.ldb = d->ldb; a.b_rows = d->b_rows;
   a.bias = d->bias; a.act = d->act; a.R = d->R; a.ldr = d->ldr; a.G = d->G; a.ldg = d->ldg;
   a.beta = d->beta; a.C = d->C; a.ldc = d->ldc; a.c_rows = d->c_rows;
+  a.C2 = d->C2; a.ldc2 = d->ldc2;
+  a.slab = static_cast<float*>(d->ws);
+  a.splits = 1; a.kc = d->K;
 
-  if (d->M <= 8 && akm && bkm) {
+  if (d->M <= 8 && akm && bkm && !d->C2 && d->act != AZ_ACT_DRELU) {
     launch_gemv(a, s);
     return check_launch("gemv_f32");
   }
   const long t128 = (long)((d->M + 127) / 128) * ((d->N + 127) / 128);
-  if (t128 >= 240) launch_tile<128, 128>(a, akm, bkm, s);
-  else launch_tile<64, 64>(a, akm, bkm, s);
-  return check_launch("gemm_f32_mfma");
+  if (t128 >= 64) {
+    plan(a, 128, 128, 32, d->ws_bytes);
+    launch_tile<128, 128, 32>(a, akm, bkm, s);
+  } else {
+    plan(a, 64, 64, 32, d->ws_bytes);
+    launch_tile<64, 64, 32>(a, akm, bkm, s);
+  }
+  int rc = check_launch("gemm_f32_mfma");
+  if (rc || a.splits <= 1) return rc;
+  const long total = (long)a.M * a.N;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, a);
+  return check_launch("splitk_reduce_kernel");
 }
 
 }  // namespace az

@@ -49,8 +49,11 @@ __global__ __launch_bounds__(256) void attn_score_kernel(int E, const int* __res
   if (l == 0) alpha[e] = sigmoidf_ref(acc + b2[0]);
 }
 
-// LPR lanes per destination row (F <= 4*LPR*k, loop over the row in LPR*4-float strides).
-template <int LPR>
+// Segmented weighted reduce.  LPR lanes own one destination row; each lane covers NV
+// float4 column slices per pass (F == 4*LPR*NV exactly for the grid shapes, a loop otherwise).
+// Dependent-load chain per destination: rowptr -> (col, alpha) -> x rows; for degree <= 4 (the
+// grid) all of a destination's col/alpha loads are issued together, then all its x rows.
+template <int LPR, int NV>
 __global__ __launch_bounds__(256) void aggregate_lanes_kernel(
     int D, int identity, const int* __restrict__ dst_rows, const int* __restrict__ rowptr,
     const int* __restrict__ col, const float* __restrict__ alpha, const float* __restrict__ x,
@@ -61,6 +64,47 @@ __global__ __launch_bounds__(256) void aggregate_lanes_kernel(
   if (i >= D) return;
   const int d = identity ? i : dst_rows[i];
   const int e0 = rowptr[d], e1 = rowptr[d + 1];
+  const int deg = e1 - e0;
+  if (deg <= 4) {
+    int s[4];
+    float a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[j] = j < deg ? col[e0 + j] : 0;
+      a[j] = j < deg ? alpha[e0 + j] : 0.f;
+    }
+    float S = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < deg) S += a[j];
+    const bool norm = S > 0.f;
+    float w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = norm ? a[j] / S : a[j];
+    for (int f0 = l * 4; f0 < F; f0 += LPR * 4 * NV) {
+      f32x4 v[4][NV];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+          const int f = f0 + q * LPR * 4;
+          v[j][q] = (j < deg && f < F) ? *reinterpret_cast<const f32x4*>(x + (size_t)s[j] * ldx + f)
+                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        const int f = f0 + q * LPR * 4;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < deg)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] = fmaf(w[j], v[j][q][c], acc[c]);
+        if (f < F) *reinterpret_cast<f32x4*>(agg + (size_t)d * ldagg + f) = acc;
+      }
+    }
+    return;
+  }
   float S = 0.f;
   for (int e = e0; e < e1; ++e) S += alpha[e];
   const bool norm = S > 0.f;
@@ -93,24 +137,23 @@ __global__ __launch_bounds__(256) void aggregate_lanes_kernel(
   }
 }
 
+template <int LPR, int NV>
+static void launch_aggregate(const az_graph* g, int identity, const float* x, int ldx, int F,
+                             const float* alpha, float* agg, int ldagg, hipStream_t s) {
+  const long threads = (long)g->D * LPR;
+  const int blocks = (int)((threads + 255) / 256);
+  hipLaunchKernelGGL((aggregate_lanes_kernel<LPR, NV>), dim3(blocks), dim3(256), 0, s, g->D,
+                     identity, g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg, ldagg);
+}
+
 int aggregate(const az_graph* g, const float* x, int ldx, int F, const float* alpha, float* agg,
               int ldagg, hipStream_t s) {
+  if (g->D == 0) return AZ_OK;
   const int identity = (g->D == g->V) ? 1 : 0;
-  int lpr = 64;
-  if (F <= 64) lpr = 16;
-  else if (F <= 128) lpr = 32;
-  const long threads = (long)g->D * lpr;
-  const int blocks = (int)((threads + 255) / 256);
-  if (blocks == 0) return AZ_OK;
-  if (lpr == 16)
-    hipLaunchKernelGGL(aggregate_lanes_kernel<16>, dim3(blocks), dim3(256), 0, s, g->D, identity,
-                       g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg, ldagg);
-  else if (lpr == 32)
-    hipLaunchKernelGGL(aggregate_lanes_kernel<32>, dim3(blocks), dim3(256), 0, s, g->D, identity,
-                       g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg, ldagg);
-  else
-    hipLaunchKernelGGL(aggregate_lanes_kernel<64>, dim3(blocks), dim3(256), 0, s, g->D, identity,
-                       g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg, ldagg);
+  if (F <= 32) launch_aggregate<8, 1>(g, identity, x, ldx, F, alpha, agg, ldagg, s);
+  else if (F <= 64) launch_aggregate<8, 2>(g, identity, x, ldx, F, alpha, agg, ldagg, s);
+  else if (F <= 128) launch_aggregate<16, 2>(g, identity, x, ldx, F, alpha, agg, ldagg, s);
+  else launch_aggregate<64, 1>(g, identity, x, ldx, F, alpha, agg, ldagg, s);
   return check_launch("aggregate_lanes_kernel");
 }
 
@@ -133,8 +176,11 @@ static int check_graph(const az_graph* g) {
 
 static size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
+constexpr size_t kSplitWsBytes = size_t(16) << 20;  // split-K slabs for the layer's GEMMs
+
 struct LayerWs {
   float *P, *alpha, *agg, *gate, *u1;
+  void* split;
 };
 
 static LayerWs carve(void* ws, int V, int E, int D, int F, int H) {
@@ -144,7 +190,8 @@ static LayerWs carve(void* ws, int V, int E, int D, int F, int H) {
   w.alpha = reinterpret_cast<float*>(p); p += align256((size_t)E * 4);
   w.agg = reinterpret_cast<float*>(p); p += align256((size_t)V * F * 4);
   w.gate = reinterpret_cast<float*>(p); p += align256((size_t)D * F * 4);
-  w.u1 = reinterpret_cast<float*>(p);
+  w.u1 = reinterpret_cast<float*>(p); p += align256((size_t)D * F * 4);
+  w.split = p;
   return w;
 }
 
@@ -176,7 +223,7 @@ extern "C" int az_gnn_aggregate_fwd(const az_graph* g, const float* x, int ldx, 
 
 extern "C" size_t az_gnn_layer_ws_bytes(int V, int E, int D, int F, int H) {
   return align256((size_t)V * 2 * H * 4) + align256((size_t)E * 4) + align256((size_t)V * F * 4) +
-         align256((size_t)D * F * 4) + align256((size_t)D * F * 4);
+         align256((size_t)D * F * 4) + align256((size_t)D * F * 4) + kSplitWsBytes;
 }
 
 extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
@@ -201,6 +248,7 @@ extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
   d.A = x; d.lda = F; d.a_kmajor = 1;
   d.B = w->att_w1; d.ldb = F; d.b_kmajor = 1;
   d.C = L.P; d.ldc = 2 * H;
+  d.ws = L.split; d.ws_bytes = kSplitWsBytes;
   if ((rc = gemm_f32(&d, s))) return rc;
   // 2. per-edge attention weights, 3. normalised aggregation
   if ((rc = attn_score(g, L.P, 2 * H, H, w->att_b1, w->att_w2, w->att_b2, L.alpha, s))) return rc;
@@ -211,6 +259,7 @@ extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
   c.A = x; c.lda = F; c.a_kmajor = 1; c.A2 = L.agg; c.lda2 = F; c.K0 = F;
   c.a_rows = (g->D == g->V) ? nullptr : g->dst_rows;
   c.b_kmajor = 1; c.ldb = 2 * F; c.ldc = F;
+  c.ws = L.split; c.ws_bytes = kSplitWsBytes;
   c.B = w->gate_w; c.bias = w->gate_b; c.act = AZ_ACT_SIGMOID; c.C = L.gate;
   if ((rc = gemm_f32(&c, s))) return rc;
   c.B = w->upd_w1; c.bias = w->upd_b1; c.act = AZ_ACT_RELU; c.C = L.u1;
@@ -222,12 +271,13 @@ extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
   o.B = w->upd_w2; o.ldb = F; o.b_kmajor = 1; o.bias = w->upd_b2;
   o.R = x; o.ldr = F; o.G = L.gate; o.ldg = F;
   o.C = x_out; o.ldc = F; o.c_rows = (g->D == g->V) ? nullptr : g->dst_rows;
+  o.ws = L.split; o.ws_bytes = kSplitWsBytes;
   return gemm_f32(&o, s);
 }
 
 extern "C" int az_mlp2_fwd(const float* x, int M, int F, const float* w0, const float* b0,
-                           const float* w2, const float* b2, float* hidden, float* y,
-                           void* stream) {
+                           const float* w2, const float* b2, float* hidden, float* y, void* ws,
+                           size_t ws_bytes, void* stream) {
   AZ_REQUIRE(x && w0 && b0 && w2 && b2 && hidden && y, AZ_EINVAL, "az_mlp2_fwd: null");
   hipStream_t s = as_stream(stream);
   az_gemm_desc d = {};
@@ -235,6 +285,7 @@ extern "C" int az_mlp2_fwd(const float* x, int M, int F, const float* w0, const 
   d.A = x; d.lda = F; d.a_kmajor = 1;
   d.B = w0; d.ldb = F; d.b_kmajor = 1; d.bias = b0; d.act = AZ_ACT_RELU;
   d.C = hidden; d.ldc = F;
+  d.ws = ws; d.ws_bytes = ws ? ws_bytes : 0;
   int rc = gemm_f32(&d, s);
   if (rc) return rc;
   d.A = hidden; d.B = w2; d.bias = b2; d.act = AZ_ACT_NONE; d.C = y;

@@ -130,61 +130,92 @@ __global__ __launch_bounds__(256) void conv3x3_relu_kernel(const void* __restric
   }
 }
 
-// Heads: one wave per board row.  Policy logits + log_softmax (+ exp), value + tanh.
+// Heads in two deterministic passes (no weight re-reads per row):
+//  1. heads_partial_kernel: block (chunk c of 256 K-columns, group of rows).  Each thread owns
+//     one float4 column slice of the chunk and keeps the A+1 weight slices for it in VGPRs;
+//     every wave sweeps rows, reduces its 64 lanes and writes part[c][row][0..A].
+//  2. heads_finalize_kernel: sum the chunks in order, add biases, log_softmax / exp / tanh.
+constexpr int HEADS_KC = 256;        // K columns per chunk (64 lanes x float4)
+constexpr int HEADS_ROWS = 16;       // rows per block (4 per wave)
+
 template <int AMAX>
-__global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ hp, int ldhp,
-                                                   const float* __restrict__ hv, int ldhv, int B,
-                                                   int K, const float* __restrict__ wp,
-                                                   const float* __restrict__ bp, int A,
-                                                   const float* __restrict__ wv,
-                                                   const float* __restrict__ bv,
-                                                   float* __restrict__ logp,
-                                                   float* __restrict__ pi,
-                                                   float* __restrict__ v) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= B) return;
-  float acc[AMAX];
-#pragma unroll
-  for (int a = 0; a < AMAX; ++a) acc[a] = 0.f;
-  float accv = 0.f;
+__global__ __launch_bounds__(256) void heads_partial_kernel(
+    const float* __restrict__ hp, int ldhp, const float* __restrict__ hv, int ldhv, int B, int K,
+    const float* __restrict__ wp, int A, const float* __restrict__ wv, float* __restrict__ part) {
+  const int c = blockIdx.x;                 // K chunk
+  const int r0 = blockIdx.y * HEADS_ROWS;   // row group
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int k = c * HEADS_KC + lane * 4;
+  const bool kin = k < K;
   const bool same = (hp == hv && ldhp == ldhv);
-  for (int k = lane * 4; k < K; k += 256) {
-    const f32x4 x = *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + k);
+  f32x4 w[AMAX + 1];
 #pragma unroll
-    for (int a = 0; a < AMAX; ++a) {
-      if (a < A) {
-        const f32x4 w = *reinterpret_cast<const f32x4*>(wp + (size_t)a * K + k);
-        acc[a] = fmaf(x[3], w[3], fmaf(x[2], w[2], fmaf(x[1], w[1], fmaf(x[0], w[0], acc[a]))));
+  for (int a = 0; a < AMAX; ++a)
+    w[a] = (a < A && kin) ? *reinterpret_cast<const f32x4*>(wp + (size_t)a * K + k)
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+  w[AMAX] = kin ? *reinterpret_cast<const f32x4*>(wv + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int rr = wave; rr < HEADS_ROWS; rr += 4) {
+    const int row = r0 + rr;
+    if (row >= B) break;
+    const f32x4 x = kin ? *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + k)
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 y = same ? x
+                  : (kin ? *reinterpret_cast<const f32x4*>(hv + (size_t)row * ldhv + k)
+                         : f32x4{0.f, 0.f, 0.f, 0.f});
+    float* out = part + ((size_t)c * B + row) * (A + 1);
+#pragma unroll
+    for (int a = 0; a <= AMAX; ++a) {
+      if (a < A || a == AMAX) {
+        const f32x4 in = (a == AMAX) ? y : x;
+        float s = fmaf(in[3], w[a][3], fmaf(in[2], w[a][2], fmaf(in[1], w[a][1], in[0] * w[a][0])));
+        s = wave_sum(s);
+        if (lane == 0) out[a == AMAX ? A : a] = s;
       }
     }
-    const f32x4 y = same ? x : *reinterpret_cast<const f32x4*>(hv + (size_t)row * ldhv + k);
-    const f32x4 wvv = *reinterpret_cast<const f32x4*>(wv + k);
-    accv = fmaf(y[3], wvv[3], fmaf(y[2], wvv[2], fmaf(y[1], wvv[1], fmaf(y[0], wvv[0], accv))));
+  }
+}
+
+template <int AMAX>
+__global__ __launch_bounds__(256) void heads_finalize_kernel(const float* __restrict__ part,
+                                                            int nchunks, int B, int A,
+                                                            const float* __restrict__ bp,
+                                                            const float* __restrict__ bv,
+                                                            float* __restrict__ logp,
+                                                            float* __restrict__ pi,
+                                                            float* __restrict__ v) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= B) return;
+  float l[AMAX];
+  float sv = 0.f;
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) l[a] = 0.f;
+  for (int c = 0; c < nchunks; ++c) {
+    const float* p = part + ((size_t)c * B + row) * (A + 1);
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a)
+      if (a < A) l[a] += p[a];
+    sv += p[A];
   }
   float mx = -INFINITY;
 #pragma unroll
-  for (int a = 0; a < AMAX; ++a) {
+  for (int a = 0; a < AMAX; ++a)
     if (a < A) {
-      acc[a] = wave_sum(acc[a]) + bp[a];
-      mx = fmaxf(mx, acc[a]);
+      l[a] += bp[a];
+      mx = fmaxf(mx, l[a]);
     }
-  }
   float se = 0.f;
 #pragma unroll
   for (int a = 0; a < AMAX; ++a)
-    if (a < A) se += expf(acc[a] - mx);
+    if (a < A) se += expf(l[a] - mx);
   const float lse = logf(se);
-  accv = wave_sum(accv);
 #pragma unroll
-  for (int a = 0; a < AMAX; ++a) {
-    if (a < A && lane == a) {
-      const float l = (acc[a] - mx) - lse;
-      logp[(size_t)row * A + a] = l;
-      if (pi) pi[(size_t)row * A + a] = expf(l);
+  for (int a = 0; a < AMAX; ++a)
+    if (a < A) {
+      const float o = (l[a] - mx) - lse;
+      logp[(size_t)row * A + a] = o;
+      if (pi) pi[(size_t)row * A + a] = expf(o);
     }
-  }
-  if (lane == 0) v[row] = tanhf(accv + bv[0]);
+  v[row] = tanhf(sv + bv[0]);
 }
 
 }  // namespace az
@@ -236,25 +267,42 @@ extern "C" int az_conv3x3_relu_fwd(const void* in, int in_int8, int B, int Cin, 
   return check_launch("conv3x3_relu_kernel");
 }
 
+extern "C" size_t az_heads_ws_bytes(int B, int K, int A) {
+  return (size_t)((K + HEADS_KC - 1) / HEADS_KC) * (size_t)B * (size_t)(A + 1) * 4;
+}
+
+template <int AMAX>
+static void launch_heads(const float* hp, int ldhp, const float* hv, int ldhv, int B, int K,
+                         const float* wp, const float* bp, int A, const float* wv,
+                         const float* bv, float* logp, float* pi, float* v, float* part,
+                         hipStream_t s) {
+  const int nchunks = (K + HEADS_KC - 1) / HEADS_KC;
+  dim3 g(nchunks, (B + HEADS_ROWS - 1) / HEADS_ROWS);
+  hipLaunchKernelGGL(heads_partial_kernel<AMAX>, g, dim3(256), 0, s, hp, ldhp, hv, ldhv, B, K, wp,
+                     A, wv, part);
+  hipLaunchKernelGGL(heads_finalize_kernel<AMAX>, dim3((B + 255) / 256), dim3(256), 0, s, part,
+                     nchunks, B, A, bp, bv, logp, pi, v);
+}
+
 extern "C" int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv, int B, int K,
                             const float* wp, const float* bp, int A, const float* wv,
-                            const float* bv, float* logp, float* pi, float* v, void* stream) {
-  AZ_REQUIRE(B >= 0 && K > 0 && K % 4 == 0 && A > 0 && A <= 64, AZ_EINVAL,
+                            const float* bv, float* logp, float* pi, float* v, void* ws,
+                            size_t ws_bytes, void* stream) {
+  AZ_REQUIRE(B >= 0 && K > 0 && K % 4 == 0 && A > 0 && A <= 32, AZ_EINVAL,
              "az_heads_fwd: bad shape B=%d K=%d A=%d", B, K, A);
   if (B == 0) return AZ_OK;
-  AZ_REQUIRE(hp && hv && wp && bp && wv && bv && logp && v, AZ_EINVAL, "az_heads_fwd: null");
+  AZ_REQUIRE(hp && hv && wp && bp && wv && bv && logp && v && ws, AZ_EINVAL, "az_heads_fwd: null");
+  AZ_REQUIRE(ws_bytes >= az_heads_ws_bytes(B, K, A), AZ_EINVAL, "az_heads_fwd: workspace too small");
   AZ_REQUIRE(aligned16(hp) && aligned16(hv) && aligned16(wp) && aligned16(wv) && ldhp % 4 == 0 &&
                  ldhv % 4 == 0,
              AZ_EINVAL, "az_heads_fwd: operands need 16B alignment");
   hipStream_t s = as_stream(stream);
-  dim3 g((B + 3) / 4), blk(256);
+  float* part = static_cast<float*>(ws);
   if (A <= 8)
-    hipLaunchKernelGGL(heads_kernel<8>, g, blk, 0, s, hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v);
+    launch_heads<8>(hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v, part, s);
   else if (A <= 16)
-    hipLaunchKernelGGL(heads_kernel<16>, g, blk, 0, s, hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v);
-  else if (A <= 32)
-    hipLaunchKernelGGL(heads_kernel<32>, g, blk, 0, s, hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v);
+    launch_heads<16>(hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v, part, s);
   else
-    hipLaunchKernelGGL(heads_kernel<64>, g, blk, 0, s, hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v);
-  return check_launch("heads_kernel");
+    launch_heads<32>(hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v, part, s);
+  return check_launch("heads_kernels");
 }

@@ -100,7 +100,7 @@ def aggregate_roofline(torch, ops, device, graphs=512):
     ms = float(np.mean([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps)]))
     nbytes = V * Fd * 4 + E * 4 + E * 4 + (V + 1) * 4 + V * Fd * 4
     gbs = nbytes / (ms * 1e-3) / 1e9
-    return {"kernel": "aggregate_lanes_kernel<16>", "bound": "hbm", "achieved": round(gbs, 1),
+    return {"kernel": "aggregate_lanes_kernel<8,2>", "bound": "hbm", "achieved": round(gbs, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
             "traffic": None, "avg_launch_us": round(ms * 1e3, 2),
             "workload": f"{graphs} 32x32 grids, V={V}, E={E}, F=64 (config-5 shard per GPU)"}

@@ -39,6 +39,7 @@ extern "C" {
 #define AZ_ACT_RELU 1
 #define AZ_ACT_SIGMOID 2
 #define AZ_ACT_TANH 3
+#define AZ_ACT_DRELU 4     /* backward of ReLU: v * (G[i][j] > 0), G = saved activation */
 
 int az_abi_version(void);
 const char* az_last_error(void);
@@ -53,14 +54,19 @@ int az_check_device(void);
  *   A(i,k) = a_kmajor ? A[r(i)*lda + k] : A[k*lda + i]      r(i) = a_rows ? a_rows[i] : i
  *            (k >= K0 reads A2[r(i)*lda2 + k-K0] when A2 != NULL: concatenation [A | A2]
  *             along K, i.e. torch.cat([t, agg], dim=1) of gnn_utils.py:31,68)
- *   B(k,j) = b_kmajor ? B[j*ldb + k] : B[k*ldb + j]          (b_kmajor = nn.Linear weight)
- *   v      = act(sum_k A(i,k) B(k,j) + bias[j])
+ *   B(k,j) = b_kmajor ? B[j*ldb + k] : B[q(k)*ldb + j]       q(k) = b_rows ? b_rows[k] : k
+ *            (b_kmajor = nn.Linear weight [N][K]; b_rows gathers rows of an N-major B)
+ *   v      = act(sum_k A(i,k) B(k,j) + bias[j])     (AZ_ACT_DRELU: v * (G[i*ldg+j] > 0))
+ *   C2[i*ldc2 + j] = v                                        when C2 != NULL
  *   v      = R ? R[c(i)*ldr + j] + (G ? G[i*ldg + j] : 1) * v : v   (gated residual,
  *            gnn_utils.py:71)
  *   C[c(i)*ldc + j] = v + beta * C[c(i)*ldc + j]             c(i) = c_rows ? c_rows[i] : i
- * Requirements: K % 4 == 0; lda, lda2, ldb % 4 == 0 and 16-byte aligned A/A2/B when the
- * corresponding operand is read along its contiguous dimension; K0 % 16 == 0; a_rows only
- * with a_kmajor; M % 4 == 0 when !a_kmajor; N % 4 == 0 when !b_kmajor.
+ * ws/ws_bytes: optional device workspace; when the tile grid cannot fill the GPU the K loop is
+ * split over workgroups and the fp32 partial slabs (splits*M*N*4 bytes) are reduced in a
+ * fixed order (results are deterministic run to run).
+ * Requirements: K % 4 == 0 when an operand is K-major; lda, lda2, ldb % 4 == 0 and 16-byte
+ * aligned A/A2/B; K0 % 4 == 0; a_rows only with a_kmajor, b_rows only with !b_kmajor;
+ * M % 4 == 0 when !a_kmajor; N % 4 == 0 when !b_kmajor.
  * --------------------------------------------------------------------------------- */
 typedef struct az_gemm_desc {
   int M, N, K;
@@ -68,6 +74,7 @@ typedef struct az_gemm_desc {
   const float* A2; int lda2; int K0;
   const int* a_rows;
   const float* B; int ldb; int b_kmajor;
+  const int* b_rows;
   const float* bias;
   int act;
   const float* R; int ldr;
@@ -75,6 +82,8 @@ typedef struct az_gemm_desc {
   float beta;
   float* C; int ldc;
   const int* c_rows;
+  float* C2; int ldc2;
+  void* ws; size_t ws_bytes;
 } az_gemm_desc;
 
 int az_gemm_f32(const az_gemm_desc* d, void* stream);
@@ -100,11 +109,14 @@ int az_conv3x3_relu_fwd(const void* in, int in_int8, int B, int Cin, int H, int 
 
 /* Policy/value heads: logits = hp . wp^T + bp  -> log_softmax;  v = tanh(hv . wv^T + bv).
  * Connect4GNN.py:48-57 (hp = hv = features, K = 3136) and the last layers of
- * TicTacToeGNN.py:36-45 (hp = relu(fc1), hv = relu(fc2), K = 512).  A <= 64.
- *   logp [B][A], pi [B][A] = exp(logp) (may be NULL), v [B]. */
+ * TicTacToeGNN.py:36-45 (hp = relu(fc1), hv = relu(fc2), K = 512).  A <= 32.
+ *   logp [B][A], pi [B][A] = exp(logp) (may be NULL), v [B].
+ * ws: device scratch of az_heads_ws_bytes(B, K, A) bytes (per-chunk partial dot products,
+ * summed in a fixed order). */
+size_t az_heads_ws_bytes(int B, int K, int A);
 int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv, int B, int K,
                  const float* wp, const float* bp, int A, const float* wv, const float* bv,
-                 float* logp, float* pi, float* v, void* stream);
+                 float* logp, float* pi, float* v, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * GNN message passing (gnn_utils.py:5-74) over a destination-sorted CSR graph.
@@ -156,9 +168,10 @@ int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H, const az_g
                      float* x_out, void* ws, size_t ws_bytes, void* stream);
 
 /* output_transform, gnn_utils.py:101-105,115: y = W2 relu(W0 x + b0) + b2 on M rows.
- * hidden: [M][F] scratch (kept for the backward pass). */
+ * hidden: [M][F] scratch (kept for the backward pass); ws: optional split-K workspace. */
 int az_mlp2_fwd(const float* x, int M, int F, const float* w0, const float* b0,
-                const float* w2, const float* b2, float* hidden, float* y, void* stream);
+                const float* w2, const float* b2, float* hidden, float* y,
+                void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * torch.optim.Adam step (defaults of Connect4GNN.py:132-133: betas (0.9,0.999), eps 1e-8,
