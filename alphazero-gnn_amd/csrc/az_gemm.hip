@@ -52,41 +52,63 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int c
   *dst = v;
 }
 
-// One BK-deep slice of a K-major operand (rows x BK, contiguous along k) as float4s.
+// Loaders.  Every per-thread row pointer is resolved ONCE before the K loop, each load in the
+// loop is unconditional (rows past M/N are clamped to row 0: they only feed outputs that are
+// never stored) and the K-tail mask is applied when the staged registers are written to LDS,
+// after the MFMA block of the previous tile.  A branch or a select on a loaded value next to
+// the load makes hipcc wait vmcnt(0) right there, which serialises the prefetch
+// (cdna_hip_programming.md §5 item 4(c)).
+template <int ROWS, int BK>
+struct KMajorSlots {
+  static constexpr int NF4 = ROWS * BK / 4 / 256;
+  const float* p0[NF4];   // row pointer in segment 0 (A or B)
+  const float* p1[NF4];   // row pointer in segment 1 (A2, pre-offset by -K0), k >= K0
+  int kq[NF4];
+};
+
 template <int ROWS, int BK, bool IS_A>
-__device__ __forceinline__ void load_kmajor(const GemmArgs& p, int r0, int k0, int kend, int nrows,
-                                            f32x4 (&reg)[ROWS * BK / 4 / 256]) {
-  constexpr int NF4 = ROWS * BK / 4 / 256;
+__device__ __forceinline__ void init_kmajor(const GemmArgs& p, int r0, int nrows,
+                                            KMajorSlots<ROWS, BK>& sl) {
   constexpr int F4_PER_ROW = BK / 4;
 #pragma unroll
-  for (int q = 0; q < NF4; ++q) {
+  for (int q = 0; q < KMajorSlots<ROWS, BK>::NF4; ++q) {
     const int idx = threadIdx.x + q * 256;
-    const int row = idx / F4_PER_ROW, kq = idx % F4_PER_ROW;
-    const int gr = r0 + row, k = k0 + kq * 4;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (gr < nrows && k < kend) {
-      if (IS_A) {
-        const int ar = p.a_rows ? p.a_rows[gr] : gr;
-        const float* src = (p.A2 && k >= p.K0) ? p.A2 + (size_t)ar * p.lda2 + (k - p.K0)
-                                               : p.A + (size_t)ar * p.lda + k;
-        v = *reinterpret_cast<const f32x4*>(src);
-      } else {
-        v = *reinterpret_cast<const f32x4*>(p.B + (size_t)gr * p.ldb + k);
-      }
+    const int gr = r0 + idx / F4_PER_ROW;
+    const int cr = gr < nrows ? gr : 0;
+    sl.kq[q] = (idx % F4_PER_ROW) * 4;
+    if (IS_A) {
+      const int ar = p.a_rows ? p.a_rows[cr] : cr;
+      sl.p0[q] = p.A + (size_t)ar * p.lda;
+      sl.p1[q] = p.A2 ? p.A2 + (size_t)ar * p.lda2 - p.K0 : sl.p0[q];
+    } else {
+      sl.p0[q] = p.B + (size_t)cr * p.ldb;
+      sl.p1[q] = sl.p0[q];
     }
-    reg[q] = v;
+  }
+}
+
+template <int ROWS, int BK>
+__device__ __forceinline__ void load_kmajor(const KMajorSlots<ROWS, BK>& sl, int k0, int kend,
+                                            int K0, f32x4 (&reg)[ROWS * BK / 4 / 256]) {
+#pragma unroll
+  for (int q = 0; q < KMajorSlots<ROWS, BK>::NF4; ++q) {
+    const int k = k0 + sl.kq[q];
+    const int kk = k < kend ? k : 0;
+    reg[q] = *reinterpret_cast<const f32x4*>((kk >= K0 ? sl.p1[q] : sl.p0[q]) + kk);
   }
 }
 
 template <int ROWS, int BK, int LDK>
-__device__ __forceinline__ void store_kmajor(float* lds, const f32x4 (&reg)[ROWS * BK / 4 / 256]) {
+__device__ __forceinline__ void store_kmajor(float* lds, const f32x4 (&reg)[ROWS * BK / 4 / 256],
+                                             int k0, int kend) {
   constexpr int NF4 = ROWS * BK / 4 / 256;
   constexpr int F4_PER_ROW = BK / 4;
 #pragma unroll
   for (int q = 0; q < NF4; ++q) {
     const int idx = threadIdx.x + q * 256;
     const int row = idx / F4_PER_ROW, kq = idx % F4_PER_ROW;
-    *reinterpret_cast<f32x4*>(lds + row * LDK + kq * 4) = reg[q];
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4*>(lds + row * LDK + kq * 4) = (k0 + kq * 4 < kend) ? reg[q] : z;
   }
 }
 
@@ -103,25 +125,24 @@ __device__ __forceinline__ void load_mnmajor(const float* base, int ld, const in
     const int idx = threadIdx.x + q * 256;
     const int kr = idx / PER_K, mq = idx % PER_K;
     const int gr = r0 + mq * 4, k = k0 + kr;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (k < kend && gr < nrows) {
-      const int rk = rows ? rows[k] : k;
-      v = *reinterpret_cast<const f32x4*>(base + (size_t)rk * ld + gr);
-    }
-    reg[q] = v;
+    const int kk = k < kend ? k : 0;
+    const int rk = rows ? rows[kk] : kk;
+    reg[q] = *reinterpret_cast<const f32x4*>(base + (size_t)rk * ld + (gr < nrows ? gr : 0));
   }
 }
 
 template <int ROWS, int BK, int LDK>
-__device__ __forceinline__ void store_mnmajor(float* lds, const f32x4 (&reg)[ROWS * BK / 4 / 256]) {
+__device__ __forceinline__ void store_mnmajor(float* lds, const f32x4 (&reg)[ROWS * BK / 4 / 256],
+                                              int k0, int kend) {
   constexpr int NF4 = ROWS * BK / 4 / 256;
   constexpr int PER_K = ROWS / 4;
 #pragma unroll
   for (int q = 0; q < NF4; ++q) {
     const int idx = threadIdx.x + q * 256;
     const int kr = idx / PER_K, mq = idx % PER_K;
+    const bool ok = k0 + kr < kend;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) lds[(mq * 4 + e) * LDK + kr] = reg[q][e];
+    for (int e = 0; e < 4; ++e) lds[(mq * 4 + e) * LDK + kr] = ok ? reg[q][e] : 0.f;
   }
 }
 
@@ -156,23 +177,27 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   f32x4 ra[AF4], rb[BF4];
+  KMajorSlots<BM, BK> sa;
+  KMajorSlots<BN, BK> sb;
+  if constexpr (A_KM) init_kmajor<BM, BK, true>(p, m0, p.M, sa);
+  if constexpr (B_KM) init_kmajor<BN, BK, false>(p, n0, p.N, sb);
   auto load = [&](int k0) {
-    if constexpr (A_KM) load_kmajor<BM, BK, true>(p, m0, k0, kend, p.M, ra);
+    if constexpr (A_KM) load_kmajor<BM, BK>(sa, k0, kend, p.K0, ra);
     else load_mnmajor<BM, BK>(p.A, p.lda, nullptr, m0, k0, kend, p.M, ra);
-    if constexpr (B_KM) load_kmajor<BN, BK, false>(p, n0, k0, kend, p.N, rb);
+    if constexpr (B_KM) load_kmajor<BN, BK>(sb, k0, kend, p.K, rb);
     else load_mnmajor<BN, BK>(p.B, p.ldb, p.b_rows, n0, k0, kend, p.N, rb);
   };
-  auto store = [&](int buf) {
-    if constexpr (A_KM) store_kmajor<BM, BK, LDK>(As[buf], ra);
-    else store_mnmajor<BM, BK, LDK>(As[buf], ra);
-    if constexpr (B_KM) store_kmajor<BN, BK, LDK>(Bs[buf], rb);
-    else store_mnmajor<BN, BK, LDK>(Bs[buf], rb);
+  auto store = [&](int buf, int k0) {
+    if constexpr (A_KM) store_kmajor<BM, BK, LDK>(As[buf], ra, k0, kend);
+    else store_mnmajor<BM, BK, LDK>(As[buf], ra, k0, kend);
+    if constexpr (B_KM) store_kmajor<BN, BK, LDK>(Bs[buf], rb, k0, kend);
+    else store_mnmajor<BN, BK, LDK>(Bs[buf], rb, k0, kend);
   };
 
   const int nk = (kend - kbeg + BK - 1) / BK;
   if (nk > 0) {
     load(kbeg);
-    store(0);
+    store(0, kbeg);
   }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
@@ -197,7 +222,7 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs p) {
           for (int j = 0; j < TJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store(cur ^ 1);
+    if (kt + 1 < nk) store(cur ^ 1, kbeg + (kt + 1) * BK);
     __syncthreads();
   }
 
@@ -262,17 +287,16 @@ __global__ __launch_bounds__(256) void gemv_f32(GemmArgs p) {
       *reinterpret_cast<f32x4*>(&As[m * GV_KC + k4]) = v;
     }
     __syncthreads();
+    // unconditional loads: rows past N are clamped to row 0 (never stored), k past the chunk
+    // re-reads the chunk start and meets zeros in the staged A
     f32x4 w[GV_ROWS][GV_KC / 256];
 #pragma unroll
     for (int r = 0; r < GV_ROWS; ++r) {
-      const int n = n_base + r;
+      const int n = n_base + r < p.N ? n_base + r : 0;
 #pragma unroll
       for (int s = 0; s < GV_KC / 256; ++s) {
         const int k4 = (lane + 64 * s) * 4;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (n < p.N && k4 < klen)
-          v = *reinterpret_cast<const f32x4*>(p.B + (size_t)n * p.ldb + kc + k4);
-        w[r][s] = v;
+        w[r][s] = *reinterpret_cast<const f32x4*>(p.B + (size_t)n * p.ldb + kc + (k4 < klen ? k4 : 0));
       }
     }
 #pragma unroll
