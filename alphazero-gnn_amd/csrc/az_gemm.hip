@@ -9,6 +9,8 @@
 // of its A row / B column with one ds_read_b128 and feeds 4 MFMAs; the k order inside an
 // 8-k group is permuted (lane half h owns k = 4h..4h+3, MFMA t sums k = t and 4+t), which
 // changes only the fp32 summation order.
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "az_common.h"
@@ -350,7 +352,11 @@ static void launch_gemv(const GemmArgs& a, hipStream_t s) {
 static void plan(GemmArgs& a, int bm, int bn, int bk, size_t ws_bytes) {
   const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
   int S = 1;
-  if (tiles < 256 && a.slab) {
+  static const char* env_split = getenv("AZ_GEMM_SPLITS");
+  if (env_split && a.slab) {
+    S = std::max(1, atoi(env_split));
+    while (S > 1 && (size_t)S * a.M * a.N * 4 > ws_bytes) --S;
+  } else if (tiles < 256 && a.slab) {
     S = (int)std::min<long>((512 + tiles - 1) / tiles, a.K / (bk * 4));
     while (S > 1 && (size_t)S * a.M * a.N * 4 > ws_bytes) --S;
     if (S < 1) S = 1;
@@ -399,7 +405,10 @@ int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
     return check_launch("gemv_f32");
   }
   const long t128 = (long)((d->M + 127) / 128) * ((d->N + 127) / 128);
-  if (t128 >= 64) {
+  // tuning overrides (experiments only): AZ_GEMM_TILE=64|128, AZ_GEMM_SPLITS=n
+  static const char* env_tile = getenv("AZ_GEMM_TILE");
+  const int force_tile = env_tile ? atoi(env_tile) : 0;
+  if (force_tile == 128 || (force_tile == 0 && t128 >= 64)) {
     plan(a, 128, 128, 32, d->ws_bytes);
     launch_tile<128, 128, 32>(a, akm, bkm, s);
   } else {

@@ -1,0 +1,51 @@
+"""GEMM tuning sweep on the GPU box: time az_gemm_f32 for the output_transform shape under
+tile/split overrides (each variant in its own subprocess since the overrides are read once)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r'''
+import sys, json, torch
+sys.path.insert(0, "%s/alphazero-gnn_amd")
+from azhip import ops
+M, N, K = %d, %d, %d
+x = torch.rand((M, K), device="cuda") * 2 - 1
+w = (torch.rand((N, K), device="cuda") * 2 - 1) / K ** 0.5
+b = torch.rand((N,), device="cuda")
+y = torch.empty((M, N), device="cuda")
+for _ in range(5):
+    ops.linear(x, w, b, act=1, out=y)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+reps = 50
+e0.record()
+for _ in range(reps):
+    ops.linear(x, w, b, act=1, out=y)
+e1.record()
+torch.cuda.synchronize()
+us = e0.elapsed_time(e1) / reps * 1e3
+print(json.dumps({"us": us, "tflops": 2 * M * N * K / us / 1e6}))
+'''
+
+
+def run(env, M=512, N=3136, K=3136):
+    e = dict(os.environ)
+    e.update(env)
+    r = subprocess.run([sys.executable, "-c", CHILD % (ROOT, M, N, K)], env=e,
+                       capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        return {"error": r.stderr[-300:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+if __name__ == "__main__":
+    shapes = [(512, 3136, 3136), (4096, 3136, 3136), (64, 3136, 3136)]
+    for (M, N, K) in shapes:
+        for tile in ("64", "128"):
+            for split in ("1", "2", "4", "6", "8"):
+                res = run({"AZ_GEMM_TILE": tile, "AZ_GEMM_SPLITS": split}, M, N, K)
+                print(json.dumps({"M": M, "N": N, "K": K, "tile": tile, "splits": split, **res}),
+                      flush=True)
+        print(json.dumps({"M": M, "N": N, "K": K, "tile": "auto", **run({}, M, N, K)}), flush=True)
