@@ -60,21 +60,21 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int c
 // after the MFMA block of the previous tile.  A branch or a select on a loaded value next to
 // the load makes hipcc wait vmcnt(0) right there, which serialises the prefetch
 // (cdna_hip_programming.md §5 item 4(c)).
-template <int ROWS, int BK>
+template <int ROWS, int BK, int NT>
 struct KMajorSlots {
-  static constexpr int NF4 = ROWS * BK / 4 / 256;
+  static constexpr int NF4 = ROWS * BK / 4 / NT;
   const float* p0[NF4];   // row pointer in segment 0 (A or B)
   const float* p1[NF4];   // row pointer in segment 1 (A2, pre-offset by -K0), k >= K0
   int kq[NF4];
 };
 
-template <int ROWS, int BK, bool IS_A>
+template <int ROWS, int BK, int NT, bool IS_A>
 __device__ __forceinline__ void init_kmajor(const GemmArgs& p, int r0, int nrows,
-                                            KMajorSlots<ROWS, BK>& sl) {
+                                            KMajorSlots<ROWS, BK, NT>& sl) {
   constexpr int F4_PER_ROW = BK / 4;
 #pragma unroll
-  for (int q = 0; q < KMajorSlots<ROWS, BK>::NF4; ++q) {
-    const int idx = threadIdx.x + q * 256;
+  for (int q = 0; q < KMajorSlots<ROWS, BK, NT>::NF4; ++q) {
+    const int idx = threadIdx.x + q * NT;
     const int gr = r0 + idx / F4_PER_ROW;
     const int cr = gr < nrows ? gr : 0;
     sl.kq[q] = (idx % F4_PER_ROW) * 4;
@@ -89,25 +89,25 @@ __device__ __forceinline__ void init_kmajor(const GemmArgs& p, int r0, int nrows
   }
 }
 
-template <int ROWS, int BK>
-__device__ __forceinline__ void load_kmajor(const KMajorSlots<ROWS, BK>& sl, int k0, int kend,
-                                            int K0, f32x4 (&reg)[ROWS * BK / 4 / 256]) {
+template <int ROWS, int BK, int NT>
+__device__ __forceinline__ void load_kmajor(const KMajorSlots<ROWS, BK, NT>& sl, int k0, int kend,
+                                            int K0, f32x4 (&reg)[ROWS * BK / 4 / NT]) {
 #pragma unroll
-  for (int q = 0; q < KMajorSlots<ROWS, BK>::NF4; ++q) {
+  for (int q = 0; q < KMajorSlots<ROWS, BK, NT>::NF4; ++q) {
     const int k = k0 + sl.kq[q];
     const int kk = k < kend ? k : 0;
     reg[q] = *reinterpret_cast<const f32x4*>((kk >= K0 ? sl.p1[q] : sl.p0[q]) + kk);
   }
 }
 
-template <int ROWS, int BK, int LDK>
-__device__ __forceinline__ void store_kmajor(float* lds, const f32x4 (&reg)[ROWS * BK / 4 / 256],
+template <int ROWS, int BK, int NT, int LDK>
+__device__ __forceinline__ void store_kmajor(float* lds, const f32x4 (&reg)[ROWS * BK / 4 / NT],
                                              int k0, int kend) {
-  constexpr int NF4 = ROWS * BK / 4 / 256;
+  constexpr int NF4 = ROWS * BK / 4 / NT;
   constexpr int F4_PER_ROW = BK / 4;
 #pragma unroll
   for (int q = 0; q < NF4; ++q) {
-    const int idx = threadIdx.x + q * 256;
+    const int idx = threadIdx.x + q * NT;
     const int row = idx / F4_PER_ROW, kq = idx % F4_PER_ROW;
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
     *reinterpret_cast<f32x4*>(lds + row * LDK + kq * 4) = (k0 + kq * 4 < kend) ? reg[q] : z;
@@ -116,15 +116,15 @@ __device__ __forceinline__ void store_kmajor(float* lds, const f32x4 (&reg)[ROWS
 
 // Operand contiguous along its M/N dimension: element (k, i) at base[row(k)*ld + i] with
 // row(k) = rows ? rows[k] : k (row gather for weight gradients of gathered destinations).
-template <int ROWS, int BK>
+template <int ROWS, int BK, int NT>
 __device__ __forceinline__ void load_mnmajor(const float* base, int ld, const int* rows, int r0,
                                              int k0, int kend, int nrows,
-                                             f32x4 (&reg)[ROWS * BK / 4 / 256]) {
-  constexpr int NF4 = ROWS * BK / 4 / 256;
+                                             f32x4 (&reg)[ROWS * BK / 4 / NT]) {
+  constexpr int NF4 = ROWS * BK / 4 / NT;
   constexpr int PER_K = ROWS / 4;
 #pragma unroll
   for (int q = 0; q < NF4; ++q) {
-    const int idx = threadIdx.x + q * 256;
+    const int idx = threadIdx.x + q * NT;
     const int kr = idx / PER_K, mq = idx % PER_K;
     const int gr = r0 + mq * 4, k = k0 + kr;
     const int kk = k < kend ? k : 0;
@@ -133,14 +133,14 @@ __device__ __forceinline__ void load_mnmajor(const float* base, int ld, const in
   }
 }
 
-template <int ROWS, int BK, int LDK>
-__device__ __forceinline__ void store_mnmajor(float* lds, const f32x4 (&reg)[ROWS * BK / 4 / 256],
+template <int ROWS, int BK, int NT, int LDK>
+__device__ __forceinline__ void store_mnmajor(float* lds, const f32x4 (&reg)[ROWS * BK / 4 / NT],
                                               int k0, int kend) {
-  constexpr int NF4 = ROWS * BK / 4 / 256;
+  constexpr int NF4 = ROWS * BK / 4 / NT;
   constexpr int PER_K = ROWS / 4;
 #pragma unroll
   for (int q = 0; q < NF4; ++q) {
-    const int idx = threadIdx.x + q * 256;
+    const int idx = threadIdx.x + q * NT;
     const int kr = idx / PER_K, mq = idx % PER_K;
     const bool ok = k0 + kr < kend;
 #pragma unroll
@@ -148,27 +148,38 @@ __device__ __forceinline__ void store_mnmajor(float* lds, const f32x4 (&reg)[ROW
   }
 }
 
-template <int BM, int BN, int BK, bool A_KM, bool B_KM>
-__global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs p) {
+// Bijective XCD-aware remap for any grid size: hardware deals blocks round-robin over the 8
+// XCDs (b -> XCD b % 8); XCD x gets the contiguous id range [start(x), start(x) + count(x)).
+__device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
+  const int xcd = bid & 7, local = bid >> 3;
+  const int base = nwg >> 3, rem = nwg & 7;
+  return xcd * base + min(xcd, rem) + local;
+}
+
+// Waves arranged WGM x WGN; each wave computes a (BM/WGM) x (BN/WGN) sub-tile as TI x TJ
+// 32x32 MFMA accumulators.
+template <int BM, int BN, int BK, int WGM, int WGN, bool A_KM, bool B_KM>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_mfma(GemmArgs p) {
+  constexpr int NT = 64 * WGM * WGN;
   constexpr int LDK = BK + 4;
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TI = WM / 32, TJ = WN / 32;
-  constexpr int AF4 = BM * BK / 4 / 256, BF4 = BN * BK / 4 / 256;
+  constexpr int AF4 = BM * BK / 4 / NT, BF4 = BN * BK / 4 / NT;
+  static_assert(TI >= 1 && TJ >= 1 && AF4 >= 1 && BF4 >= 1, "bad tile");
   __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
 
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
   const int nwg = mt_n * nt_n * p.splits;
-  int bid = blockIdx.x;
-  // XCD-aware remap (blocks b, b+8 share an XCD): each XCD gets a contiguous run of ids;
-  // consecutive ids share (split, B panel) -> the weight slice is re-read from that XCD's L2.
-  if ((nwg & 7) == 0) bid = (bid & 7) * (nwg >> 3) + (bid >> 3);
+  // consecutive ids share (split, B panel): keep them on one XCD so the weight slice is
+  // fetched into that XCD's L2 once and re-read from there by the M tiles.
+  const int bid = xcd_swizzle(blockIdx.x, nwg);
   const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
   const int m0 = mt * BM, n0 = nt * BN;
   const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
 
   f32x16 acc[TI][TJ];
 #pragma unroll
@@ -179,21 +190,21 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   f32x4 ra[AF4], rb[BF4];
-  KMajorSlots<BM, BK> sa;
-  KMajorSlots<BN, BK> sb;
-  if constexpr (A_KM) init_kmajor<BM, BK, true>(p, m0, p.M, sa);
-  if constexpr (B_KM) init_kmajor<BN, BK, false>(p, n0, p.N, sb);
+  KMajorSlots<BM, BK, NT> sa;
+  KMajorSlots<BN, BK, NT> sb;
+  if constexpr (A_KM) init_kmajor<BM, BK, NT, true>(p, m0, p.M, sa);
+  if constexpr (B_KM) init_kmajor<BN, BK, NT, false>(p, n0, p.N, sb);
   auto load = [&](int k0) {
-    if constexpr (A_KM) load_kmajor<BM, BK>(sa, k0, kend, p.K0, ra);
-    else load_mnmajor<BM, BK>(p.A, p.lda, nullptr, m0, k0, kend, p.M, ra);
-    if constexpr (B_KM) load_kmajor<BN, BK>(sb, k0, kend, p.K, rb);
-    else load_mnmajor<BN, BK>(p.B, p.ldb, p.b_rows, n0, k0, kend, p.N, rb);
+    if constexpr (A_KM) load_kmajor<BM, BK, NT>(sa, k0, kend, p.K0, ra);
+    else load_mnmajor<BM, BK, NT>(p.A, p.lda, nullptr, m0, k0, kend, p.M, ra);
+    if constexpr (B_KM) load_kmajor<BN, BK, NT>(sb, k0, kend, p.K, rb);
+    else load_mnmajor<BN, BK, NT>(p.B, p.ldb, p.b_rows, n0, k0, kend, p.N, rb);
   };
   auto store = [&](int buf, int k0) {
-    if constexpr (A_KM) store_kmajor<BM, BK, LDK>(As[buf], ra, k0, kend);
-    else store_mnmajor<BM, BK, LDK>(As[buf], ra, k0, kend);
-    if constexpr (B_KM) store_kmajor<BN, BK, LDK>(Bs[buf], rb, k0, kend);
-    else store_mnmajor<BN, BK, LDK>(Bs[buf], rb, k0, kend);
+    if constexpr (A_KM) store_kmajor<BM, BK, NT, LDK>(As[buf], ra, k0, kend);
+    else store_mnmajor<BM, BK, NT, LDK>(As[buf], ra, k0, kend);
+    if constexpr (B_KM) store_kmajor<BN, BK, NT, LDK>(Bs[buf], rb, k0, kend);
+    else store_mnmajor<BN, BK, NT, LDK>(Bs[buf], rb, k0, kend);
   };
 
   const int nk = (kend - kbeg + BK - 1) / BK;
@@ -328,13 +339,31 @@ __global__ __launch_bounds__(256) void gemv_f32(GemmArgs p) {
   }
 }
 
-template <int BM, int BN, int BK>
+struct TileCfg { int bm, bn, bk, wgm, wgn; };
+// 0: 64x64x32 (4 waves 2x2)   1: 128x128x32 (4 waves 2x2)   2: 64x64x64 (4 waves)
+// 3: 128x64x32 (4 waves 2x2)  4: 128x128x32 (8 waves 2x4)   5: 256x128x32 (8 waves 4x2)
+static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 64, 64, 2, 2},
+                                {128, 64, 32, 2, 2}, {128, 128, 32, 2, 4}, {256, 128, 32, 4, 2}};
+
+template <int BM, int BN, int BK, int WGM, int WGN>
 static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
-  if (akm && bkm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, true, true>), dim3(nwg), dim3(256), 0, s, a);
-  else if (akm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, true, false>), dim3(nwg), dim3(256), 0, s, a);
-  else if (bkm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, false, true>), dim3(nwg), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, false, false>), dim3(nwg), dim3(256), 0, s, a);
+  dim3 g(nwg), b(64 * WGM * WGN);
+  if (akm && bkm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, WGM, WGN, true, true>), g, b, 0, s, a);
+  else if (akm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, WGM, WGN, true, false>), g, b, 0, s, a);
+  else if (bkm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, WGM, WGN, false, true>), g, b, 0, s, a);
+  else hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, WGM, WGN, false, false>), g, b, 0, s, a);
+}
+
+static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
+  switch (cfg) {
+    case 1: launch_tile<128, 128, 32, 2, 2>(a, akm, bkm, s); break;
+    case 2: launch_tile<64, 64, 64, 2, 2>(a, akm, bkm, s); break;
+    case 3: launch_tile<128, 64, 32, 2, 2>(a, akm, bkm, s); break;
+    case 4: launch_tile<128, 128, 32, 2, 4>(a, akm, bkm, s); break;
+    case 5: launch_tile<256, 128, 32, 4, 2>(a, akm, bkm, s); break;
+    default: launch_tile<64, 64, 32, 2, 2>(a, akm, bkm, s); break;
+  }
 }
 
 static void launch_gemv(const GemmArgs& a, hipStream_t s) {
@@ -404,17 +433,18 @@ int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
     launch_gemv(a, s);
     return check_launch("gemv_f32");
   }
-  const long t128 = (long)((d->M + 127) / 128) * ((d->N + 127) / 128);
-  // tuning overrides (experiments only): AZ_GEMM_TILE=64|128, AZ_GEMM_SPLITS=n
-  static const char* env_tile = getenv("AZ_GEMM_TILE");
-  const int force_tile = env_tile ? atoi(env_tile) : 0;
-  if (force_tile == 128 || (force_tile == 0 && t128 >= 64)) {
-    plan(a, 128, 128, 32, d->ws_bytes);
-    launch_tile<128, 128, 32>(a, akm, bkm, s);
+  // tile choice (tuning override for experiments: AZ_GEMM_CFG=<index into kCfgs>)
+  static const char* env_cfg = getenv("AZ_GEMM_CFG");
+  int cfg = 0;
+  if (env_cfg) {
+    cfg = std::min(std::max(atoi(env_cfg), 0), 5);
   } else {
-    plan(a, 64, 64, 32, d->ws_bytes);
-    launch_tile<64, 64, 32>(a, akm, bkm, s);
+    const long t128 = (long)((d->M + 127) / 128) * ((d->N + 127) / 128);
+    cfg = t128 >= 64 ? 1 : 0;
   }
+  const TileCfg& tc = kCfgs[cfg];
+  plan(a, tc.bm, tc.bn, tc.bk, d->ws_bytes);
+  launch_cfg(cfg, a, akm, bkm, s);
   int rc = check_launch("gemm_f32_mfma");
   if (rc || a.splits <= 1) return rc;
   const long total = (long)a.M * a.N;

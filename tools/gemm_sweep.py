@@ -43,9 +43,11 @@ def run(env, M=512, N=3136, K=3136):
 if __name__ == "__main__":
     shapes = [(512, 3136, 3136), (4096, 3136, 3136), (64, 3136, 3136)]
     for (M, N, K) in shapes:
-        for tile in ("64", "128"):
-            for split in ("1", "2", "4", "6", "8"):
-                res = run({"AZ_GEMM_TILE": tile, "AZ_GEMM_SPLITS": split}, M, N, K)
-                print(json.dumps({"M": M, "N": N, "K": K, "tile": tile, "splits": split, **res}),
+        for cfg in ("0", "1", "2", "3", "4", "5"):
+            for split in ("1", "2", "3", "4", "6"):
+                if M >= 4096 and split != "1":
+                    continue
+                res = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_SPLITS": split}, M, N, K)
+                print(json.dumps({"M": M, "N": N, "K": K, "cfg": cfg, "splits": split, **res}),
                       flush=True)
         print(json.dumps({"M": M, "N": N, "K": K, "tile": "auto", **run({}, M, N, K)}), flush=True)
