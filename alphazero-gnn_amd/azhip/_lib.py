@@ -40,13 +40,21 @@ class GemmDesc(ctypes.Structure):
 
 class Graph(ctypes.Structure):
     _fields_ = [("V", c_int), ("E", c_int), ("rowptr", c_void_p), ("col", c_void_p),
-                ("edge_dst", c_void_p), ("D", c_int), ("dst_rows", c_void_p)]
+                ("edge_dst", c_void_p), ("D", c_int), ("dst_rows", c_void_p),
+                ("src_rowptr", c_void_p), ("src_edges", c_void_p), ("dst_index", c_void_p),
+                ("max_deg", c_int)]
+
+
+LAYER_FIELDS = ("att_w1", "att_b1", "att_w2", "att_b2", "upd_w1", "upd_b1", "upd_w2", "upd_b2",
+                "gate_w", "gate_b")
 
 
 class LayerW(ctypes.Structure):
-    _fields_ = [(n, c_void_p) for n in (
-        "att_w1", "att_b1", "att_w2", "att_b2", "upd_w1", "upd_b1", "upd_w2", "upd_b2",
-        "gate_w", "gate_b")]
+    _fields_ = [(n, c_void_p) for n in LAYER_FIELDS]
+
+
+class LayerGrads(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in LAYER_FIELDS]
 
 
 # name -> (restype, argtypes); every symbol here must be declared in include/az_hip.h
@@ -72,6 +80,29 @@ SIGNATURES = {
                                  ctypes.POINTER(LayerW), c_void_p, c_void_p, c_size_t, c_void_p]),
     "az_mlp2_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "az_heads_loss_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                  c_void_p, c_void_p, c_void_p, c_void_p]),
+    "az_heads_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                             c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_int, c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
+    "az_colsum_ws_bytes": (c_size_t, [c_int, c_int]),
+    "az_colsum": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_float, c_void_p, c_size_t,
+                          c_void_p]),
+    "az_dropout_mask": (c_int, [c_void_p, c_int64, c_double, ctypes.c_uint64, c_void_p]),
+    "az_mask_scale": (c_int, [c_void_p, c_void_p, c_float, c_int64, c_void_p, c_void_p]),
+    "az_nchw_drelu_to_pm": (c_int, [c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_int,
+                                    c_void_p, c_void_p]),
+    "az_im2col3x3": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                             c_void_p]),
+    "az_col2im3x3_drelu": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                   c_void_p, c_void_p]),
+    "az_gnn_layer_bwd_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "az_gnn_layer_bwd": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int,
+                                 ctypes.POINTER(LayerW), c_void_p, c_void_p, c_void_p,
+                                 ctypes.POINTER(LayerGrads), c_void_p, c_size_t, c_void_p]),
+    "az_mlp2_bwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_size_t, c_void_p]),
     "az_adam_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_double, c_double,
                             c_double, c_double, c_int, c_void_p]),
 }

@@ -5,7 +5,8 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, GemmDesc, Graph, LayerW  # noqa: F401
+from ._lib import (ACT_DRELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, GemmDesc, Graph,  # noqa: F401
+                   LayerGrads, LayerW)
 
 
 def _p(t):
@@ -28,7 +29,7 @@ def _need(t, dtype=torch.float32, name="tensor"):
 _WS = {}
 
 
-def workspace(device, nbytes=64 << 20):
+def workspace(device, nbytes=96 << 20):
     """Per-device split-K workspace (kept for the process lifetime; grows on demand)."""
     key = str(device)
     t = _WS.get(key)
@@ -155,8 +156,8 @@ def heads(hp, wp, bp, wv, bv, hv=None, want_pi=True, logp=None, pi=None, v=None)
 
 
 class DeviceGraph:
-    """A destination-sorted CSR graph resident in HBM (+ its edge->dst map and the list of
-    destinations with at least one in-edge)."""
+    """A destination-sorted CSR graph resident in HBM, with the edge->dst map, the list of
+    destinations that have in-edges, and the reverse (by-source) CSR the backward pass uses."""
 
     def __init__(self, rowptr, col, device="cuda"):
         import numpy as np
@@ -168,10 +169,19 @@ class DeviceGraph:
         dst = np.repeat(np.arange(V), deg)
         rows = np.flatnonzero(deg > 0)
         self.D = len(rows)
+        self.max_deg = int(deg.max()) if V else 0
+        order = np.argsort(col, kind="stable")           # edges grouped by source
+        src_rowptr = np.zeros(V + 1, np.int64)
+        np.cumsum(np.bincount(col, minlength=V), out=src_rowptr[1:])
+        dst_index = np.full(V, -1, np.int64)
+        dst_index[rows] = np.arange(self.D)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.int32)).to(device)  # noqa: E731
         self.rowptr, self.col, self.edge_dst, self.dst_rows = t(rowptr), t(col), t(dst), t(rows)
+        self.src_rowptr, self.src_edges, self.dst_index = t(src_rowptr), t(order), t(dst_index)
         self.c = Graph(V, self.E, self.rowptr.data_ptr(), self.col.data_ptr(),
-                       self.edge_dst.data_ptr(), self.D, self.dst_rows.data_ptr())
+                       self.edge_dst.data_ptr(), self.D, self.dst_rows.data_ptr(),
+                       self.src_rowptr.data_ptr(), self.src_edges.data_ptr(),
+                       self.dst_index.data_ptr(), self.max_deg)
 
     @staticmethod
     def star(n, device="cuda"):
@@ -199,12 +209,18 @@ def aggregate(g, x, alpha, agg=None):
     return agg
 
 
+LAYER_KEYS = ("attention.0.weight", "attention.0.bias", "attention.2.weight", "attention.2.bias",
+              "update_net.0.weight", "update_net.0.bias", "update_net.2.weight",
+              "update_net.2.bias", "gate.0.weight", "gate.0.bias")
+
+
 def layer_weights(Wl):
     """LayerW from a dict with GNNLayer state_dict suffixes."""
-    return LayerW(*[Wl[k].data_ptr() for k in (
-        "attention.0.weight", "attention.0.bias", "attention.2.weight", "attention.2.bias",
-        "update_net.0.weight", "update_net.0.bias", "update_net.2.weight", "update_net.2.bias",
-        "gate.0.weight", "gate.0.bias")])
+    return LayerW(*[Wl[k].data_ptr() for k in LAYER_KEYS])
+
+
+def layer_grads(Gl):
+    return LayerGrads(*[Gl[k].data_ptr() for k in LAYER_KEYS])
 
 
 def layer_ws_bytes(g, F, H=128):
@@ -240,3 +256,118 @@ def adam(p, g, m, v, lr, step, beta1=0.9, beta2=0.999, eps=1e-8):
     L = _lib.lib()
     _lib.check(L.az_adam_f32(_p(p), _p(g), _p(m), _p(v), p.numel(), lr, beta1, beta2, eps, step,
                              _stream()), "az_adam_f32")
+
+
+# ----------------------------------------------------------------------------- backward
+def heads_loss_bwd(logp, v, target_pi, target_v, B_norm=None, loss_rows=None):
+    B, A = logp.shape
+    dl = torch.empty_like(logp)
+    dv = torch.empty_like(v)
+    L = _lib.lib()
+    _lib.check(L.az_heads_loss_bwd(_p(logp), _p(v), _p(target_pi), _p(target_v), B, A,
+                                   B_norm or B, _p(dl), _p(dv), _p(loss_rows), _stream()),
+               "az_heads_loss_bwd")
+    return dl, dv
+
+
+def heads_bwd(dl, dv, hp, wp, wv, hv=None, grads=None, dh=None, dhv=None):
+    """grads: dict with 'wp','bp','wv','bv' tensors to write (or None); dh: input-grad buffer
+    (dhv None -> both heads summed into dh)."""
+    hv = hp if hv is None else hv
+    B, K = hp.shape
+    A = wp.shape[0]
+    L = _lib.lib()
+    ws = workspace(hp.device)
+    g = grads or {}
+    dhv_t = dh if dhv is None else dhv
+    _lib.check(L.az_heads_bwd(_p(dl), _p(dv), _p(hp), hp.stride(0), _p(hv), hv.stride(0), B, K,
+                              _p(wp), A, _p(wv), _p(g.get("wp")), _p(g.get("bp")),
+                              _p(g.get("wv")), _p(g.get("bv")), _p(dh),
+                              dh.stride(0) if dh is not None else 0, _p(dhv_t),
+                              dhv_t.stride(0) if dhv_t is not None else 0, _p(ws),
+                              ctypes.c_size_t(ws.numel()), _stream()), "az_heads_bwd")
+
+
+def colsum(X, out, beta=0.0):
+    R, C = X.shape
+    L = _lib.lib()
+    ws = workspace(X.device)
+    _lib.check(L.az_colsum(_p(X), R, C, X.stride(0), _p(out), beta, _p(ws),
+                           ctypes.c_size_t(ws.numel()), _stream()), "az_colsum")
+    return out
+
+
+def dropout_mask(n, p, seed, device):
+    m = torch.empty((n,), dtype=torch.uint8, device=device)
+    L = _lib.lib()
+    _lib.check(L.az_dropout_mask(_p(m), n, float(p), int(seed) & ((1 << 64) - 1), _stream()),
+               "az_dropout_mask")
+    return m
+
+
+def mask_scale(x, mask, scale, out=None):
+    out = torch.empty_like(x) if out is None else out
+    L = _lib.lib()
+    _lib.check(L.az_mask_scale(_p(x), _p(mask), float(scale), x.numel(), _p(out), _stream()),
+               "az_mask_scale")
+    return out
+
+
+def nchw_drelu_to_pm(dy, y, B, C, HW, mask=None, scale=1.0, out=None):
+    out = torch.empty((B * HW, C), device=dy.device) if out is None else out
+    L = _lib.lib()
+    _lib.check(L.az_nchw_drelu_to_pm(_p(dy), _p(y), _p(mask), float(scale), B, C, HW, _p(out),
+                                     _stream()), "az_nchw_drelu_to_pm")
+    return out
+
+
+def im2col3x3(x, pad, ldc=None):
+    is_i8 = x.dtype == torch.int8
+    if is_i8:
+        B, H, W = x.shape
+        C = 1
+    else:
+        B, C, H, W = x.shape
+    ldc = ldc or (C * 9 + 3) // 4 * 4
+    Ho, Wo = H + 2 * pad - 2, W + 2 * pad - 2
+    cols = torch.empty((B * Ho * Wo, ldc), device=x.device)
+    L = _lib.lib()
+    _lib.check(L.az_im2col3x3(_p(x), int(is_i8), B, C, H, W, pad, ldc, _p(cols), _stream()),
+               "az_im2col3x3")
+    return cols
+
+
+def col2im3x3_drelu(dcols, a, pad):
+    B, C, H, W = a.shape
+    dz = torch.empty((B * H * W, C), device=a.device)
+    L = _lib.lib()
+    _lib.check(L.az_col2im3x3_drelu(_p(dcols), dcols.stride(0), _p(a), B, C, H, W, pad, _p(dz),
+                                    _stream()), "az_col2im3x3_drelu")
+    return dz
+
+
+def gnn_layer_bwd(g, x, Wl, fwd_ws, dout, grads, dx=None, H=128):
+    V, F = x.shape
+    dx = torch.empty_like(x) if dx is None else dx
+    L = _lib.lib()
+    nbytes = int(L.az_gnn_layer_bwd_ws_bytes(g.V, g.E, g.D, F, H))
+    ws = workspace(x.device, max(nbytes, 64 << 20))
+    lw, lg = layer_weights(Wl), layer_grads(grads)
+    _lib.check(L.az_gnn_layer_bwd(ctypes.byref(g.c), _p(x), F, H, ctypes.byref(lw), _p(fwd_ws),
+                                  _p(dout), _p(dx), ctypes.byref(lg), _p(ws),
+                                  ctypes.c_size_t(ws.numel()), _stream()), "az_gnn_layer_bwd")
+    return dx
+
+
+def mlp2_bwd(x, w0, w2, hidden, dy, grads, dx=None, want_dx=True):
+    M, F = x.shape
+    if want_dx and dx is None:
+        dx = torch.empty_like(x)
+    dh = torch.empty_like(x)
+    L = _lib.lib()
+    ws = workspace(x.device)
+    _lib.check(L.az_mlp2_bwd(_p(x), M, F, _p(w0), _p(w2), _p(hidden), _p(dy),
+                             _p(dx) if want_dx else None, _p(grads["w0"]), _p(grads["b0"]),
+                             _p(grads["w2"]), _p(grads["b2"]), _p(dh), _p(ws),
+                             ctypes.c_size_t(ws.numel()), _stream()), "az_mlp2_bwd")
+    return dx

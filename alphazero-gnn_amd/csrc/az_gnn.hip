@@ -176,10 +176,10 @@ static int check_graph(const az_graph* g) {
 
 static size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
-constexpr size_t kSplitWsBytes = size_t(16) << 20;  // split-K slabs for the layer's GEMMs
+constexpr size_t kSplitWsBytes = size_t(40) << 20;  // stream-K partial slots for the layer GEMMs
 
 struct LayerWs {
-  float *P, *alpha, *agg, *gate, *u1;
+  float *P, *alpha, *agg, *gate, *u1, *u;
   void* split;
 };
 
@@ -191,8 +191,18 @@ static LayerWs carve(void* ws, int V, int E, int D, int F, int H) {
   w.agg = reinterpret_cast<float*>(p); p += align256((size_t)V * F * 4);
   w.gate = reinterpret_cast<float*>(p); p += align256((size_t)D * F * 4);
   w.u1 = reinterpret_cast<float*>(p); p += align256((size_t)D * F * 4);
+  w.u = reinterpret_cast<float*>(p); p += align256((size_t)D * F * 4);
   w.split = p;
   return w;
+}
+
+// Activations the backward pass reads back from a forward workspace (az_backward.hip).
+struct FwdSaved {
+  const float *P, *alpha, *agg, *gate, *u1, *u;
+};
+FwdSaved fwd_saved(const void* ws, int V, int E, int D, int F, int H) {
+  LayerWs L = carve(const_cast<void*>(ws), V, E, D, F, H);
+  return FwdSaved{L.P, L.alpha, L.agg, L.gate, L.u1, L.u};
 }
 
 }  // namespace az
@@ -223,7 +233,7 @@ extern "C" int az_gnn_aggregate_fwd(const az_graph* g, const float* x, int ldx, 
 
 extern "C" size_t az_gnn_layer_ws_bytes(int V, int E, int D, int F, int H) {
   return align256((size_t)V * 2 * H * 4) + align256((size_t)E * 4) + align256((size_t)V * F * 4) +
-         align256((size_t)D * F * 4) + align256((size_t)D * F * 4) + kSplitWsBytes;
+         align256((size_t)D * F * 4) * 3 + kSplitWsBytes;
 }
 
 extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
@@ -270,6 +280,7 @@ extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
   o.A = L.u1; o.lda = F; o.a_kmajor = 1;
   o.B = w->upd_w2; o.ldb = F; o.b_kmajor = 1; o.bias = w->upd_b2;
   o.R = x; o.ldr = F; o.G = L.gate; o.ldg = F;
+  o.C2 = L.u; o.ldc2 = F;  // pre-gate update, kept for the backward pass
   o.C = x_out; o.ldc = F; o.c_rows = (g->D == g->V) ? nullptr : g->dst_rows;
   o.ws = L.split; o.ws_bytes = kSplitWsBytes;
   return gemm_f32(&o, s);

@@ -66,7 +66,7 @@ int az_check_device(void);
  * fixed order (results are deterministic run to run).
  * Requirements: K % 4 == 0 when an operand is K-major; lda, lda2, ldb % 4 == 0 and 16-byte
  * aligned A/A2/B; K0 % 4 == 0; a_rows only with a_kmajor, b_rows only with !b_kmajor;
- * M % 4 == 0 when !a_kmajor; N % 4 == 0 when !b_kmajor.
+ * round_up(M, 4) <= lda when !a_kmajor; round_up(N, 4) <= ldb when !b_kmajor.
  * --------------------------------------------------------------------------------- */
 typedef struct az_gemm_desc {
   int M, N, K;
@@ -130,6 +130,11 @@ typedef struct az_graph {
   const int* edge_dst;  /* [E] destination node of edge e */
   int D;                /* number of destinations with >= 1 in-edge */
   const int* dst_rows;  /* [D] those destinations (ascending) */
+  /* backward only (may be NULL for forward use): */
+  const int* src_rowptr;  /* [V+1] reverse CSR by source */
+  const int* src_edges;   /* [E] edge ids grouped by source (ascending within a source) */
+  const int* dst_index;   /* [V] compact destination index, -1 when no in-edge */
+  int max_deg;            /* max in-degree (backward supports <= 256) */
 } az_graph;
 
 typedef struct az_gnn_layer_w {     /* GNNLayer parameters, state_dict order */
@@ -139,6 +144,12 @@ typedef struct az_gnn_layer_w {     /* GNNLayer parameters, state_dict order */
   const float* upd_w2; const float* upd_b2;   /* update_net.2 [F][F],  [F] */
   const float* gate_w; const float* gate_b;   /* gate.0       [F][2F], [F] */
 } az_gnn_layer_w;
+
+typedef struct az_gnn_layer_grads { /* gradients, same layout as az_gnn_layer_w (written) */
+  float* att_w1; float* att_b1; float* att_w2; float* att_b2;
+  float* upd_w1; float* upd_b1; float* upd_w2; float* upd_b2;
+  float* gate_w; float* gate_b;
+} az_gnn_layer_grads;
 
 /* alpha[e] = sigmoid(w2 . relu(P[dst(e)][2q] + P[col(e)][2q+1] + b1) + b2)
  * the factored attention MLP of GNNLayer.compute_attention (gnn_utils.py:30-32,48-55):
@@ -172,6 +183,59 @@ int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H, const az_g
 int az_mlp2_fwd(const float* x, int M, int F, const float* w0, const float* b0,
                 const float* w2, const float* b2, float* hidden, float* y,
                 void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Backward pass (Connect4GNN.py:150-156,187-197 / TicTacToeGNN.py:217-264), deterministic:
+ * every reduction runs in a fixed order, no float atomics.
+ * --------------------------------------------------------------------------------- */
+/* d loss / d logits and d loss / d tanh-input of the value head for
+ * l = -sum(pi*logp)/B_norm + sum((z-v)^2)/B_norm (Connect4GNN.py:150-152).
+ * loss_rows (nullable): [B][2] per-row (policy, value) loss terms. */
+int az_heads_loss_bwd(const float* logp, const float* v, const float* target_pi,
+                      const float* target_v, int B, int A, int B_norm, float* dlogits,
+                      float* dvpre, float* loss_rows, void* stream);
+/* Heads backward: dwp/dbp/dwv/dbv (nullable as a group) and dhp/dhv (nullable as a pair;
+ * dhv == dhp sums both heads into one buffer, the Connect4 case hp == hv).
+ * ws >= az_colsum_ws_bytes(B, A+1) bytes when weight grads are requested. */
+int az_heads_bwd(const float* dlogits, const float* dvpre, const float* hp, int ldhp,
+                 const float* hv, int ldhv, int B, int K, const float* wp, int A,
+                 const float* wv, float* dwp, float* dbp, float* dwv, float* dbv,
+                 float* dhp, int lddhp, float* dhv, int lddhv, void* ws, size_t ws_bytes,
+                 void* stream);
+/* out[j] = beta*out[j] + sum_i X[i][j] (bias gradients), fixed-order two-pass reduce. */
+size_t az_colsum_ws_bytes(int R, int C);
+int az_colsum(const float* X, int R, int C, int ldx, float* out, float beta, void* ws,
+              size_t ws_bytes, void* stream);
+/* Dropout (Connect4Net.py:52, F.dropout semantics y = x * keep / (1-p)): a counter-based
+ * keep mask (mask[i] = 1 with probability 1-p, reproducible from `seed`), and y = mask ? x*scale : 0
+ * (forward with scale = 1/(1-p); backward on the gradient with the same mask). */
+int az_dropout_mask(uint8_t* mask, int64_t n, double p, uint64_t seed, void* stream);
+int az_mask_scale(const float* x, const uint8_t* mask, float scale, int64_t n, float* y,
+                  void* stream);
+/* Conv trunk backward helpers (3x3, stride 1; pad in {0,1}):
+ *   dz[b*HW+p][c] = dy[b][c*HW+p] * (mask ? mask*scale : 1) * (y > 0)   NCHW -> position-major
+ *   cols[(b,y,x)][c*9+kh*3+kw] = in[b][c][y+kh-pad][x+kw-pad]           row stride ldc >= 9C
+ *   dz[(b,y,x)][c] = sum_{kh,kw} dcols[(b,y-kh+pad,x-kw+pad)][c*9+kh*3+kw] * (a[b][c][y][x] > 0)
+ * With them a conv layer's grads are GEMMs: dW = dz^T cols, db = colsum(dz),
+ * dcols = dz W (then col2im for the layer below). */
+int az_nchw_drelu_to_pm(const float* dy, const float* y, const uint8_t* mask, float scale,
+                        int B, int C, int HW, float* dz, void* stream);
+int az_im2col3x3(const void* in, int in_int8, int B, int C, int H, int W, int pad, int ldc,
+                 float* cols, void* stream);
+int az_col2im3x3_drelu(const float* dcols, int ldc, const float* a, int B, int C, int H, int W,
+                       int pad, float* dz, void* stream);
+/* GNNLayer backward (gnn_utils.py:34-74, per destination) from the activations the forward
+ * kept in fwd_ws: writes dx [V][F] (input gradient) and every parameter gradient in `gr`.
+ * The graph must carry the reverse CSR (src_rowptr/src_edges/dst_index). */
+size_t az_gnn_layer_bwd_ws_bytes(int V, int E, int D, int F, int H);
+int az_gnn_layer_bwd(const az_graph* g, const float* x, int F, int H, const az_gnn_layer_w* w,
+                     const void* fwd_ws, const float* dout, float* dx,
+                     const az_gnn_layer_grads* gr, void* ws, size_t ws_bytes, void* stream);
+/* output_transform backward (gnn_utils.py:101-105): dW2, db2, dW0, db0, dh (scratch [M][F])
+ * and dx (nullable).  ws >= az_colsum_ws_bytes(M, F) (+ split-K room). */
+int az_mlp2_bwd(const float* x, int M, int F, const float* w0, const float* w2,
+                const float* hidden, const float* dy, float* dx, float* dw0, float* db0,
+                float* dw2, float* db2, float* dh, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * torch.optim.Adam step (defaults of Connect4GNN.py:132-133: betas (0.9,0.999), eps 1e-8,

@@ -41,13 +41,20 @@ def run(env, M=512, N=3136, K=3136):
 
 
 if __name__ == "__main__":
-    shapes = [(512, 3136, 3136), (4096, 3136, 3136), (64, 3136, 3136)]
+    mode = sys.argv[1] if len(sys.argv) > 1 else "sweep"
+    if mode == "ablate":
+        for (M, N, K) in [(4096, 3136, 3136), (512, 3136, 3136)]:
+            for cfg in ("0", "1"):
+                for abl in ("0", "1", "2"):
+                    res = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_ABLATE": abl}, M, N, K)
+                    print(json.dumps({"M": M, "cfg": cfg, "ablate": abl, **res}), flush=True)
+        sys.exit(0)
+    shapes = [(512, 3136, 3136), (4096, 3136, 3136), (64, 3136, 3136), (64, 6272, 3136),
+              (4096, 256, 64)]
     for (M, N, K) in shapes:
         for cfg in ("0", "1", "2", "3", "4", "5"):
-            for split in ("1", "2", "3", "4", "6"):
-                if M >= 4096 and split != "1":
-                    continue
-                res = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_SPLITS": split}, M, N, K)
-                print(json.dumps({"M": M, "N": N, "K": K, "cfg": cfg, "splits": split, **res}),
+            for sk in ("0", "1"):
+                res = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_STREAMK": sk}, M, N, K)
+                print(json.dumps({"M": M, "N": N, "K": K, "cfg": cfg, "streamk": sk, **res}),
                       flush=True)
-        print(json.dumps({"M": M, "N": N, "K": K, "tile": "auto", **run({}, M, N, K)}), flush=True)
+        print(json.dumps({"M": M, "N": N, "K": K, "cfg": "auto", **run({}, M, N, K)}), flush=True)
