@@ -31,10 +31,11 @@ struct GemmArgs {
   float* C; int ldc;
   const int* c_rows;
   float* C2; int ldc2;
-  // stream-K (see gemm_f32_mfma): partial-tile slots, 2 per block
-  int streamk;
+  // split-K: block (tile, s) covers k in [s*kc, min(K, (s+1)*kc)) and writes raw partial sums
+  // to slab[s][M][N]; splitk_reduce_kernel sums the slabs in s order (deterministic) and runs
+  // the epilogue.
+  int splits, kc;
   float* slab;
-  int ablate;  // experiments only (AZ_GEMM_ABLATE): 1 = no loads/stores in the K loop, 2 = + no barrier
 };
 
 __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int col, float acc) {
@@ -157,14 +158,6 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
 
 // Waves arranged WGM x WGN; each wave computes a (BM/WGM) x (BN/WGN) sub-tile as TI x TJ
 // 32x32 MFMA accumulators.
-//
-// Work decomposition.  The flattened (tile, BK-step) iteration space [0, T) is cut into
-// gridDim.x equal contiguous ranges ("stream-K"): with gridDim.x = CUs x resident blocks per
-// CU every CU gets the same MFMA work whatever M, N (no partial last wave of tiles, which at
-// M = 512 alone cost ~25 %).  A tile completed inside one range runs the epilogue directly; a
-// tile cut between ranges leaves fp32 partials in the workspace (2 slots per block: its first
-// and its last tile) and streamk_fixup_kernel adds them in range order (deterministic) and
-// runs the epilogue.  Without a workspace each block owns exactly one tile.
 template <int BM, int BN, int BK, int WGM, int WGN, bool A_KM, bool B_KM>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_mfma(GemmArgs p) {
   constexpr int NT = 64 * WGM * WGN;
@@ -177,134 +170,99 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_mfma(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
 
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
-  const int ipt = (p.K + BK - 1) / BK;
-  const int P = gridDim.x;
-  // consecutive logical blocks cover consecutive tiles, and consecutive tiles share the B
-  // (weight) panel: keep them on one XCD so that panel is re-read from that XCD's L2.
-  const int lb = xcd_swizzle(blockIdx.x, P);
-  long lo, hi;
-  if (p.streamk) {
-    const long T = (long)mt_n * nt_n * ipt;
-    lo = (long)lb * T / P;
-    hi = (long)(lb + 1) * T / P;
-  } else {
-    lo = (long)lb * ipt;
-    hi = lo + ipt;
-  }
-  const long blo = lo;
+  const int nwg = mt_n * nt_n * p.splits;
+  // consecutive ids share (split, B panel): keep them on one XCD so the weight slice is
+  // fetched into that XCD's L2 once and re-read from there by the M tiles.
+  const int bid = xcd_swizzle(blockIdx.x, nwg);
+  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
 
-  while (lo < hi) {
-    const int tile = (int)(lo / ipt);
-    const int k0i = (int)(lo % ipt);
-    const int k1i = (int)std::min<long>(ipt, k0i + (hi - lo));
-    const int mt = tile % mt_n, nt = tile / mt_n;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int kbeg = k0i * BK, kend = min(p.K, k1i * BK);
-
-    f32x16 acc[TI][TJ];
+  f32x16 acc[TI][TJ];
 #pragma unroll
-    for (int i = 0; i < TI; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)
+    for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    f32x4 ra[AF4], rb[BF4];
-    KMajorSlots<BM, BK, NT> sa;
-    KMajorSlots<BN, BK, NT> sb;
-    if constexpr (A_KM) init_kmajor<BM, BK, NT, true>(p, m0, p.M, sa);
-    if constexpr (B_KM) init_kmajor<BN, BK, NT, false>(p, n0, p.N, sb);
-    auto load = [&](int k0) {
-      if constexpr (A_KM) load_kmajor<BM, BK, NT>(sa, k0, kend, p.K0, ra);
-      else load_mnmajor<BM, BK, NT>(p.A, p.lda, nullptr, m0, k0, kend, p.M, ra);
-      if constexpr (B_KM) load_kmajor<BN, BK, NT>(sb, k0, kend, p.K, rb);
-      else load_mnmajor<BN, BK, NT>(p.B, p.ldb, p.b_rows, n0, k0, kend, p.N, rb);
-    };
-    auto store = [&](int buf, int k0) {
-      if constexpr (A_KM) store_kmajor<BM, BK, NT, LDK>(As[buf], ra, k0, kend);
-      else store_mnmajor<BM, BK, NT, LDK>(As[buf], ra, k0, kend);
-      if constexpr (B_KM) store_kmajor<BN, BK, NT, LDK>(Bs[buf], rb, k0, kend);
-      else store_mnmajor<BN, BK, NT, LDK>(Bs[buf], rb, k0, kend);
-    };
+  f32x4 ra[AF4], rb[BF4];
+  KMajorSlots<BM, BK, NT> sa;
+  KMajorSlots<BN, BK, NT> sb;
+  if constexpr (A_KM) init_kmajor<BM, BK, NT, true>(p, m0, p.M, sa);
+  if constexpr (B_KM) init_kmajor<BN, BK, NT, false>(p, n0, p.N, sb);
+  auto load = [&](int k0) {
+    if constexpr (A_KM) load_kmajor<BM, BK, NT>(sa, k0, kend, p.K0, ra);
+    else load_mnmajor<BM, BK, NT>(p.A, p.lda, nullptr, m0, k0, kend, p.M, ra);
+    if constexpr (B_KM) load_kmajor<BN, BK, NT>(sb, k0, kend, p.K, rb);
+    else load_mnmajor<BN, BK, NT>(p.B, p.ldb, p.b_rows, n0, k0, kend, p.N, rb);
+  };
+  auto store = [&](int buf, int k0) {
+    if constexpr (A_KM) store_kmajor<BM, BK, NT, LDK>(As[buf], ra, k0, kend);
+    else store_mnmajor<BM, BK, NT, LDK>(As[buf], ra, k0, kend);
+    if constexpr (B_KM) store_kmajor<BN, BK, NT, LDK>(Bs[buf], rb, k0, kend);
+    else store_mnmajor<BN, BK, NT, LDK>(Bs[buf], rb, k0, kend);
+  };
 
-    const int nk = k1i - k0i;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
     load(kbeg);
     store(0, kbeg);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = p.ablate ? 0 : (kt & 1);
-      if (kt + 1 < nk && !p.ablate) load(kbeg + (kt + 1) * BK);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load(kbeg + (kt + 1) * BK);
 #pragma unroll
-      for (int g = 0; g < BK / 8; ++g) {
-        f32x4 a[TI], b[TJ];
+    for (int g = 0; g < BK / 8; ++g) {
+      f32x4 a[TI], b[TJ];
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
-          a[i] = *reinterpret_cast<const f32x4*>(
-              &As[cur][(wm * WM + i * 32 + (lane & 31)) * LDK + g * 8 + (lane >> 5) * 4]);
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          b[j] = *reinterpret_cast<const f32x4*>(
-              &Bs[cur][(wn * WN + j * 32 + (lane & 31)) * LDK + g * 8 + (lane >> 5) * 4]);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int i = 0; i < TI; ++i)
-#pragma unroll
-            for (int j = 0; j < TJ; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
-      }
-      if (kt + 1 < nk && !p.ablate) store(cur ^ 1, kbeg + (kt + 1) * BK);
-      if (p.ablate < 2) __syncthreads();
-    }
-
-    const bool whole = (k0i == 0 && k1i == ipt);
-    float* part = whole ? nullptr
-                        : p.slab + ((size_t)lb * 2 + (lo == blo ? 0 : 1)) * (size_t)(BM * BN);
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
+      for (int i = 0; i < TI; ++i)
+        a[i] = *reinterpret_cast<const f32x4*>(
+            &As[cur][(wm * WM + i * 32 + (lane & 31)) * LDK + g * 8 + (lane >> 5) * 4]);
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
+        b[j] = *reinterpret_cast<const f32x4*>(
+            &Bs[cur][(wn * WN + j * 32 + (lane & 31)) * LDK + g * 8 + (lane >> 5) * 4]);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const int cl = wn * WN + j * 32 + (lane & 31);
-          if (part) part[rl * BN + cl] = acc[i][j][r];
-          else epilogue_store(p, m0 + rl, n0 + cl, acc[i][j][r]);
-        }
-    lo += k1i - k0i;
-  }
-}
-
-__device__ __forceinline__ long sk_lo(long b, long T, int P) { return b * T / P; }
-
-__device__ int sk_owner(long i, long T, int P) {
-  long b = i * P / T;
-  while (b + 1 < P && sk_lo(b + 1, T, P) <= i) ++b;
-  while (b > 0 && sk_lo(b, T, P) > i) --b;
-  return (int)b;
-}
-
-template <int BM, int BN, int BK>
-__global__ __launch_bounds__(256) void streamk_fixup_kernel(GemmArgs p, int P) {
-  const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
-  const int ipt = (p.K + BK - 1) / BK;
-  const long T = (long)mt_n * nt_n * ipt;
-  const int tile = blockIdx.x;
-  const long istart = (long)tile * ipt, iend = istart + ipt;
-  const int q0 = sk_owner(istart, T, P), q1 = sk_owner(iend - 1, T, P);
-  if (q0 == q1) return;  // one range held the whole tile: it ran the epilogue itself
-  const int m0 = (tile % mt_n) * BM, n0 = (tile / mt_n) * BN;
-  for (int e = threadIdx.x; e < BM * BN; e += 256) {
-    const int rl = e / BN, cl = e % BN;
-    float v = 0.f;
-    for (int q = q0; q <= q1; ++q) {
-      const int seg = (q == q0 && sk_lo(q, T, P) < istart) ? 1 : 0;
-      v += p.slab[((size_t)q * 2 + seg) * (size_t)(BM * BN) + e];
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
     }
-    epilogue_store(p, m0 + rl, n0 + cl, v);
+    if (kt + 1 < nk) store(cur ^ 1, kbeg + (kt + 1) * BK);
+    __syncthreads();
+  }
+
+  float* slab = p.splits > 1 ? p.slab + (size_t)sp * p.M * p.N : nullptr;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = n0 + wn * WN + j * 32 + (lane & 31);
+        if (slab) {
+          if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][r];
+        } else {
+          epilogue_store(p, row, col, acc[i][j][r]);
+        }
+      }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
+  const long total = (long)p.M * p.N;
+  const size_t plane = (size_t)p.M * p.N;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int k = 0; k < p.splits; ++k) s += p.slab[k * plane + idx];
+    epilogue_store(p, (int)(idx / p.N), (int)(idx % p.N), s);
   }
 }
 
@@ -381,48 +339,31 @@ __global__ __launch_bounds__(256) void gemv_f32(GemmArgs p) {
   }
 }
 
-struct TileCfg { int bm, bn, bk, wgm, wgn, per_cu; };
-// per_cu = resident blocks per CU (LDS-limited).
+struct TileCfg { int bm, bn, bk, wgm, wgn; };
 // 0: 64x64x32 (4 waves 2x2)   1: 128x128x32 (4 waves 2x2)   2: 64x64x64 (4 waves)
 // 3: 128x64x32 (4 waves 2x2)  4: 128x128x32 (8 waves 2x4)   5: 256x128x32 (8 waves 4x2)
-static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2, 4},  {128, 128, 32, 2, 2, 2},
-                                {64, 64, 64, 2, 2, 2},  {128, 64, 32, 2, 2, 2},
-                                {128, 128, 32, 2, 4, 2}, {256, 128, 32, 4, 2, 1}};
+static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 64, 64, 2, 2},
+                                {128, 64, 32, 2, 2}, {128, 128, 32, 2, 4}, {256, 128, 32, 4, 2}};
 
 template <int BM, int BN, int BK, int WGM, int WGN>
-static void launch_tile(const GemmArgs& a, int grid, bool akm, bool bkm, hipStream_t s) {
-  dim3 g(grid), b(64 * WGM * WGN);
+static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
+  dim3 g(nwg), b(64 * WGM * WGN);
   if (akm && bkm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, WGM, WGN, true, true>), g, b, 0, s, a);
   else if (akm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, WGM, WGN, true, false>), g, b, 0, s, a);
   else if (bkm) hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, WGM, WGN, false, true>), g, b, 0, s, a);
   else hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, WGM, WGN, false, false>), g, b, 0, s, a);
-  if (a.streamk) {
-    const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-    hipLaunchKernelGGL((streamk_fixup_kernel<BM, BN, BK>), dim3(tiles), dim3(256), 0, s, a, grid);
-  }
 }
 
-static void launch_cfg(int cfg, const GemmArgs& a, int grid, bool akm, bool bkm, hipStream_t s) {
+static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
   switch (cfg) {
-    case 1: launch_tile<128, 128, 32, 2, 2>(a, grid, akm, bkm, s); break;
-    case 2: launch_tile<64, 64, 64, 2, 2>(a, grid, akm, bkm, s); break;
-    case 3: launch_tile<128, 64, 32, 2, 2>(a, grid, akm, bkm, s); break;
-    case 4: launch_tile<128, 128, 32, 2, 4>(a, grid, akm, bkm, s); break;
-    case 5: launch_tile<256, 128, 32, 4, 2>(a, grid, akm, bkm, s); break;
-    default: launch_tile<64, 64, 32, 2, 2>(a, grid, akm, bkm, s); break;
+    case 1: launch_tile<128, 128, 32, 2, 2>(a, akm, bkm, s); break;
+    case 2: launch_tile<64, 64, 64, 2, 2>(a, akm, bkm, s); break;
+    case 3: launch_tile<128, 64, 32, 2, 2>(a, akm, bkm, s); break;
+    case 4: launch_tile<128, 128, 32, 2, 4>(a, akm, bkm, s); break;
+    case 5: launch_tile<256, 128, 32, 4, 2>(a, akm, bkm, s); break;
+    default: launch_tile<64, 64, 32, 2, 2>(a, akm, bkm, s); break;
   }
-}
-
-static int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-            ? prop.multiProcessorCount
-            : 256;
-  }
-  return n;
 }
 
 static void launch_gemv(const GemmArgs& a, hipStream_t s) {
@@ -433,6 +374,26 @@ static void launch_gemv(const GemmArgs& a, hipStream_t s) {
     case 3: case 4: hipLaunchKernelGGL(gemv_f32<4>, dim3(nblk), dim3(256), 0, s, a); break;
     default: hipLaunchKernelGGL(gemv_f32<8>, dim3(nblk), dim3(256), 0, s, a); break;
   }
+}
+
+// Pick the block tile and the split-K factor: aim for ~2 blocks per CU (512) on the 256 CUs,
+// keep >= 4 BK steps per split, and only split when the caller's workspace holds the slabs.
+static void plan(GemmArgs& a, int bm, int bn, int bk, size_t ws_bytes) {
+  const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+  int S = 1;
+  static const char* env_split = getenv("AZ_GEMM_SPLITS");
+  if (env_split && a.slab) {
+    S = std::max(1, atoi(env_split));
+  } else if (tiles < 1024 && a.slab) {
+    // measured on MI355X (tools/gemm_sweep.py): M=512 x 3136^2 best at S=3 (1176 blocks),
+    // M=64 at S=4..8; keep >= 4 BK steps per split
+    S = (int)std::min<long>(std::min<long>((1024 + tiles - 1) / tiles, 8), a.K / (bk * 4));
+  }
+  while (S > 1 && (size_t)S * a.M * a.N * 4 > ws_bytes) --S;
+  if (S < 1) S = 1;
+  a.splits = S;
+  a.kc = S > 1 ? ((a.K + S - 1) / S + bk - 1) / bk * bk : a.K;
+  if (S > 1) a.splits = (a.K + a.kc - 1) / a.kc;
 }
 
 int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
@@ -469,39 +430,29 @@ int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
   a.beta = d->beta; a.C = d->C; a.ldc = d->ldc; a.c_rows = d->c_rows;
   a.C2 = d->C2; a.ldc2 = d->ldc2;
   a.slab = static_cast<float*>(d->ws);
-  static const char* env_abl = getenv("AZ_GEMM_ABLATE");
-  a.ablate = env_abl ? atoi(env_abl) : 0;
-  a.streamk = 0;
+  a.splits = 1; a.kc = d->K;
 
   if (d->M <= 8 && akm && bkm && !d->C2 && d->act != AZ_ACT_DRELU) {
     launch_gemv(a, s);
     return check_launch("gemv_f32");
   }
-  // tile choice (tuning override for experiments: AZ_GEMM_CFG=<index into kCfgs>,
-  // AZ_GEMM_STREAMK=0|1)
+  // tile choice (tuning override for experiments: AZ_GEMM_CFG=<index into kCfgs>)
   static const char* env_cfg = getenv("AZ_GEMM_CFG");
-  static const char* env_sk = getenv("AZ_GEMM_STREAMK");
   int cfg = 0;
   if (env_cfg) {
     cfg = std::min(std::max(atoi(env_cfg), 0), 5);
   } else {
-    const long t128 = (long)((d->M + 127) / 128) * ((d->N + 127) / 128);
-    cfg = t128 >= 1024 ? 1 : 0;
+    cfg = 0;  // 64x64x32 measured fastest for every shape of the path (tools/gemm_sweep.py)
   }
   const TileCfg& tc = kCfgs[cfg];
-  const long tiles = (long)((d->M + tc.bm - 1) / tc.bm) * ((d->N + tc.bn - 1) / tc.bn);
-  const long ipt = (d->K + tc.bk - 1) / tc.bk;
-  const long slots = (long)num_cus() * tc.per_cu;
-  long grid = tiles;
-  bool sk = a.slab && (tiles % slots) != 0 && tiles < 16 * slots && ipt > 1;
-  if (env_sk) sk = a.slab && atoi(env_sk) != 0;
-  if (sk) {
-    grid = std::min(slots, tiles * ipt);
-    if ((size_t)grid * 2 * tc.bm * tc.bn * 4 > d->ws_bytes) sk = false, grid = tiles;
-  }
-  a.streamk = sk ? 1 : 0;
-  launch_cfg(cfg, a, (int)grid, akm, bkm, s);
-  return check_launch("gemm_f32_mfma");
+  plan(a, tc.bm, tc.bn, tc.bk, d->ws_bytes);
+  launch_cfg(cfg, a, akm, bkm, s);
+  int rc = check_launch("gemm_f32_mfma");
+  if (rc || a.splits <= 1) return rc;
+  const long total = (long)a.M * a.N;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, a);
+  return check_launch("splitk_reduce_kernel");
 }
 
 }  // namespace az

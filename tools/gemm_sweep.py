@@ -42,6 +42,13 @@ def run(env, M=512, N=3136, K=3136):
 
 if __name__ == "__main__":
     mode = sys.argv[1] if len(sys.argv) > 1 else "sweep"
+    if mode == "quick":
+        for (M, N, K) in [(512, 3136, 3136), (4096, 3136, 3136), (64, 3136, 3136)]:
+            for cfg in ("0", "1", "2", "3", "4", "5"):
+                for sk in ("0", "1"):
+                    res = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_STREAMK": sk}, M, N, K)
+                    print(json.dumps({"M": M, "cfg": cfg, "streamk": sk, **res}), flush=True)
+        sys.exit(0)
     if mode == "ablate":
         for (M, N, K) in [(4096, 3136, 3136), (512, 3136, 3136)]:
             for cfg in ("0", "1"):
