@@ -1,0 +1,176 @@
+"""The reference's NeuralNet wrappers (Net.py:1-61 duck type) on libaz_hip.
+
+Same constructor signature (game, args), same methods and return types as
+connect4/Connect4Net.py:62-147, connect4/Connect4GNN.py:14-220, tictactoe/TicTacToeNet.py:50-104
+and tictactoe/TicTacToeGNN.py:9-181, plus batched entry points (predict_batch,
+predict_batch_with_gnn, predict_both) for lock-step self-play.  Checkpoints are the same
+torch.save dict ({'state_dict': ..., 'gnn': ...}) with the same keys, so files move freely
+between the reference and this implementation.
+"""
+import os
+
+import numpy as np
+import torch
+
+from . import nets, train as T
+from .nets import boards_to_device
+
+
+def _dev_array(rows, dtype, device):
+    return torch.from_numpy(np.ascontiguousarray(np.array(rows), dtype=dtype)).to(device)
+
+
+class NetWrapper:
+    """Common body; subclasses choose the board network class and whether a GNN exists."""
+
+    net_class = None
+    has_gnn = False
+    makedirs_on_save = True
+
+    def __init__(self, game, args):
+        self.device = nets.default_device()
+        self.nnet = self.net_class(game, args, device=self.device)
+        self.board_x, self.board_y = game.getBoardSize()
+        self.action_size = game.getActionSize()
+        self.args = args
+        if self.has_gnn:
+            self.feature_dim = self.nnet.feature_dim
+            num_layers = nets._args_get(args, "gnn_layers", 2)
+            self.gnn = nets.PolicyValueGNN(self.feature_dim, num_layers, device=self.device)
+        self.train_seed = 0
+
+    # -- evaluation ------------------------------------------------------------------------
+    def _eval(self, boards, gnn):
+        b = boards_to_device(boards, self.device)
+        if b.dim() == 2:
+            b = b.view(1, self.board_x, self.board_y)
+        f = self.nnet.features(b)
+        if gnn:
+            f = self.gnn.forward_per_row(f)
+        _, pi, v = self.nnet.heads(f)
+        return pi, v
+
+    def predict(self, board, neighbor_states=None):
+        """Net.predict: (pi float32[A], v float32) for one canonical board
+        (Connect4GNN.py:59-84; `neighbor_states` is accepted and unused as in
+        Connect4Net.py:110)."""
+        self.nnet.eval()
+        pi, v = self._eval(board, False)
+        out = torch.cat([pi[0], v]).cpu().numpy()
+        return out[:-1], out[-1]
+
+    def predict_batch(self, boards):
+        """Row-wise predict for [B,n,n] boards -> (pi float32[B,A], v float32[B])."""
+        self.nnet.eval()
+        pi, v = self._eval(boards, False)
+        return pi.cpu().numpy(), v.cpu().numpy()
+
+    def save_checkpoint(self, folder, filename):
+        if self.makedirs_on_save and not os.path.exists(folder):
+            os.makedirs(folder)
+        filepath = os.path.join(folder, filename) if self.has_gnn else folder + "/" + filename
+        payload = {"state_dict": self.nnet.params.cpu_state_dict()}
+        if self.has_gnn:
+            payload["gnn"] = self.gnn.params.cpu_state_dict()
+        torch.save(payload, filepath)
+
+    def load_checkpoint(self, folder, filename):
+        filepath = os.path.join(folder, filename) if self.has_gnn else folder + "/" + filename
+        checkpoint = torch.load(filepath, map_location="cpu", weights_only=True)
+        self.nnet.load_state_dict(checkpoint["state_dict"])
+        if self.has_gnn:
+            if "gnn" in checkpoint:
+                self.gnn.load_state_dict(checkpoint["gnn"])
+            else:
+                print(f"GNN state not found in {filepath}, initializing new GNN")
+
+    # -- training --------------------------------------------------------------------------
+    def _cnn_batch(self, examples):
+        batch_idx = np.random.randint(0, len(examples), min(len(examples), self.args.batch_size))
+        boards, pis, vs = list(zip(*[examples[i] for i in batch_idx]))
+        return (_dev_array(boards, np.int8, self.device),
+                _dev_array(pis, np.float32, self.device),
+                _dev_array(np.array(vs).astype(np.float64), np.float32, self.device))
+
+    def _gnn_batch(self, gnn_examples):
+        batch_idx = np.random.randint(0, len(gnn_examples),
+                                      min(len(gnn_examples), self.args.batch_size))
+        batch = [gnn_examples[i] for i in batch_idx]
+        boards = [b for b, _, _, _, _, _, _ in batch]
+        pis = [p for _, _, _, _, p, _, _ in batch]
+        vs = [v for _, _, _, _, _, v, _ in batch]
+        return (_dev_array(boards, np.int8, self.device),
+                _dev_array(pis, np.float32, self.device),
+                _dev_array(np.array(vs).astype(np.float64), np.float32, self.device))
+
+    def _train(self, examples, gnn_examples=None):
+        """Connect4GNN.py:122-197: fresh Adam per call, `epochs` x (CNN step on a batch sampled
+        with replacement by np.random.randint; GNN step on a second sample)."""
+        lr = self.args.lr
+        self.nnet.params.reset_adam()
+        if self.has_gnn:
+            self.gnn.params.reset_adam()
+        for _ in range(self.args.epochs):
+            self.nnet.train()
+            if self.has_gnn:
+                self.gnn.train()
+            if examples:
+                b, p, v = self._cnn_batch(examples)
+                self.train_seed += 1
+                T.cnn_step(self.nnet, b, p, v, lr, seed=self.train_seed)
+            if self.has_gnn and gnn_examples and len(gnn_examples) > 0:
+                b, p, v = self._gnn_batch(gnn_examples)
+                self.train_seed += 1
+                T.gnn_step(self.nnet, self.gnn, b, p, v, lr, seed=self.train_seed)
+        torch.cuda.current_stream().synchronize()
+
+
+class GNNWrapperMixin:
+    """predict / predict_with_gnn pair of the GNN wrappers (Connect4GNN.py:59-120)."""
+
+    has_gnn = True
+
+    def predict(self, board):
+        return NetWrapper.predict(self, board)
+
+    def predict_with_gnn(self, board):
+        """GNN-enhanced prediction: a 1-row input, so the message-passing layers are the
+        identity (gnn_utils.py:35-36) and only output_transform runs before the heads."""
+        self.nnet.eval()
+        self.gnn.eval()
+        pi, v = self._eval(board, True)
+        out = torch.cat([pi[0], v]).cpu().numpy()
+        return out[:-1], out[-1]
+
+    def predict_batch_with_gnn(self, boards):
+        self.nnet.eval()
+        self.gnn.eval()
+        pi, v = self._eval(boards, True)
+        return pi.cpu().numpy(), v.cpu().numpy()
+
+    def predict_both(self, boards):
+        """Standard and GNN predictions of a batch from ONE trunk pass (what MCTS.search asks
+        for every new leaf, MCTS.py:169-174) -> (pi, v, gnn_pi, gnn_v), one host copy."""
+        self.nnet.eval()
+        self.gnn.eval()
+        b = boards_to_device(boards, self.device)
+        f = self.nnet.features(b)
+        _, pi, v = self.nnet.heads(f)
+        _, gpi, gv = self.nnet.heads(self.gnn.forward_per_row(f))
+        out = torch.cat([pi, v[:, None], gpi, gv[:, None]], dim=1).cpu().numpy()
+        A = self.action_size
+        return out[:, :A], out[:, A], out[:, A + 1:2 * A + 1], out[:, 2 * A + 1]
+
+    def train(self, examples, gnn_examples=None):
+        self._train(examples, gnn_examples)
+
+    def extract_features(self, board_tensor):
+        """Connect4GNN.py:31-46 on device boards (eval-mode features)."""
+        return self.nnet.features(boards_to_device(board_tensor, self.device))
+
+
+class CNNWrapperMixin:
+    has_gnn = False
+
+    def train(self, examples):
+        self._train(examples, None)
