@@ -12,7 +12,7 @@ import os
 import numpy as np
 import torch
 
-from . import nets, train as T
+from . import nets, ops, train as T
 from .nets import boards_to_device
 
 
@@ -165,8 +165,26 @@ class GNNWrapperMixin:
         self._train(examples, gnn_examples)
 
     def extract_features(self, board_tensor):
-        """Connect4GNN.py:31-46 on device boards (eval-mode features)."""
-        return self.nnet.features(boards_to_device(board_tensor, self.device))
+        """Connect4GNN.py:31-46 / TicTacToeGNN.py:25-34 on device boards.  As in the reference,
+        the Connect4 features go through dropout while `nnet.training` is set (the mask comes
+        from the counter-based device RNG, not torch's generator)."""
+        b = boards_to_device(board_tensor, self.device)
+        if b.dim() == 2:
+            b = b.view(1, self.board_x, self.board_y)
+        f = self.nnet.features(b)
+        p = float(getattr(self.nnet, "dropout", 0.0)) if isinstance(self.nnet, nets.Connect4Net) \
+            else 0.0
+        if self.nnet.training and p > 0.0:
+            self.train_seed += 1
+            mask = ops.dropout_mask(f.numel(), p, self.train_seed, f.device)
+            f = ops.mask_scale(f, mask, 1.0 / (1.0 - p))
+        return f
+
+    def apply_policy_value_heads(self, features):
+        """Connect4GNN.py:48-57 / TicTacToeGNN.py:36-45: features [B,F] on HBM ->
+        (log_pi [B,A], v [B,1])."""
+        logp, _, v = self.nnet.heads(features.contiguous(), want_pi=False)
+        return logp, v.view(-1, 1)
 
 
 class CNNWrapperMixin:

@@ -106,6 +106,16 @@ def aggregate_roofline(torch, ops, device, graphs=512):
             "workload": f"{graphs} 32x32 grids, V={V}, E={E}, F=64 (config-5 shard per GPU)"}
 
 
+def pmc_traffic(key):
+    """HBM bytes per launch from the committed PMC pass (profiles/pmc.json, written from the
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs; see profiles/README.md)."""
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "pmc.json")))[key][
+            "hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     args = parse()
     import torch
@@ -180,13 +190,9 @@ def main():
     if not args.no_aggregate:
         agg = aggregate_roofline(torch, ops, device)
 
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "gemm_pmc.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic = pmc_traffic("gemm")
+    if agg is not None:
+        agg["traffic"] = pmc_traffic("aggregate")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
