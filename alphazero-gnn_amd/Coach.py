@@ -15,6 +15,7 @@ from tqdm import tqdm
 
 from Arena import Arena
 from MCTS import MCTS
+from azhip import dist as D
 
 log = logging.getLogger(__name__)
 
@@ -24,6 +25,44 @@ def _flag(args, name, default=False):
         return args[name] if isinstance(args, dict) else getattr(args, name)
     except (KeyError, AttributeError):
         return default
+
+
+def episode_g(game, args, mcts, rng=None):
+    """Coach.py:27-79 as a search generator (see MCTS.py): one self-play game ->
+    (std_examples, gnn_examples), with the final result r signed per example by whether its
+    player is the one to move at the end.  `rng` (default: the global np.random stream, as the
+    reference) draws the moves; mcts.rng draws the temp-0 tie-breaks."""
+    choice = (np.random if rng is None else rng).choice
+    use_gnn = _flag(args, "use_gnn")
+    examples, gnn_examples = [], []
+    board = game.getInitBoard()
+    cur = 1
+    step = 0
+    while True:
+        step += 1
+        canonical = game.getCanonicalForm(board, cur)
+        temp = int(step < args.tempThreshold)
+        pi = yield from mcts.getActionProb_g(canonical, temp=temp)
+        sym = game.getSymmetries(canonical, pi)
+        examples.extend([b, cur, p, None] for b, p in sym)
+        if use_gnn:
+            nodes = yield from mcts.expand_tree_g(canonical, expand_by=_flag(args, "expand_by", 5))
+            for s, (ipi, iv, epi, ev) in nodes.items():
+                for b, _ in sym:
+                    if game.stringRepresentation(b) == s:
+                        gnn_examples.append([b, cur, ipi, iv, epi, ev, None])
+                        break
+        action = choice(len(pi), p=pi)
+        board, cur = game.getNextState(board, cur, action)
+        r = game.getGameEnded(board, cur)
+        if r != 0:
+            def sign(p):
+                return r * ((-1) ** (p != cur))
+            std = [(x[0], x[2], sign(x[1])) for x in examples]
+            if use_gnn and gnn_examples:
+                return std, [(x[0], x[1], x[2], x[3], x[4], x[5], sign(x[1]))
+                             for x in gnn_examples]
+            return std, []
 
 
 class Coach:
@@ -37,55 +76,57 @@ class Coach:
         self.skipFirstSelfPlay = False
 
     def executeEpisode(self):
-        """Coach.py:27-79: one self-play game -> (std_examples, gnn_examples) with the final
-        result r signed per example by whether its player is the one to move at the end."""
-        use_gnn = _flag(self.args, "use_gnn")
-        examples, gnn_examples = [], []
-        board = self.game.getInitBoard()
-        self.curPlayer = 1
-        step = 0
-        while True:
-            step += 1
-            canonical = self.game.getCanonicalForm(board, self.curPlayer)
-            temp = int(step < self.args.tempThreshold)
-            pi = self.mcts.getActionProb(canonical, temp=temp)
-            sym = self.game.getSymmetries(canonical, pi)
-            examples.extend([b, self.curPlayer, p, None] for b, p in sym)
-            if use_gnn:
-                nodes = self.mcts.expand_tree(canonical,
-                                              expand_by=_flag(self.args, "expand_by", 5))
-                for s, (ipi, iv, epi, ev) in nodes.items():
-                    for b, _ in sym:
-                        if self.game.stringRepresentation(b) == s:
-                            gnn_examples.append([b, self.curPlayer, ipi, iv, epi, ev, None])
-                            break
-            action = np.random.choice(len(pi), p=pi)
-            board, self.curPlayer = self.game.getNextState(board, self.curPlayer, action)
-            r = self.game.getGameEnded(board, self.curPlayer)
-            if r != 0:
-                def sign(p):
-                    return r * ((-1) ** (p != self.curPlayer))
-                std = [(x[0], x[2], sign(x[1])) for x in examples]
-                if use_gnn and gnn_examples:
-                    return std, [(x[0], x[1], x[2], x[3], x[4], x[5], sign(x[1]))
-                                 for x in gnn_examples]
-                return std, []
+        """Coach.py:27-79: one self-play game -> (std_examples, gnn_examples)."""
+        return self.mcts.drive(episode_g(self.game, self.args, self.mcts))
 
     def getCheckpointFile(self, iteration):
         return f"checkpoint_{iteration}" + ("_gnn" if _flag(self.args, "use_gnn") else "") + \
             ".pth.tar"
 
+    def selfPlay(self):
+        """One iteration's self-play (Coach.py:95-100) -> [(std, gnn)] in episode order.
+
+        parallel_games <= 1 on one rank: the reference's sequential loop on the global RNG.
+        Otherwise lock-step batched games (selfplay.py), episode e on rank e mod P with its own
+        RandomState; results gathered on every rank and ordered by episode, so every P and G
+        produce the same examples."""
+        n = self.args.numEps
+        parallel = int(_flag(self.args, "parallel_games", 1) or 1)
+        world, rank = D.world_rank()
+        if parallel <= 1 and world == 1:
+            out = []
+            for _ in tqdm(range(n), desc="Self Play"):
+                self.mcts = MCTS(self.game, self.nnet, self.args)
+                out.append(self.executeEpisode())
+            return out
+        from selfplay import episode_seeds, play_episodes
+        base = D.broadcast_int(np.random.randint(0, 2 ** 31 - 1))
+        seeds = episode_seeds(base, range(n))
+        local = play_episodes(self.game, self.nnet, self.args, D.my_episodes(n, world, rank),
+                              seeds, parallel_games=max(1, parallel))
+        allr = D.gather_episodes(local)
+        return [allr[e] for e in range(n)]
+
+    def _is_writer(self):
+        return D.world_rank()[1] == 0
+
+    def _barrier(self):
+        if D.dist_ok():
+            import torch.distributed as dist
+            dist.barrier()
+
     def learn(self):
-        """Coach.py:87-176."""
+        """Coach.py:87-176.  Under torch.distributed every rank runs this loop on identical
+        data (host RNGs synchronised here); only rank 0 writes files."""
         use_gnn = _flag(self.args, "use_gnn")
+        if D.world_rank()[0] > 1:
+            D.sync_host_rngs()
         for i in range(1, self.args.numIters + 1):
             log.info(f"Starting Iter #{i} ...")
             if not self.skipFirstSelfPlay or i > 1:
                 it_std = deque([], maxlen=self.args.maxlenOfQueue)
                 it_gnn = deque([], maxlen=self.args.maxlenOfQueue)
-                for _ in tqdm(range(self.args.numEps), desc="Self Play"):
-                    self.mcts = MCTS(self.game, self.nnet, self.args)
-                    std, gnn = self.executeEpisode()
+                for std, gnn in self.selfPlay():
                     it_std += std
                     if gnn:
                         it_gnn += gnn
@@ -94,7 +135,8 @@ class Coach:
                 log.warning("Removing the oldest entry in trainExamples. "
                             f"len(trainExamplesHistory) = {len(self.trainExamplesHistory)}")
                 self.trainExamplesHistory.pop(0)
-            self.saveTrainExamples(i - 1)
+            if self._is_writer():
+                self.saveTrainExamples(i - 1)
 
             trainExamples, gnnExamples = [], []
             for std_ex, gnn_ex in self.trainExamplesHistory:
@@ -106,7 +148,9 @@ class Coach:
                 shuffle(gnnExamples)
 
             temp = "temp.pth.tar"
-            self.nnet.save_checkpoint(folder=self.args.checkpoint, filename=temp)
+            if self._is_writer():
+                self.nnet.save_checkpoint(folder=self.args.checkpoint, filename=temp)
+            self._barrier()
             self.pnet.load_checkpoint(folder=self.args.checkpoint, filename=temp)
             pmcts = MCTS(self.game, self.pnet, self.args)
             if use_gnn and gnnExamples:
@@ -135,8 +179,10 @@ class Coach:
                 log.info("ACCEPTING NEW MODEL")
                 best = "best_gnn.pth.tar" if use_gnn else "best.pth.tar"
                 it_name = f"checkpoint_{i}_gnn.pth.tar" if use_gnn else f"checkpoint_{i}.pth.tar"
-                self.nnet.save_checkpoint(folder=self.args.checkpoint, filename=it_name)
-                self.nnet.save_checkpoint(folder=self.args.checkpoint, filename=best)
+                if self._is_writer():
+                    self.nnet.save_checkpoint(folder=self.args.checkpoint, filename=it_name)
+                    self.nnet.save_checkpoint(folder=self.args.checkpoint, filename=best)
+            self._barrier()
 
     def saveTrainExamples(self, iteration):
         folder = self.args.checkpoint

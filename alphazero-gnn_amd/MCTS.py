@@ -10,6 +10,14 @@ The descent is iterative (path recorded, then backed up) instead of recursive; t
 sign convention is kept: a new leaf or a terminal state hands its value UN-negated to its
 parent, and every interior node updates with the value it receives and passes on its negation
 (MCTS.py:154-157,190-193,226-240).
+
+Every search routine is written once, as a generator (`*_g`) that YIELDS a leaf-evaluation
+request `(board, want_gnn)` and receives `(std, gnn, err)` back: std/gnn are `(pi, v)` pairs or
+None, err the exception a failed evaluation raised.  The reference-shaped methods
+(`search`, `getActionProb`, `expand_tree`) drive that generator with batch-1 `predict` /
+`predict_with_gnn` calls; selfplay.py drives many of them in lock step with one batched
+`predict_both` launch per simulation.  Same code either way, so the lock-step driver inherits
+the search parity.
 """
 import logging
 import math
@@ -22,10 +30,11 @@ log = logging.getLogger(__name__)
 
 
 class MCTS:
-    def __init__(self, game, nnet, args):
+    def __init__(self, game, nnet, args, rng=None):
         self.game = game
         self.nnet = nnet
         self.args = args
+        self.rng = rng            # None: the global np.random stream, as the reference
         self.Qsa = {}
         self.Nsa = {}
         self.Ns = {}
@@ -41,22 +50,56 @@ class MCTS:
         return bool(getattr(self.args, "use_gnn", False)) if not isinstance(self.args, dict) \
             else bool(self.args.get("use_gnn", False))
 
+    def _choice(self, *a, **k):
+        return (np.random if self.rng is None else self.rng).choice(*a, **k)
+
+    # ------------------------------------------------------------------ batch-1 driver
+    def evaluate_request(self, request):
+        """Serve one leaf request with the reference's batch-1 calls (MCTS.py:169-174)."""
+        board, want_gnn = request
+        std = gnn = err = None
+        try:
+            std = self.nnet.predict(board)
+            if want_gnn:
+                gnn = self.nnet.predict_with_gnn(board)
+        except Exception as e:  # handled where the reference handles it (search / expand_tree)
+            err = e
+        return std, gnn, err
+
+    def drive(self, gen):
+        """Run a search generator to completion with batch-1 network calls."""
+        try:
+            request = next(gen)
+            while True:
+                request = gen.send(self.evaluate_request(request))
+        except StopIteration as stop:
+            return stop.value
+
+    def getActionProb(self, canonicalBoard, temp=1):
+        return self.drive(self.getActionProb_g(canonicalBoard, temp))
+
+    def expand_tree(self, canonicalBoard, expand_by=5):
+        return self.drive(self.expand_tree_g(canonicalBoard, expand_by))
+
+    def search(self, canonicalBoard, expansion=False):
+        return self.drive(self.search_g(canonicalBoard, expansion))
+
     # ------------------------------------------------------------------ root policies
     def _root_counts(self, s):
         return [self.Nsa[(s, a)] if (s, a) in self.Nsa else 0
                 for a in range(self.game.getActionSize())]
 
-    def getActionProb(self, canonicalBoard, temp=1):
+    def getActionProb_g(self, canonicalBoard, temp=1):
         """MCTS.py:29-58: numMCTSSims searches, then visit counts -> policy (temp 0: argmax
         with a np.random.choice tie-break)."""
         self.standard_predictions = {}
         self.gnn_predictions = {}
         for _ in range(self.args.numMCTSSims):
-            self.search(canonicalBoard)
+            yield from self.search_g(canonicalBoard)
         counts = self._root_counts(self.game.stringRepresentation(canonicalBoard))
         if temp == 0:
             best = np.array(np.argwhere(counts == np.max(counts))).flatten()
-            a = np.random.choice(best)
+            a = self._choice(best)
             probs = [0] * len(counts)
             probs[a] = 1
             return probs
@@ -69,7 +112,7 @@ class MCTS:
             return np.ones(len(counts)) / len(counts)
         return [x / total for x in counts]
 
-    def expand_tree(self, canonicalBoard, expand_by=5):
+    def expand_tree_g(self, canonicalBoard, expand_by=5):
         """MCTS.py:60-149: extra searches from the root; returns
         {root: (initial_pi, initial_v, expanded_pi, expanded_v)} for GNN training targets."""
         s = self.game.stringRepresentation(canonicalBoard)
@@ -83,7 +126,7 @@ class MCTS:
         initial_counts = root_visits()
         if not initial_counts:
             for _ in range(self.args.numMCTSSims):
-                self.search(canonicalBoard)
+                yield from self.search_g(canonicalBoard)
             initial_counts = root_visits()
         initial_policy = np.zeros(A)
         for a, c in initial_counts.items():
@@ -96,12 +139,15 @@ class MCTS:
             initial_policy = valids / np.sum(valids)
 
         if s not in self.standard_predictions:
-            std_pi, std_v = self.nnet.predict(canonicalBoard)
+            std, _, err = yield (canonicalBoard, False)    # unguarded in the reference (:108-113)
+            if std is None:
+                raise err
+            std_pi, std_v = std
             self.standard_predictions[s] = (std_pi, std_v)
         initial_value = self.standard_predictions[s][1]
 
         for _ in range(expand_by):
-            self.search(canonicalBoard)
+            yield from self.search_g(canonicalBoard)
 
         expanded_policy = np.zeros(A)
         for a, c in root_visits().items():
@@ -125,17 +171,23 @@ class MCTS:
         return self.expanded_nodes
 
     # ------------------------------------------------------------------ search
-    def _evaluate_leaf(self, s, board):
+    def _evaluate_leaf_g(self, s, board):
         """New leaf: NN priors masked by the valid moves and renormalised; returns the leaf
         value (MCTS.py:162-200).  Network errors degrade to uniform priors and value 0."""
         if s not in self.Vs:
             self.Vs[s] = self.game.getValidMoves(board, 1)
         valids = self.Vs[s]
+        use_gnn = self._use_gnn()
+        std, gnn, err = yield (board, use_gnn)
         try:
-            std_pi, std_v = self.nnet.predict(board)
+            if std is None:
+                raise err
+            std_pi, std_v = std
             self.standard_predictions[s] = (std_pi, std_v)
-            if self._use_gnn():
-                gnn_pi, gnn_v = self.nnet.predict_with_gnn(board)
+            if use_gnn:
+                if gnn is None:
+                    raise err
+                gnn_pi, gnn_v = gnn
                 self.gnn_predictions[s] = (gnn_pi, gnn_v)
                 self.Ps[s] = gnn_pi
             else:
@@ -174,7 +226,7 @@ class MCTS:
                 best_u, best_a = u, a
         return best_a
 
-    def search(self, canonicalBoard, expansion=False):
+    def search_g(self, canonicalBoard, expansion=False):
         path = []                     # (s, a) edges taken from the root
         board = canonicalBoard
         two_player = bool(getattr(self.game, "is_two_player", False))
@@ -189,7 +241,7 @@ class MCTS:
                 v = 0
                 break
             if s not in self.Ps:
-                v = self._evaluate_leaf(s, board)
+                v = yield from self._evaluate_leaf_g(s, board)
                 break
             a = self._select(s)
             if a == -1:

@@ -1,4 +1,7 @@
-"""Build libaz_hip.so in-tree with hipcc for gfx950 (no torch involved in the build).
+"""Build the two in-tree libraries (no torch involved in either build):
+
+    libaz_hip.so   hipcc --offload-arch=gfx950   the device kernels + C-ABI (include/az_hip.h)
+    libaz_mcts.so  g++ -fopenmp                  the native MCTS engine (include/az_mcts.h)
 
     python -m azhip.build          # from alphazero-gnn_amd/
 """
@@ -11,6 +14,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(HERE, "libaz_hip.so")
+HOST_OUT = os.path.join(HERE, "libaz_mcts.so")
+HOST_SOURCES = ["az_mcts.cpp"]
+# -ffp-contract=off: no FMA contraction, so the float64/float32 search arithmetic rounds
+# exactly like the reference's NumPy operations.
+HOST_FLAGS = ["-O3", "-fPIC", "-shared", "-std=c++17", "-fopenmp", "-ffp-contract=off",
+              "-Wall", "-Wl,-z,defs"]
 OBJ = os.path.join(CSRC, "build")
 SOURCES = ["az_runtime.hip", "az_gemm.hip", "az_trunk.hip", "az_gnn.hip", "az_optim.hip",
            "az_backward.hip"]
@@ -54,6 +63,22 @@ def build(verbose=True):
     return OUT
 
 
+def build_host(verbose=True):
+    srcs = [os.path.join(CSRC, f) for f in HOST_SOURCES]
+    deps = srcs + [os.path.join(os.path.dirname(PKG), "include", "az_mcts.h")]
+    if os.path.exists(HOST_OUT) and all(os.path.getmtime(HOST_OUT) >= os.path.getmtime(d)
+                                        for d in deps):
+        return HOST_OUT
+    cmd = ["g++"] + HOST_FLAGS + srcs + ["-o", HOST_OUT]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"g++ failed for libaz_mcts.so:\n{r.stderr}")
+    if verbose:
+        print(f"built {HOST_OUT}")
+    return HOST_OUT
+
+
 if __name__ == "__main__":
+    build_host()
     build()
     sys.exit(0)

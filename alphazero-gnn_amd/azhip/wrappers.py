@@ -117,12 +117,60 @@ class NetWrapper:
             if examples:
                 b, p, v = self._cnn_batch(examples)
                 self.train_seed += 1
-                T.cnn_step(self.nnet, b, p, v, lr, seed=self.train_seed)
+                if self._dp_world() > 1:
+                    self._cnn_step_allreduce(b, p, v, lr)
+                else:
+                    T.cnn_step(self.nnet, b, p, v, lr, seed=self.train_seed)
             if self.has_gnn and gnn_examples and len(gnn_examples) > 0:
                 b, p, v = self._gnn_batch(gnn_examples)
                 self.train_seed += 1
                 T.gnn_step(self.nnet, self.gnn, b, p, v, lr, seed=self.train_seed)
         torch.cuda.current_stream().synchronize()
+
+
+    def _dp_world(self):
+        """>1 when the CNN step is data-parallel over ranks (args.train_parallel ==
+        "allreduce" under torch.distributed); "replicas" (default) runs it whole everywhere."""
+        from . import dist as D
+        if nets._args_get(self.args, "train_parallel", "replicas") != "allreduce":
+            return 1
+        return D.world_rank()[0]
+
+    def _cnn_step_allreduce(self, b, p, v, lr):
+        """CNN step with the sampled rows split over ranks: each rank's loss is normalised by
+        the GLOBAL batch, the flat gradient is summed with one all_reduce (RCCL), then every
+        rank applies the identical Adam step.  The dropout mask is the global batch's mask
+        (same counter-based seed), sliced to this rank's rows."""
+        from . import dist as D
+        world, rank = D.world_rank()
+        Bg = b.shape[0]
+        r0, r1 = D.row_shard(Bg, world, rank)
+        F = self.nnet.feature_dim
+        drop = float(getattr(self.nnet, "dropout", 0.0)) \
+            if isinstance(self.nnet, nets.Connect4Net) else 0.0
+        mask = None
+        if drop > 0.0:
+            mask = ops.dropout_mask(Bg * F, drop, self.train_seed, self.device)[r0 * F:r1 * F]
+        P = self.nnet.params
+        if r1 > r0:
+            T.cnn_grads(self.nnet, b[r0:r1], p[r0:r1], v[r0:r1], seed=self.train_seed,
+                        drop_mask=mask, B_norm=Bg)
+        else:
+            P.grad_flat.zero_()
+        D.allreduce_sum_(P.grad_flat)
+        T.adam_step(self.nnet, lr)
+
+    def snapshot(self):
+        """Device copy of every parameter buffer (Coach's temp checkpoint, in memory)."""
+        snap = {"nnet": self.nnet.params.flat.clone()}
+        if self.has_gnn:
+            snap["gnn"] = self.gnn.params.flat.clone()
+        return snap
+
+    def restore(self, snap):
+        self.nnet.params.flat.copy_(snap["nnet"])
+        if self.has_gnn:
+            self.gnn.params.flat.copy_(snap["gnn"])
 
 
 class GNNWrapperMixin:

@@ -1,0 +1,661 @@
+// az_mcts.cpp — native lock-step MCTS engine (see include/az_mcts.h for the contract).
+//
+// One tree per game slot: an open-addressing table from the 128-bit board key (two 64-bit
+// occupancy masks, +1 and -1 stones) to nodes; per-node edge arrays (prior, visit count,
+// typed Q) are allocated when a node first becomes a leaf (Vs, MCTS.py:163-165).  A search is
+// a descent recorded as a path of (node, action) and backed up once its value is known
+// (terminal: immediately; new leaf: when the batched network result is fed back).
+//
+// Numeric parity with the reference (MCTS.py under NumPy 2 / NEP 50):
+//   Qsa  <- (Nsa * Qsa + v) / (Nsa + 1)    (:228-233) with Python-int / Python-float /
+//          np.float32 operands: int*f32 -> f32, float+f32 -> f32 (weak Python scalar cast to
+//          f32 first), int+float -> float, int/int -> float, f32/int -> f32;
+//   u    =  Q + cpuct * P[a] * sqrt(Ns) / (1 + Nsa)   or   cpuct * P[a] * sqrt(Ns + 1e-8)
+//          in float64, left to right (:202-216), strict '>' keeps the first maximum;
+//   P    =  float32 pi * int64 valids -> float64, divided by np.sum (pairwise summation).
+#include "../../include/az_mcts.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+// ----------------------------------------------------------------------------- typed values
+enum : uint8_t { T_INT = 0, T_F64 = 1, T_F32 = 2, T_NONE = 255 };
+
+struct Val {
+  double x;
+  uint8_t tag;
+};
+
+inline Val vint(double x) { return {x == 0.0 ? 0.0 : x, T_INT}; }   // Python int has no -0
+inline Val vneg(Val v) { return v.tag == T_INT ? vint(-v.x) : Val{-v.x, v.tag}; }
+
+inline Val mul_n(long n, Val q) {                 // Nsa * Qsa, Nsa a Python int
+  switch (q.tag) {
+    case T_INT: return vint((double)n * q.x);
+    case T_F64: return {(double)n * q.x, T_F64};
+    default: return {(double)((float)n * (float)q.x), T_F32};
+  }
+}
+
+inline Val add(Val a, Val b) {
+  if (a.tag == T_F32 || b.tag == T_F32) return {(double)((float)a.x + (float)b.x), T_F32};
+  if (a.tag == T_F64 || b.tag == T_F64) return {a.x + b.x, T_F64};
+  return vint(a.x + b.x);
+}
+
+inline Val div_n(Val s, long d) {                 // ... / (Nsa + 1)
+  if (s.tag == T_F32) return {(double)((float)s.x / (float)d), T_F32};
+  return {s.x / (double)d, T_F64};                // int / int -> float (true division)
+}
+
+// NumPy's pairwise summation (numpy/_core/src/umath/loops_utils.h.src), float64.
+double pairwise(const double* a, long n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (long i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    long i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  long n2 = n / 2;
+  n2 -= n2 % 8;
+  return pairwise(a, n2) + pairwise(a + n2, n - n2);
+}
+
+// ----------------------------------------------------------------------------- rules
+struct Key {
+  uint64_t p, q;   // bit i = cell i (i = x*n + y) holds +1 / -1
+  bool operator==(const Key& o) const { return p == o.p && q == o.q; }
+};
+
+inline uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+inline uint64_t khash(const Key& k) { return mix64(k.p ^ mix64(k.q)); }
+
+struct Rules {
+  int game = 0, n = 0, A = 0, cells = 0;
+  std::vector<uint64_t> lines;   // winning line masks
+  uint64_t top = 0;              // Connect4: cells (x, n-1)
+  uint64_t all = 0;
+
+  bool init(int g, int nn) {
+    if (nn < 1 || nn * nn > 64 || (g != AZM_GAME_CONNECT4 && g != AZM_GAME_TICTACTOE))
+      return false;
+    game = g;
+    n = nn;
+    cells = n * n;
+    all = cells == 64 ? ~0ull : ((1ull << cells) - 1);
+    auto bit = [&](int x, int y) { return 1ull << (x * n + y); };
+    if (g == AZM_GAME_CONNECT4) {
+      A = n + 1;
+      int w = n < 4 ? n : 4;                     // min(4, n) in a row (Connect4Game.py:67-99)
+      for (int x = 0; x < n; ++x) top |= bit(x, n - 1);
+      const int dirs[4][2] = {{1, 0}, {0, 1}, {1, 1}, {1, -1}};
+      for (auto& d : dirs)
+        for (int x = 0; x < n; ++x)
+          for (int y = 0; y < n; ++y) {
+            int ex = x + d[0] * (w - 1), ey = y + d[1] * (w - 1);
+            if (ex < 0 || ex >= n || ey < 0 || ey >= n) continue;
+            uint64_t m = 0;
+            for (int i = 0; i < w; ++i) m |= bit(x + d[0] * i, y + d[1] * i);
+            lines.push_back(m);
+          }
+    } else {
+      A = n * n + 1;                              // full rows, columns, two diagonals
+      for (int j = 0; j < n; ++j) {
+        uint64_t c = 0, r = 0;
+        for (int i = 0; i < n; ++i) {
+          c |= bit(i, j);
+          r |= bit(j, i);
+        }
+        lines.push_back(c);
+        lines.push_back(r);
+      }
+      uint64_t d1 = 0, d2 = 0;
+      for (int i = 0; i < n; ++i) {
+        d1 |= bit(i, i);
+        d2 |= bit(i, n - 1 - i);
+      }
+      lines.push_back(d1);
+      lines.push_back(d2);
+    }
+    return true;
+  }
+
+  bool run(uint64_t m) const {
+    for (uint64_t l : lines)
+      if ((m & l) == l) return true;
+    return false;
+  }
+
+  // getGameEnded(board, 1) (Connect4Game.py:169-183, TicTacToeGame.py:60-107)
+  Val ended(const Key& k) const {
+    if (run(k.p)) return vint(1);
+    if (run(k.q)) return vint(-1);
+    uint64_t occ = k.p | k.q;
+    if (game == AZM_GAME_CONNECT4) {
+      if ((occ & top) != top) return vint(0);
+    } else if ((occ & all) != all) {
+      return vint(0);
+    }
+    return {1e-4, T_F64};
+  }
+
+  // getValidMoves(board, 1) (Connect4Game.py:154-167, TicTacToeGame.py:44-58)
+  void valids(const Key& k, uint8_t* v) const {
+    uint64_t occ = k.p | k.q;
+    bool any = false;
+    if (game == AZM_GAME_CONNECT4) {
+      for (int x = 0; x < n; ++x) {
+        v[x] = !((occ >> (x * n + n - 1)) & 1);
+        any |= v[x];
+      }
+    } else {
+      for (int i = 0; i < cells; ++i) {
+        v[i] = !((occ >> i) & 1);
+        any |= v[i];
+      }
+    }
+    v[A - 1] = !any;
+  }
+
+  // getCanonicalForm(getNextState(board, 1, a), -1): the mover's stone is +1, then the
+  // board is negated for the opponent.  Pass (the last action) only negates.
+  bool next(const Key& k, int a, Key* out) const {
+    if (a == A - 1) {
+      *out = {k.q, k.p};
+      return true;
+    }
+    uint64_t occ = k.p | k.q, b;
+    if (game == AZM_GAME_CONNECT4) {
+      uint64_t col = ((occ >> (a * n)) & ((1ull << n) - 1));
+      uint64_t free_ = ~col & ((1ull << n) - 1);
+      if (!free_) return false;                  // "Column is full!" (Connect4Game.py:149)
+      b = 1ull << (a * n + __builtin_ctzll(free_));
+    } else {
+      b = 1ull << a;
+      if (occ & b) return false;
+    }
+    *out = {k.q, k.p | b};
+    return true;
+  }
+
+  bool from_board(const int8_t* s, Key* k) const {
+    k->p = k->q = 0;
+    for (int i = 0; i < cells; ++i) {
+      if (s[i] == 1) k->p |= 1ull << i;
+      else if (s[i] == -1) k->q |= 1ull << i;
+      else if (s[i] != 0) return false;
+    }
+    return true;
+  }
+
+  void to_board(const Key& k, int8_t* s) const {
+    for (int i = 0; i < cells; ++i)
+      s[i] = (int8_t)(((k.p >> i) & 1) ? 1 : (((k.q >> i) & 1) ? -1 : 0));
+  }
+};
+
+// ----------------------------------------------------------------------------- trees
+struct Node {
+  Key key;
+  Val es;            // Es[s]
+  int32_t edge;      // offset / A into the edge pools; -1 until Vs[s] exists
+  int32_t ns;        // Ns[s] (valid when has_ns)
+  int32_t std_epoch; // standard_predictions epoch holding std_v
+  float std_v;
+  uint8_t has_ns, expanded;
+};
+
+struct Tree {
+  std::vector<Node> nodes;
+  std::vector<int32_t> table;   // open addressing, -1 = empty
+  uint64_t mask = 0;
+  // edge pools, A entries per allocated node
+  std::vector<double> P;
+  std::vector<int32_t> N;
+  std::vector<Val> Q;
+  std::vector<uint8_t> V;
+  int32_t edges = 0;
+  int32_t epoch = 1;
+  // search state
+  Key root{0, 0};
+  int remaining = 0;
+  int pending_leaf = -1;                      // node waiting for the network
+  std::vector<std::pair<int32_t, int32_t>> path;
+  int64_t nsa_total = 0, ps_count = 0;
+
+  void clear() {
+    nodes.clear();
+    table.assign(1024, -1);
+    mask = 1023;
+    P.clear();
+    N.clear();
+    Q.clear();
+    V.clear();
+    edges = 0;
+    epoch = 1;
+    remaining = 0;
+    pending_leaf = -1;
+    path.clear();
+    nsa_total = ps_count = 0;
+  }
+
+  int32_t find(const Key& k) const {
+    if (table.empty()) return -1;
+    for (uint64_t h = khash(k) & mask;; h = (h + 1) & mask) {
+      int32_t i = table[h];
+      if (i < 0) return -1;
+      if (nodes[i].key == k) return i;
+    }
+  }
+
+  void grow() {
+    std::vector<int32_t> t(table.size() * 2, -1);
+    uint64_t m = t.size() - 1;
+    for (int32_t i = 0; i < (int32_t)nodes.size(); ++i) {
+      uint64_t h = khash(nodes[i].key) & m;
+      while (t[h] >= 0) h = (h + 1) & m;
+      t[h] = i;
+    }
+    table.swap(t);
+    mask = m;
+  }
+
+  int32_t find_or_add(const Key& k, const Rules& R) {
+    if (table.empty()) clear();
+    uint64_t h = khash(k) & mask;
+    for (;; h = (h + 1) & mask) {
+      int32_t i = table[h];
+      if (i < 0) break;
+      if (nodes[i].key == k) return i;
+    }
+    Node nd;
+    nd.key = k;
+    nd.es = R.ended(k);                          // Es[s] on first visit (MCTS.py:152-153)
+    nd.edge = -1;
+    nd.ns = 0;
+    nd.std_epoch = 0;
+    nd.std_v = 0.f;
+    nd.has_ns = nd.expanded = 0;
+    int32_t id = (int32_t)nodes.size();
+    nodes.push_back(nd);
+    table[h] = id;
+    if ((uint64_t)nodes.size() * 2 > table.size()) grow();
+    return id;
+  }
+
+  void alloc_edges(int32_t id, const Rules& R) {
+    Node& nd = nodes[id];
+    if (nd.edge >= 0) return;
+    nd.edge = edges++;
+    size_t A = R.A;
+    P.resize(P.size() + A, 0.0);
+    N.resize(N.size() + A, 0);
+    Q.resize(Q.size() + A, Val{0.0, T_NONE});
+    V.resize(V.size() + A, 0);
+    R.valids(nd.key, &V[(size_t)nd.edge * A]);
+  }
+};
+
+}  // namespace
+
+struct az_mcts {
+  Rules R;
+  double cpuct = 1.0;
+  int use_gnn = 0;
+  std::vector<Tree> trees;
+  std::vector<int32_t> last_order;             // slots of the last collect, in output order
+  std::vector<int8_t> leafbuf;
+};
+
+namespace {
+
+bool slot_ok(const az_mcts* m, int s) { return m && s >= 0 && s < (int)m->trees.size(); }
+
+// UCB selection (MCTS.py:202-218); -1 when no valid action.
+int select_action(const az_mcts* m, const Tree& t, const Node& nd) {
+  const int A = m->R.A;
+  const size_t o = (size_t)nd.edge * A;
+  const double sq = std::sqrt((double)nd.ns);
+  const double sq_eps = std::sqrt((double)nd.ns + 1e-8);
+  double best = -INFINITY;
+  int ba = -1;
+  for (int a = 0; a < A; ++a) {
+    if (!t.V[o + a]) continue;
+    const Val& q = t.Q[o + a];
+    double u;
+    if (q.tag != T_NONE)
+      u = q.x + m->cpuct * t.P[o + a] * sq / (double)(1 + t.N[o + a]);
+    else
+      u = m->cpuct * t.P[o + a] * sq_eps;
+    if (u > best) {
+      best = u;
+      ba = a;
+    }
+  }
+  return ba;
+}
+
+void backup(az_mcts* m, Tree& t, Val v) {
+  const int A = m->R.A;
+  for (size_t i = t.path.size(); i-- > 0;) {
+    Node& nd = t.nodes[t.path[i].first];
+    int a = t.path[i].second;
+    size_t e = (size_t)nd.edge * A + a;
+    Val& q = t.Q[e];
+    if (q.tag != T_NONE) {
+      q = div_n(add(mul_n(t.N[e], q), v), (long)t.N[e] + 1);
+      t.N[e] += 1;
+    } else {
+      q = v;
+      t.N[e] = 1;
+    }
+    t.nsa_total += 1;
+    nd.ns += 1;
+    v = vneg(v);                                 // two-player games (MCTS.py:236-240)
+  }
+  t.path.clear();
+}
+
+// Run searches of one slot until it waits on a leaf (returns 1) or has none left (0).
+int advance(az_mcts* m, Tree& t) {
+  while (t.remaining > 0 && t.pending_leaf < 0) {
+    t.path.clear();
+    Key k = t.root;
+    Val v;
+    for (;;) {
+      int32_t id = t.find_or_add(k, m->R);
+      Node& nd = t.nodes[id];
+      if (nd.es.x != 0.0) {                      // terminal (MCTS.py:152-157)
+        v = nd.es;
+        break;
+      }
+      if (!nd.expanded) {                        // new leaf: Vs, then the network
+        t.alloc_edges(id, m->R);
+        t.pending_leaf = id;
+        return 1;
+      }
+      int a = select_action(m, t, nd);
+      if (a < 0) {                               // MCTS.py:220-221
+        v = vint(0);
+        break;
+      }
+      t.path.emplace_back(id, a);
+      Key nk;
+      m->R.next(t.nodes[id].key, a, &nk);
+      k = nk;
+    }
+    backup(m, t, v);
+    t.remaining -= 1;
+  }
+  return 0;
+}
+
+// Expand the pending leaf with one network row and back its value up (MCTS.py:162-200).
+void expand(az_mcts* m, Tree& t, const float* pi, float v_std, const float* gpi, float gv,
+            bool failed) {
+  const int A = m->R.A;
+  Node& nd = t.nodes[t.pending_leaf];
+  const size_t o = (size_t)nd.edge * A;
+  double* P = &t.P[o];
+  const uint8_t* V = &t.V[o];
+  Val v;
+  auto uniform = [&]() {
+    long cnt = 0;
+    for (int a = 0; a < A; ++a) cnt += V[a];
+    for (int a = 0; a < A; ++a) P[a] = (double)V[a] / (double)cnt;
+  };
+  if (failed) {
+    uniform();
+    v = vint(0);
+  } else {
+    nd.std_v = v_std;                            // standard_predictions[s] = (pi, v)
+    nd.std_epoch = t.epoch;
+    const float* src = m->use_gnn ? gpi : pi;
+    for (int a = 0; a < A; ++a) P[a] = (double)src[a] * (double)V[a];
+    double s = pairwise(P, A);
+    if (s > 0) {
+      for (int a = 0; a < A; ++a) P[a] /= s;
+    } else {
+      uniform();                                 // "All valid moves were masked"
+    }
+    v = {(double)(m->use_gnn ? gv : v_std), T_F32};
+  }
+  nd.expanded = 1;
+  nd.has_ns = 1;
+  nd.ns = 0;
+  t.ps_count += 1;
+  t.pending_leaf = -1;
+  backup(m, t, v);
+  t.remaining -= 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* az_mcts_last_error(void) { return g_err.c_str(); }
+
+az_mcts* az_mcts_create(int game, int n, int slots, double cpuct, int use_gnn) {
+  if (slots < 1) {
+    fail(AZM_EINVAL, "az_mcts_create: slots must be >= 1");
+    return nullptr;
+  }
+  az_mcts* m = new az_mcts();
+  if (!m->R.init(game, n)) {
+    delete m;
+    fail(AZM_EINVAL, "az_mcts_create: unsupported game / board size (n*n must be <= 64)");
+    return nullptr;
+  }
+  m->cpuct = cpuct;
+  m->use_gnn = use_gnn;
+  m->trees.resize(slots);
+  for (auto& t : m->trees) t.clear();
+  m->leafbuf.resize((size_t)slots * m->R.cells);
+  return m;
+}
+
+void az_mcts_destroy(az_mcts* m) { delete m; }
+
+int az_mcts_action_size(const az_mcts* m) { return m ? m->R.A : AZM_EINVAL; }
+
+int az_mcts_reset(az_mcts* m, int slot) {
+  if (!slot_ok(m, slot)) return fail(AZM_EINVAL, "az_mcts_reset: bad slot");
+  m->trees[slot].clear();
+  return AZM_OK;
+}
+
+int az_mcts_clear_predictions(az_mcts* m, int slot) {
+  if (!slot_ok(m, slot)) return fail(AZM_EINVAL, "az_mcts_clear_predictions: bad slot");
+  m->trees[slot].epoch += 1;
+  return AZM_OK;
+}
+
+int az_mcts_begin(az_mcts* m, int slot, const int8_t* board, int sims) {
+  if (!slot_ok(m, slot) || !board || sims < 0) return fail(AZM_EINVAL, "az_mcts_begin: bad args");
+  Tree& t = m->trees[slot];
+  if (t.remaining > 0 || t.pending_leaf >= 0)
+    return fail(AZM_ESTATE, "az_mcts_begin: slot still has searches queued");
+  Key k;
+  if (!m->R.from_board(board, &k)) return fail(AZM_EINVAL, "az_mcts_begin: cells must be -1/0/1");
+  t.root = k;
+  t.remaining = sims;
+  return AZM_OK;
+}
+
+int az_mcts_remaining(const az_mcts* m, int slot) {
+  if (!slot_ok(m, slot)) return fail(AZM_EINVAL, "az_mcts_remaining: bad slot");
+  return m->trees[slot].remaining;
+}
+
+int az_mcts_remaining_all(const az_mcts* m, int32_t* out) {
+  if (!m || !out) return fail(AZM_EINVAL, "az_mcts_remaining_all: bad args");
+  for (size_t s = 0; s < m->trees.size(); ++s) out[s] = m->trees[s].remaining;
+  return AZM_OK;
+}
+
+int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int threads) {
+  if (!m || !boards || !slots || cap < 0) return fail(AZM_EINVAL, "az_mcts_collect: bad args");
+  for (auto& t : m->trees)
+    if (t.pending_leaf >= 0 && !m->last_order.empty())
+      return fail(AZM_ESTATE, "az_mcts_collect: the previous leaves were not fed");
+  const int S = (int)m->trees.size();
+  std::vector<uint8_t> has(S, 0);
+  if (threads < 1) threads = 1;
+#pragma omp parallel for schedule(dynamic, 8) num_threads(threads)
+  for (int s = 0; s < S; ++s) {
+    Tree& t = m->trees[s];
+    if (t.pending_leaf < 0) advance(m, t);
+    if (t.pending_leaf >= 0) {
+      has[s] = 1;
+      m->R.to_board(t.nodes[t.pending_leaf].key, &m->leafbuf[(size_t)s * m->R.cells]);
+    }
+  }
+  m->last_order.clear();
+  int cnt = 0;
+  for (int s = 0; s < S; ++s) {
+    if (!has[s]) continue;
+    if (cnt >= cap) return fail(AZM_EINVAL, "az_mcts_collect: cap smaller than the live slots");
+    std::memcpy(boards + (size_t)cnt * m->R.cells, &m->leafbuf[(size_t)s * m->R.cells],
+                m->R.cells);
+    slots[cnt++] = s;
+    m->last_order.push_back(s);
+  }
+  return cnt;
+}
+
+int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const float* gpi,
+                 const float* gv, int failed) {
+  if (!m || count != (int)m->last_order.size())
+    return fail(AZM_EINVAL, "az_mcts_feed: count differs from the last collect");
+  if (!failed && (!pi || !v || (m->use_gnn && (!gpi || !gv))))
+    return fail(AZM_EINVAL, "az_mcts_feed: missing network outputs");
+  const int A = m->R.A;
+  for (int i = 0; i < count; ++i) {
+    Tree& t = m->trees[m->last_order[i]];
+    if (t.pending_leaf < 0) return fail(AZM_ESTATE, "az_mcts_feed: slot has no pending leaf");
+    expand(m, t, failed ? nullptr : pi + (size_t)i * A, failed ? 0.f : v[i],
+           (failed || !m->use_gnn) ? nullptr : gpi + (size_t)i * A,
+           (failed || !m->use_gnn) ? 0.f : gv[i], failed != 0);
+  }
+  m->last_order.clear();
+  return AZM_OK;
+}
+
+int az_mcts_root_edges(const az_mcts* m, int slot, const int8_t* board, int32_t* nsa, double* q,
+                       int8_t* qtag) {
+  if (!slot_ok(m, slot) || !board) return fail(AZM_EINVAL, "az_mcts_root_edges: bad args");
+  const Tree& t = m->trees[slot];
+  Key k;
+  if (!m->R.from_board(board, &k)) return fail(AZM_EINVAL, "az_mcts_root_edges: bad board");
+  const int A = m->R.A;
+  int32_t id = t.find(k);
+  for (int a = 0; a < A; ++a) {
+    nsa[a] = 0;
+    q[a] = 0.0;
+    qtag[a] = AZM_TAG_NONE;
+  }
+  if (id < 0 || t.nodes[id].edge < 0) return AZM_OK;
+  size_t o = (size_t)t.nodes[id].edge * A;
+  for (int a = 0; a < A; ++a) {
+    const Val& v = t.Q[o + a];
+    if (v.tag == T_NONE) continue;
+    nsa[a] = t.N[o + a];
+    q[a] = v.x;
+    qtag[a] = v.tag == T_INT ? AZM_TAG_INT : (v.tag == T_F64 ? AZM_TAG_FLOAT : AZM_TAG_F32);
+  }
+  return AZM_OK;
+}
+
+int az_mcts_get_std(const az_mcts* m, int slot, const int8_t* board, float* v) {
+  if (!slot_ok(m, slot) || !board || !v) return fail(AZM_EINVAL, "az_mcts_get_std: bad args");
+  const Tree& t = m->trees[slot];
+  Key k;
+  if (!m->R.from_board(board, &k)) return fail(AZM_EINVAL, "az_mcts_get_std: bad board");
+  int32_t id = t.find(k);
+  if (id < 0 || t.nodes[id].std_epoch != t.epoch) return 0;
+  *v = t.nodes[id].std_v;
+  return 1;
+}
+
+int az_mcts_set_std(az_mcts* m, int slot, const int8_t* board, float v) {
+  if (!slot_ok(m, slot) || !board) return fail(AZM_EINVAL, "az_mcts_set_std: bad args");
+  Tree& t = m->trees[slot];
+  Key k;
+  if (!m->R.from_board(board, &k)) return fail(AZM_EINVAL, "az_mcts_set_std: bad board");
+  Node& nd = t.nodes[t.find_or_add(k, m->R)];
+  nd.std_v = v;
+  nd.std_epoch = t.epoch;
+  return AZM_OK;
+}
+
+int az_mcts_tree_stats(const az_mcts* m, int slot, int64_t* out) {
+  if (!slot_ok(m, slot) || !out) return fail(AZM_EINVAL, "az_mcts_tree_stats: bad args");
+  const Tree& t = m->trees[slot];
+  int64_t ns = 0;
+  for (const auto& nd : t.nodes) ns += nd.has_ns;
+  out[0] = (int64_t)t.nodes.size();
+  out[1] = ns;
+  out[2] = t.ps_count;
+  out[3] = t.nsa_total;
+  return AZM_OK;
+}
+
+int az_game_ended(int game, int n, const int8_t* board, int* tag, double* value) {
+  Rules R;
+  Key k;
+  if (!R.init(game, n) || !R.from_board(board, &k)) return fail(AZM_EINVAL, "az_game_ended");
+  Val v = R.ended(k);
+  *tag = v.tag == T_INT ? AZM_TAG_INT : AZM_TAG_FLOAT;
+  *value = v.x;
+  return AZM_OK;
+}
+
+int az_game_valids(int game, int n, const int8_t* board, int8_t* valids) {
+  Rules R;
+  Key k;
+  if (!R.init(game, n) || !R.from_board(board, &k)) return fail(AZM_EINVAL, "az_game_valids");
+  std::vector<uint8_t> v(R.A);
+  R.valids(k, v.data());
+  for (int a = 0; a < R.A; ++a) valids[a] = (int8_t)v[a];
+  return AZM_OK;
+}
+
+int az_game_next_canonical(int game, int n, const int8_t* board, int action, int8_t* out) {
+  Rules R;
+  Key k, nk;
+  if (!R.init(game, n) || !R.from_board(board, &k) || action < 0 || action >= R.A)
+    return fail(AZM_EINVAL, "az_game_next_canonical: bad args");
+  if (!R.next(k, action, &nk)) return fail(AZM_EINVAL, "az_game_next_canonical: illegal move");
+  R.to_board(nk, out);
+  return AZM_OK;
+}
+
+double az_np_pairwise_sum(const double* a, int n) { return pairwise(a, n); }
+
+}  // extern "C"

@@ -1,0 +1,273 @@
+"""Native MCTS (libaz_mcts.so, include/az_mcts.h) behind the reference's MCTS interface.
+
+`Engine` binds the C-ABI with ctypes.  `NativeMCTS` is one game slot of an engine, with the
+generator methods `getActionProb_g` / `expand_tree_g` that Coach.episode_g drives, so the
+episode logic (temperature, sampling, symmetries, GNN targets) is the same Python code as the
+sequential path, while the searches (MCTS.py:151-240) and the rules they call run natively
+for every slot at once.  The generators yield
+
+    ("search", board_int8, sims)   run `sims` searches from this root (engine-side)
+    ("predict", board_int64)       the root's standard prediction (MCTS.py:108-113)
+
+and selfplay.play_episodes_native serves both kinds for all slots with one batched network
+call per round.  Q values come back with their Python type (int / float / np.float32), so the
+root statistics and everything computed from them are the reference's bit for bit
+(tests/test_native_mcts.py).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+EPS = 1e-8
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "azhip", "libaz_mcts.so")
+
+GAME_CONNECT4, GAME_TICTACTOE = 0, 1
+TAG_NONE, TAG_INT, TAG_FLOAT, TAG_F32 = -1, 0, 1, 2
+
+_lib = None
+
+_P = ctypes.c_void_p
+_SIGS = {
+    "az_mcts_last_error": (ctypes.c_char_p, []),
+    "az_mcts_create": (_P, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                            ctypes.c_int]),
+    "az_mcts_destroy": (None, [_P]),
+    "az_mcts_action_size": (ctypes.c_int, [_P]),
+    "az_mcts_reset": (ctypes.c_int, [_P, ctypes.c_int]),
+    "az_mcts_clear_predictions": (ctypes.c_int, [_P, ctypes.c_int]),
+    "az_mcts_begin": (ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.c_int]),
+    "az_mcts_remaining": (ctypes.c_int, [_P, ctypes.c_int]),
+    "az_mcts_remaining_all": (ctypes.c_int, [_P, _P]),
+    "az_mcts_collect": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, ctypes.c_int]),
+    "az_mcts_feed": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int]),
+    "az_mcts_root_edges": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P]),
+    "az_mcts_get_std": (ctypes.c_int, [_P, ctypes.c_int, _P, _P]),
+    "az_mcts_set_std": (ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.c_float]),
+    "az_mcts_tree_stats": (ctypes.c_int, [_P, ctypes.c_int, _P]),
+    "az_game_ended": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _P, _P]),
+    "az_game_valids": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _P]),
+    "az_game_next_canonical": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, _P]),
+    "az_np_pairwise_sum": (ctypes.c_double, [_P, ctypes.c_int]),
+}
+
+
+def lib():
+    """The engine library (built by __graft_entry__.build() / azhip.build.build_host())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run `python -m azhip.build` (or "
+                               "__graft_entry__.build()) first")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data        # a plain int is accepted for a c_void_p argument
+
+
+def _check(rc, what):
+    if rc < 0:
+        raise RuntimeError(f"{what}: {lib().az_mcts_last_error().decode()}")
+    return rc
+
+
+def game_kind(game):
+    """(engine game id, n) for the two registered games; ValueError for anything else."""
+    name = type(game).__name__
+    if name == "Connect4Game":
+        return GAME_CONNECT4, int(game.board_size)
+    if name == "TicTacToeGame":
+        return GAME_TICTACTOE, int(game.n)
+    raise ValueError(f"native MCTS supports Connect4Game / TicTacToeGame, not {name}")
+
+
+def typed_q(tag, x):
+    """The Python object the reference's Qsa holds."""
+    if tag == TAG_INT:
+        return int(x)
+    if tag == TAG_FLOAT:
+        return float(x)
+    return np.float32(x)
+
+
+class Engine:
+    """One libaz_mcts engine: `slots` concurrent game trees of one game kind."""
+
+    def __init__(self, game, slots, cpuct, use_gnn):
+        self.kind, self.n = game_kind(game)
+        self.cells = self.n * self.n
+        self.slots = slots
+        self.use_gnn = bool(use_gnn)
+        h = lib().az_mcts_create(self.kind, self.n, slots, float(cpuct), int(self.use_gnn))
+        if not h:
+            raise RuntimeError("az_mcts_create: " + lib().az_mcts_last_error().decode())
+        self.h = ctypes.c_void_p(h)
+        self.A = lib().az_mcts_action_size(self.h)
+        self.leaf_boards = np.zeros((slots, self.n, self.n), np.int8)
+        self.leaf_slots = np.zeros(slots, np.int32)
+        self._rem = np.zeros(slots, np.int32)
+        self._nsa = np.zeros(self.A, np.int32)
+        self._q = np.zeros(self.A, np.float64)
+        self._tag = np.zeros(self.A, np.int8)
+        self._b = np.zeros((self.n, self.n), np.int8)
+        self._pb, self._ps, self._pr = (_ptr(self.leaf_boards), _ptr(self.leaf_slots),
+                                        _ptr(self._rem))
+        self._pn, self._pq, self._pt, self._pbb = (_ptr(self._nsa), _ptr(self._q),
+                                                   _ptr(self._tag), _ptr(self._b))
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and _lib is not None:
+            _lib.az_mcts_destroy(h)
+            self.h = None
+
+    @staticmethod
+    def _b8(board):
+        return np.ascontiguousarray(board, dtype=np.int8)
+
+    def _bp(self, board):
+        """Pointer to an int8 copy of `board` in a reused buffer."""
+        self._b[...] = board
+        return self._pbb
+
+    def reset(self, slot):
+        _check(lib().az_mcts_reset(self.h, slot), "az_mcts_reset")
+
+    def clear_predictions(self, slot):
+        _check(lib().az_mcts_clear_predictions(self.h, slot), "az_mcts_clear_predictions")
+
+    def begin(self, slot, board, sims):
+        b = self._b8(board)
+        _check(lib().az_mcts_begin(self.h, slot, _ptr(b), int(sims)), "az_mcts_begin")
+
+    def remaining(self, slot):
+        return _check(lib().az_mcts_remaining(self.h, slot), "az_mcts_remaining")
+
+    def remaining_all(self):
+        """int32 [slots] view (overwritten by the next call)."""
+        _check(lib().az_mcts_remaining_all(self.h, self._pr), "az_mcts_remaining_all")
+        return self._rem
+
+    def collect(self, threads=1):
+        """-> number of leaves; boards in self.leaf_boards[:k], slots in self.leaf_slots[:k]."""
+        return _check(lib().az_mcts_collect(self.h, self._pb, self._ps, self.slots,
+                                            int(threads)), "az_mcts_collect")
+
+    def feed(self, k, pi=None, v=None, gpi=None, gv=None, failed=False):
+        arrs = [None if a is None else np.ascontiguousarray(a[:k], dtype=np.float32)
+                for a in (pi, v, gpi, gv)]
+        ptrs = [None if a is None else _ptr(a) for a in arrs]
+        _check(lib().az_mcts_feed(self.h, int(k), *ptrs, int(bool(failed))), "az_mcts_feed")
+
+    def root_edges(self, slot, board):
+        """-> (nsa list[int], q list[float64], tags list[int])."""
+        _check(lib().az_mcts_root_edges(self.h, slot, self._bp(board), self._pn, self._pq,
+                                        self._pt), "az_mcts_root_edges")
+        return self._nsa.tolist(), self._q.tolist(), self._tag.tolist()
+
+    def get_std(self, slot, board):
+        b = self._b8(board)
+        v = np.zeros(1, np.float32)
+        r = _check(lib().az_mcts_get_std(self.h, slot, _ptr(b), _ptr(v)), "az_mcts_get_std")
+        return v[0] if r == 1 else None
+
+    def set_std(self, slot, board, v):
+        b = self._b8(board)
+        _check(lib().az_mcts_set_std(self.h, slot, _ptr(b), float(v)), "az_mcts_set_std")
+
+    def tree_stats(self, slot):
+        out = np.zeros(4, np.int64)
+        _check(lib().az_mcts_tree_stats(self.h, slot, _ptr(out)), "az_mcts_tree_stats")
+        return {"Es": int(out[0]), "Ns": int(out[1]), "Ps": int(out[2]), "nsa_total": int(out[3])}
+
+
+class NativeMCTS:
+    """One slot of an Engine with the reference MCTS's root-level logic (MCTS.py:29-149)."""
+
+    def __init__(self, engine, slot, game, args, rng=None):
+        self.engine, self.slot, self.game, self.args = engine, slot, game, args
+        self.rng = rng
+
+    def _choice(self, *a, **k):
+        return (np.random if self.rng is None else self.rng).choice(*a, **k)
+
+    def _root(self, board):
+        nsa, q, tag = self.engine.root_edges(self.slot, board)
+        return nsa, q, tag
+
+    def getActionProb_g(self, canonicalBoard, temp=1):
+        """MCTS.py:29-58 (the searches run in the engine)."""
+        self.engine.clear_predictions(self.slot)
+        yield ("search", canonicalBoard, self.args.numMCTSSims)
+        counts = self._root(canonicalBoard)[0]
+        if temp == 0:
+            best = np.array(np.argwhere(counts == np.max(counts))).flatten()
+            a = self._choice(best)
+            probs = [0] * len(counts)
+            probs[a] = 1
+            return probs
+        counts = [(x + EPS) ** (1. / temp) for x in counts]
+        total = float(sum(counts))
+        if total <= 0:
+            valids = self.game.getValidMoves(canonicalBoard, 1)
+            if np.sum(valids) > 0:
+                return valids / np.sum(valids)
+            return np.ones(len(counts)) / len(counts)
+        return [x / total for x in counts]
+
+    def expand_tree_g(self, canonicalBoard, expand_by=5):
+        """MCTS.py:60-149."""
+        s = self.game.stringRepresentation(canonicalBoard)
+        A = self.game.getActionSize()
+
+        def root_visits():
+            nsa, _, tag = self._root(canonicalBoard)
+            return {a: nsa[a] for a in range(A) if tag[a] != TAG_NONE}
+
+        initial_counts = root_visits()
+        if not initial_counts:
+            yield ("search", canonicalBoard, self.args.numMCTSSims)
+            initial_counts = root_visits()
+        initial_policy = np.zeros(A)
+        for a, c in initial_counts.items():
+            initial_policy[a] = c
+        isum = np.sum(initial_policy)
+        if isum > 0:
+            initial_policy = initial_policy / isum
+        else:
+            valids = self.game.getValidMoves(canonicalBoard, 1)
+            initial_policy = valids / np.sum(valids)
+
+        initial_value = self.engine.get_std(self.slot, canonicalBoard)
+        if initial_value is None:
+            _, std_v = yield ("predict", canonicalBoard)
+            self.engine.set_std(self.slot, canonicalBoard, std_v)
+            initial_value = np.float32(std_v)
+
+        yield ("search", canonicalBoard, expand_by)
+
+        nsa, q, tag = self._root(canonicalBoard)
+        expanded_policy = np.zeros(A)
+        for a in range(A):
+            if tag[a] != TAG_NONE:
+                expanded_policy[a] = nsa[a]
+        esum = np.sum(expanded_policy)
+        if esum > 0:
+            expanded_policy = expanded_policy / esum
+        else:
+            expanded_policy = initial_policy
+        expanded_value = 0
+        valid_count = 0
+        for a in range(A):
+            if tag[a] != TAG_NONE and nsa[a] > 0:
+                expanded_value += typed_q(tag[a], q[a]) * nsa[a]
+                valid_count += nsa[a]
+        expanded_value = expanded_value / valid_count if valid_count > 0 else initial_value
+        return {s: (initial_policy, initial_value, expanded_policy, expanded_value)}

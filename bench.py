@@ -39,6 +39,11 @@ def parse():
                     help="bounded CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-aggregate", action="store_true")
+    ap.add_argument("--no-selfplay", action="store_true")
+    ap.add_argument("--sp-games", type=int, default=256,
+                    help="self-play leg: games per GPU, all played in lock step")
+    ap.add_argument("--sp-sims", type=int, default=100, help="numMCTSSims (SURVEY §8d config 3)")
+    ap.add_argument("--sp-threads", type=int, default=16, help="host threads for the engine")
     return ap.parse_args()
 
 
@@ -104,6 +109,92 @@ def aggregate_roofline(torch, ops, device, graphs=512):
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
             "traffic": None, "avg_launch_us": round(ms * 1e3, 2),
             "workload": f"{graphs} 32x32 grids, V={V}, E={E}, F=64 (config-5 shard per GPU)"}
+
+
+def selfplay_args(sims):
+    """Connect4 config 3: connect4/config.yaml + --use_gnn --numMCTSSims 100."""
+    from types import SimpleNamespace
+    return SimpleNamespace(numMCTSSims=sims, cpuct=1.0, tempThreshold=15, use_gnn=True,
+                           expand_by=5, dropout=0.3, gnn_layers=2)
+
+
+def selfplay_leg(W, G, args, device, rank):
+    """Self-play games/s: `sp_games` Connect4 GNN games per GPU played in lock step (native
+    MCTS engine on the host, one batched predict_both per round on the GPU)."""
+    import torch
+    from connect4.Connect4GNN import Connect4GNNWrapper
+    from connect4.Connect4Game import Connect4Game
+    from selfplay import play_episodes_native
+    sa = selfplay_args(args.sp_sims)
+    net = Connect4GNNWrapper(Connect4Game(7), sa)
+    net.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()})
+    net.gnn.load_state_dict({k: torch.from_numpy(v) for k, v in G.items()})
+    eps = list(range(rank * args.sp_games, (rank + 1) * args.sp_games))
+    seeds = {e: 12345 + e for e in eps}
+    play_episodes_native(Connect4Game(7), net, selfplay_args(2), eps[:8], seeds, 8,
+                         threads=args.sp_threads)                       # warm-up
+    st = {}
+    t0 = time.perf_counter()
+    out = play_episodes_native(Connect4Game(7), net, sa, eps, seeds, args.sp_games,
+                               threads=args.sp_threads, stats=st)
+    dt = time.perf_counter() - t0
+    moves = sum(len(std) // 2 for std, _ in out.values())
+    return dt, {"games": len(out), "moves": moves, "evals": st["rows"], "rounds": st["rounds"],
+                "net_s": round(st["net_s"], 3), "host_s": round(st["host_s"], 3)}
+
+
+def selfplay_cpu_baseline(W, G, sims, seconds):
+    """The reference's sequential loop (Coach.executeEpisode over the Python MCTS, batch-1
+    predict + predict_with_gnn per new leaf) with the numpy fp32 oracle as the network, on
+    the host: games/s from the games (and the fraction of one) finished in `seconds`."""
+    import Coach as C
+    import MCTS as M
+    from connect4.Connect4Game import Connect4Game
+    from oracle import nets as O
+    f = np.float32
+    W32 = {k: np.asarray(v, f) for k, v in W.items()}
+    G32 = {k: np.asarray(v, f) for k, v in G.items() if k.startswith("output_transform")}
+
+    class OracleNet:
+        def predict(self, b):
+            lp, v = O.c4_heads(O.c4_features(np.asarray(b)[None], W32, f), W32, f)
+            return np.exp(lp[0]).astype(f), f(v[0])
+
+        def predict_with_gnn(self, b):
+            x = O.policy_value_gnn_per_row(O.c4_features(np.asarray(b)[None], W32, f), G32, f)
+            lp, v = O.c4_heads(x, W32, f)
+            return np.exp(lp[0]).astype(f), f(v[0])
+
+    game = Connect4Game(7)
+    sa = selfplay_args(sims)
+    moves = 0
+    t0 = time.perf_counter()
+    done = 0
+    est = None
+
+    class Counting(M.MCTS):
+        def getActionProb_g(self, board, temp=1):
+            nonlocal moves
+            pi = yield from super().getActionProb_g(board, temp)
+            moves += 1
+            if time.perf_counter() - t0 > seconds:
+                raise TimeoutError
+            return pi
+
+    coach = C.Coach.__new__(C.Coach)
+    coach.game, coach.args, coach.nnet = game, sa, OracleNet()
+    try:
+        while True:
+            np.random.seed(done)
+            coach.mcts = Counting(game, coach.nnet, sa)
+            coach.executeEpisode()
+            done += 1
+    except TimeoutError:
+        pass
+    dt = time.perf_counter() - t0
+    # a partial game counts by its moves at the mean game length of the GPU leg (set later)
+    est = {"games_done": done, "moves": moves, "seconds": round(dt, 1)}
+    return est
 
 
 def pmc_traffic(key):
@@ -194,9 +285,36 @@ def main():
     if agg is not None:
         agg["traffic"] = pmc_traffic("aggregate")
 
+    sp = None
+    if not args.no_selfplay:
+        if world > 1:
+            dist.barrier()
+        dt, sp = selfplay_leg(W, G, args, device, rank)
+        if world > 1:
+            t = torch.tensor([dt], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        sp.update({"games_per_s": round(world * sp["games"] / dt, 3),
+                   "evals_per_s": round(world * sp["evals"] / dt, 1),
+                   "seconds": round(dt, 2), "games_per_gpu": args.sp_games,
+                   "config": "Connect4 7x7, use_gnn, numMCTSSims %d, expand_by 5, cpuct 1.0, "
+                             "tempThreshold 15; native lock-step MCTS, %d host threads"
+                             % (args.sp_sims, args.sp_threads)})
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(W, G, args.cpu_seconds, B)
+        if sp is not None:
+            b = selfplay_cpu_baseline(W, G, args.sp_sims, args.cpu_seconds)
+            mean_moves = sp["moves"] / max(1, sp["games"])
+            games = b["moves"] / mean_moves
+            sp["cpu_baseline"] = {
+                "value": round(games / b["seconds"], 4), "unit": "games/s", "cores": 1,
+                "kind": "port",
+                "sample": f"reference sequential loop (Python MCTS, batch-1 predict + "
+                          f"predict_with_gnn) with the numpy fp32 oracle as the network: "
+                          f"{b['moves']} moves in {b['seconds']} s = {games:.2f} games at the "
+                          f"GPU leg's mean {mean_moves:.1f} moves/game"}
 
     if rank == 0:
         value = world * B * args.steps / elapsed
@@ -219,6 +337,7 @@ def main():
                          "avg_launch_us": round(avg_gemm_s * 1e6, 2),
                          "flop_per_launch": flop},
             "aggregate_roofline": agg,
+            "selfplay": sp,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

@@ -1,0 +1,102 @@
+/* az_mcts.h — native lock-step MCTS engine (host C++, libaz_mcts.so).
+ *
+ * The caller side of the hot path: the search statistics and descent of the reference's
+ * MCTS.search (MCTS.py:151-240) and the rules it calls per node (Connect4Game.py:116-219,
+ * TicTacToeGame.py:60-200), for many concurrent games ("slots"), each with its own tree.
+ * Leaf boards are handed out in batches for ONE network launch (predict_both on the
+ * MI355X) and the results fed back, so the per-leaf host cost is native instead of Python
+ * (SURVEY.md §8f ranks 1-2).
+ *
+ * Parity: every statistic keeps the reference's numeric type.  A Q value carries a tag
+ * (Python int / Python float / np.float32) and is updated with NumPy 2 (NEP 50) promotion
+ * rules, priors are float64 (float32 pi x int64 valids) normalised with NumPy's pairwise
+ * summation, and UCB scores are float64 in the reference's operation order — so visit counts
+ * and Q values equal the Python MCTS (itself pinned to the reference's traces) bit for bit
+ * given the same network outputs (tests/test_native_mcts.py).
+ *
+ * Episode logic (temperature, move sampling with the game's RandomState, symmetries, the
+ * expand_tree targets) stays in Python (mcts_native.py) and reads the root statistics back.
+ *
+ * Boards are int8 [n][n] in the reference's [x][y] order (board.tobytes() order), canonical
+ * (player to move = +1).  Threading: az_mcts_collect may run the slots on `threads` host
+ * threads; every other call is single-threaded per engine.  All calls return AZM_OK (0) or
+ * a negative code with the text in az_mcts_last_error().
+ */
+#ifndef AZ_MCTS_H
+#define AZ_MCTS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AZM_OK 0
+#define AZM_EINVAL -1
+#define AZM_ESTATE -2
+
+#define AZM_GAME_CONNECT4 0   /* Connect4Game(board_size=n): n x n + pass, 4 in a row */
+#define AZM_GAME_TICTACTOE 1  /* TicTacToeGame(n): n x n + pass, n in a row           */
+
+/* Q value type tags (az_mcts_root_edges): the Python type the reference's Qsa holds. */
+#define AZM_TAG_NONE -1       /* no (s, a) entry                                      */
+#define AZM_TAG_INT 0         /* Python int                                           */
+#define AZM_TAG_FLOAT 1       /* Python float (float64)                               */
+#define AZM_TAG_F32 2         /* np.float32                                           */
+
+typedef struct az_mcts az_mcts;
+
+const char* az_mcts_last_error(void);
+
+/* An engine for `slots` concurrent games of one kind.  n*n <= 64.  cpuct as args.cpuct;
+ * use_gnn selects the GNN outputs for priors and leaf values (MCTS.py:172-193). */
+az_mcts* az_mcts_create(int game, int n, int slots, double cpuct, int use_gnn);
+void az_mcts_destroy(az_mcts* m);
+int az_mcts_action_size(const az_mcts* m);
+
+/* Fresh, empty tree for a slot (a new MCTS object, Coach.py:97). */
+int az_mcts_reset(az_mcts* m, int slot);
+/* getActionProb's reset of standard_predictions / gnn_predictions (MCTS.py:30-31). */
+int az_mcts_clear_predictions(az_mcts* m, int slot);
+/* Queue `sims` searches from the canonical root `board` (MCTS.py:33-34, 104-106). */
+int az_mcts_begin(az_mcts* m, int slot, const int8_t* board, int sims);
+/* Searches still to finish for a slot (a search waiting for its leaf counts). */
+int az_mcts_remaining(const az_mcts* m, int slot);
+/* The same for every slot at once: out[slots]. */
+int az_mcts_remaining_all(const az_mcts* m, int32_t* out);
+
+/* Advance every slot with queued searches until it waits on a new leaf or has none left.
+ * Writes up to `cap` leaf boards [n*n] and their slot ids, in ascending slot order; returns
+ * the number written (>= 0) or an error code.  Terminal-only searches finish in here. */
+int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int threads);
+
+/* Network outputs for the leaves of the last collect, same order: pi/gpi [count][A] float32
+ * probabilities, v/gv [count] float32 (gpi/gv may be NULL when use_gnn == 0).  failed != 0
+ * applies the reference's exception path to every leaf (uniform priors, value 0,
+ * MCTS.py:195-200).  Expands each leaf and backs its value up the searched path. */
+int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const float* gpi,
+                 const float* gv, int failed);
+
+/* Root statistics: nsa[A] visit counts (0 = no entry), q[A] values, qtag[A] AZM_TAG_*. */
+int az_mcts_root_edges(const az_mcts* m, int slot, const int8_t* board, int32_t* nsa, double* q,
+                       int8_t* qtag);
+/* standard_predictions[s][1] when s is present in the current prediction epoch: returns 1 and
+ * writes *v, else 0.  az_mcts_set_std records one (expand_tree's root predict, MCTS.py:108-113). */
+int az_mcts_get_std(const az_mcts* m, int slot, const int8_t* board, float* v);
+int az_mcts_set_std(az_mcts* m, int slot, const int8_t* board, float v);
+/* Tree sizes of a slot: out[0] = len(Es), out[1] = len(Ns), out[2] = len(Ps), out[3] = sum(Nsa). */
+int az_mcts_tree_stats(const az_mcts* m, int slot, int64_t* out);
+
+/* Rules, exposed for differential tests against the Python games. ended: tag + value of
+ * getGameEnded(board, 1); valids [A] int8; next: canonical board after action (player 1 moves,
+ * then the board is seen from the opponent). */
+int az_game_ended(int game, int n, const int8_t* board, int* tag, double* value);
+int az_game_valids(int game, int n, const int8_t* board, int8_t* valids);
+int az_game_next_canonical(int game, int n, const int8_t* board, int action, int8_t* out);
+/* np.sum of a float64 vector (NumPy's pairwise summation), for tests. */
+double az_np_pairwise_sum(const double* a, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

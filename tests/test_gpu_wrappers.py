@@ -1,0 +1,223 @@
+"""The reference's NeuralNet surface on the MI355X: wrapper predict / predict_with_gnn against
+the reference goldens (G1, G2, G4), the batched entry points against the batch-1 calls, the
+checkpoint format, lock-step self-play with the real network, one full Coach iteration
+(config 1, G7) and the data-parallel CNN step (2 ranks on one GPU, gloo)."""
+import json
+import os
+import socket
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden, split_weights
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+TOL = 1e-5      # north-star policy/value tolerance
+
+
+@pytest.fixture(scope="module")
+def c4_wrapper(c4_gnn_weights):
+    from connect4.Connect4GNN import Connect4GNNWrapper
+    from connect4.Connect4Game import Connect4Game
+    w = Connect4GNNWrapper(Connect4Game(7), SimpleNamespace(dropout=0.3, gnn_layers=2))
+    w.nnet.load_state_dict(split_weights(golden("c4_net.npz"), "w/"))
+    w.gnn.load_state_dict(c4_gnn_weights)
+    return w
+
+
+def test_c4_wrapper_predict_matches_reference(c4_wrapper):
+    z = golden("c4_net.npz")
+    for i in range(0, 256, 17):
+        pi, v = c4_wrapper.predict(z["boards"][i].astype(np.int64))
+        assert pi.dtype == np.float32 and isinstance(v, np.float32) and pi.shape == (8,)
+        np.testing.assert_allclose(pi, z["pi_b1"][i], atol=TOL)
+        assert abs(float(v) - float(z["v_b1"][i])) <= TOL
+
+
+def test_c4_wrapper_predict_with_gnn_matches_reference(c4_wrapper):
+    z = golden("c4_gnn.npz")
+    for i in range(0, 64, 5):
+        b = z["boards"][i].astype(np.int64)
+        b0 = b.copy()
+        pi, v = c4_wrapper.predict_with_gnn(b)
+        assert np.array_equal(b, b0)                       # caller-owned board not mutated
+        np.testing.assert_allclose(pi, z["pi_gnn_b1"][i], atol=TOL)
+        assert abs(float(v) - float(z["v_gnn_b1"][i])) <= TOL
+
+
+def test_c4_batched_entry_points_equal_batch1(c4_wrapper):
+    z1, z2 = golden("c4_net.npz"), golden("c4_gnn.npz")
+    boards = np.concatenate([z1["boards"], z2["boards"]]).astype(np.int64)
+    pi, v, gpi, gv = c4_wrapper.predict_both(boards)
+    pb, vb = c4_wrapper.predict_batch(boards)
+    gpb, gvb = c4_wrapper.predict_batch_with_gnn(boards)
+    for a, b in ((pi, pb), (v, vb), (gpi, gpb), (gv, gvb)):
+        np.testing.assert_allclose(a, b, atol=TOL)
+    np.testing.assert_allclose(pi[:256], z1["pi_b1"], atol=TOL)
+    np.testing.assert_allclose(v[:256], z1["v_b1"], atol=TOL)
+    np.testing.assert_allclose(gpi[256:], z2["pi_gnn_b1"], atol=TOL)
+    np.testing.assert_allclose(gv[256:], z2["v_gnn_b1"], atol=TOL)
+    for i in (0, 100, 300):
+        p1, v1 = c4_wrapper.predict_with_gnn(boards[i])
+        np.testing.assert_allclose(gpi[i], p1, atol=TOL)
+        assert abs(float(gv[i]) - float(v1)) <= TOL
+
+
+def test_c4_heads_and_features_surface(c4_wrapper):
+    z = golden("c4_net.npz")
+    c4_wrapper.nnet.eval()
+    f = c4_wrapper.extract_features(torch.from_numpy(z["boards"][:32].astype(np.float32)))
+    logp, v = c4_wrapper.apply_policy_value_heads(f)
+    assert tuple(logp.shape) == (32, 8) and tuple(v.shape) == (32, 1)
+    np.testing.assert_allclose(logp.cpu().numpy(), z["logp_batch"][:32], atol=TOL)
+    np.testing.assert_allclose(v.cpu().numpy()[:, 0], z["v_batch"][:32], atol=TOL)
+
+
+def test_ttt3_all_positions_match_reference():
+    """All 5,478 reachable 3x3 positions (G4), standard and GNN heads, in one batch."""
+    from tictactoe.TicTacToeGNN import TicTacToeGNNWrapper
+    from tictactoe.TicTacToeGame import TicTacToeGame
+    z = golden("ttt3.npz")
+    w = TicTacToeGNNWrapper(TicTacToeGame(3), SimpleNamespace(gnn_layers=2))
+    w.nnet.load_state_dict(split_weights(z, "w/"))
+    w.gnn.load_state_dict(split_weights(z, "g/"))
+    pi, v, gpi, gv = w.predict_both(z["boards"].astype(np.int64))
+    np.testing.assert_allclose(pi, z["pi"], atol=TOL)
+    np.testing.assert_allclose(v, z["v"], atol=TOL)
+    np.testing.assert_allclose(gpi, z["pi_gnn"], atol=TOL)
+    np.testing.assert_allclose(gv, z["v_gnn"], atol=TOL)
+    p1, v1 = w.predict_with_gnn(z["boards"][7].astype(np.int64))
+    np.testing.assert_allclose(p1, z["pi_gnn"][7], atol=TOL)
+
+
+def test_checkpoint_roundtrip_and_format(tmp_path, c4_wrapper):
+    from connect4.Connect4GNN import Connect4GNNWrapper
+    from connect4.Connect4Game import Connect4Game
+    c4_wrapper.save_checkpoint(str(tmp_path / "ck"), "best_gnn.pth.tar")
+    ck = torch.load(tmp_path / "ck" / "best_gnn.pth.tar", map_location="cpu", weights_only=True)
+    assert set(ck) == {"state_dict", "gnn"}
+    assert list(ck["state_dict"]) == ["conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias",
+                                      "fc_policy.weight", "fc_policy.bias", "fc_value.weight",
+                                      "fc_value.bias"]
+    assert len(ck["gnn"]) == 24 and tuple(ck["gnn"]["output_transform.0.weight"].shape) == \
+        (3136, 3136)
+    w2 = Connect4GNNWrapper(Connect4Game(7), SimpleNamespace(dropout=0.3, gnn_layers=2))
+    w2.load_checkpoint(str(tmp_path / "ck"), "best_gnn.pth.tar")
+    b = golden("c4_gnn.npz")["boards"][3].astype(np.int64)
+    for a, c in zip(c4_wrapper.predict_with_gnn(b), w2.predict_with_gnn(b)):
+        np.testing.assert_array_equal(a, c)
+
+
+def test_lockstep_selfplay_on_gpu(c4_wrapper):
+    """Lock-step games with the real network: every episode completes, one batched call per
+    round, and the rows served equal the leaves the searches asked for."""
+    from connect4.Connect4Game import Connect4Game
+    from selfplay import BatchEvaluator, play_episodes
+    args = SimpleNamespace(numMCTSSims=6, cpuct=1.0, tempThreshold=15, use_gnn=True,
+                           expand_by=2)
+    ev = BatchEvaluator(c4_wrapper)
+    stats = {}
+    out = play_episodes(Connect4Game(7), c4_wrapper, args, range(12), {e: 7 * e for e in range(12)},
+                        parallel_games=8, evaluator=ev, stats=stats)
+    assert sorted(out) == list(range(12))
+    for std, gnn in out.values():
+        assert len(std) >= 2 and len(gnn) == len(std) // 2      # 2 symmetries, 1 GNN ex/move
+        for b, p, r in std:
+            assert b.shape == (7, 7) and abs(sum(p) - 1) < 1e-6 and r in (1, -1, 1e-4, -1e-4)
+    assert stats["calls"] == stats["rounds"] and stats["rows"] >= stats["rounds"]
+
+
+def test_coach_iteration_matches_reference_counts(tmp_path):
+    """Config 1 (G7): main.py wiring, --game tictactoe --board_size 3 --use_gnn --numIters 1,
+    seeds random/np/torch = 0 -> the reference's example counts and checkpoint files."""
+    import random
+    import main as M
+    from Coach import Coach
+    from register import get_game
+    ref = json.load(open(os.path.join(GOLDEN, "coach_ttt3.json")))
+    args = M.config_to_args(M.load_config(os.path.join(M.HERE, "tictactoe", "config.yaml")))
+    args.board_size, args.numIters, args.use_gnn, args.gnn_layers = 3, 1, True, 2
+    args.game, args.load_model = "tictactoe", False
+    folder = str(tmp_path / "tictactoe")
+    os.makedirs(folder)
+    args.checkpoint, args.load_folder_file = folder, (folder, "best_gnn.pth.tar")
+    random.seed(0)
+    np.random.seed(0)
+    torch.manual_seed(0)
+    GameClass, NNet = get_game("tictactoe", use_gnn=True)
+    game = M.create_game_instance(GameClass, args)
+    coach = Coach(game, NNet(game, args), args)
+    import Arena as A
+    seen = []
+    orig = A.Arena.playGames
+
+    def pg(self, num, verbose=False):
+        r = orig(self, num, verbose)
+        seen.append([int(x) for x in r])
+        return r
+
+    A.Arena.playGames = pg
+    try:
+        coach.learn()
+    finally:
+        A.Arena.playGames = orig
+    std, gnn = coach.trainExamplesHistory[0]
+    assert (len(std), len(gnn)) == (ref["n_std"], ref["n_gnn"])
+    assert sorted(os.listdir(folder)) == ref["files"]
+    assert seen[0] == ref["arena_pwins_nwins_draws"], seen
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    import torch.distributed as dist
+    from connect4.Connect4GNN import Connect4GNNWrapper
+    from connect4.Connect4Game import Connect4Game
+    from azhip import dist as D
+    from test_gpu_train import _examples
+    zz = golden("train_c4.npz")
+    ex, _ = _examples(zz)
+    w0 = split_weights(golden("c4_net.npz"), "w/")
+
+    def make(mode):
+        a = SimpleNamespace(lr=0.001, epochs=3, batch_size=64, gnn_layers=2, dropout=0.3,
+                            train_parallel=mode)
+        w = Connect4GNNWrapper(Connect4Game(7), a)
+        w.nnet.load_state_dict(w0)
+        return w
+
+    single = make("replicas")                   # before init: a plain 1-rank step
+    np.random.seed(5)
+    single.train(ex)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dp = make("allreduce")
+    np.random.seed(5)
+    dp.train(ex)
+    torch.cuda.synchronize()
+    res = {"single": single.nnet.params.flat.cpu(), "dp": dp.nnet.params.flat.cpu(),
+           "sync": D.params_in_sync(dp.nnet.params.flat)}
+    torch.save(res, os.path.join(outdir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_data_parallel_cnn_step_equals_single_rank(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_dp_worker, args=(2, _port(), str(tmp_path)), nprocs=2)
+    r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(2)]
+    assert r[0]["sync"] and r[1]["sync"]
+    assert torch.equal(r[0]["dp"], r[1]["dp"])
+    assert torch.equal(r[0]["single"], r[1]["single"])
+    np.testing.assert_allclose(r[0]["dp"].numpy(), r[0]["single"].numpy(), atol=1e-5)

@@ -65,10 +65,10 @@ def run_golden(name, game, n):
             coach.mcts = M.MCTS(game, net, args)
             mc = coach.mcts
             seen = []
-            orig = mc.getActionProb
+            orig = mc.getActionProb_g
 
             def gap(board, temp=1, mc=mc, orig=orig, seen=seen):
-                pi = orig(board, temp=temp)
+                pi = yield from orig(board, temp=temp)
                 s = game.stringRepresentation(board)
                 A = game.getActionSize()
                 seen.append(dict(
@@ -79,7 +79,7 @@ def run_golden(name, game, n):
                     pi=[float(x) for x in pi]))
                 return pi
 
-            mc.getActionProb = gap
+            mc.getActionProb_g = gap
             c0 = len(choices)
             std, gnn = coach.executeEpisode()
             assert len(seen) == len(ep_moves)

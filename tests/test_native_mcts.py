@@ -1,0 +1,221 @@
+"""Native MCTS engine (libaz_mcts.so) on the host, no GPU.
+
+* rules: Connect4 / TicTacToe ended / valids / next-canonical equal the Python games on random
+  reachable positions (which are differential-tested against the reference);
+* np.sum emulation: NumPy's pairwise summation bit for bit;
+* search parity: lock-step native self-play driven by the reference's recorded network outputs
+  reproduces the reference's episodes (G6): per move the root visit counts, Q values and their
+  Python types, pi, and every emitted example;
+* differential fuzz: native vs the Python MCTS (golden-pinned) on pseudo-random networks, many
+  seeds, both games, with and without the GNN path.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden
+from test_mcts_golden import Args, _tag
+from test_selfplay import BatchedRecordedNet, _norm_gnn, _norm_std
+
+
+@pytest.fixture(scope="module", autouse=True)
+def host_lib():
+    from azhip.build import build_host
+    build_host(verbose=False)
+    import mcts_native
+    return mcts_native.lib()
+
+
+def _games():
+    from connect4.Connect4Game import Connect4Game
+    from tictactoe.TicTacToeGame import TicTacToeGame
+    return [(0, 7, Connect4Game(7)), (0, 5, Connect4Game(5)), (1, 3, TicTacToeGame(3)),
+            (1, 4, TicTacToeGame(4))]
+
+
+def _random_positions(game, rng, count):
+    out = []
+    for _ in range(count):
+        b, p = game.getInitBoard(), 1
+        for _ in range(rng.integers(0, 60)):
+            if game.getGameEnded(b, p) != 0:
+                break
+            v = game.getValidMoves(b, p)
+            a = rng.choice(np.flatnonzero(v))
+            b, p = game.getNextState(b, p, a)
+        out.append(game.getCanonicalForm(b, p))
+    return out
+
+
+def test_rules_match_python_games(host_lib):
+    import ctypes
+    rng = np.random.default_rng(0)
+    P = ctypes.c_void_p
+    for kind, n, game in _games():
+        A = game.getActionSize()
+        for b in _random_positions(game, rng, 300):
+            b8 = np.ascontiguousarray(b, np.int8)
+            tag, val = ctypes.c_int(), ctypes.c_double()
+            assert host_lib.az_game_ended(kind, n, b8.ctypes.data_as(P), ctypes.byref(tag),
+                                          ctypes.byref(val)) == 0
+            ref = game.getGameEnded(b, 1)
+            assert (val.value, tag.value) == (float(ref), 0 if isinstance(ref, int) else 1)
+            vv = np.zeros(A, np.int8)
+            host_lib.az_game_valids(kind, n, b8.ctypes.data_as(P), vv.ctypes.data_as(P))
+            valids = game.getValidMoves(b, 1)
+            assert vv.tolist() == valids.tolist()
+            for a in np.flatnonzero(valids):
+                nb, pl = game.getNextState(b, 1, a)
+                want = game.getCanonicalForm(nb, pl)
+                out = np.zeros((n, n), np.int8)
+                assert host_lib.az_game_next_canonical(kind, n, b8.ctypes.data_as(P), int(a),
+                                                       out.ctypes.data_as(P)) == 0
+                assert out.tolist() == want.tolist()
+
+
+def test_pairwise_sum_is_numpy_sum(host_lib):
+    import ctypes
+    rng = np.random.default_rng(1)
+    for n in (1, 2, 7, 8, 9, 10, 16, 17, 65, 129, 300):
+        for _ in range(300):
+            a = rng.random(n) * 10.0 ** rng.integers(-8, 8, n)
+            a *= rng.random(n) < 0.8
+            got = host_lib.az_np_pairwise_sum(a.ctypes.data_as(ctypes.c_void_p), n)
+            assert got == float(np.sum(a))
+
+
+def _native_episodes(game, net, args, eps, seeds, parallel, threads=2, per_move=None):
+    from selfplay import play_episodes_native
+    import mcts_native
+    if per_move is not None:
+        orig = mcts_native.NativeMCTS.getActionProb_g
+
+        def gap(self, board, temp=1):
+            pi = yield from orig(self, board, temp=temp)
+            nsa, q, tag = self.engine.root_edges(self.slot, board)
+            per_move.setdefault(self.slot, []).append(dict(
+                board=board.astype(np.int8).tolist(), temp=temp, counts=nsa,
+                q=[float(mcts_native.typed_q(t, x)) if t >= 0 else None for t, x in zip(tag, q)],
+                qtype=[_tag(mcts_native.typed_q(t, x)) if t >= 0 else None
+                       for t, x in zip(tag, q)],
+                pi=[float(x) for x in pi]))
+            return pi
+        mcts_native.NativeMCTS.getActionProb_g = gap
+    try:
+        return play_episodes_native(game, net, args, eps, seeds, parallel_games=parallel,
+                                    threads=threads)
+    finally:
+        if per_move is not None:
+            mcts_native.NativeMCTS.getActionProb_g = orig
+
+
+@pytest.mark.parametrize("case", ["mcts_c4", "mcts_ttt3"])
+def test_native_episodes_equal_reference(case):
+    from connect4.Connect4Game import Connect4Game
+    from tictactoe.TicTacToeGame import TicTacToeGame
+    game = Connect4Game(7) if case == "mcts_c4" else TicTacToeGame(3)
+    meta = json.load(open(os.path.join(GOLDEN, case + ".json")))
+    net = BatchedRecordedNet(golden(case + ".npz"), 0)
+    eps = [ep["episode"] for ep in meta["episodes"]]
+    # one slot: per-move root statistics against the reference trace, in order
+    for ep, moves in zip(meta["episodes"], meta["moves"]):
+        per = {}
+        out = _native_episodes(game, net, Args(meta["args"]), [ep["episode"]],
+                               {ep["episode"]: ep["episode"]}, 1, per_move=per)
+        seen = per[0]
+        assert len(seen) == len(moves)
+        for i, (a, b) in enumerate(zip(seen, moves)):
+            for key in ("board", "temp", "counts", "q", "qtype", "pi"):
+                assert a[key] == b[key], (case, ep["episode"], i, key, a[key], b[key])
+        std, gnn = out[ep["episode"]]
+        assert _norm_std(std) == [tuple(x) for x in ep["std_examples"]]
+        assert _norm_gnn(gnn) == [tuple(x) for x in ep["gnn_examples"]]
+    # all episodes at once (lock step over slots, 3 host threads)
+    out = _native_episodes(game, net, Args(meta["args"]), eps, {e: e for e in eps}, 64,
+                           threads=3)
+    for ep in meta["episodes"]:
+        std, gnn = out[ep["episode"]]
+        assert _norm_std(std) == [tuple(x) for x in ep["std_examples"]]
+        assert _norm_gnn(gnn) == [tuple(x) for x in ep["gnn_examples"]]
+
+
+class HashNet:
+    """Deterministic pseudo-random network: (pi, v) a function of the board bytes only, with
+    exact zeros and ties sprinkled in to exercise the masked / tie-break paths."""
+
+    def __init__(self, A, salt):
+        self.A, self.salt = A, salt
+
+    def _row(self, b):
+        b = np.asarray(b, np.int64)
+        h = np.random.default_rng([self.salt] + [int(x) + 1 for x in b.ravel()])
+        p = h.random(self.A).astype(np.float32)
+        if h.random() < 0.2:
+            p[h.integers(0, self.A)] = 0.0
+        if h.random() < 0.1:
+            p[:] = np.float32(0.25)
+        p /= p.sum()
+        v = np.float32(h.uniform(-1, 1))
+        if h.random() < 0.05:
+            v = np.float32(0.0)
+        return p.astype(np.float32), v
+
+    def predict(self, board):
+        return self._row(board)
+
+    def predict_with_gnn(self, board):
+        p, v = self._row(-np.asarray(board))
+        return p, np.float32(-v * 0.5)
+
+    def predict_batch(self, boards):
+        rows = [self._row(b) for b in boards]
+        return np.stack([p for p, _ in rows]), np.array([v for _, v in rows], np.float32)
+
+    def predict_both(self, boards):
+        pi, v = self.predict_batch(boards)
+        rows = [self.predict_with_gnn(b) for b in boards]
+        return pi, v, np.stack([p for p, _ in rows]), np.array([x for _, x in rows], np.float32)
+
+
+@pytest.mark.parametrize("gi", [0, 2, 3])
+@pytest.mark.parametrize("use_gnn", [False, True])
+def test_native_matches_python_mcts_fuzz(gi, use_gnn):
+    from selfplay import play_episodes
+    _, _, game = _games()[gi]
+    args = Args(numMCTSSims=[7, 12, 25][gi % 3], cpuct=[1.0, 1.5, 0.7][gi % 3], tempThreshold=6,
+                use_gnn=use_gnn, expand_by=3)
+    net = HashNet(game.getActionSize(), 17 + gi)
+    eps = list(range(6))
+    seeds = {e: 1000 * gi + e for e in eps}
+    py = play_episodes(game, net, args, eps, seeds, parallel_games=3)
+    nat = _native_episodes(game, net, args, eps, seeds, 4, threads=2)
+    for e in eps:
+        assert _norm_std(nat[e][0]) == _norm_std(py[e][0]), e
+        assert _norm_gnn(nat[e][1]) == _norm_gnn(py[e][1]), e
+
+
+def test_native_engine_errors_and_failed_batches():
+    from connect4.Connect4Game import Connect4Game
+    from mcts_native import Engine
+    from selfplay import play_episodes_native
+    eng = Engine(Connect4Game(7), 2, 1.0, False)
+    b = np.zeros((7, 7), np.int8)
+    eng.begin(0, b, 3)
+    with pytest.raises(RuntimeError):
+        eng.begin(0, b, 3)                       # still queued
+    with pytest.raises(RuntimeError):
+        eng.begin(5, b, 3)                       # bad slot
+    k = eng.collect()
+    assert k == 1 and eng.leaf_slots[0] == 0
+    with pytest.raises(RuntimeError):
+        eng.feed(2, np.ones((2, 8), np.float32) / 8, np.zeros(2, np.float32))
+
+    class Broken:
+        def predict_batch(self, boards):
+            raise RuntimeError("device lost")
+
+    args = Args(numMCTSSims=4, cpuct=1.0, tempThreshold=15, use_gnn=False)
+    out = play_episodes_native(Connect4Game(7), Broken(), args, [0, 1], {0: 0, 1: 1}, 2)
+    assert len(out) == 2 and all(len(std) > 0 for std, _ in out.values())

@@ -1,0 +1,86 @@
+"""Lock-step batched self-play (alphazero-gnn_amd/selfplay.py) on the host, no GPU: driven by
+the reference's recorded network outputs, every lock-step game must emit exactly the training
+examples of the reference's sequential episode with the same seed (tests/golden G6), for any
+number of concurrent games, with or without a batched network entry point."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden
+from test_mcts_golden import Args, RecordedNet
+
+
+class BatchedRecordedNet(RecordedNet):
+    """RecordedNet with the wrappers' batched entry points (predict_batch / predict_both)."""
+
+    def __init__(self, z, n):
+        super().__init__(z, n)
+        self.batches = []
+
+    def predict_batch(self, boards):
+        self.batches.append(len(boards))
+        rows = [self.predict(b.astype(np.int64)) for b in boards]
+        return (np.stack([p for p, _ in rows]).astype(np.float32),
+                np.array([v for _, v in rows], np.float32))
+
+    def predict_both(self, boards):
+        pi, v = self.predict_batch(boards)
+        rows = [self.predict_with_gnn(b.astype(np.int64)) for b in boards]
+        return (pi, v, np.stack([p for p, _ in rows]).astype(np.float32),
+                np.array([x for _, x in rows], np.float32))
+
+
+def _norm_std(std):
+    return [(np.asarray(b).astype(int).tolist(), [float(x) for x in p], float(z))
+            for b, p, z in std]
+
+
+def _norm_gnn(gnn):
+    return [(np.asarray(x[0]).astype(int).tolist(), int(x[1]), [float(t) for t in x[2]],
+             float(x[3]), [float(t) for t in x[4]], float(x[5]), float(x[6])) for x in gnn]
+
+
+def _cases():
+    from connect4.Connect4Game import Connect4Game
+    from tictactoe.TicTacToeGame import TicTacToeGame
+    return [("mcts_c4", lambda: Connect4Game(7), 7), ("mcts_ttt3", lambda: TicTacToeGame(3), 3)]
+
+
+@pytest.mark.parametrize("case", [0, 1])
+@pytest.mark.parametrize("parallel", [1, 2, 64])
+@pytest.mark.parametrize("batched", [False, True])
+def test_lockstep_games_equal_reference_episodes(case, parallel, batched):
+    from selfplay import play_episodes
+    name, make_game, n = _cases()[case]
+    meta = json.load(open(os.path.join(GOLDEN, name + ".json")))
+    z = golden(name + ".npz")
+    net = (BatchedRecordedNet if batched else RecordedNet)(z, n)
+    args = Args(meta["args"])
+    eps = [ep["episode"] for ep in meta["episodes"]]
+    out = play_episodes(make_game(), net, args, eps, {e: e for e in eps},
+                        parallel_games=parallel)
+    assert sorted(out) == sorted(eps)
+    for ep in meta["episodes"]:
+        std, gnn = out[ep["episode"]]
+        assert _norm_std(std) == [tuple(x) for x in ep["std_examples"]]
+        assert _norm_gnn(gnn) == [tuple(x) for x in ep["gnn_examples"]]
+    if batched and parallel > 1 and len(eps) > 1:
+        assert max(net.batches) > 1          # leaves really were evaluated together
+
+
+def test_lockstep_batch_failure_degrades_like_reference():
+    """A failing batched call gives every waiting leaf uniform priors and value 0
+    (MCTS.py:195-200), and the games still finish."""
+    from connect4.Connect4Game import Connect4Game
+    from selfplay import play_episodes
+
+    class Broken:
+        def predict_batch(self, boards):
+            raise RuntimeError("device lost")
+
+    args = Args(numMCTSSims=4, cpuct=1.0, tempThreshold=15, use_gnn=False)
+    out = play_episodes(Connect4Game(7), Broken(), args, [0, 1], {0: 0, 1: 1},
+                        parallel_games=2)
+    assert len(out) == 2 and all(len(std) > 0 for std, _ in out.values())
