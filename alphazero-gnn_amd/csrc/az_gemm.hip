@@ -256,6 +256,157 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_mfma(GemmArgs p) {
       }
 }
 
+// ------------------------------------------------------------------------------ LDS-DMA tile
+// Both operands K-major with no row gather / concatenation (the forward Linear layers).  Tiles
+// of BM x BK and BN x BK floats go global -> LDS with global_load_lds_dwordx4 (no VGPR round
+// trip): one wave-instruction fills 8 rows x 128 B.  The LDS image is unpadded, [row][32 k],
+// with the 16-B chunk index XOR-swizzled by (row >> 1) & 7 -- applied on the per-lane GLOBAL
+// address, since the LDS destination of a DMA is lane-linear -- so the fragment reads
+// (ds_read_b128, 16 lanes = 16 consecutive rows at one k chunk) hit 16 distinct bank groups.
+// Two LDS buffers: tile t+1 is in flight while tile t feeds the MFMAs; one barrier per tile.
+// Rows past M/N read row 0 and k past the range reads k = 0 of the same row (valid memory,
+// finite values); the A tail of a partial last tile is zeroed in LDS before use.
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds(GemmArgs p) {
+  constexpr int BK = 32;
+  constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TI = WM / 32, TJ = WN / 32;
+  constexpr int APC = BM / 8 / NW, BPC = BN / 8 / NW;   // 8-row pieces per wave
+  static_assert(TI >= 1 && TJ >= 1 && APC >= 1 && BPC >= 1, "bad tile");
+  __shared__ __attribute__((aligned(1024))) float smem[2 * (BM + BN) * BK];
+
+  const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
+  const int nwg = mt_n * nt_n * p.splits;
+  const int bid = xcd_swizzle(blockIdx.x, nwg);
+  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+
+  // per-lane DMA sources: piece q of this wave covers rows (q*NW + wave)*8 .. +8
+  const int lrow = lane >> 3, pch = lane & 7;
+  const float* asrc[APC];
+  const float* bsrc[BPC];
+  int akq[APC], bkq[BPC];
+#pragma unroll
+  for (int q = 0; q < APC; ++q) {
+    const int r = (q * NW + wave) * 8 + lrow;
+    const int gr = m0 + r < p.M ? m0 + r : 0;
+    asrc[q] = p.A + (size_t)gr * p.lda;
+    akq[q] = (pch ^ ((r >> 1) & 7)) * 4;
+  }
+#pragma unroll
+  for (int q = 0; q < BPC; ++q) {
+    const int r = (q * NW + wave) * 8 + lrow;
+    const int gr = n0 + r < p.N ? n0 + r : 0;
+    bsrc[q] = p.B + (size_t)gr * p.ldb;
+    bkq[q] = (pch ^ ((r >> 1) & 7)) * 4;
+  }
+  auto issue = [&](int buf, int k0) {
+    float* As = smem + buf * (BM + BN) * BK;
+    float* Bs = As + BM * BK;
+#pragma unroll
+    for (int q = 0; q < APC; ++q) {
+      const int k = k0 + akq[q];
+      const float* src = asrc[q] + (k < p.K ? k : 0);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(As + (q * NW + wave) * 8 * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < BPC; ++q) {
+      const int k = k0 + bkq[q];
+      const float* src = bsrc[q] + (k < p.K ? k : 0);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(Bs + (q * NW + wave) * 8 * BK), 16, 0, 0);
+    }
+  };
+  // zero A's k >= kend columns of a partial tile.  Rows were DMA'd by other waves: every wave
+  // has waited for its own DMAs (vmcnt(0)) before this point, and the barrier makes all of them
+  // complete before any zero is written over them.
+  auto zero_tail = [&](int buf, int k0) {
+    if (k0 + BK <= kend) return;
+    __syncthreads();
+    float* As = smem + buf * (BM + BN) * BK;
+    for (int idx = threadIdx.x; idx < BM * 8; idx += NT) {
+      const int r = idx >> 3, lc = idx & 7;
+      if (k0 + lc * 4 >= kend) {
+        // kend is a multiple of 4 (K % 4 == 0 and kc % BK == 0)
+        *reinterpret_cast<f32x4*>(As + r * BK + ((lc ^ ((r >> 1) & 7)) * 4)) =
+            f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    issue(0, kbeg);
+    __builtin_amdgcn_s_waitcnt(0);
+    zero_tail(0, kbeg);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) issue(cur ^ 1, kbeg + (kt + 1) * BK);
+    const float* As = smem + cur * (BM + BN) * BK;
+    const float* Bs = As + BM * BK;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      f32x4 a[TI], b[TJ];
+      const int lc = g * 2 + (lane >> 5);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int r = wm * WM + i * 32 + (lane & 31);
+        a[i] = *reinterpret_cast<const f32x4*>(As + r * BK + ((lc ^ ((r >> 1) & 7)) * 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int r = wn * WN + j * 32 + (lane & 31);
+        b[j] = *reinterpret_cast<const f32x4*>(Bs + r * BK + ((lc ^ ((r >> 1) & 7)) * 4));
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      __builtin_amdgcn_s_waitcnt(0);
+      zero_tail(cur ^ 1, kbeg + (kt + 1) * BK);
+    }
+    __syncthreads();
+  }
+
+  float* slab = p.splits > 1 ? p.slab + (size_t)sp * p.M * p.N : nullptr;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = n0 + wn * WN + j * 32 + (lane & 31);
+        if (slab) {
+          if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][r];
+        } else {
+          epilogue_store(p, row, col, acc[i][j][r]);
+        }
+      }
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
   const long total = (long)p.M * p.N;
   const size_t plane = (size_t)p.M * p.N;
@@ -340,10 +491,15 @@ __global__ __launch_bounds__(256) void gemv_f32(GemmArgs p) {
 }
 
 struct TileCfg { int bm, bn, bk, wgm, wgn; };
-// 0: 64x64x32 (4 waves 2x2)   1: 128x128x32 (4 waves 2x2)   2: 64x64x64 (4 waves)
+// register-staged: 0: 64x64x32 (4 waves 2x2)   1: 128x128x32 (4 waves 2x2)   2: 64x64x64
 // 3: 128x64x32 (4 waves 2x2)  4: 128x128x32 (8 waves 2x4)   5: 256x128x32 (8 waves 4x2)
+// LDS-DMA (K-major A and B only): 6: 128x128x32 (4 waves 2x2)  7: 64x64x32  8: 128x64x32
+// 9: 128x128x32 (8 waves 2x4)
 static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 64, 64, 2, 2},
-                                {128, 64, 32, 2, 2}, {128, 128, 32, 2, 4}, {256, 128, 32, 4, 2}};
+                                {128, 64, 32, 2, 2}, {128, 128, 32, 2, 4}, {256, 128, 32, 4, 2},
+                                {128, 128, 32, 2, 2}, {64, 64, 32, 2, 2},  {128, 64, 32, 2, 2},
+                                {128, 128, 32, 2, 4}};
+constexpr int kNumCfgs = 10;
 
 template <int BM, int BN, int BK, int WGM, int WGN>
 static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
@@ -355,8 +511,18 @@ static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
   else hipLaunchKernelGGL((gemm_f32_mfma<BM, BN, BK, WGM, WGN, false, false>), g, b, 0, s, a);
 }
 
+template <int BM, int BN, int WGM, int WGN>
+static void launch_glds(const GemmArgs& a, hipStream_t s) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
+  hipLaunchKernelGGL((gemm_f32_glds<BM, BN, WGM, WGN>), dim3(nwg), dim3(64 * WGM * WGN), 0, s, a);
+}
+
 static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
   switch (cfg) {
+    case 6: launch_glds<128, 128, 2, 2>(a, s); break;
+    case 7: launch_glds<64, 64, 2, 2>(a, s); break;
+    case 8: launch_glds<128, 64, 2, 2>(a, s); break;
+    case 9: launch_glds<128, 128, 2, 4>(a, s); break;
     case 1: launch_tile<128, 128, 32, 2, 2>(a, akm, bkm, s); break;
     case 2: launch_tile<64, 64, 64, 2, 2>(a, akm, bkm, s); break;
     case 3: launch_tile<128, 64, 32, 2, 2>(a, akm, bkm, s); break;
@@ -438,9 +604,11 @@ int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
   }
   // tile choice (tuning override for experiments: AZ_GEMM_CFG=<index into kCfgs>)
   static const char* env_cfg = getenv("AZ_GEMM_CFG");
+  const bool glds_ok = akm && bkm && !d->A2 && !d->a_rows;
   int cfg = 0;
   if (env_cfg) {
-    cfg = std::min(std::max(atoi(env_cfg), 0), 5);
+    cfg = std::min(std::max(atoi(env_cfg), 0), kNumCfgs - 1);
+    if (cfg >= 6 && !glds_ok) cfg = 0;
   } else {
     cfg = 0;  // 64x64x32 measured fastest for every shape of the path (tools/gemm_sweep.py)
   }

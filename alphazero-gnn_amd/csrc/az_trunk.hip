@@ -154,14 +154,24 @@ __global__ __launch_bounds__(256) void heads_partial_kernel(
     w[a] = (a < A && kin) ? *reinterpret_cast<const f32x4*>(wp + (size_t)a * K + k)
                           : f32x4{0.f, 0.f, 0.f, 0.f};
   w[AMAX] = kin ? *reinterpret_cast<const f32x4*>(wv + k) : f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int rr = wave; rr < HEADS_ROWS; rr += 4) {
-    const int row = r0 + rr;
+  // all of this wave's rows are loaded before any reduction, so the loads overlap
+  constexpr int RPW = HEADS_ROWS / 4;
+  f32x4 xs[RPW], ys[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int row = r0 + wave + 4 * i;
+    const bool ok = kin && row < B;
+    xs[i] = ok ? *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + k)
+               : f32x4{0.f, 0.f, 0.f, 0.f};
+    ys[i] = same ? xs[i]
+                 : (ok ? *reinterpret_cast<const f32x4*>(hv + (size_t)row * ldhv + k)
+                       : f32x4{0.f, 0.f, 0.f, 0.f});
+  }
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int row = r0 + wave + 4 * i;
     if (row >= B) break;
-    const f32x4 x = kin ? *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + k)
-                        : f32x4{0.f, 0.f, 0.f, 0.f};
-    const f32x4 y = same ? x
-                  : (kin ? *reinterpret_cast<const f32x4*>(hv + (size_t)row * ldhv + k)
-                         : f32x4{0.f, 0.f, 0.f, 0.f});
+    const f32x4 x = xs[i], y = ys[i];
     float* out = part + ((size_t)c * B + row) * (A + 1);
 #pragma unroll
     for (int a = 0; a <= AMAX; ++a) {
@@ -175,6 +185,11 @@ __global__ __launch_bounds__(256) void heads_partial_kernel(
   }
 }
 
+// 16 rows x 16 chunk lanes per block: every (row, chunk) partial is loaded in parallel into
+// LDS, then one thread per row sums its chunks in chunk order (the same order as a serial loop,
+// so the result does not depend on the launch shape) and applies the head nonlinearities.
+constexpr int FIN_ROWS = 16;
+
 template <int AMAX>
 __global__ __launch_bounds__(256) void heads_finalize_kernel(const float* __restrict__ part,
                                                             int nchunks, int B, int A,
@@ -183,14 +198,24 @@ __global__ __launch_bounds__(256) void heads_finalize_kernel(const float* __rest
                                                             float* __restrict__ logp,
                                                             float* __restrict__ pi,
                                                             float* __restrict__ v) {
-  const int row = blockIdx.x * 256 + threadIdx.x;
-  if (row >= B) return;
+  extern __shared__ float sm[];                       // [FIN_ROWS][nchunks][A+1]
+  const int r = threadIdx.x >> 4, cl = threadIdx.x & 15;
+  const int row = blockIdx.x * FIN_ROWS + r;
+  const int W = A + 1;
+  if (row < B)
+    for (int c = cl; c < nchunks; c += 16) {
+      const float* p = part + ((size_t)c * B + row) * W;
+      float* d = sm + ((size_t)r * nchunks + c) * W;
+      for (int a = 0; a < W; ++a) d[a] = p[a];
+    }
+  __syncthreads();
+  if (cl != 0 || row >= B) return;
   float l[AMAX];
   float sv = 0.f;
 #pragma unroll
   for (int a = 0; a < AMAX; ++a) l[a] = 0.f;
   for (int c = 0; c < nchunks; ++c) {
-    const float* p = part + ((size_t)c * B + row) * (A + 1);
+    const float* p = sm + ((size_t)r * nchunks + c) * W;
 #pragma unroll
     for (int a = 0; a < AMAX; ++a)
       if (a < A) l[a] += p[a];
@@ -280,8 +305,9 @@ static void launch_heads(const float* hp, int ldhp, const float* hv, int ldhv, i
   dim3 g(nchunks, (B + HEADS_ROWS - 1) / HEADS_ROWS);
   hipLaunchKernelGGL(heads_partial_kernel<AMAX>, g, dim3(256), 0, s, hp, ldhp, hv, ldhv, B, K, wp,
                      A, wv, part);
-  hipLaunchKernelGGL(heads_finalize_kernel<AMAX>, dim3((B + 255) / 256), dim3(256), 0, s, part,
-                     nchunks, B, A, bp, bv, logp, pi, v);
+  const size_t lds = (size_t)FIN_ROWS * nchunks * (A + 1) * sizeof(float);
+  hipLaunchKernelGGL(heads_finalize_kernel<AMAX>, dim3((B + FIN_ROWS - 1) / FIN_ROWS), dim3(256),
+                     lds, s, part, nchunks, B, A, bp, bv, logp, pi, v);
 }
 
 extern "C" int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv, int B, int K,
@@ -293,6 +319,8 @@ extern "C" int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv
   if (B == 0) return AZ_OK;
   AZ_REQUIRE(hp && hv && wp && bp && wv && bv && logp && v && ws, AZ_EINVAL, "az_heads_fwd: null");
   AZ_REQUIRE(ws_bytes >= az_heads_ws_bytes(B, K, A), AZ_EINVAL, "az_heads_fwd: workspace too small");
+  AZ_REQUIRE((size_t)FIN_ROWS * ((K + HEADS_KC - 1) / HEADS_KC) * (A + 1) * sizeof(float) <= 65536,
+             AZ_EINVAL, "az_heads_fwd: K=%d too large for the finalize stage", K);
   AZ_REQUIRE(aligned16(hp) && aligned16(hv) && aligned16(wp) && aligned16(wv) && ldhp % 4 == 0 &&
                  ldhv % 4 == 0,
              AZ_EINVAL, "az_heads_fwd: operands need 16B alignment");

@@ -26,7 +26,10 @@ for _ in range(reps):
 e1.record()
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) / reps * 1e3
-print(json.dumps({"us": us, "tflops": 2 * M * N * K / us / 1e6}))
+ref = torch.relu(x.double() @ w.double().T + b.double())
+scale = x.double().abs() @ w.double().abs().T
+err = float(((y.double() - ref).abs() / (scale + 1e-30)).max())
+print(json.dumps({"us": us, "tflops": 2 * M * N * K / us / 1e6, "rel_err": err}))
 '''
 
 
@@ -48,6 +51,25 @@ if __name__ == "__main__":
                 for sk in ("0", "1"):
                     res = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_STREAMK": sk}, M, N, K)
                     print(json.dumps({"M": M, "cfg": cfg, "streamk": sk, **res}), flush=True)
+        sys.exit(0)
+    if mode == "quickcheck":      # one small run per glds config: correctness before the sweep
+        for cfg in ("6", "7", "8", "9"):
+            for (M, N, K) in [(100, 200, 96), (100, 200, 100), (512, 3136, 3136)]:
+                res = run({"AZ_GEMM_CFG": cfg}, M, N, K)
+                print(json.dumps({"M": M, "N": N, "K": K, "cfg": cfg, **res}), flush=True)
+                if "error" in res or res.get("rel_err", 1) > 1e-5:
+                    sys.exit(3)
+        sys.exit(0)
+    if mode == "glds":
+        for (M, N, K) in [(512, 3136, 3136), (256, 3136, 3136), (4096, 3136, 3136)]:
+            for cfg in ("0", "6", "7", "8", "9"):
+                for sp in ("", "2", "3", "4", "5", "6", "8"):
+                    env = {"AZ_GEMM_CFG": cfg}
+                    if sp:
+                        env["AZ_GEMM_SPLITS"] = sp
+                    res = run(env, M, N, K)
+                    print(json.dumps({"M": M, "cfg": cfg, "splits": sp or "auto", **res}),
+                          flush=True)
         sys.exit(0)
     if mode == "ablate":
         for (M, N, K) in [(4096, 3136, 3136), (512, 3136, 3136)]:
