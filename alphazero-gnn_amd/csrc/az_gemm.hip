@@ -562,6 +562,32 @@ static void plan(GemmArgs& a, int bm, int bn, int bk, size_t ws_bytes) {
   if (S > 1) a.splits = (a.K + a.kc - 1) / a.kc;
 }
 
+// Split factor for the 128x128 LDS-DMA tile when its grid alone is small.  At most 2 blocks fit
+// a CU (64 KB of LDS each), so the launch runs in ceil(blocks / 256) block-rounds per CU, each
+// as long as one split's k-tiles; two co-resident blocks hide each other's latency (~1.1x,
+// measured), and every extra split costs an M x N slab written and re-read.  The model
+// reproduces the MI355X sweep ranking (tools/gemm_sweep.py glds: M=512 -> S=5, M=256 -> S=5).
+static int glds_splits(const GemmArgs& a, long tiles, size_t ws_bytes) {
+  const int bk = 32;
+  int best = 1;
+  double best_cost = 1e30;
+  for (int S = 1; S <= 16; ++S) {
+    const long kc = ((a.K + S - 1) / S + bk - 1) / bk * bk;
+    if (S > 1 && (kc < 4 * bk || (size_t)S * a.M * a.N * 4 > ws_bytes || !a.slab)) break;
+    const long splits = (a.K + kc - 1) / kc;
+    const long nwg = tiles * splits;
+    const long rounds = (nwg + 255) / 256;
+    double cost = (double)rounds * (double)(kc / bk) / (nwg > 256 ? 1.1 : 1.0);
+    // slab round trip (S x M x N x 8 B at ~5 TB/s) in units of one k-tile (~2 us)
+    if (splits > 1) cost += (double)splits * a.M * a.N * 8.0 / 5e12 / 2e-6;
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = (int)splits;
+    }
+  }
+  return best;
+}
+
 int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
   AZ_REQUIRE(d != nullptr, AZ_EINVAL, "az_gemm_f32: null descriptor");
   AZ_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, AZ_EINVAL, "az_gemm_f32: negative size");
@@ -609,11 +635,22 @@ int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
   if (env_cfg) {
     cfg = std::min(std::max(atoi(env_cfg), 0), kNumCfgs - 1);
     if (cfg >= 6 && !glds_ok) cfg = 0;
+  } else if (glds_ok && d->M > 128) {
+    // LDS-DMA tiles (tools/gemm_sweep.py glds on MI355X): 128x64 once the grid fills the chip,
+    // 128x128 + split-K below that
+    const long t128 = (long)((d->M + 127) / 128) * ((d->N + 127) / 128);
+    cfg = t128 >= 256 ? 8 : 6;
   } else {
-    cfg = 0;  // 64x64x32 measured fastest for every shape of the path (tools/gemm_sweep.py)
+    cfg = 0;  // register-staged 64x64x32: gathered / concatenated operands, small M
   }
   const TileCfg& tc = kCfgs[cfg];
   plan(a, tc.bm, tc.bn, tc.bk, d->ws_bytes);
+  if (cfg == 6 && !getenv("AZ_GEMM_SPLITS")) {
+    const int S = glds_splits(a, (long)((a.M + 127) / 128) * ((a.N + 127) / 128), d->ws_bytes);
+    a.splits = S;
+    a.kc = S > 1 ? ((a.K + S - 1) / S + 31) / 32 * 32 : a.K;
+    if (S > 1) a.splits = (a.K + a.kc - 1) / a.kc;
+  }
   launch_cfg(cfg, a, akm, bkm, s);
   int rc = check_launch("gemm_f32_mfma");
   if (rc || a.splits <= 1) return rc;
