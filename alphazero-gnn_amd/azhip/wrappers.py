@@ -20,6 +20,42 @@ def _dev_array(rows, dtype, device):
     return torch.from_numpy(np.ascontiguousarray(np.array(rows), dtype=dtype)).to(device)
 
 
+class PendingPrediction:
+    """A batched prediction in flight on the device stream: boards went up from pinned host
+    memory, the kernels are queued, the outputs come back into pinned host memory behind an
+    event.  result() waits for that event only (the host keeps working meanwhile)."""
+
+    def __init__(self, out_host, event, n, A, both):
+        self.out_host, self.event, self.n, self.A, self.both = out_host, event, n, A, both
+
+    def result(self):
+        self.event.synchronize()
+        out = self.out_host[:self.n].numpy().copy()
+        A = self.A
+        if self.both:
+            return out[:, :A], out[:, A], out[:, A + 1:2 * A + 1], out[:, 2 * A + 1]
+        return out[:, :A], out[:, A], None, None
+
+
+class _PinnedRing:
+    """Pinned host staging buffers reused round-robin (`depth` predictions in flight)."""
+
+    def __init__(self, depth=4):
+        self.depth, self.i, self.bufs = depth, 0, {}
+
+    def get(self, key, shape, dtype):
+        k = (key, self.i % self.depth)
+        b = self.bufs.get(k)
+        if b is None or b.shape[0] < shape[0] or tuple(b.shape[1:]) != tuple(shape[1:]):
+            b = torch.empty((max(shape[0], 1024),) + tuple(shape[1:]), dtype=dtype,
+                            pin_memory=True)
+            self.bufs[k] = b
+        return b
+
+    def advance(self):
+        self.i += 1
+
+
 class NetWrapper:
     """Common body; subclasses choose the board network class and whether a GNN exists."""
 
@@ -64,6 +100,36 @@ class NetWrapper:
         self.nnet.eval()
         pi, v = self._eval(boards, False)
         return pi.cpu().numpy(), v.cpu().numpy()
+
+    def _launch(self, boards, both):
+        """Queue a batched prediction; returns a PendingPrediction (see predict_*_async)."""
+        if not hasattr(self, "_ring"):
+            self._ring = _PinnedRing()
+        boards = np.asarray(boards)
+        n = boards.shape[0]
+        A = self.action_size
+        hb = self._ring.get("in", (n,) + boards.shape[1:], torch.int8)
+        hb[:n].numpy()[...] = boards
+        b = hb[:n].to(self.device, non_blocking=True)
+        self.nnet.eval()
+        f = self.nnet.features(b)
+        _, pi, v = self.nnet.heads(f)
+        if both:
+            self.gnn.eval()
+            _, gpi, gv = self.nnet.heads(self.gnn.forward_per_row(f))
+            out = torch.cat([pi, v[:, None], gpi, gv[:, None]], dim=1)
+        else:
+            out = torch.cat([pi, v[:, None]], dim=1)
+        ho = self._ring.get("out", tuple(out.shape), torch.float32)
+        ho[:n].copy_(out, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ring.advance()
+        return PendingPrediction(ho, ev, n, A, both)
+
+    def predict_batch_async(self, boards):
+        """predict_batch without waiting: .result() -> (pi, v, None, None)."""
+        return self._launch(boards, False)
 
     def save_checkpoint(self, folder, filename):
         if self.makedirs_on_save and not os.path.exists(folder):
@@ -208,6 +274,10 @@ class GNNWrapperMixin:
         out = torch.cat([pi, v[:, None], gpi, gv[:, None]], dim=1).cpu().numpy()
         A = self.action_size
         return out[:, :A], out[:, A], out[:, A + 1:2 * A + 1], out[:, 2 * A + 1]
+
+    def predict_both_async(self, boards):
+        """predict_both without waiting: .result() -> (pi, v, gnn_pi, gnn_v)."""
+        return self._launch(boards, True)
 
     def train(self, examples, gnn_examples=None):
         self._train(examples, gnn_examples)

@@ -12,22 +12,25 @@ import numpy as np
 
 
 def _has_run(mask, w):
-    """True when `mask` (bool [n, n]) has w consecutive Trues along axis 0, axis 1 or either
-    diagonal (the four scans of Connect4Game.py:75-97)."""
+    """True when `mask` (bool [n, n], [column x][row y]) has w consecutive Trues along a column,
+    a row or either diagonal (the four scans of Connect4Game.py:75-97), as a bitboard test:
+    cell (x, y) is bit x*(n+1) + y, the extra bit per column is always 0 so no run wraps, and
+    a run of w along direction step s exists iff bb & bb>>s & ... & bb>>(w-1)s != 0."""
     n = mask.shape[0]
     if w > n:
         return False
-    m = mask.astype(np.int8)
-    span = n - w + 1
-    # axis 0 (x varies, y fixed) and axis 1
-    a0 = sum(m[i:i + span, :] for i in range(w))
-    a1 = sum(m[:, i:i + span] for i in range(w))
-    if (a0 == w).any() or (a1 == w).any():
-        return True
-    # x+i, y+i  and  x+i, y-i
-    d1 = sum(m[i:i + span, i:i + span] for i in range(w))
-    d2 = sum(m[i:i + span, w - 1 - i:w - 1 - i + span] for i in range(w))
-    return bool((d1 == w).any() or (d2 == w).any())
+    padded = np.zeros((n, n + 1), dtype=bool)
+    padded[:, :n] = mask
+    bb = int.from_bytes(np.packbits(padded.ravel(), bitorder="little").tobytes(), "little")
+    for s in (1, n + 1, n + 2, n):       # along y, along x, (x+1, y+1), (x+1, y-1)
+        m = bb
+        for k in range(1, w):
+            m &= bb >> (k * s)
+            if not m:
+                break
+        if m:
+            return True
+    return False
 
 
 class Connect4Game:

@@ -39,6 +39,31 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Sum NV per-lane values (NV a power of two <= 64) over the 64 lanes at once: each halving step
+// exchanges the half of the values a lane does not keep (xor 32, 16, ...), so NV values cost
+// NV-1 + (6 - log2 NV) shuffles instead of 6 NV.  Returns the sum of value index
+// lane >> (6 - log2 NV) (every lane of that group holds it).
+template <int NV>
+__device__ __forceinline__ float wave_multi_sum(float (&v)[NV]) {
+  static_assert(NV >= 1 && NV <= 64 && (NV & (NV - 1)) == 0, "NV must be a power of two");
+  const int lane = threadIdx.x & 63;
+  int m = 32;
+#pragma unroll
+  for (int n = NV; n > 1; n >>= 1, m >>= 1) {
+    const bool hi = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < n / 2; ++i) {
+      const float keep = hi ? v[i + n / 2] : v[i];
+      const float send = hi ? v[i] : v[i + n / 2];
+      v[i] = keep + __shfl_xor(send, m, 64);
+    }
+  }
+  float r = v[0];
+#pragma unroll
+  for (; m > 0; m >>= 1) r += __shfl_xor(r, m, 64);
+  return r;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

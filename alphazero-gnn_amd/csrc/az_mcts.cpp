@@ -331,6 +331,7 @@ struct az_mcts {
   std::vector<Tree> trees;
   std::vector<int32_t> last_order;             // slots of the last collect, in output order
   std::vector<int8_t> leafbuf;
+  int threads = 1;                             // host threads of the last collect (feed too)
 };
 
 namespace {
@@ -527,6 +528,7 @@ int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int thr
   const int S = (int)m->trees.size();
   std::vector<uint8_t> has(S, 0);
   if (threads < 1) threads = 1;
+  m->threads = threads;
 #pragma omp parallel for schedule(dynamic, 8) num_threads(threads)
   for (int s = 0; s < S; ++s) {
     Tree& t = m->trees[s];
@@ -556,9 +558,13 @@ int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const f
   if (!failed && (!pi || !v || (m->use_gnn && (!gpi || !gv))))
     return fail(AZM_EINVAL, "az_mcts_feed: missing network outputs");
   const int A = m->R.A;
+  for (int i = 0; i < count; ++i)
+    if (m->trees[m->last_order[i]].pending_leaf < 0)
+      return fail(AZM_ESTATE, "az_mcts_feed: slot has no pending leaf");
+  // every leaf belongs to a different slot's tree: the expansions are independent
+#pragma omp parallel for schedule(dynamic, 8) num_threads(m->threads) if (count >= 32)
   for (int i = 0; i < count; ++i) {
     Tree& t = m->trees[m->last_order[i]];
-    if (t.pending_leaf < 0) return fail(AZM_ESTATE, "az_mcts_feed: slot has no pending leaf");
     expand(m, t, failed ? nullptr : pi + (size_t)i * A, failed ? 0.f : v[i],
            (failed || !m->use_gnn) ? nullptr : gpi + (size_t)i * A,
            (failed || !m->use_gnn) ? 0.f : gv[i], failed != 0);

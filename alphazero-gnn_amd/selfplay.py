@@ -137,109 +137,178 @@ def _net_call(nnet, boards, want_gnn):
         np.array([x for _, x in g], np.float32)
 
 
+class _Immediate:
+    """A prediction computed synchronously (network without *_async entry points)."""
+
+    def __init__(self, out=None, err=None):
+        self.out, self.err = out, err
+
+    def result(self):
+        if self.err is not None:
+            raise self.err
+        return self.out
+
+
+def _launch(nnet, boards, want_gnn):
+    fn = getattr(nnet, "predict_both_async" if want_gnn else "predict_batch_async", None)
+    try:
+        if fn is not None:
+            return fn(boards)
+        return _Immediate(_net_call(nnet, boards, want_gnn))
+    except Exception as ex:
+        return _Immediate(err=ex)
+
+
+class _Lane:
+    """One native engine and the episodes running in its slots."""
+
+    def __init__(self, game, nnet, args, G, cpuct, use_gnn, threads, queue, seeds, results):
+        from mcts_native import Engine
+        self.game, self.nnet, self.args = game, nnet, args
+        self.use_gnn, self.threads = use_gnn, threads
+        self.eng = Engine(game, G, cpuct, use_gnn)
+        self.queue, self.seeds, self.results = queue, seeds, results
+        self.free = list(range(G))[::-1]
+        self.gens = {}            # slot -> [episode, generator]
+        self.searching = set()    # slots waiting for their engine searches
+        self.predicting = {}      # slot -> board waiting for a standard prediction
+        self.k, self.pred = 0, []
+        self.rounds = self.rows = 0
+
+    def _handle(self, slot, req):
+        if req[0] == "search":
+            self.eng.begin(slot, req[1], req[2])
+            self.searching.add(slot)
+        else:
+            self.predicting[slot] = req[1]
+
+    def _resume(self, slot, value=None, exc=None):
+        e, gen = self.gens[slot]
+        try:
+            req = gen.throw(exc) if exc is not None else gen.send(value)
+        except StopIteration as stop:
+            self.results[e] = stop.value
+            del self.gens[slot]
+            self.free.append(slot)
+            return
+        self._handle(slot, req)
+
+    def start(self):
+        from mcts_native import NativeMCTS
+        while self.queue and self.free:
+            slot = self.free.pop()
+            e = self.queue.pop()
+            self.eng.reset(slot)
+            rng = np.random.RandomState(self.seeds[e])
+            gen = episode_g(self.game, self.args, NativeMCTS(self.eng, slot, self.game, self.args,
+                                                             rng), rng)
+            self.gens[slot] = [e, gen]
+            try:
+                req = next(gen)
+            except StopIteration as stop:
+                self.results[e] = stop.value
+                del self.gens[slot]
+                self.free.append(slot)
+                continue
+            self._handle(slot, req)
+
+    def gather(self):
+        """Advance the searches to their next leaves -> boards to evaluate (or None)."""
+        self.k = self.eng.collect(self.threads)
+        self.pred = list(self.predicting.items())
+        self.predicting.clear()
+        if not self.k and not self.pred:
+            return None
+        boards = self.eng.leaf_boards[:self.k]
+        if self.pred:
+            boards = np.concatenate([boards, np.stack([np.asarray(b, np.int8)
+                                                       for _, b in self.pred])])
+        self.rounds += 1
+        self.rows += len(boards)
+        return boards
+
+    def deliver(self, pending):
+        """Feed a finished prediction (or none), resume every slot that can move on."""
+        if pending is not None:
+            try:
+                pi, v, gpi, gv = pending.result()
+                err = None
+            except Exception as ex:   # the reference's per-leaf degradation (MCTS.py:195-200)
+                err = ex
+            k = self.k
+            if k:
+                if err is None:
+                    self.eng.feed(k, pi, v, gpi, gv)
+                else:
+                    self.eng.feed(k, failed=True)
+            for i, (slot, _) in enumerate(self.pred):
+                if err is None:
+                    self._resume(slot, (pi[k + i], v[k + i]))
+                else:
+                    self._resume(slot, exc=err)     # unguarded in the reference (MCTS.py:108-113)
+        rem = self.eng.remaining_all()
+        for s in [s for s in sorted(self.searching) if rem[s] == 0]:
+            self.searching.discard(s)
+            self._resume(s)
+        self.start()
+
+    def live(self):
+        return bool(self.gens)
+
+
 def play_episodes_native(game, nnet, args, episodes, seeds, parallel_games=256, threads=None,
-                         stats=None):
+                         stats=None, lanes=2):
     """play_episodes with the searches in the native engine (mcts_native.py, libaz_mcts.so).
 
-    Every round: the engine advances all slots' searches to their next new leaf (host
-    threads), the leaves plus any pending root predictions go to the network as ONE batch,
-    the results are fed back, and slots whose searches finished resume their episode logic
-    (Coach.episode_g over NativeMCTS).  Same per-episode results as play_episodes."""
+    The games are split over `lanes` engines that take turns: while one lane's leaf batch is
+    on the GPU (predict_*_async: pinned copies + kernels + an event), the host advances the
+    other lane's searches to their next leaves (engine threads) and resumes its finished
+    moves.  Every round of a lane is: collect its leaves (+ pending root predictions) -> ONE
+    batched network launch -> feed -> resume.  Same per-episode results as play_episodes for
+    any lane count or slot count (each game owns its RandomState and tree)."""
     import time
-    from mcts_native import Engine, NativeMCTS
     threads = int(threads or min(16, os.cpu_count() or 1))
     use_gnn = bool(getattr(args, "use_gnn", False) if not isinstance(args, dict)
                    else args.get("use_gnn", False))
     cpuct = args["cpuct"] if isinstance(args, dict) else args.cpuct
     episodes = list(episodes)
     G = max(1, min(int(parallel_games), len(episodes) or 1))
-    eng = Engine(game, G, cpuct, use_gnn)
-    pending = episodes[::-1]
-    free = list(range(G))[::-1]
-    gens = {}             # slot -> [episode, generator]
-    searching = set()     # slots waiting for their engine searches
-    predicting = {}       # slot -> board waiting for a standard prediction
+    lanes = max(1, min(int(lanes), G))
+    queue = episodes[::-1]
     results = {}
-    t_net = t_host = 0.0
-    rounds = rows = 0
-
-    def handle(slot, req):
-        if req[0] == "search":
-            eng.begin(slot, req[1], req[2])
-            searching.add(slot)
-        else:
-            predicting[slot] = req[1]
-
-    def resume(slot, value=None, exc=None):
-        e, gen = gens[slot]
-        try:
-            req = gen.throw(exc) if exc is not None else gen.send(value)
-        except StopIteration as stop:
-            results[e] = stop.value
-            del gens[slot]
-            free.append(slot)
-            return
-        handle(slot, req)
-
-    def start():
-        while pending and free:
-            slot = free.pop()
-            e = pending.pop()
-            eng.reset(slot)
-            rng = np.random.RandomState(seeds[e])
-            gen = episode_g(game, args, NativeMCTS(eng, slot, game, args, rng), rng)
-            gens[slot] = [e, gen]
-            try:
-                req = next(gen)
-            except StopIteration as stop:
-                results[e] = stop.value
-                del gens[slot]
-                free.append(slot)
-                continue
-            handle(slot, req)
-
-    start()
-    while gens:
-        t0 = time.perf_counter()
-        k = eng.collect(threads)
-        pred = list(predicting.items())
-        t1 = time.perf_counter()
-        t_host += t1 - t0
-        if k or pred:
-            boards = eng.leaf_boards[:k]
-            if pred:
-                boards = np.concatenate([boards, np.stack([np.asarray(b, np.int8)
-                                                           for _, b in pred])])
-            try:
-                pi, v, gpi, gv = _net_call(nnet, boards, use_gnn)
-                err = None
-            except Exception as ex:  # the reference's per-leaf degradation (MCTS.py:195-200)
-                err = ex
-            t2 = time.perf_counter()
-            t_net += t2 - t1
-            rounds += 1
-            rows += len(boards)
-            if k:
-                if err is None:
-                    eng.feed(k, pi, v, gpi, gv)
-                else:
-                    eng.feed(k, failed=True)
-            predicting.clear()
-            for i, (slot, _) in enumerate(pred):
-                if err is None:
-                    resume(slot, (pi[k + i], v[k + i]))
-                else:
-                    resume(slot, exc=err)     # unguarded in the reference (MCTS.py:108-113)
-        t3 = time.perf_counter()
-        rem = eng.remaining_all()
-        done = [s for s in sorted(searching) if rem[s] == 0]
-        for s in done:
-            searching.discard(s)
-            resume(s)
-        start()
-        t_host += time.perf_counter() - t3
-        if not (k or pred or done) and gens:
-            raise RuntimeError("native self-play made no progress (engine/driver state bug)")
+    per = [G // lanes + (1 if i < G % lanes else 0) for i in range(lanes)]
+    L = [_Lane(game, nnet, args, n, cpuct, use_gnn, threads, queue, seeds, results) for n in per]
+    for lane in L:
+        lane.start()
+    inflight = [None] * lanes
+    t0 = time.perf_counter()
+    t_wait = 0.0
+    idle = 0
+    i = 0
+    while any(lane.live() for lane in L) or any(x is not None for x in inflight):
+        lane = L[i]
+        if inflight[i] is not None:
+            tw = time.perf_counter()
+            p, inflight[i] = inflight[i], None
+            if hasattr(p, "event"):
+                p.event.synchronize()
+            t_wait += time.perf_counter() - tw
+            lane.deliver(p)
+            idle = 0
+        if lane.live():
+            boards = lane.gather()
+            if boards is not None:
+                inflight[i] = _launch(nnet, boards, use_gnn)
+                idle = 0
+            else:
+                lane.deliver(None)          # searches that finished without a leaf
+                idle += 1
+                if idle > 4 * lanes + 4 and not any(x is not None for x in inflight):
+                    if all(not ln.live() for ln in L):
+                        break
+                    raise RuntimeError("native self-play made no progress (engine/driver bug)")
+        i = (i + 1) % lanes
     if stats is not None:
-        stats.update(rounds=rounds, rows=rows, net_s=t_net, host_s=t_host)
+        stats.update(rounds=sum(ln.rounds for ln in L), rows=sum(ln.rows for ln in L),
+                     net_s=t_wait, host_s=time.perf_counter() - t0 - t_wait, lanes=lanes)
     return results

@@ -44,6 +44,8 @@ def parse():
                     help="self-play leg: games per GPU, all played in lock step")
     ap.add_argument("--sp-sims", type=int, default=100, help="numMCTSSims (SURVEY §8d config 3)")
     ap.add_argument("--sp-threads", type=int, default=16, help="host threads for the engine")
+    ap.add_argument("--sp-lanes", type=int, default=2,
+                    help="engines taking turns so host search overlaps the GPU batch")
     return ap.parse_args()
 
 
@@ -131,12 +133,13 @@ def selfplay_leg(W, G, args, device, rank):
     net.gnn.load_state_dict({k: torch.from_numpy(v) for k, v in G.items()})
     eps = list(range(rank * args.sp_games, (rank + 1) * args.sp_games))
     seeds = {e: 12345 + e for e in eps}
+    lanes = getattr(args, "sp_lanes", 2)
     play_episodes_native(Connect4Game(7), net, selfplay_args(2), eps[:8], seeds, 8,
-                         threads=args.sp_threads)                       # warm-up
+                         threads=args.sp_threads, lanes=lanes)          # warm-up
     st = {}
     t0 = time.perf_counter()
     out = play_episodes_native(Connect4Game(7), net, sa, eps, seeds, args.sp_games,
-                               threads=args.sp_threads, stats=st)
+                               threads=args.sp_threads, stats=st, lanes=lanes)
     dt = time.perf_counter() - t0
     moves = sum(len(std) // 2 for std, _ in out.values())
     return dt, {"games": len(out), "moves": moves, "evals": st["rows"], "rounds": st["rounds"],
@@ -298,8 +301,8 @@ def main():
                    "evals_per_s": round(world * sp["evals"] / dt, 1),
                    "seconds": round(dt, 2), "games_per_gpu": args.sp_games,
                    "config": "Connect4 7x7, use_gnn, numMCTSSims %d, expand_by 5, cpuct 1.0, "
-                             "tempThreshold 15; native lock-step MCTS, %d host threads"
-                             % (args.sp_sims, args.sp_threads)})
+                             "tempThreshold 15; native lock-step MCTS, %d host threads, %d lanes"
+                             % (args.sp_sims, args.sp_threads, args.sp_lanes)})
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -22,6 +22,9 @@ Fixtures:
                          every NN output the search requested, the examples
      mcts_ttt3.npz/json  TicTacToe 3x3 GNN self-play episodes with expand_tree
   G7 coach_ttt3.json     one full TicTacToe 3x3 GNN Coach iteration (seeds 0): counts, arena W/L/D
+  G8 rules.npz           game rules on random-play positions (Connect4 n=7,5; TicTacToe n=3,4):
+                         getGameEnded for both players, getValidMoves, every legal next state,
+                         getSymmetries boards and policies
 """
 import argparse
 import importlib.util
@@ -485,12 +488,65 @@ def g7():
     print("  G7", res)
 
 
+# ----------------------------------------------------------------------------------- G8
+def g8():
+    """Connect4Game.py:116-219 / TicTacToeGame.py on positions reached by seeded random play
+    (terminal ones included)."""
+    out = {}
+    rng = np.random.default_rng(8)
+    for name, game, count in (("c4n7", Connect4Game(7), 400), ("c4n5", Connect4Game(5), 200),
+                              ("ttt3", TicTacToeGame(3), 200), ("ttt4", TicTacToeGame(4), 200)):
+        A = game.getActionSize()
+        n = game.getBoardSize()[0]
+        boards, ended, valids, nxt, nxt_player, sym_b, sym_p = [], [], [], [], [], [], []
+        for _ in range(count):
+            b, p = game.getInitBoard(), 1
+            for _ in range(int(rng.integers(0, n * n + 2))):
+                if game.getGameEnded(b, p) != 0:
+                    break
+                v = game.getValidMoves(b, p)
+                b, p = game.getNextState(b, p, int(rng.choice(np.flatnonzero(v))))
+            c = game.getCanonicalForm(b, p)
+            boards.append(c.astype(np.int8))
+            e1, e2 = game.getGameEnded(c, 1), game.getGameEnded(c, -1)
+            ended.append([float(e1), float(e2), isinstance(e1, int), isinstance(e2, int)])
+            vm = np.asarray(game.getValidMoves(c, 1))
+            valids.append(vm.astype(np.int8))
+            ns = np.zeros((A, n, n), np.int8)
+            npl = np.zeros(A, np.int8)
+            for a in np.flatnonzero(vm):
+                nb, pl = game.getNextState(c, 1, int(a))
+                ns[a] = nb
+                npl[a] = pl
+            nxt.append(ns)
+            nxt_player.append(npl)
+            pi = rng.random(A)
+            pi /= pi.sum()
+            sym = game.getSymmetries(c, pi)
+            sym_b.append(np.stack([np.asarray(x).astype(np.int8) for x, _ in sym]))
+            sym_p.append(np.stack([np.asarray(y, np.float64) for _, y in sym]))
+            sym_p[-1] = np.concatenate([pi[None], sym_p[-1]])
+        out.update({f"{name}/boards": np.stack(boards), f"{name}/ended": np.array(ended),
+                    f"{name}/valids": np.stack(valids), f"{name}/next": np.stack(nxt),
+                    f"{name}/next_player": np.stack(nxt_player),
+                    f"{name}/sym_boards": np.stack(sym_b), f"{name}/sym_pi": np.stack(sym_p)})
+    np.savez_compressed(out_path("rules.npz"), **out)
+
+
+def out_path(name):
+    return os.path.join(HERE, name)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", nargs="*", default=None)
     a = ap.parse_args()
-    want = set(a.only) if a.only else {"g1", "g2", "g3", "g4", "g5", "g6", "g7"}
+    want = set(a.only) if a.only else {"g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8"}
     t0 = time.time()
+    if want == {"g8"}:
+        g8()
+        print(f"G8 done {time.time() - t0:.1f}s")
+        return
     c4net, c4b = g1()
     print(f"G1 done {time.time() - t0:.1f}s")
     c4sd = sd_np(c4net.nnet)
@@ -511,6 +567,9 @@ def main():
     if "g7" in want:
         g7()
         print(f"G7 done {time.time() - t0:.1f}s")
+    if "g8" in want:
+        g8()
+        print(f"G8 done {time.time() - t0:.1f}s")
 
 
 if __name__ == "__main__":
