@@ -27,6 +27,17 @@ def _flag(args, name, default=False):
         return default
 
 
+def _native_ok(game):
+    """The native engine covers Connect4Game / TicTacToeGame boards up to 64 cells."""
+    try:
+        import mcts_native
+        mcts_native.game_kind(game)
+        mcts_native.lib()
+        return True
+    except (ValueError, RuntimeError, OSError):
+        return False
+
+
 def episode_g(game, args, mcts, rng=None):
     """Coach.py:27-79 as a search generator (see MCTS.py): one self-play game ->
     (std_examples, gnn_examples), with the final result r signed per example by whether its
@@ -87,9 +98,10 @@ class Coach:
         """One iteration's self-play (Coach.py:95-100) -> [(std, gnn)] in episode order.
 
         parallel_games <= 1 on one rank: the reference's sequential loop on the global RNG.
-        Otherwise lock-step batched games (selfplay.py), episode e on rank e mod P with its own
-        RandomState; results gathered on every rank and ordered by episode, so every P and G
-        produce the same examples."""
+        Otherwise lock-step batched games, episode e on rank e mod P with its own RandomState:
+        whole episodes in the native engine (selfplay.play_episodes_engine; args.selfplay_engine
+        = "python" selects the Python search generators instead); results gathered on every
+        rank and ordered by episode, so every P and G produce the same examples."""
         n = self.args.numEps
         parallel = int(_flag(self.args, "parallel_games", 1) or 1)
         world, rank = D.world_rank()
@@ -99,11 +111,16 @@ class Coach:
                 self.mcts = MCTS(self.game, self.nnet, self.args)
                 out.append(self.executeEpisode())
             return out
-        from selfplay import episode_seeds, play_episodes
+        from selfplay import episode_seeds, play_episodes, play_episodes_engine
         base = D.broadcast_int(np.random.randint(0, 2 ** 31 - 1))
         seeds = episode_seeds(base, range(n))
-        local = play_episodes(self.game, self.nnet, self.args, D.my_episodes(n, world, rank),
-                              seeds, parallel_games=max(1, parallel))
+        mine = D.my_episodes(n, world, rank)
+        if _flag(self.args, "selfplay_engine", "native") == "native" and _native_ok(self.game):
+            local = play_episodes_engine(self.game, self.nnet, self.args, mine, seeds,
+                                         parallel_games=max(1, parallel))
+        else:
+            local = play_episodes(self.game, self.nnet, self.args, mine, seeds,
+                                  parallel_games=max(1, parallel))
         allr = D.gather_episodes(local)
         return [allr[e] for e in range(n)]
 

@@ -220,6 +220,95 @@ struct Rules {
   }
 };
 
+// ----------------------------------------------------------------------------- numpy RandomState
+// np.random.RandomState(seed) (legacy MT19937: init_genrand seeding, 53-bit doubles from two
+// draws, masked-rejection bounded ints) and the two RandomState.choice forms the episode uses
+// (Coach.py:62 `choice(len(pi), p=pi)`, MCTS.py:41 `choice(bestAs)`), draw for draw.
+struct MT19937 {
+  uint32_t s[624];
+  int i = 624;
+  void seed(uint32_t x) {
+    s[0] = x;
+    for (int k = 1; k < 624; ++k) s[k] = 1812433253u * (s[k - 1] ^ (s[k - 1] >> 30)) + (uint32_t)k;
+    i = 624;
+  }
+  void twist() {
+    for (int k = 0; k < 624; ++k) {
+      const uint32_t y = (s[k] & 0x80000000u) | (s[(k + 1) % 624] & 0x7fffffffu);
+      s[k] = s[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    i = 0;
+  }
+  uint32_t next() {
+    if (i >= 624) twist();
+    uint32_t y = s[i++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+  double next_double() {                        // random_sample()
+    const uint32_t a = next() >> 5, b = next() >> 6;
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+  int64_t randint(int64_t n) {                  // randint(0, n), legacy masked rejection
+    const uint64_t rng = (uint64_t)(n - 1);
+    if (rng == 0) return 0;
+    uint64_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
+    mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
+    uint32_t v;
+    while ((v = next() & (uint32_t)mask) > rng) {}
+    return v;
+  }
+  int choice_p(const double* p, int n) {        // choice(n, p=p): cumsum / last, searchsorted right
+    double cdf[130];
+    cdf[0] = p[0];
+    for (int k = 1; k < n; ++k) cdf[k] = cdf[k - 1] + p[k];
+    const double last = cdf[n - 1];
+    for (int k = 0; k < n; ++k) cdf[k] /= last;
+    const double u = next_double();
+    int k = 0;
+    while (k < n && !(cdf[k] > u)) ++k;
+    return k;
+  }
+};
+
+// ----------------------------------------------------------------------------- episodes
+// Coach.executeEpisode (Coach.py:27-79) as a per-slot state machine: getActionProb's searches,
+// its pi and temp-0 tie-break, expand_tree's extra searches and root prediction, the move draw,
+// the rules.  Every move is recorded; Python assembles the examples from the records with the
+// same code as the sequential path (mcts_native.assemble_episode).
+enum Phase : uint8_t { E_IDLE, E_START_MOVE, E_AP, E_EXP_CHECK, E_EXP_PRE, E_EXP_STD, E_EXP, E_MOVE,
+                       E_DONE };
+
+struct Episode {
+  Phase phase = E_IDLE;
+  bool harvested = true;
+  MT19937 rng;
+  Key board{0, 0};        // canonical board of the player to move
+  int cur = 1, step = 0;
+  int sims = 0, expand_by = 0, temp_threshold = 0;
+  Val result{0.0, T_INT};
+  // per-move records, A-strided
+  std::vector<Key> boards;
+  std::vector<int8_t> curs, temps;
+  std::vector<int32_t> actions, counts, init_nsa, exp_nsa;
+  std::vector<int8_t> init_has, exp_tag;
+  std::vector<double> pi, exp_q;
+  std::vector<float> std_v;
+  void reset() {
+    boards.clear(); curs.clear(); temps.clear(); actions.clear(); counts.clear();
+    init_nsa.clear(); exp_nsa.clear(); init_has.clear(); exp_tag.clear(); pi.clear();
+    exp_q.clear(); std_v.clear();
+    board = {0, 0};
+    cur = 1;
+    step = 0;
+    result = {0.0, T_INT};
+  }
+};
+
 // ----------------------------------------------------------------------------- trees
 struct Node {
   Key key;
@@ -248,6 +337,8 @@ struct Tree {
   int pending_leaf = -1;                      // node waiting for the network
   std::vector<std::pair<int32_t, int32_t>> path;
   int64_t nsa_total = 0, ps_count = 0;
+  bool pending_std = false;                   // episode mode: waiting for the root's predict
+  Episode ep;
 
   void clear() {
     nodes.clear();
@@ -261,6 +352,7 @@ struct Tree {
     epoch = 1;
     remaining = 0;
     pending_leaf = -1;
+    pending_std = false;
     path.clear();
     nsa_total = ps_count = 0;
   }
@@ -456,6 +548,147 @@ void expand(az_mcts* m, Tree& t, const float* pi, float v_std, const float* gpi,
   t.remaining -= 1;
 }
 
+// Root statistics into A-strided record arrays.
+void root_snapshot(const az_mcts* m, const Tree& t, const Key& root, int32_t* nsa, double* q,
+                   int8_t* tag) {
+  const int A = m->R.A;
+  for (int a = 0; a < A; ++a) {
+    nsa[a] = 0;
+    if (q) q[a] = 0.0;
+    tag[a] = AZM_TAG_NONE;
+  }
+  const int32_t id = t.find(root);
+  if (id < 0 || t.nodes[id].edge < 0) return;
+  const size_t o = (size_t)t.nodes[id].edge * A;
+  for (int a = 0; a < A; ++a) {
+    const Val& v = t.Q[o + a];
+    if (v.tag == T_NONE) continue;
+    nsa[a] = t.N[o + a];
+    if (q) q[a] = v.x;
+    tag[a] = v.tag == T_INT ? AZM_TAG_INT : (v.tag == T_F64 ? AZM_TAG_FLOAT : AZM_TAG_F32);
+  }
+}
+
+// getActionProb's tail (MCTS.py:36-58): counts -> pi, temp-0 tie-break on the slot's RNG.
+void finish_action_prob(const az_mcts* m, Tree& t) {
+  Episode& E = t.ep;
+  const int A = m->R.A;
+  const size_t mv = E.curs.size() - 1;
+  int32_t* cnt = &E.counts[mv * A];
+  std::vector<int8_t> tag(A);
+  root_snapshot(m, t, E.board, cnt, nullptr, tag.data());
+  double* pi = &E.pi[mv * A];
+  if (E.temps[mv] == 0) {
+    int32_t mx = cnt[0];
+    for (int a = 1; a < A; ++a) mx = cnt[a] > mx ? cnt[a] : mx;
+    int best[130], nb = 0;
+    for (int a = 0; a < A; ++a)
+      if (cnt[a] == mx) best[nb++] = a;
+    const int a = best[E.rng.randint(nb)];
+    for (int k = 0; k < A; ++k) pi[k] = k == a ? 1.0 : 0.0;
+  } else {
+    double total = 0.0;                         // float(sum(...)), sequential
+    for (int a = 0; a < A; ++a) total += (double)cnt[a] + 1e-8;
+    for (int a = 0; a < A; ++a) pi[a] = ((double)cnt[a] + 1e-8) / total;
+  }
+}
+
+// Advance one episode-mode slot until it waits on the network (1) or is done (0).
+int drive_episode(az_mcts* m, Tree& t) {
+  Episode& E = t.ep;
+  const int A = m->R.A;
+  for (;;) {
+    switch (E.phase) {
+      case E_START_MOVE: {
+        E.step += 1;
+        t.epoch += 1;                           // getActionProb resets the predictions
+        E.boards.push_back(E.board);
+        E.curs.push_back((int8_t)E.cur);
+        E.temps.push_back((int8_t)(E.step < E.temp_threshold ? 1 : 0));
+        E.actions.push_back(-1);
+        E.counts.resize(E.counts.size() + A, 0);
+        E.pi.resize(E.pi.size() + A, 0.0);
+        E.init_nsa.resize(E.init_nsa.size() + A, 0);
+        E.init_has.resize(E.init_has.size() + A, (int8_t)AZM_TAG_NONE);
+        E.exp_nsa.resize(E.exp_nsa.size() + A, 0);
+        E.exp_q.resize(E.exp_q.size() + A, 0.0);
+        E.exp_tag.resize(E.exp_tag.size() + A, (int8_t)AZM_TAG_NONE);
+        E.std_v.push_back(0.f);
+        t.root = E.board;
+        t.remaining = E.sims;
+        E.phase = E_AP;
+        break;
+      }
+      case E_AP:
+        if (advance(m, t)) return 1;
+        finish_action_prob(m, t);
+        E.phase = m->use_gnn ? E_EXP_CHECK : E_MOVE;
+        break;
+      case E_EXP_CHECK: {                       // expand_tree (MCTS.py:60-149)
+        const size_t mv = E.curs.size() - 1;
+        root_snapshot(m, t, E.board, &E.init_nsa[mv * A], nullptr, &E.init_has[mv * A]);
+        bool any = false;
+        for (int a = 0; a < A; ++a) any |= E.init_has[mv * A + a] != AZM_TAG_NONE;
+        if (any) {
+          E.phase = E_EXP_STD;
+        } else {
+          t.root = E.board;
+          t.remaining = E.sims;
+          E.phase = E_EXP_PRE;
+        }
+        break;
+      }
+      case E_EXP_PRE: {
+        if (advance(m, t)) return 1;
+        const size_t mv = E.curs.size() - 1;
+        root_snapshot(m, t, E.board, &E.init_nsa[mv * A], nullptr, &E.init_has[mv * A]);
+        E.phase = E_EXP_STD;
+        break;
+      }
+      case E_EXP_STD: {
+        const int32_t id = t.find(E.board);
+        if (id >= 0 && t.nodes[id].std_epoch == t.epoch) {
+          E.std_v.back() = t.nodes[id].std_v;
+          t.root = E.board;
+          t.remaining = E.expand_by;
+          E.phase = E_EXP;
+        } else {
+          t.pending_std = true;                 // root predict (served by the next batch)
+          return 1;
+        }
+        break;
+      }
+      case E_EXP: {
+        if (advance(m, t)) return 1;
+        const size_t mv = E.curs.size() - 1;
+        root_snapshot(m, t, E.board, &E.exp_nsa[mv * A], &E.exp_q[mv * A], &E.exp_tag[mv * A]);
+        E.phase = E_MOVE;
+        break;
+      }
+      case E_MOVE: {                            // Coach.py:62-79
+        const size_t mv = E.curs.size() - 1;
+        const int a = E.rng.choice_p(&E.pi[mv * A], A);
+        E.actions[mv] = a;
+        Key nk;
+        m->R.next(E.board, a, &nk);
+        E.board = nk;
+        E.cur = -E.cur;
+        const Val r = m->R.ended(nk);
+        if (r.x != 0.0) {
+          E.result = r;
+          E.phase = E_DONE;
+          E.harvested = false;
+          return 0;
+        }
+        E.phase = E_START_MOVE;
+        break;
+      }
+      default:
+        return 0;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -488,6 +721,86 @@ int az_mcts_action_size(const az_mcts* m) { return m ? m->R.A : AZM_EINVAL; }
 int az_mcts_reset(az_mcts* m, int slot) {
   if (!slot_ok(m, slot)) return fail(AZM_EINVAL, "az_mcts_reset: bad slot");
   m->trees[slot].clear();
+  m->trees[slot].ep.phase = E_IDLE;
+  m->trees[slot].ep.harvested = true;
+  return AZM_OK;
+}
+
+int az_mcts_episode_begin(az_mcts* m, int slot, uint32_t seed, int sims, int expand_by,
+                          int temp_threshold) {
+  if (!slot_ok(m, slot) || sims < 0 || expand_by < 0)
+    return fail(AZM_EINVAL, "az_mcts_episode_begin: bad args");
+  Tree& t = m->trees[slot];
+  t.clear();
+  Episode& E = t.ep;
+  E.reset();
+  E.rng.seed(seed);
+  E.sims = sims;
+  E.expand_by = expand_by;
+  E.temp_threshold = temp_threshold;
+  E.harvested = true;
+  E.phase = E_START_MOVE;
+  return AZM_OK;
+}
+
+int az_mcts_episode_finished(az_mcts* m, int32_t* slots, int cap) {
+  if (!m || !slots) return fail(AZM_EINVAL, "az_mcts_episode_finished: bad args");
+  int n = 0;
+  for (int s = 0; s < (int)m->trees.size() && n < cap; ++s) {
+    Episode& E = m->trees[s].ep;
+    if (E.phase == E_DONE && !E.harvested) {
+      E.harvested = true;
+      slots[n++] = s;
+    }
+  }
+  return n;
+}
+
+int az_mcts_episode_moves(const az_mcts* m, int slot) {
+  if (!slot_ok(m, slot)) return fail(AZM_EINVAL, "az_mcts_episode_moves: bad slot");
+  return (int)m->trees[slot].ep.curs.size();
+}
+
+int az_mcts_episode_record(const az_mcts* m, int slot, int8_t* boards, int8_t* curs,
+                           int8_t* temps, int32_t* actions, double* pi, int32_t* init_nsa,
+                           int8_t* init_has, float* std_v, int32_t* exp_nsa, double* exp_q,
+                           int8_t* exp_tag, int* result_tag, double* result) {
+  if (!slot_ok(m, slot)) return fail(AZM_EINVAL, "az_mcts_episode_record: bad slot");
+  const Episode& E = m->trees[slot].ep;
+  const int A = m->R.A, C = m->R.cells;
+  const size_t n = E.curs.size();
+  for (size_t i = 0; i < n; ++i) m->R.to_board(E.boards[i], boards + i * C);
+  std::memcpy(curs, E.curs.data(), n);
+  std::memcpy(temps, E.temps.data(), n);
+  std::memcpy(actions, E.actions.data(), n * 4);
+  std::memcpy(pi, E.pi.data(), n * A * 8);
+  std::memcpy(init_nsa, E.init_nsa.data(), n * A * 4);
+  std::memcpy(init_has, E.init_has.data(), n * A);
+  std::memcpy(std_v, E.std_v.data(), n * 4);
+  std::memcpy(exp_nsa, E.exp_nsa.data(), n * A * 4);
+  std::memcpy(exp_q, E.exp_q.data(), n * A * 8);
+  std::memcpy(exp_tag, E.exp_tag.data(), n * A);
+  *result_tag = E.result.tag == T_INT ? AZM_TAG_INT : AZM_TAG_FLOAT;
+  *result = E.result.x;
+  return AZM_OK;
+}
+
+int az_rng_test(uint32_t seed, int op, int n, const double* p, int np_, int64_t* out) {
+  // differential-test hook: op 0 = n x next uint32, 1 = n x randint(np_), 2 = n x choice(np_, p)
+  MT19937 r;
+  r.seed(seed);
+  for (int i = 0; i < n; ++i) {
+    if (op == 0) out[i] = r.next();
+    else if (op == 1) out[i] = r.randint(np_);
+    else out[i] = r.choice_p(p, np_);
+  }
+  return AZM_OK;
+}
+
+int az_rng_doubles(uint32_t seed, int n, double* out) {
+  MT19937 r;
+  r.seed(seed);
+  for (int i = 0; i < n; ++i) out[i] = r.next_double();
   return AZM_OK;
 }
 
@@ -532,10 +845,16 @@ int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int thr
 #pragma omp parallel for schedule(dynamic, 8) num_threads(threads)
   for (int s = 0; s < S; ++s) {
     Tree& t = m->trees[s];
-    if (t.pending_leaf < 0) advance(m, t);
+    if (t.pending_leaf < 0 && !t.pending_std) {
+      if (t.ep.phase != E_IDLE) drive_episode(m, t);
+      else advance(m, t);
+    }
     if (t.pending_leaf >= 0) {
       has[s] = 1;
       m->R.to_board(t.nodes[t.pending_leaf].key, &m->leafbuf[(size_t)s * m->R.cells]);
+    } else if (t.pending_std) {
+      has[s] = 1;
+      m->R.to_board(t.ep.board, &m->leafbuf[(size_t)s * m->R.cells]);
     }
   }
   m->last_order.clear();
@@ -558,13 +877,22 @@ int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const f
   if (!failed && (!pi || !v || (m->use_gnn && (!gpi || !gv))))
     return fail(AZM_EINVAL, "az_mcts_feed: missing network outputs");
   const int A = m->R.A;
-  for (int i = 0; i < count; ++i)
-    if (m->trees[m->last_order[i]].pending_leaf < 0)
-      return fail(AZM_ESTATE, "az_mcts_feed: slot has no pending leaf");
+  for (int i = 0; i < count; ++i) {
+    const Tree& t = m->trees[m->last_order[i]];
+    if (t.pending_leaf < 0 && !t.pending_std)
+      return fail(AZM_ESTATE, "az_mcts_feed: slot has no pending request");
+  }
   // every leaf belongs to a different slot's tree: the expansions are independent
 #pragma omp parallel for schedule(dynamic, 8) num_threads(m->threads) if (count >= 32)
   for (int i = 0; i < count; ++i) {
     Tree& t = m->trees[m->last_order[i]];
+    if (t.pending_std) {                        // expand_tree's root predict: v only
+      Node& nd = t.nodes[t.find_or_add(t.ep.board, m->R)];
+      nd.std_v = failed ? 0.f : v[i];
+      nd.std_epoch = t.epoch;
+      t.pending_std = false;
+      continue;
+    }
     expand(m, t, failed ? nullptr : pi + (size_t)i * A, failed ? 0.f : v[i],
            (failed || !m->use_gnn) ? nullptr : gpi + (size_t)i * A,
            (failed || !m->use_gnn) ? 0.f : gv[i], failed != 0);

@@ -50,6 +50,14 @@ _SIGS = {
     "az_game_valids": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _P]),
     "az_game_next_canonical": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, _P]),
     "az_np_pairwise_sum": (ctypes.c_double, [_P, ctypes.c_int]),
+    "az_mcts_episode_begin": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int]),
+    "az_mcts_episode_finished": (ctypes.c_int, [_P, _P, ctypes.c_int]),
+    "az_mcts_episode_moves": (ctypes.c_int, [_P, ctypes.c_int]),
+    "az_mcts_episode_record": (ctypes.c_int, [_P, ctypes.c_int] + [_P] * 13),
+    "az_rng_test": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int,
+                                   _P]),
+    "az_rng_doubles": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, _P]),
 }
 
 
@@ -182,10 +190,111 @@ class Engine:
         b = self._b8(board)
         _check(lib().az_mcts_set_std(self.h, slot, _ptr(b), float(v)), "az_mcts_set_std")
 
+    # -- episode mode ----------------------------------------------------------------------
+    def episode_begin(self, slot, seed, sims, expand_by, temp_threshold):
+        _check(lib().az_mcts_episode_begin(self.h, slot, int(seed) & 0xFFFFFFFF, int(sims),
+                                           int(expand_by), int(temp_threshold)),
+               "az_mcts_episode_begin")
+
+    def episodes_finished(self):
+        out = np.zeros(self.slots, np.int32)
+        k = _check(lib().az_mcts_episode_finished(self.h, _ptr(out), self.slots),
+                   "az_mcts_episode_finished")
+        return out[:k].tolist()
+
+    def episode_record(self, slot):
+        """Per-move records of a finished episode (see include/az_mcts.h)."""
+        n = _check(lib().az_mcts_episode_moves(self.h, slot), "az_mcts_episode_moves")
+        A, c = self.A, self.n
+        r = {"boards": np.zeros((n, c, c), np.int8), "cur": np.zeros(n, np.int8),
+             "temp": np.zeros(n, np.int8), "action": np.zeros(n, np.int32),
+             "pi": np.zeros((n, A), np.float64), "init_nsa": np.zeros((n, A), np.int32),
+             "init_has": np.zeros((n, A), np.int8), "std_v": np.zeros(n, np.float32),
+             "exp_nsa": np.zeros((n, A), np.int32), "exp_q": np.zeros((n, A), np.float64),
+             "exp_tag": np.zeros((n, A), np.int8)}
+        tag, val = ctypes.c_int(), ctypes.c_double()
+        keys = ("boards", "cur", "temp", "action", "pi", "init_nsa", "init_has", "std_v",
+                "exp_nsa", "exp_q", "exp_tag")
+        _check(lib().az_mcts_episode_record(self.h, slot, *[_ptr(r[k]) for k in keys],
+                                            ctypes.byref(tag), ctypes.byref(val)),
+               "az_mcts_episode_record")
+        r["result"] = int(val.value) if tag.value == TAG_INT else float(val.value)
+        return r
+
     def tree_stats(self, slot):
         out = np.zeros(4, np.int64)
         _check(lib().az_mcts_tree_stats(self.h, slot, _ptr(out)), "az_mcts_tree_stats")
         return {"Es": int(out[0]), "Ns": int(out[1]), "Ps": int(out[2]), "nsa_total": int(out[3])}
+
+
+def expand_result(A, init_counts, initial_value, nsa, q, tag, game=None, board=None):
+    """expand_tree's return values (MCTS.py:115-146) from root statistics: init_counts
+    {a: visits} before the expand searches, the root's standard value, and the root's
+    (nsa, q, tag) after them."""
+    initial_policy = np.zeros(A)
+    for a, c in init_counts.items():
+        initial_policy[a] = c
+    isum = np.sum(initial_policy)
+    if isum > 0:
+        initial_policy = initial_policy / isum
+    else:
+        valids = game.getValidMoves(board, 1)
+        initial_policy = valids / np.sum(valids)
+    expanded_policy = np.zeros(A)
+    for a in range(A):
+        if tag[a] != TAG_NONE:
+            expanded_policy[a] = nsa[a]
+    esum = np.sum(expanded_policy)
+    if esum > 0:
+        expanded_policy = expanded_policy / esum
+    else:
+        expanded_policy = initial_policy
+    expanded_value = 0
+    valid_count = 0
+    for a in range(A):
+        if tag[a] != TAG_NONE and nsa[a] > 0:
+            expanded_value += typed_q(tag[a], q[a]) * nsa[a]
+            valid_count += nsa[a]
+    expanded_value = expanded_value / valid_count if valid_count > 0 else initial_value
+    return initial_policy, initial_value, expanded_policy, expanded_value
+
+
+def assemble_episode(game, args, rec):
+    """Coach.executeEpisode's examples (Coach.py:27-79, the same steps as Coach.episode_g)
+    from an engine episode record."""
+    use_gnn = bool(args.get("use_gnn", False) if isinstance(args, dict)
+                   else getattr(args, "use_gnn", False))
+    A = game.getActionSize()
+    examples, gnn_examples = [], []
+    for i in range(len(rec["cur"])):
+        canonical = rec["boards"][i].astype(np.int64)
+        cur = int(rec["cur"][i])
+        if rec["temp"][i] == 0:
+            pi = [int(x) for x in rec["pi"][i]]
+        else:
+            pi = rec["pi"][i].tolist()
+        sym = game.getSymmetries(canonical, pi)
+        examples.extend([b, cur, p, None] for b, p in sym)
+        if use_gnn:
+            s = game.stringRepresentation(canonical)
+            init_counts = {a: int(rec["init_nsa"][i][a]) for a in range(A)
+                           if rec["init_has"][i][a] != TAG_NONE}
+            res = expand_result(A, init_counts, np.float32(rec["std_v"][i]),
+                                rec["exp_nsa"][i].tolist(), rec["exp_q"][i].tolist(),
+                                rec["exp_tag"][i].tolist(), game, canonical)
+            for b, _ in sym:
+                if game.stringRepresentation(b) == s:
+                    gnn_examples.append([b, cur, *res, None])
+                    break
+    r = rec["result"]
+    cur = -int(rec["cur"][-1])
+
+    def sign(p):
+        return r * ((-1) ** (p != cur))
+    std = [(x[0], x[2], sign(x[1])) for x in examples]
+    if use_gnn and gnn_examples:
+        return std, [(x[0], x[1], x[2], x[3], x[4], x[5], sign(x[1])) for x in gnn_examples]
+    return std, []
 
 
 class NativeMCTS:
@@ -235,39 +344,13 @@ class NativeMCTS:
         if not initial_counts:
             yield ("search", canonicalBoard, self.args.numMCTSSims)
             initial_counts = root_visits()
-        initial_policy = np.zeros(A)
-        for a, c in initial_counts.items():
-            initial_policy[a] = c
-        isum = np.sum(initial_policy)
-        if isum > 0:
-            initial_policy = initial_policy / isum
-        else:
-            valids = self.game.getValidMoves(canonicalBoard, 1)
-            initial_policy = valids / np.sum(valids)
-
-        initial_value = self.engine.get_std(self.slot, canonicalBoard)
-        if initial_value is None:
+        std_v = self.engine.get_std(self.slot, canonicalBoard)
+        if std_v is None:
             _, std_v = yield ("predict", canonicalBoard)
             self.engine.set_std(self.slot, canonicalBoard, std_v)
-            initial_value = np.float32(std_v)
-
+        initial_value = np.float32(std_v)
         yield ("search", canonicalBoard, expand_by)
-
         nsa, q, tag = self._root(canonicalBoard)
-        expanded_policy = np.zeros(A)
-        for a in range(A):
-            if tag[a] != TAG_NONE:
-                expanded_policy[a] = nsa[a]
-        esum = np.sum(expanded_policy)
-        if esum > 0:
-            expanded_policy = expanded_policy / esum
-        else:
-            expanded_policy = initial_policy
-        expanded_value = 0
-        valid_count = 0
-        for a in range(A):
-            if tag[a] != TAG_NONE and nsa[a] > 0:
-                expanded_value += typed_q(tag[a], q[a]) * nsa[a]
-                valid_count += nsa[a]
-        expanded_value = expanded_value / valid_count if valid_count > 0 else initial_value
-        return {s: (initial_policy, initial_value, expanded_policy, expanded_value)}
+        res = expand_result(A, initial_counts, initial_value, nsa, q, tag, self.game,
+                            canonicalBoard)
+        return {s: res}

@@ -312,3 +312,121 @@ def play_episodes_native(game, nnet, args, episodes, seeds, parallel_games=256, 
         stats.update(rounds=sum(ln.rounds for ln in L), rows=sum(ln.rows for ln in L),
                      net_s=t_wait, host_s=time.perf_counter() - t0 - t_wait, lanes=lanes)
     return results
+
+
+class _EpisodeLane:
+    """One native engine running whole episodes in its slots (engine episode mode)."""
+
+    def __init__(self, game, args, G, cpuct, use_gnn, threads, queue, seeds, results, sims,
+                 expand_by, temp_threshold):
+        from mcts_native import Engine
+        self.game, self.args, self.threads = game, args, threads
+        self.eng = Engine(game, G, cpuct, use_gnn)
+        self.queue, self.seeds, self.results = queue, seeds, results
+        self.sims, self.expand_by, self.temp_threshold = sims, expand_by, temp_threshold
+        self.free = list(range(G))[::-1]
+        self.running = {}          # slot -> episode
+        self.k = 0
+        self.rounds = self.rows = 0
+        self.assemble_s = 0.0
+
+    def start(self):
+        while self.queue and self.free:
+            slot = self.free.pop()
+            e = self.queue.pop()
+            self.eng.episode_begin(slot, self.seeds[e], self.sims, self.expand_by,
+                                   self.temp_threshold)
+            self.running[slot] = e
+
+    def harvest(self):
+        import time
+        from mcts_native import assemble_episode
+        t = time.perf_counter()
+        for slot in self.eng.episodes_finished():
+            e = self.running.pop(slot)
+            self.results[e] = assemble_episode(self.game, self.args, self.eng.episode_record(slot))
+            self.free.append(slot)
+        self.assemble_s += time.perf_counter() - t
+        self.start()
+
+    def gather(self):
+        self.k = self.eng.collect(self.threads)
+        if not self.k:
+            return None
+        self.rounds += 1
+        self.rows += self.k
+        return self.eng.leaf_boards[:self.k]
+
+    def deliver(self, pending):
+        if pending is not None:
+            try:
+                pi, v, gpi, gv = pending.result()
+                self.eng.feed(self.k, pi, v, gpi, gv)
+            except Exception:     # the reference's per-leaf degradation (MCTS.py:195-200)
+                self.eng.feed(self.k, failed=True)
+        self.harvest()
+
+    def live(self):
+        return bool(self.running)
+
+
+def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024, threads=None,
+                         stats=None, lanes=2):
+    """Whole self-play episodes in the native engine (episode mode, include/az_mcts.h): search,
+    pi, move draws with each game's RandomState emulated draw for draw, expand_tree, rules --
+    Python only batches the leaves for the network and assembles each finished game's
+    examples.  Same results as play_episodes / Coach.executeEpisode per episode
+    (tests/test_native_mcts.py)."""
+    import time
+    _ = _args_val(args, "numMCTSSims")
+    threads = int(threads or min(16, os.cpu_count() or 1))
+    use_gnn = bool(_args_val(args, "use_gnn", False))
+    episodes = list(episodes)
+    G = max(1, min(int(parallel_games), len(episodes) or 1))
+    lanes = max(1, min(int(lanes), G))
+    queue = episodes[::-1]
+    results = {}
+    per = [G // lanes + (1 if i < G % lanes else 0) for i in range(lanes)]
+    L = [_EpisodeLane(game, args, n, _args_val(args, "cpuct"), use_gnn, threads, queue, seeds,
+                      results, _args_val(args, "numMCTSSims"), _args_val(args, "expand_by", 5),
+                      _args_val(args, "tempThreshold")) for n in per]
+    for lane in L:
+        lane.start()
+    inflight = [None] * lanes
+    t0 = time.perf_counter()
+    t_wait = 0.0
+    idle = 0
+    i = 0
+    while any(lane.live() for lane in L) or any(x is not None for x in inflight):
+        lane = L[i]
+        if inflight[i] is not None:
+            tw = time.perf_counter()
+            p, inflight[i] = inflight[i], None
+            if hasattr(p, "event"):
+                p.event.synchronize()
+            t_wait += time.perf_counter() - tw
+            lane.deliver(p)
+            idle = 0
+        if lane.live():
+            boards = lane.gather()
+            if boards is not None:
+                inflight[i] = _launch(nnet, boards, use_gnn)
+                idle = 0
+            else:
+                lane.deliver(None)
+                idle += 1
+                if idle > 4 * lanes + 4 and not any(x is not None for x in inflight) and \
+                        any(ln.live() for ln in L):
+                    raise RuntimeError("native self-play made no progress (engine/driver bug)")
+        i = (i + 1) % lanes
+    if stats is not None:
+        stats.update(rounds=sum(ln.rounds for ln in L), rows=sum(ln.rows for ln in L),
+                     net_s=t_wait, host_s=time.perf_counter() - t0 - t_wait, lanes=lanes,
+                     assemble_s=sum(ln.assemble_s for ln in L))
+    return results
+
+
+def _args_val(args, name, default=None):
+    if isinstance(args, dict):
+        return args.get(name, default)
+    return getattr(args, name, default)

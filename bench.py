@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-aggregate", action="store_true")
     ap.add_argument("--no-selfplay", action="store_true")
-    ap.add_argument("--sp-games", type=int, default=256,
+    ap.add_argument("--sp-games", type=int, default=1024,
                     help="self-play leg: games per GPU, all played in lock step")
     ap.add_argument("--sp-sims", type=int, default=100, help="numMCTSSims (SURVEY §8d config 3)")
     ap.add_argument("--sp-threads", type=int, default=16, help="host threads for the engine")
@@ -126,7 +126,7 @@ def selfplay_leg(W, G, args, device, rank):
     import torch
     from connect4.Connect4GNN import Connect4GNNWrapper
     from connect4.Connect4Game import Connect4Game
-    from selfplay import play_episodes_native
+    from selfplay import play_episodes_engine
     sa = selfplay_args(args.sp_sims)
     net = Connect4GNNWrapper(Connect4Game(7), sa)
     net.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()})
@@ -134,16 +134,17 @@ def selfplay_leg(W, G, args, device, rank):
     eps = list(range(rank * args.sp_games, (rank + 1) * args.sp_games))
     seeds = {e: 12345 + e for e in eps}
     lanes = getattr(args, "sp_lanes", 2)
-    play_episodes_native(Connect4Game(7), net, selfplay_args(2), eps[:8], seeds, 8,
+    play_episodes_engine(Connect4Game(7), net, selfplay_args(2), eps[:8], seeds, 8,
                          threads=args.sp_threads, lanes=lanes)          # warm-up
     st = {}
     t0 = time.perf_counter()
-    out = play_episodes_native(Connect4Game(7), net, sa, eps, seeds, args.sp_games,
+    out = play_episodes_engine(Connect4Game(7), net, sa, eps, seeds, args.sp_games,
                                threads=args.sp_threads, stats=st, lanes=lanes)
     dt = time.perf_counter() - t0
     moves = sum(len(std) // 2 for std, _ in out.values())
     return dt, {"games": len(out), "moves": moves, "evals": st["rows"], "rounds": st["rounds"],
-                "net_s": round(st["net_s"], 3), "host_s": round(st["host_s"], 3)}
+                "net_wait_s": round(st["net_s"], 3), "host_s": round(st["host_s"], 3),
+                "assemble_s": round(st.get("assemble_s", 0.0), 3)}
 
 
 def selfplay_cpu_baseline(W, G, sims, seconds):
@@ -301,7 +302,8 @@ def main():
                    "evals_per_s": round(world * sp["evals"] / dt, 1),
                    "seconds": round(dt, 2), "games_per_gpu": args.sp_games,
                    "config": "Connect4 7x7, use_gnn, numMCTSSims %d, expand_by 5, cpuct 1.0, "
-                             "tempThreshold 15; native lock-step MCTS, %d host threads, %d lanes"
+                             "tempThreshold 15; native lock-step episodes (engine), %d host "
+                             "threads, %d lanes"
                              % (args.sp_sims, args.sp_threads, args.sp_lanes)})
 
     cpu = None

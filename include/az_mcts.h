@@ -87,6 +87,28 @@ int az_mcts_set_std(az_mcts* m, int slot, const int8_t* board, float v);
 /* Tree sizes of a slot: out[0] = len(Es), out[1] = len(Ns), out[2] = len(Ps), out[3] = sum(Nsa). */
 int az_mcts_tree_stats(const az_mcts* m, int slot, int64_t* out);
 
+/* Episode mode (Coach.executeEpisode, Coach.py:27-79, run natively per slot): a fresh tree and
+ * np.random.RandomState(seed) for the slot; az_mcts_collect / az_mcts_feed then drive the
+ * whole game (getActionProb with `sims` searches and its temp-0 tie-break, expand_tree with
+ * `expand_by` searches when use_gnn, the move draw, the rules).  Requests from an episode slot
+ * are leaves or, for expand_tree, the root's standard prediction (only v is used).  Finished
+ * slots are reported once by az_mcts_episode_finished; az_mcts_episode_record copies the
+ * per-move records (n = az_mcts_episode_moves): canonical boards [n][cells], player to move,
+ * temp, action, pi [n][A] (float64; temp 0 one-hot), expand_tree root visits before/after
+ * (nsa, has/tag, q) and the root's standard value, and getGameEnded's final value + type. */
+int az_mcts_episode_begin(az_mcts* m, int slot, uint32_t seed, int sims, int expand_by,
+                          int temp_threshold);
+int az_mcts_episode_finished(az_mcts* m, int32_t* slots, int cap);
+int az_mcts_episode_moves(const az_mcts* m, int slot);
+int az_mcts_episode_record(const az_mcts* m, int slot, int8_t* boards, int8_t* curs,
+                           int8_t* temps, int32_t* actions, double* pi, int32_t* init_nsa,
+                           int8_t* init_has, float* std_v, int32_t* exp_nsa, double* exp_q,
+                           int8_t* exp_tag, int* result_tag, double* result);
+/* np.random.RandomState emulation, for tests: op 0 = n raw uint32 draws, 1 = n x randint(0, np_),
+ * 2 = n x choice(np_, p=p); az_rng_doubles = n x random_sample(). */
+int az_rng_test(uint32_t seed, int op, int n, const double* p, int np_, int64_t* out);
+int az_rng_doubles(uint32_t seed, int n, double* out);
+
 /* Rules, exposed for differential tests against the Python games. ended: tag + value of
  * getGameEnded(board, 1); valids [A] int8; next: canonical board after action (player 1 moves,
  * then the board is seen from the opponent). */

@@ -219,3 +219,75 @@ def test_native_engine_errors_and_failed_batches():
     args = Args(numMCTSSims=4, cpuct=1.0, tempThreshold=15, use_gnn=False)
     out = play_episodes_native(Connect4Game(7), Broken(), args, [0, 1], {0: 0, 1: 1}, 2)
     assert len(out) == 2 and all(len(std) > 0 for std, _ in out.values())
+
+
+def test_rng_emulation_matches_numpy_randomstate(host_lib):
+    import ctypes
+    rng = np.random.default_rng(3)
+    for seed in (0, 1, 5, 12345, 2 ** 32 - 1):
+        out = np.zeros(1500, np.int64)          # raw draws = the MT19937 key stream
+        host_lib.az_rng_test(seed, 0, 1500, None, 0, out.ctypes.data)
+        rs = np.random.RandomState(seed)
+        assert out.tolist() == [int(x) for x in rs.randint(0, 2 ** 32, size=1500,
+                                                              dtype=np.uint64)]
+        d = np.zeros(700, np.float64)
+        host_lib.az_rng_doubles(seed, 700, d.ctypes.data)
+        assert d.tolist() == np.random.RandomState(seed).random_sample(700).tolist()
+        for n in (1, 2, 3, 5, 7, 8, 10, 17):
+            out = np.zeros(300, np.int64)
+            host_lib.az_rng_test(seed, 1, 300, None, n, out.ctypes.data)
+            rs = np.random.RandomState(seed)
+            arr = np.arange(n)
+            assert out.tolist() == [int(rs.choice(arr)) for _ in range(300)], (seed, n)
+        for n in (8, 10, 17):
+            for trial in range(5):
+                p = rng.random(n) * (rng.random(n) < 0.7)
+                if p.sum() == 0:
+                    p[0] = 1.0
+                p = [float(x) for x in p / p.sum()]
+                pa = np.array(p)
+                out = np.zeros(200, np.int64)
+                host_lib.az_rng_test(seed, 2, 200, pa.ctypes.data, n, out.ctypes.data)
+                rs = np.random.RandomState(seed)
+                assert out.tolist() == [int(rs.choice(n, p=p)) for _ in range(200)], (seed, n)
+
+
+@pytest.mark.parametrize("case", ["mcts_c4", "mcts_ttt3"])
+def test_engine_episodes_equal_reference(case):
+    """Whole episodes in the engine (episode mode) reproduce the reference's examples."""
+    from connect4.Connect4Game import Connect4Game
+    from tictactoe.TicTacToeGame import TicTacToeGame
+    from selfplay import play_episodes_engine
+    game = Connect4Game(7) if case == "mcts_c4" else TicTacToeGame(3)
+    meta = json.load(open(os.path.join(GOLDEN, case + ".json")))
+    net = BatchedRecordedNet(golden(case + ".npz"), 0)
+    eps = [ep["episode"] for ep in meta["episodes"]]
+    for parallel, lanes in ((1, 1), (64, 2), (3, 3)):
+        out = play_episodes_engine(game, net, Args(meta["args"]), eps, {e: e for e in eps},
+                                   parallel_games=parallel, threads=2, lanes=lanes)
+        for ep in meta["episodes"]:
+            std, gnn = out[ep["episode"]]
+            assert _norm_std(std) == [tuple(x) for x in ep["std_examples"]]
+            assert _norm_gnn(gnn) == [tuple(x) for x in ep["gnn_examples"]]
+
+
+@pytest.mark.parametrize("gi", [0, 1, 2, 3])
+@pytest.mark.parametrize("use_gnn", [False, True])
+def test_engine_episodes_match_python_fuzz(gi, use_gnn):
+    """Engine episodes == Python MCTS episodes (same seeds, pseudo-random networks), including
+    example value types (int / float / np.float32) and pi list element types."""
+    from selfplay import play_episodes, play_episodes_engine
+    _, _, game = _games()[gi]
+    args = Args(numMCTSSims=[7, 12, 25, 4][gi], cpuct=[1.0, 1.5, 0.7, 1.0][gi], tempThreshold=6,
+                use_gnn=use_gnn, expand_by=[3, 5, 2, 1][gi])
+    net = HashNet(game.getActionSize(), 31 + gi)
+    eps = list(range(6))
+    seeds = {e: 777 * gi + e for e in eps}
+    py = play_episodes(game, net, args, eps, seeds, parallel_games=3)
+    nat = play_episodes_engine(game, net, args, eps, seeds, parallel_games=4, threads=2)
+
+    def typed(ex):
+        return [tuple((type(x).__name__, np.asarray(x).tolist()) for x in row) for row in ex]
+    for e in eps:
+        assert typed(nat[e][0]) == typed(py[e][0]), e
+        assert typed(nat[e][1]) == typed(py[e][1]), e

@@ -16,8 +16,8 @@ from azhip.weights import connect4_net_spec, gnn_spec, synthetic_state_dict  # n
 sims = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 W = synthetic_state_dict(connect4_net_spec(7), 1)
 G = synthetic_state_dict(gnn_spec(3136, 2), 2)
-for games, lanes, threads in [(256, 1, 16), (256, 2, 16), (512, 2, 16), (1024, 2, 16),
-                              (1024, 3, 16), (2048, 2, 16)]:
+for games, lanes, threads in [(256, 1, 16), (512, 1, 16), (512, 2, 16), (1024, 2, 16),
+                              (2048, 2, 16), (2048, 3, 16), (4096, 2, 16), (2048, 2, 32)]:
     args = SimpleNamespace(sp_games=games, sp_sims=sims, sp_threads=threads, sp_lanes=lanes)
     t = time.perf_counter()
     dt, sp = bench.selfplay_leg(W, G, args, None, 0)
