@@ -40,7 +40,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-aggregate", action="store_true")
     ap.add_argument("--no-selfplay", action="store_true")
-    ap.add_argument("--sp-games", type=int, default=1024,
+    ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--sp-games", type=int, default=2048,
                     help="self-play leg: games per GPU, all played in lock step")
     ap.add_argument("--sp-sims", type=int, default=100, help="numMCTSSims (SURVEY §8d config 3)")
     ap.add_argument("--sp-threads", type=int, default=16, help="host threads for the engine")
@@ -145,6 +146,59 @@ def selfplay_leg(W, G, args, device, rank):
     return dt, {"games": len(out), "moves": moves, "evals": st["rows"], "rounds": st["rounds"],
                 "net_wait_s": round(st["net_s"], 3), "host_s": round(st["host_s"], 3),
                 "assemble_s": round(st.get("assemble_s", 0.0), 3)}
+
+
+def train_leg(W, G, device):
+    """Net.train (Connect4GNN.py:122-197) on synthetic examples: one full train() call =
+    20 epochs x (CNN step on 64 sampled rows + GNN step on a 64-row star), fresh Adam per call,
+    plus the Adam kernel alone over the 119.6 M GNN parameters (HBM roofline: 28 B/param =
+    read p, g, m, v + write p, m, v)."""
+    import torch
+    from azhip import ops
+    from connect4.Connect4GNN import Connect4GNNWrapper
+    from connect4.Connect4Game import Connect4Game
+    sa = selfplay_args(2)
+    sa.lr, sa.epochs, sa.batch_size = 0.001, 20, 64
+    net = Connect4GNNWrapper(Connect4Game(7), sa)
+    net.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()})
+    net.gnn.load_state_dict({k: torch.from_numpy(v) for k, v in G.items()})
+    rng = np.random.default_rng(7)
+    boards = rng.integers(-1, 2, size=(256, 7, 7)).astype(np.int64)
+    pis = rng.dirichlet(np.ones(8), 256)
+    zs = rng.choice([-1, 1], 256)
+    ex = [(boards[i], pis[i], int(zs[i])) for i in range(256)]
+    gex = [(boards[i], 1, pis[i], np.float32(0.1), pis[i], np.float32(zs[i] * 0.5), int(zs[i]))
+           for i in range(128)]
+    np.random.seed(0)
+    net.train(ex, gex)                                  # warm-up (allocations)
+    torch.cuda.synchronize()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        net.train(ex, gex)
+    torch.cuda.synchronize()
+    train_ms = (time.perf_counter() - t0) / reps * 1e3
+    P = net.gnn.params
+    n = P.numel
+    P.grad_flat.normal_()
+    P.reset_adam()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for _ in range(2):
+        ops.adam(P.flat, P.grad_flat, P.m, P.v, 1e-9, 1)
+    evs[0].record()
+    for _ in range(10):
+        ops.adam(P.flat, P.grad_flat, P.m, P.v, 1e-9, 1)
+    evs[1].record()
+    torch.cuda.synchronize()
+    us = evs[0].elapsed_time(evs[1]) / 10 * 1e3
+    gbs = 28.0 * n / (us * 1e-6) / 1e9
+    return {"train_call_ms": round(train_ms, 2),
+            "workload": "Connect4GNNWrapper.train: 20 epochs x (CNN step + GNN star step), "
+                        "batch 64, fresh Adam, 256 std / 128 GNN synthetic examples",
+            "adam_roofline": {"kernel": "adam_kernel (GNN params)", "bound": "hbm",
+                              "params": n, "avg_launch_us": round(us, 1),
+                              "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(gbs / HBM_PEAK_GBS, 4)}}
 
 
 def selfplay_cpu_baseline(W, G, sims, seconds):
@@ -306,6 +360,10 @@ def main():
                              "threads, %d lanes"
                              % (args.sp_sims, args.sp_threads, args.sp_lanes)})
 
+    tr = None
+    if not args.no_train and rank == 0 and world == 1:
+        tr = train_leg(W, G, device)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(W, G, args.cpu_seconds, B)
@@ -343,6 +401,7 @@ def main():
                          "flop_per_launch": flop},
             "aggregate_roofline": agg,
             "selfplay": sp,
+            "train": tr,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

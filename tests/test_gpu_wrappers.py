@@ -221,3 +221,26 @@ def test_data_parallel_cnn_step_equals_single_rank(tmp_path):
     assert torch.equal(r[0]["dp"], r[1]["dp"])
     assert torch.equal(r[0]["single"], r[1]["single"])
     np.testing.assert_allclose(r[0]["dp"].numpy(), r[0]["single"].numpy(), atol=1e-5)
+
+
+def test_coach_learn_with_native_lockstep_selfplay(tmp_path):
+    """Coach.learn end to end with parallel_games > 1: self-play runs as native engine episodes
+    (selfplay.play_episodes_engine), then train, arena and checkpoints as in the reference."""
+    import main as M
+    from Coach import Coach
+    from register import get_game
+    args = M.config_to_args(M.load_config(os.path.join(M.HERE, "tictactoe", "config.yaml")))
+    args.update(board_size=3, numIters=1, use_gnn=True, gnn_layers=2, game="tictactoe",
+                load_model=False, numEps=8, parallel_games=4, numMCTSSims=6, arenaCompare=2,
+                epochs=2)
+    folder = str(tmp_path / "tictactoe")
+    os.makedirs(folder)
+    args.checkpoint, args.load_folder_file = folder, (folder, "best_gnn.pth.tar")
+    np.random.seed(1)
+    GameClass, NNet = get_game("tictactoe", use_gnn=True)
+    game = M.create_game_instance(GameClass, args)
+    coach = Coach(game, NNet(game, args), args)
+    coach.learn()
+    std, gnn = coach.trainExamplesHistory[0]
+    assert len(std) > 8 * 5 * 8 // 2 and len(gnn) > 8 * 2
+    assert "best_gnn.pth.tar" in os.listdir(folder)
