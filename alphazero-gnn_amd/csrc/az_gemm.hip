@@ -407,6 +407,170 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds(GemmArgs p) {
       }
 }
 
+// Multi-stage LDS-DMA tile: NBUF buffers, tile t+NBUF-1 is issued while tile t is consumed, so
+// NBUF-1 tiles of DMA are in flight across each barrier.  No __syncthreads() in the loop (its
+// fence would drain the DMAs, vmcnt(0)): a counted `s_waitcnt vmcnt(N)` retires exactly the
+// oldest tile, then a raw s_barrier publishes it to every wave (cdna_hip_programming.md §5,
+// "Pipelining across barriers").  The LDS image is [row][BK] with the 16-B chunk XOR-swizzled
+// by the row bits that would otherwise put a 16-lane ds_read_b128 group on one bank set.
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int BK>
+__device__ __forceinline__ int swz(int r) {
+  // chunks per row = BK/4; rows per 256-B bank row = 256 / (BK*4)
+  if constexpr (BK == 32) return (r >> 1) & 7;
+  else if constexpr (BK == 16) return (r >> 2) & 3;
+  else return (r >> 0) & 15;   // BK = 64
+}
+
+template <int BM, int BN, int BK, int NBUF, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds_pipe(GemmArgs p) {
+  constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TI = WM / 32, TJ = WN / 32;
+  constexpr int CPR = BK / 4;                    // 16-B chunks per row
+  constexpr int RPP = 64 / CPR;                  // rows per 1-KB wave piece
+  constexpr int APC = BM / RPP / NW, BPC = BN / RPP / NW;
+  constexpr int DPT = APC + BPC;                 // DMAs per thread per tile
+  constexpr int TILE = (BM + BN) * BK;
+  static_assert(TI >= 1 && TJ >= 1 && APC >= 1 && BPC >= 1 && NBUF >= 2, "bad tile");
+  static_assert(DPT * (NBUF - 2) <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(1024))) float smem[NBUF * TILE];
+
+  const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
+  const int nwg = mt_n * nt_n * p.splits;
+  const int bid = xcd_swizzle(blockIdx.x, nwg);
+  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+
+  const int lrow = lane / CPR, pch = lane % CPR;
+  const float* asrc[APC];
+  const float* bsrc[BPC];
+  int akq[APC], bkq[BPC];
+#pragma unroll
+  for (int q = 0; q < APC; ++q) {
+    const int r = (q * NW + wave) * RPP + lrow;
+    const int gr = m0 + r < p.M ? m0 + r : 0;
+    asrc[q] = p.A + (size_t)gr * p.lda;
+    akq[q] = (pch ^ swz<BK>(r)) * 4;
+  }
+#pragma unroll
+  for (int q = 0; q < BPC; ++q) {
+    const int r = (q * NW + wave) * RPP + lrow;
+    const int gr = n0 + r < p.N ? n0 + r : 0;
+    bsrc[q] = p.B + (size_t)gr * p.ldb;
+    bkq[q] = (pch ^ swz<BK>(r)) * 4;
+  }
+  auto issue = [&](int buf, int k0) {
+    float* As = smem + buf * TILE;
+    float* Bs = As + BM * BK;
+#pragma unroll
+    for (int q = 0; q < APC; ++q) {
+      const int k = k0 + akq[q];
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(asrc[q] + (k < p.K ? k : 0)),
+          (__attribute__((address_space(3))) void*)(As + (q * NW + wave) * RPP * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < BPC; ++q) {
+      const int k = k0 + bkq[q];
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(bsrc[q] + (k < p.K ? k : 0)),
+          (__attribute__((address_space(3))) void*)(Bs + (q * NW + wave) * RPP * BK), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+#pragma unroll
+  for (int t = 0; t < NBUF - 1; ++t)
+    if (t < nk) issue(t, kbeg + t * BK);
+  for (int kt = 0; kt < nk; ++kt) {
+    // tiles issued so far: min(nk, kt + NBUF - 1); retire tile kt, keep the later ones flying
+    const int later = min(nk, kt + NBUF - 1) - kt - 1;
+    if constexpr (NBUF >= 4) {
+      if (later >= 2) wait_vm<DPT * 2>();
+      else if (later == 1) wait_vm<DPT>();
+      else wait_vm<0>();
+    } else if constexpr (NBUF == 3) {
+      if (later >= 1) wait_vm<DPT>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    lds_barrier();
+    const int cur = kt % NBUF;
+    const int k0 = kbeg + kt * BK;
+    if (k0 + BK > kend) {                        // partial last tile: zero A's k >= kend
+      float* As = smem + cur * TILE;
+      for (int idx = threadIdx.x; idx < BM * CPR; idx += NT) {
+        const int r = idx / CPR, lc = idx % CPR;
+        if (k0 + lc * 4 >= kend)
+          *reinterpret_cast<f32x4*>(As + r * BK + ((lc ^ swz<BK>(r)) * 4)) =
+              f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      lds_barrier();
+    }
+    if (kt + NBUF - 1 < nk) issue((kt + NBUF - 1) % NBUF, kbeg + (kt + NBUF - 1) * BK);
+    const float* As = smem + cur * TILE;
+    const float* Bs = As + BM * BK;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      f32x4 a[TI], b[TJ];
+      const int lc = g * 2 + (lane >> 5);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int r = wm * WM + i * 32 + (lane & 31);
+        a[i] = *reinterpret_cast<const f32x4*>(As + r * BK + ((lc ^ swz<BK>(r)) * 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int r = wn * WN + j * 32 + (lane & 31);
+        b[j] = *reinterpret_cast<const f32x4*>(Bs + r * BK + ((lc ^ swz<BK>(r)) * 4));
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  float* slab = p.splits > 1 ? p.slab + (size_t)sp * p.M * p.N : nullptr;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = n0 + wn * WN + j * 32 + (lane & 31);
+        if (slab) {
+          if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][r];
+        } else {
+          epilogue_store(p, row, col, acc[i][j][r]);
+        }
+      }
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
   const long total = (long)p.M * p.N;
   const size_t plane = (size_t)p.M * p.N;
@@ -495,11 +659,14 @@ struct TileCfg { int bm, bn, bk, wgm, wgn; };
 // 3: 128x64x32 (4 waves 2x2)  4: 128x128x32 (8 waves 2x4)   5: 256x128x32 (8 waves 4x2)
 // LDS-DMA (K-major A and B only): 6: 128x128x32 (4 waves 2x2)  7: 64x64x32  8: 128x64x32
 // 9: 128x128x32 (8 waves 2x4)
+// multi-stage LDS-DMA: 10: 128x128x16 x4 buffers  11: 128x128x32 x3  12: 128x64x32 x3
+// 13: 128x128x16 x3  14: 128x64x16 x4
 static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 64, 64, 2, 2},
                                 {128, 64, 32, 2, 2}, {128, 128, 32, 2, 4}, {256, 128, 32, 4, 2},
                                 {128, 128, 32, 2, 2}, {64, 64, 32, 2, 2},  {128, 64, 32, 2, 2},
-                                {128, 128, 32, 2, 4}};
-constexpr int kNumCfgs = 10;
+                                {128, 128, 32, 2, 4}, {128, 128, 16, 2, 2}, {128, 128, 32, 2, 2},
+                                {128, 64, 32, 2, 2},  {128, 128, 16, 2, 2}, {128, 64, 16, 2, 2}};
+constexpr int kNumCfgs = 15;
 
 template <int BM, int BN, int BK, int WGM, int WGN>
 static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
@@ -517,8 +684,19 @@ static void launch_glds(const GemmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((gemm_f32_glds<BM, BN, WGM, WGN>), dim3(nwg), dim3(64 * WGM * WGN), 0, s, a);
 }
 
+template <int BM, int BN, int BK, int NBUF>
+static void launch_pipe(const GemmArgs& a, hipStream_t s) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
+  hipLaunchKernelGGL((gemm_f32_glds_pipe<BM, BN, BK, NBUF, 2, 2>), dim3(nwg), dim3(256), 0, s, a);
+}
+
 static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
   switch (cfg) {
+    case 10: launch_pipe<128, 128, 16, 4>(a, s); break;
+    case 11: launch_pipe<128, 128, 32, 3>(a, s); break;
+    case 12: launch_pipe<128, 64, 32, 3>(a, s); break;
+    case 13: launch_pipe<128, 128, 16, 3>(a, s); break;
+    case 14: launch_pipe<128, 64, 16, 4>(a, s); break;
     case 6: launch_glds<128, 128, 2, 2>(a, s); break;
     case 7: launch_glds<64, 64, 2, 2>(a, s); break;
     case 8: launch_glds<128, 64, 2, 2>(a, s); break;

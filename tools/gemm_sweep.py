@@ -53,7 +53,7 @@ if __name__ == "__main__":
                     print(json.dumps({"M": M, "cfg": cfg, "streamk": sk, **res}), flush=True)
         sys.exit(0)
     if mode == "quickcheck":      # one small run per glds config: correctness before the sweep
-        for cfg in ("6", "7", "8", "9"):
+        for cfg in sys.argv[2].split(",") if len(sys.argv) > 2 else ("6", "7", "8", "9"):
             for (M, N, K) in [(100, 200, 96), (100, 200, 100), (512, 3136, 3136)]:
                 res = run({"AZ_GEMM_CFG": cfg}, M, N, K)
                 print(json.dumps({"M": M, "N": N, "K": K, "cfg": cfg, **res}), flush=True)
@@ -61,10 +61,15 @@ if __name__ == "__main__":
                     sys.exit(3)
         sys.exit(0)
     if mode == "glds":
+        cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else ("0", "6", "7", "8", "9")
+        splits = sys.argv[3].split(",") if len(sys.argv) > 3 else ("", "2", "3", "4", "5", "6",
+                                                                   "8")
         for (M, N, K) in [(512, 3136, 3136), (256, 3136, 3136), (4096, 3136, 3136)]:
-            for cfg in ("0", "6", "7", "8", "9"):
-                for sp in ("", "2", "3", "4", "5", "6", "8"):
+            for cfg in cfgs:
+                for sp in splits:
                     env = {"AZ_GEMM_CFG": cfg}
+                    if sp == "auto":
+                        sp = ""
                     if sp:
                         env["AZ_GEMM_SPLITS"] = sp
                     res = run(env, M, N, K)
