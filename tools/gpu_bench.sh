@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/bench_$TAG
 mkdir -p $OUT
-timeout -k 10 900 python -m pytest tests -q -m gpu > $OUT/tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $OUT/tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit $?

@@ -3,7 +3,7 @@ set -u
 TAG=${1:-run}
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -q -m gpu > gpurun_out/$TAG-tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/$TAG-tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/$TAG-tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

@@ -1,0 +1,92 @@
+"""Summarise the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/gpu_profile.sh into
+profiles/<tag>_pmc_hbm.csv and profiles/pmc.json (what bench.py reports as roofline.traffic).
+
+    python tools/pmc_summary.py gpurun_out/prof_<tag> <tag>
+
+HBM bytes per dispatch = (2 * FETCH_SIZE + WRITE_SIZE) KB * 1024: on gfx950 FETCH_SIZE counts
+half of the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section).  The bench's
+output_transform call is one az_gemm_f32 = the tile kernel plus, when split-K is used, the
+splitk_reduce_kernel dispatched right after it; both are charged to that call.
+"""
+import csv
+import collections
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load(path, counter):
+    rows = []
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"]),
+                         int(r["Grid_Size"])))
+    rows.sort()
+    return rows
+
+
+def main(d, tag):
+    fetch = load(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = load(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    per = collections.defaultdict(lambda: [[], []])
+    for i, rows in enumerate((fetch, write)):
+        for _, name, kb, _ in rows:
+            per[name][i].append(kb)
+    out = os.path.join(ROOT, "profiles", f"{tag}_pmc_hbm.csv")
+    with open(out, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "dispatches", "FETCH_SIZE_KB_avg", "WRITE_SIZE_KB_avg",
+                    "hbm_bytes_corrected (2*FETCH + WRITE)"])
+        for name, (fe, wr) in sorted(per.items(), key=lambda kv: -sum(kv[1][0])):
+            if not fe or not wr:
+                continue
+            fa, wa = sum(fe) / len(fe), sum(wr) / len(wr)
+            w.writerow([name, len(fe), round(fa, 1), round(wa, 1), int((2 * fa + wa) * 1024)])
+
+    def call_bytes(rows, tile_pred):
+        """per az_gemm_f32 call: the tile kernel + the reduce that immediately follows it"""
+        tile, red = [], []
+        for i, (_, name, kb, _) in enumerate(rows):
+            if tile_pred(name):
+                tile.append(kb)
+                nxt = rows[i + 1][1] if i + 1 < len(rows) else ""
+                red.append(rows[i + 1][2] if "splitk_reduce" in nxt else 0.0)
+        n = max(1, len(tile))
+        return sum(tile) / n, sum(red) / n, len(tile)
+
+    is_fwd_gemm = lambda n: "gemm_f32_glds" in n  # the forward Linear path (bench GEMMs)
+    ft, fr, nf = call_bytes(fetch, is_fwd_gemm)
+    wt, wr, _ = call_bytes(write, is_fwd_gemm)
+    gemm_tile = int((2 * ft + wt) * 1024)
+    gemm_red = int((2 * fr + wr) * 1024)
+    agg = [kb for _, n, kb, _ in fetch if "aggregate_lanes_kernel<8, 2>" in n]
+    aggw = [kb for _, n, kb, _ in write if "aggregate_lanes_kernel<8, 2>" in n]
+    B, F = 512, 3136
+    res = {
+        "round": 1, "tag": tag,
+        "source": f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) over "
+                  f"`python3 bench.py --steps 5 --warmup 2 --no-cpu --no-selfplay --no-train` "
+                  f"(tools/gpu_profile.sh {tag}); per-kernel averages over all dispatches; "
+                  f"bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE reports "
+                  f"half of wide reads, MI355X_MICROARCH.md HBM section)",
+        "gemm": {"kernel": "az_gemm_f32 output_transform call (gemm_f32_glds tile kernel + "
+                           "splitk_reduce_kernel)",
+                 "dispatches": nf,
+                 "hbm_bytes_per_launch": gemm_tile + gemm_red,
+                 "gemm_kernel_bytes": gemm_tile, "reduce_kernel_bytes": gemm_red,
+                 "algorithmic_bytes": 4 * (B * F + F * F + F + B * F)},
+    }
+    if agg and aggw:
+        V, E = 512 * 1024, 512 * 3968
+        res["aggregate"] = {"kernel": "aggregate_lanes_kernel<8,2> (512 32x32 grids, F=64)",
+                            "hbm_bytes_per_launch": int((2 * sum(agg) / len(agg)
+                                                         + sum(aggw) / len(aggw)) * 1024),
+                            "algorithmic_bytes": V * 64 * 4 * 2 + E * 8 + (V + 1) * 4}
+    json.dump(res, open(os.path.join(ROOT, "profiles", "pmc.json"), "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
