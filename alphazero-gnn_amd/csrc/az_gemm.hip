@@ -12,6 +12,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "az_common.h"
 
@@ -156,6 +157,45 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
   return xcd * base + min(xcd, rem) + local;
 }
 
+// Tile epilogue shared by the tile kernels.  A wave owns the TI x TJ MF x MF accumulators of
+// its sub-tile at (r0, c0).  No split: the fused epilogue straight from the accumulators.
+// Split-K: the raw partial goes to slab[sp] and splitk_reduce_kernel sums the slabs in s order.
+// (An in-launch reduction by each tile's last-arriving block -- agent-scope release/acquire
+// around a ticket counter -- was measured 1.8x slower here: a tile's 5 slabs are 320 KB, far
+// above the few tens of KB where one block's serial combine beats a separate launch;
+// cdna_hip_programming.md §5 "In-launch split-K reduction".)
+template <int MF, int TI, int TJ, class Acc>
+__device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][TJ], int r0,
+                                              int c0, int sp) {
+  constexpr int NACC = MF == 32 ? 16 : 4;
+  const int lane = threadIdx.x & 63;
+  auto row_of = [&](int i, int r) {
+    return r0 + i * MF +
+           (MF == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : 4 * (lane >> 4) + r);
+  };
+  const int cl = lane & (MF - 1);
+  if (p.splits <= 1) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < NACC; ++r) epilogue_store(p, row_of(i, r), c0 + j * MF + cl, acc[i][j][r]);
+    return;
+  }
+  const size_t plane = (size_t)p.M * p.N;
+  float* slab = p.slab + (size_t)sp * plane;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < NACC; ++r) {
+        const int row = row_of(i, r), col = c0 + j * MF + cl;
+        if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][r];
+      }
+}
+
 // Waves arranged WGM x WGN; each wave computes a (BM/WGM) x (BN/WGN) sub-tile as TI x TJ
 // 32x32 MFMA accumulators.
 template <int BM, int BN, int BK, int WGM, int WGN, bool A_KM, bool B_KM>
@@ -239,21 +279,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_mfma(GemmArgs p) {
     __syncthreads();
   }
 
-  float* slab = p.splits > 1 ? p.slab + (size_t)sp * p.M * p.N : nullptr;
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int col = n0 + wn * WN + j * 32 + (lane & 31);
-        if (slab) {
-          if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][r];
-        } else {
-          epilogue_store(p, row, col, acc[i][j][r]);
-        }
-      }
+  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp);
 }
 
 // ------------------------------------------------------------------------------ LDS-DMA tile
@@ -390,21 +416,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds(GemmArgs p) {
     __syncthreads();
   }
 
-  float* slab = p.splits > 1 ? p.slab + (size_t)sp * p.M * p.N : nullptr;
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int col = n0 + wn * WN + j * 32 + (lane & 31);
-        if (slab) {
-          if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][r];
-        } else {
-          epilogue_store(p, row, col, acc[i][j][r]);
-        }
-      }
+  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp);
 }
 
 // Multi-stage LDS-DMA tile: NBUF buffers, tile t+NBUF-1 is issued while tile t is consumed, so
@@ -554,21 +566,198 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds_pipe(GemmArgs p)
     }
   }
 
-  float* slab = p.splits > 1 ? p.slab + (size_t)sp * p.M * p.N : nullptr;
+  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp);
+}
+
+// LDS-DMA tile, v2: the same LDS image and DMA schedule as gemm_f32_glds, but every wave reads
+// ALL of its fragments for the k-tile (16 ds_read_b128) before the first MFMA, so the LDS
+// latency of later fragment groups hides behind the MFMAs of earlier ones (the compiler counts
+// lgkmcnt down group by group) instead of draining once per group.  MF selects the MFMA shape:
+//   MF = 32: v_mfma_f32_32x32x2_f32, lane l holds A[row l&31][4 k of chunk 2g + (l>>5)]
+//   MF = 16: v_mfma_f32_16x16x4_f32, lane l holds A[row l&15][4 k of chunk 4g + (l>>4)]
+// Element t of the 4-k fragment feeds MFMA t, so the k order inside a group is permuted (only
+// the fp32 summation order changes).  The 16x16 shape is the lower-energy one per FLOP
+// (cdna_hip_programming.md §5.4 rule 28: the chip holds a higher clock on it).
+template <int BM, int BN, int WGM, int WGN, int MF, bool IL>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
+  constexpr int BK = 32;
+  constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TI = WM / MF, TJ = WN / MF;
+  constexpr int NG = MF == 32 ? BK / 8 : BK / 16;     // fragment groups per k-tile
+  constexpr int LSH = MF == 32 ? 5 : 4;                // lane >> LSH = chunk within a group
+  constexpr int APC = BM / 8 / NW, BPC = BN / 8 / NW;
+  using acc_t = typename std::conditional<MF == 32, f32x16, f32x4>::type;
+  constexpr int NACC = MF == 32 ? 16 : 4;
+  static_assert(TI >= 1 && TJ >= 1 && APC >= 1 && BPC >= 1, "bad tile");
+  __shared__ __attribute__((aligned(1024))) float smem[2 * (BM + BN) * BK];
+
+  const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
+  const int nwg = mt_n * nt_n * p.splits;
+  const int bid = xcd_swizzle(blockIdx.x, nwg);
+  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+
+  const int lrow = lane >> 3, pch = lane & 7;
+  const float* asrc[APC];
+  const float* bsrc[BPC];
+  int akq[APC], bkq[BPC];
+#pragma unroll
+  for (int q = 0; q < APC; ++q) {
+    const int r = (q * NW + wave) * 8 + lrow;
+    const int gr = m0 + r < p.M ? m0 + r : 0;
+    asrc[q] = p.A + (size_t)gr * p.lda;
+    akq[q] = (pch ^ ((r >> 1) & 7)) * 4;
+  }
+#pragma unroll
+  for (int q = 0; q < BPC; ++q) {
+    const int r = (q * NW + wave) * 8 + lrow;
+    const int gr = n0 + r < p.N ? n0 + r : 0;
+    bsrc[q] = p.B + (size_t)gr * p.ldb;
+    bkq[q] = (pch ^ ((r >> 1) & 7)) * 4;
+  }
+  auto issue = [&](int buf, int k0) {
+    float* As = smem + buf * (BM + BN) * BK;
+    float* Bs = As + BM * BK;
+#pragma unroll
+    for (int q = 0; q < APC; ++q) {
+      const int k = k0 + akq[q];
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(asrc[q] + (k < p.K ? k : 0)),
+          (__attribute__((address_space(3))) void*)(As + (q * NW + wave) * 8 * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < BPC; ++q) {
+      const int k = k0 + bkq[q];
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(bsrc[q] + (k < p.K ? k : 0)),
+          (__attribute__((address_space(3))) void*)(Bs + (q * NW + wave) * 8 * BK), 16, 0, 0);
+    }
+  };
+  // one 1-KB DMA piece: q < APC is A piece q, else B piece q - APC
+  auto issue_piece = [&](int buf, int k0, int q) {
+    float* As = smem + buf * (BM + BN) * BK;
+    float* Bs = As + BM * BK;
+    if (q < APC) {
+      const int k = k0 + akq[q];
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(asrc[q] + (k < p.K ? k : 0)),
+          (__attribute__((address_space(3))) void*)(As + (q * NW + wave) * 8 * BK), 16, 0, 0);
+    } else {
+      const int qb = q - APC;
+      const int k = k0 + bkq[qb];
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(bsrc[qb] + (k < p.K ? k : 0)),
+          (__attribute__((address_space(3))) void*)(Bs + (qb * NW + wave) * 8 * BK), 16, 0, 0);
+    }
+  };
+  auto zero_tail = [&](int buf, int k0) {
+    if (k0 + BK <= kend) return;
+    __syncthreads();
+    float* As = smem + buf * (BM + BN) * BK;
+    for (int idx = threadIdx.x; idx < BM * 8; idx += NT) {
+      const int r = idx >> 3, lc = idx & 7;
+      if (k0 + lc * 4 >= kend)
+        *reinterpret_cast<f32x4*>(As + r * BK + ((lc ^ ((r >> 1) & 7)) * 4)) =
+            f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  acc_t acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int col = n0 + wn * WN + j * 32 + (lane & 31);
-        if (slab) {
-          if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][r];
-        } else {
-          epilogue_store(p, row, col, acc[i][j][r]);
+      for (int r = 0; r < NACC; ++r) acc[i][j][r] = 0.f;
+
+  // per-lane fragment row offsets (in floats) and swizzle keys, fixed for the whole loop
+  int aoff[TI], boff[TJ], akey[TI], bkey[TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int r = wm * WM + i * MF + (lane & (MF - 1));
+    aoff[i] = r * BK;
+    akey[i] = (r >> 1) & 7;
+  }
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int r = wn * WN + j * MF + (lane & (MF - 1));
+    boff[j] = BM * BK + r * BK;
+    bkey[j] = (r >> 1) & 7;
+  }
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    issue(0, kbeg);
+    __builtin_amdgcn_s_waitcnt(0);
+    zero_tail(0, kbeg);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (!IL && more) issue(cur ^ 1, kbeg + (kt + 1) * BK);
+    const float* S = smem + cur * (BM + BN) * BK;
+    f32x4 a[NG][TI], b[NG][TJ];
+    auto read = [&](int g) {
+      const int lc = g * (64 >> LSH) + (lane >> LSH);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+        a[g][i] = *reinterpret_cast<const f32x4*>(S + aoff[i] + ((lc ^ akey[i]) * 4));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        b[g][j] = *reinterpret_cast<const f32x4*>(S + boff[j] + ((lc ^ bkey[j]) * 4));
+    };
+    // group g+1's fragments are read right after the first quarter of group g's MFMAs, so
+    // their LDS latency hides behind the other three quarters; sched_barrier pins the order
+    // (the scheduler would otherwise sink the reads behind all MFMAs to save registers) and
+    // keeps at most two groups of reads outstanding (lgkmcnt counts to 15).
+    read(0);
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            if constexpr (MF == 32)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][i][t], b[g][j][t], acc[i][j],
+                                                               0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][i][t], b[g][j][t], acc[i][j],
+                                                               0, 0, 0);
+          }
+        if (t == 0 && g + 1 < NG) {
+          __builtin_amdgcn_sched_barrier(0);
+          read(g + 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (IL) {
+          // IL: the next tile's DMA pieces are spread over the first half of the MFMA steps
+          // (one DMA issue stalls the wave for ~60-180 cycles; beside MFMAs it hides)
+          constexpr int STEPS = NG * 4 / 2, PER = (APC + BPC + STEPS - 1) / STEPS;
+          const int st = g * 4 + t;
+          if (st < STEPS && more) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < PER; ++u)
+              if (st * PER + u < APC + BPC) issue_piece(cur ^ 1, kbeg + (kt + 1) * BK, st * PER + u);
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
       }
+    if (more) {
+      __builtin_amdgcn_s_waitcnt(0);
+      zero_tail(cur ^ 1, kbeg + (kt + 1) * BK);
+    }
+    __syncthreads();
+  }
+
+  tile_epilogue<MF, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp);
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
@@ -661,12 +850,19 @@ struct TileCfg { int bm, bn, bk, wgm, wgn; };
 // 9: 128x128x32 (8 waves 2x4)
 // multi-stage LDS-DMA: 10: 128x128x16 x4 buffers  11: 128x128x32 x3  12: 128x64x32 x3
 // 13: 128x128x16 x3  14: 128x64x16 x4
+// LDS-DMA v2 (fragments of the whole k-tile read up front): 15: 128x128 mfma32  16: 128x128
+// mfma16  17: 128x64 mfma16  18: 128x64 mfma32  19: 128x128 mfma16 (8 waves 2x4)
+// v2 + DMA issue interleaved with the MFMAs: 20: 128x128 mfma32  21: 128x128 mfma16
+// 22: 128x64 mfma16
 static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 64, 64, 2, 2},
                                 {128, 64, 32, 2, 2}, {128, 128, 32, 2, 4}, {256, 128, 32, 4, 2},
                                 {128, 128, 32, 2, 2}, {64, 64, 32, 2, 2},  {128, 64, 32, 2, 2},
                                 {128, 128, 32, 2, 4}, {128, 128, 16, 2, 2}, {128, 128, 32, 2, 2},
-                                {128, 64, 32, 2, 2},  {128, 128, 16, 2, 2}, {128, 64, 16, 2, 2}};
-constexpr int kNumCfgs = 15;
+                                {128, 64, 32, 2, 2},  {128, 128, 16, 2, 2}, {128, 64, 16, 2, 2},
+                                {128, 128, 32, 2, 2}, {128, 128, 32, 2, 2}, {128, 64, 32, 2, 2},
+                                {128, 64, 32, 2, 2},  {128, 128, 32, 2, 4}, {128, 128, 32, 2, 2},
+                                {128, 128, 32, 2, 2}, {128, 64, 32, 2, 2}};
+constexpr int kNumCfgs = 23;
 
 template <int BM, int BN, int BK, int WGM, int WGN>
 static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
@@ -690,8 +886,23 @@ static void launch_pipe(const GemmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((gemm_f32_glds_pipe<BM, BN, BK, NBUF, 2, 2>), dim3(nwg), dim3(256), 0, s, a);
 }
 
+template <int BM, int BN, int WGM, int WGN, int MF, bool IL = false>
+static void launch_glds2(const GemmArgs& a, hipStream_t s) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
+  hipLaunchKernelGGL((gemm_f32_glds2<BM, BN, WGM, WGN, MF, IL>), dim3(nwg), dim3(64 * WGM * WGN), 0,
+                     s, a);
+}
+
 static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
   switch (cfg) {
+    case 15: launch_glds2<128, 128, 2, 2, 32>(a, s); break;
+    case 16: launch_glds2<128, 128, 2, 2, 16>(a, s); break;
+    case 17: launch_glds2<128, 64, 2, 2, 16>(a, s); break;
+    case 18: launch_glds2<128, 64, 2, 2, 32>(a, s); break;
+    case 19: launch_glds2<128, 128, 2, 4, 16>(a, s); break;
+    case 20: launch_glds2<128, 128, 2, 2, 32, true>(a, s); break;
+    case 21: launch_glds2<128, 128, 2, 2, 16, true>(a, s); break;
+    case 22: launch_glds2<128, 64, 2, 2, 16, true>(a, s); break;
     case 10: launch_pipe<128, 128, 16, 4>(a, s); break;
     case 11: launch_pipe<128, 128, 32, 3>(a, s); break;
     case 12: launch_pipe<128, 64, 32, 3>(a, s); break;
@@ -823,7 +1034,8 @@ int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
   }
   const TileCfg& tc = kCfgs[cfg];
   plan(a, tc.bm, tc.bn, tc.bk, d->ws_bytes);
-  if (cfg == 6 && !getenv("AZ_GEMM_SPLITS")) {
+  const bool is128 = tc.bm == 128 && tc.bn == 128 && cfg >= 6;
+  if (is128 && !getenv("AZ_GEMM_SPLITS")) {
     const int S = glds_splits(a, (long)((a.M + 127) / 128) * ((a.N + 127) / 128), d->ws_bytes);
     a.splits = S;
     a.kc = S > 1 ? ((a.K + S - 1) / S + 31) / 32 * 32 : a.K;
