@@ -80,6 +80,14 @@ SIGNATURES = {
                                  ctypes.POINTER(LayerW), c_void_p, c_void_p, c_size_t, c_void_p]),
     "az_mlp2_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "az_transform_heads_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "az_linear_heads_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "az_transform_heads_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_size_t, c_void_p]),
     "az_heads_loss_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "az_heads_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,

@@ -196,6 +196,21 @@ class PolicyValueGNN(_Net):
         return self.output_transform(self.run_layers(x, graph))
 
 
+def gnn_per_row_heads(nnet, gnn, feat, want_pi=True):
+    """Batched predict_with_gnn after extract_features (Connect4GNN.py:108-114 applied per row:
+    the layers are the identity on a 1-row input, gnn_utils.py:35-36) -> (logp, pi, v).
+    Connect4 heads read the transform output directly, so the whole tail is one
+    az_transform_heads_fwd call; TicTacToe's heads go through fc1/fc2 first."""
+    if isinstance(nnet, Connect4Net):
+        G, W = gnn.params, nnet.params
+        logp, pi, v, _, _ = ops.transform_heads(
+            feat, G["output_transform.0.weight"], G["output_transform.0.bias"],
+            G["output_transform.2.weight"], G["output_transform.2.bias"], W["fc_policy.weight"],
+            W["fc_policy.bias"], W["fc_value.weight"], W["fc_value.bias"], want_pi=want_pi)
+        return logp, pi, v
+    return nnet.heads(gnn.forward_per_row(feat), want_pi=want_pi)
+
+
 class C4Evaluator:
     """Connect4 board evaluator from plain state dicts (bench / smoke convenience)."""
 
@@ -211,7 +226,7 @@ class C4Evaluator:
         """Device in, device out: int8 boards [B,n,n] -> (logp, pi, v) on HBM, no sync."""
         f = self.nnet.features(b)
         if gnn:
-            f = self.gnn.forward_per_row(f)
+            return gnn_per_row_heads(self.nnet, self.gnn, f)
         return self.nnet.heads(f)
 
     def predict_batch(self, boards, gnn=False):

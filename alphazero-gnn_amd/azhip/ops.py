@@ -252,6 +252,47 @@ def mlp2(x, w0, b0, w2, b2, hidden=None, out=None):
     return out, hidden
 
 
+def transform_heads(x, w0, b0, w2, b2, wp, bp, wv, bv, hidden=None, y=None, logp=None, pi=None,
+                    v=None, want_pi=True):
+    """Per-row output_transform + heads (gnn_utils.py:115, Connect4GNN.py:48-57) in one C call:
+    the second GEMM's split-K reduction is fused with the heads' first pass.
+    Returns (logp, pi, v, y, hidden)."""
+    B, F = x.shape
+    A = wp.shape[0]
+    dev = x.device
+    hidden = torch.empty_like(x) if hidden is None else hidden
+    y = torch.empty_like(x) if y is None else y
+    logp = torch.empty((B, A), device=dev) if logp is None else logp
+    pi = (torch.empty((B, A), device=dev) if pi is None else pi) if want_pi else None
+    v = torch.empty((B,), device=dev) if v is None else v
+    L = _lib.lib()
+    ws = workspace(dev, max(int(L.az_transform_heads_ws_bytes(B, F, A)), 96 << 20))
+    _lib.check(L.az_transform_heads_fwd(_p(x), B, F, _p(w0), _p(b0), _p(w2), _p(b2), _p(wp),
+                                        _p(bp), A, _p(wv), _p(bv), _p(hidden), _p(y), _p(logp),
+                                        _p(pi), _p(v), _p(ws), ctypes.c_size_t(ws.numel()),
+                                        _stream()), "az_transform_heads_fwd")
+    return logp, pi, v, y, hidden
+
+
+def linear_heads(x, w, b, wp, bp, wv, bv, y=None, logp=None, pi=None, v=None, want_pi=True):
+    """y = x w^T + b then the heads of y, with the GEMM's split-K reduction fused into the
+    heads' first pass (the second half of transform_heads).  Returns (logp, pi, v, y)."""
+    B, F = x.shape
+    A = wp.shape[0]
+    dev = x.device
+    y = torch.empty_like(x) if y is None else y
+    logp = torch.empty((B, A), device=dev) if logp is None else logp
+    pi = (torch.empty((B, A), device=dev) if pi is None else pi) if want_pi else None
+    v = torch.empty((B,), device=dev) if v is None else v
+    L = _lib.lib()
+    ws = workspace(dev, max(int(L.az_transform_heads_ws_bytes(B, F, A)), 96 << 20))
+    _lib.check(L.az_linear_heads_fwd(_p(x), B, F, _p(w), _p(b), _p(wp), _p(bp), A, _p(wv),
+                                     _p(bv), _p(y), _p(logp), _p(pi), _p(v), _p(ws),
+                                     ctypes.c_size_t(ws.numel()), _stream()),
+               "az_linear_heads_fwd")
+    return logp, pi, v, y
+
+
 def adam(p, g, m, v, lr, step, beta1=0.9, beta2=0.999, eps=1e-8):
     L = _lib.lib()
     _lib.check(L.az_adam_f32(_p(p), _p(g), _p(m), _p(v), p.numel(), lr, beta1, beta2, eps, step,

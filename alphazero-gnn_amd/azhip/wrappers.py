@@ -82,7 +82,8 @@ class NetWrapper:
             b = b.view(1, self.board_x, self.board_y)
         f = self.nnet.features(b)
         if gnn:
-            f = self.gnn.forward_per_row(f)
+            _, pi, v = nets.gnn_per_row_heads(self.nnet, self.gnn, f)
+            return pi, v
         _, pi, v = self.nnet.heads(f)
         return pi, v
 
@@ -116,7 +117,7 @@ class NetWrapper:
         _, pi, v = self.nnet.heads(f)
         if both:
             self.gnn.eval()
-            _, gpi, gv = self.nnet.heads(self.gnn.forward_per_row(f))
+            _, gpi, gv = nets.gnn_per_row_heads(self.nnet, self.gnn, f)
             out = torch.cat([pi, v[:, None], gpi, gv[:, None]], dim=1)
         else:
             out = torch.cat([pi, v[:, None]], dim=1)
@@ -270,7 +271,7 @@ class GNNWrapperMixin:
         b = boards_to_device(boards, self.device)
         f = self.nnet.features(b)
         _, pi, v = self.nnet.heads(f)
-        _, gpi, gv = self.nnet.heads(self.gnn.forward_per_row(f))
+        _, gpi, gv = nets.gnn_per_row_heads(self.nnet, self.gnn, f)
         out = torch.cat([pi, v[:, None], gpi, gv[:, None]], dim=1).cpu().numpy()
         A = self.action_size
         return out[:, :A], out[:, A], out[:, A + 1:2 * A + 1], out[:, 2 * A + 1]

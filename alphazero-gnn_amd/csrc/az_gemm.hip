@@ -977,7 +977,11 @@ static int glds_splits(const GemmArgs& a, long tiles, size_t ws_bytes) {
   return best;
 }
 
-int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
+// The GEMM without its split-K reduction: when the plan splits K, the raw partial sums are left
+// in d->ws as slabs [*splits_out][M][N] and C is NOT written (the caller reduces them, e.g.
+// fused with its consumer: az_transform_heads_fwd); otherwise C is written and *splits_out = 1.
+int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
+  *splits_out = 1;
   AZ_REQUIRE(d != nullptr, AZ_EINVAL, "az_gemm_f32: null descriptor");
   AZ_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, AZ_EINVAL, "az_gemm_f32: negative size");
   if (d->M == 0 || d->N == 0) return AZ_OK;
@@ -1042,12 +1046,31 @@ int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
     if (S > 1) a.splits = (a.K + a.kc - 1) / a.kc;
   }
   launch_cfg(cfg, a, akm, bkm, s);
-  int rc = check_launch("gemm_f32_mfma");
-  if (rc || a.splits <= 1) return rc;
+  *splits_out = a.splits;
+  return check_launch("gemm_f32_mfma");
+}
+
+// Sums the split-K slabs a gemm_f32_partial call left in d->ws (in slab order) and applies d's
+// epilogue into d->C.
+int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s) {
+  GemmArgs a = {};
+  a.M = d->M; a.N = d->N;
+  a.bias = d->bias; a.act = d->act; a.R = d->R; a.ldr = d->ldr; a.G = d->G; a.ldg = d->ldg;
+  a.beta = d->beta; a.C = d->C; a.ldc = d->ldc; a.c_rows = d->c_rows;
+  a.C2 = d->C2; a.ldc2 = d->ldc2;
+  a.slab = static_cast<float*>(d->ws);
+  a.splits = splits;
   const long total = (long)a.M * a.N;
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, a);
   return check_launch("splitk_reduce_kernel");
+}
+
+int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
+  int splits = 1;
+  int rc = gemm_f32_partial(d, s, &splits);
+  if (rc || splits <= 1) return rc;
+  return splitk_reduce(d, splits, s);
 }
 
 }  // namespace az

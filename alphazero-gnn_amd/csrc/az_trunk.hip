@@ -187,6 +187,68 @@ __global__ __launch_bounds__(256) void heads_partial_kernel(
   }
 }
 
+// output_transform's second GEMM (gnn_utils.py:115) left as S split-K slabs, reduced here and
+// fed straight into the heads' first pass (Connect4GNN.py:48-57): block (chunk c of 256
+// columns, 16 rows) as heads_partial_kernel; each lane sums its float4 of the S slabs in slab
+// order and adds the bias -- the arithmetic of splitk_reduce_kernel -- stores y, and forms the
+// same per-chunk dot products, so y, logp, pi and v are bit-identical to the unfused path while
+// y is never re-read from HBM.
+template <int AMAX, int S>
+__global__ __launch_bounds__(256) void splitk_heads_partial_kernel(
+    const float* __restrict__ slab, int B, int K, const float* __restrict__ bias,
+    float* __restrict__ y, const float* __restrict__ wp, int A, const float* __restrict__ wv,
+    float* __restrict__ part) {
+  const int c = blockIdx.x;
+  const int r0 = blockIdx.y * HEADS_ROWS;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int k = c * HEADS_KC + lane * 4;
+  const bool kin = k < K;
+  const size_t plane = (size_t)B * K;
+  constexpr int RPW = HEADS_ROWS / 4;
+  // slab loads first (S x RPW float4 in flight per lane), weights behind them
+  f32x4 sv[RPW][S];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int row = r0 + wave + 4 * i;
+    const size_t off = (kin && row < B) ? (size_t)row * K + k : 0;
+#pragma unroll
+    for (int q = 0; q < S; ++q) sv[i][q] = *reinterpret_cast<const f32x4*>(slab + q * plane + off);
+  }
+  f32x4 w[AMAX + 1];
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a)
+    w[a] = (a < A && kin) ? *reinterpret_cast<const f32x4*>(wp + (size_t)a * K + k)
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+  w[AMAX] = kin ? *reinterpret_cast<const f32x4*>(wv + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 bb = kin ? *reinterpret_cast<const f32x4*>(bias + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int LOGV = AMAX == 8 ? 3 : (AMAX == 16 ? 4 : 5);
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int row = r0 + wave + 4 * i;
+    if (row >= B) break;
+    f32x4 x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < S; ++q) t += sv[i][q][e];
+      x[e] = kin ? t + bb[e] : 0.f;
+    }
+    if (kin) *reinterpret_cast<f32x4*>(y + (size_t)row * K + k) = x;
+    float* out = part + ((size_t)c * B + row) * (A + 1);
+    float pv[AMAX];
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a)
+      pv[a] = fmaf(x[3], w[a][3], fmaf(x[2], w[a][2], fmaf(x[1], w[a][1], x[0] * w[a][0])));
+    const float ps = wave_multi_sum<AMAX>(pv);
+    const float vs = wave_sum(
+        fmaf(x[3], w[AMAX][3], fmaf(x[2], w[AMAX][2], fmaf(x[1], w[AMAX][1], x[0] * w[AMAX][0]))));
+    const int a = lane >> (6 - LOGV);
+    if ((lane & ((1 << (6 - LOGV)) - 1)) == 0 && a < A) out[a] = ps;
+    if (lane == 0) out[A] = vs;
+  }
+}
+
 // 16 rows x 16 lanes per block: lane (row, a) sums value a's chunk partials in chunk order (the
 // same order as a serial loop, so the result does not depend on the launch shape), then one
 // thread per row applies log_softmax / exp / tanh.
@@ -292,6 +354,12 @@ extern "C" int az_conv3x3_relu_fwd(const void* in, int in_int8, int B, int Cin, 
   return check_launch("conv3x3_relu_kernel");
 }
 
+namespace az {
+int gemm_f32(const az_gemm_desc* d, hipStream_t s);
+int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out);
+int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s);
+}  // namespace az
+
 extern "C" size_t az_heads_ws_bytes(int B, int K, int A) {
   return (size_t)((K + HEADS_KC - 1) / HEADS_KC) * (size_t)B * (size_t)(A + 1) * 4;
 }
@@ -330,4 +398,95 @@ extern "C" int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv
   else
     launch_heads<32>(hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v, part, s);
   return check_launch("heads_kernels");
+}
+
+static size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
+extern "C" size_t az_transform_heads_ws_bytes(int B, int F, int A) {
+  // the heads' chunk partials, then room for 8 split-K slabs of the [B][F] GEMM outputs
+  return align256(az_heads_ws_bytes(B, F, A)) + (size_t)8 * B * F * 4;
+}
+
+template <int S>
+static void launch_splitk_heads(const float* slab, int B, int K, const float* bias, float* y,
+                                const float* wp, int A, const float* wv, float* part,
+                                hipStream_t s) {
+  dim3 g((K + HEADS_KC - 1) / HEADS_KC, (B + HEADS_ROWS - 1) / HEADS_ROWS);
+  hipLaunchKernelGGL((splitk_heads_partial_kernel<8, S>), g, dim3(256), 0, s, slab, B, K, bias, y,
+                     wp, A, wv, part);
+}
+
+extern "C" int az_linear_heads_fwd(const float* x, int B, int F, const float* w, const float* b,
+                                   const float* wp, const float* bp, int A, const float* wv,
+                                   const float* bv, float* y, float* logp, float* pi, float* v,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  AZ_REQUIRE(B >= 0 && F > 0 && F % 4 == 0 && A > 0 && A <= 32, AZ_EINVAL,
+             "az_linear_heads_fwd: bad shape B=%d F=%d A=%d", B, F, A);
+  if (B == 0) return AZ_OK;
+  AZ_REQUIRE(x && w && b && wp && bp && wv && bv && y && logp && v && ws, AZ_EINVAL,
+             "az_linear_heads_fwd: null pointer");
+  const size_t part_bytes = align256(az_heads_ws_bytes(B, F, A));
+  AZ_REQUIRE(ws_bytes >= part_bytes, AZ_EINVAL, "az_linear_heads_fwd: workspace too small");
+  AZ_REQUIRE(aligned16(x) && aligned16(y) && aligned16(wp) && aligned16(wv) && aligned16(b) &&
+                 aligned16(ws),
+             AZ_EINVAL, "az_linear_heads_fwd: operands need 16B alignment");
+  hipStream_t s = as_stream(stream);
+  float* part = static_cast<float*>(ws);
+  void* slabs = static_cast<char*>(ws) + part_bytes;
+  int rc;
+  // y = x W^T + b, its split-K reduction fused into the heads' first pass
+  az_gemm_desc d = {};
+  d.M = B; d.N = F; d.K = F;
+  d.A = x; d.lda = F; d.a_kmajor = 1;
+  d.B = w; d.ldb = F; d.b_kmajor = 1; d.bias = b; d.act = AZ_ACT_NONE;
+  d.C = y; d.ldc = F;
+  d.ws = slabs; d.ws_bytes = ws_bytes - part_bytes;
+  int S = 1;
+  if ((rc = gemm_f32_partial(&d, s, &S))) return rc;
+  const float* sl = static_cast<const float*>(slabs);
+  if (S > 1 && A <= 8 && S <= 8) {
+    switch (S) {
+      case 2: launch_splitk_heads<2>(sl, B, F, b, y, wp, A, wv, part, s); break;
+      case 3: launch_splitk_heads<3>(sl, B, F, b, y, wp, A, wv, part, s); break;
+      case 4: launch_splitk_heads<4>(sl, B, F, b, y, wp, A, wv, part, s); break;
+      case 5: launch_splitk_heads<5>(sl, B, F, b, y, wp, A, wv, part, s); break;
+      case 6: launch_splitk_heads<6>(sl, B, F, b, y, wp, A, wv, part, s); break;
+      case 7: launch_splitk_heads<7>(sl, B, F, b, y, wp, A, wv, part, s); break;
+      default: launch_splitk_heads<8>(sl, B, F, b, y, wp, A, wv, part, s); break;
+    }
+    if ((rc = check_launch("splitk_heads_partial_kernel"))) return rc;
+    hipLaunchKernelGGL(heads_finalize_kernel<8>, dim3((B + FIN_ROWS - 1) / FIN_ROWS), dim3(256), 0,
+                       s, part, (F + HEADS_KC - 1) / HEADS_KC, B, A, bp, bv, logp, pi, v);
+    return check_launch("heads_finalize_kernel");
+  }
+  if (S > 1 && (rc = splitk_reduce(&d, S, s))) return rc;
+  return az_heads_fwd(y, F, y, F, B, F, wp, bp, A, wv, bv, logp, pi, v, part, part_bytes, stream);
+}
+
+extern "C" int az_transform_heads_fwd(const float* x, int B, int F, const float* w0,
+                                      const float* b0, const float* w2, const float* b2,
+                                      const float* wp, const float* bp, int A, const float* wv,
+                                      const float* bv, float* hidden, float* y, float* logp,
+                                      float* pi, float* v, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  AZ_REQUIRE(B >= 0 && F > 0 && F % 4 == 0, AZ_EINVAL,
+             "az_transform_heads_fwd: bad shape B=%d F=%d", B, F);
+  if (B == 0) return AZ_OK;
+  AZ_REQUIRE(x && w0 && b0 && hidden && ws, AZ_EINVAL, "az_transform_heads_fwd: null pointer");
+  AZ_REQUIRE(aligned16(x) && aligned16(hidden) && aligned16(ws), AZ_EINVAL,
+             "az_transform_heads_fwd: operands need 16B alignment");
+  const size_t part_bytes = align256(az_heads_ws_bytes(B, F, A > 0 ? A : 1));
+  AZ_REQUIRE(ws_bytes >= part_bytes, AZ_EINVAL, "az_transform_heads_fwd: workspace too small");
+  // hidden = relu(x W0^T + b0)   (output_transform.0 + ReLU); slabs after the heads' partials
+  az_gemm_desc d = {};
+  d.M = B; d.N = F; d.K = F;
+  d.A = x; d.lda = F; d.a_kmajor = 1;
+  d.B = w0; d.ldb = F; d.b_kmajor = 1; d.bias = b0; d.act = AZ_ACT_RELU;
+  d.C = hidden; d.ldc = F;
+  d.ws = static_cast<char*>(ws) + part_bytes; d.ws_bytes = ws_bytes - part_bytes;
+  int rc = gemm_f32(&d, as_stream(stream));
+  if (rc) return rc;
+  // y = hidden W2^T + b2 (output_transform.2) and the heads
+  return az_linear_heads_fwd(hidden, B, F, w2, b2, wp, bp, A, wv, bv, y, logp, pi, v, ws,
+                             ws_bytes, stream);
 }

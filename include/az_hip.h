@@ -118,6 +118,28 @@ int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv, int B, in
                  const float* wp, const float* bp, int A, const float* wv, const float* bv,
                  float* logp, float* pi, float* v, void* ws, size_t ws_bytes, void* stream);
 
+/* Per-row GNN evaluation tail: output_transform then the heads, i.e. gnn_utils.py:115 (in the
+ * 1-row form of Connect4GNN.py:108-111, where the layers are the identity, gnn_utils.py:35-36)
+ * followed by Connect4GNN.py:48-57 -- the batched predict_with_gnn after extract_features:
+ *   hidden = relu(x W0^T + b0);  y = hidden W2^T + b2;  logp = log_softmax(y wp^T + bp);
+ *   pi = exp(logp) (may be NULL);  v = tanh(y wv^T + bv).
+ * x, hidden, y: [B][F]; W0, W2: [F][F] (nn.Linear layout); wp [A][F]; wv [1][F]; A <= 32.
+ * When the second GEMM is split over K, its slab reduction, bias, the store of y and the heads'
+ * dot products run in one pass (y is not re-read); results equal az_gemm_f32 + az_heads_fwd
+ * bit for bit.  ws: >= az_heads_ws_bytes(B, F, A) rounded up to 256 B; az_transform_heads_ws_bytes
+ * leaves room for the split-K slabs (a smaller workspace only limits the K split). */
+size_t az_transform_heads_ws_bytes(int B, int F, int A);
+/* Its second half alone: y = x W^T + b, then the heads of y (same fusion, same workspace). */
+int az_linear_heads_fwd(const float* x, int B, int F, const float* w, const float* b,
+                        const float* wp, const float* bp, int A, const float* wv, const float* bv,
+                        float* y, float* logp, float* pi, float* v, void* ws, size_t ws_bytes,
+                        void* stream);
+int az_transform_heads_fwd(const float* x, int B, int F, const float* w0, const float* b0,
+                           const float* w2, const float* b2, const float* wp, const float* bp,
+                           int A, const float* wv, const float* bv, float* hidden, float* y,
+                           float* logp, float* pi, float* v, void* ws, size_t ws_bytes,
+                           void* stream);
+
 /* ---------------------------------------------------------------------------------
  * GNN message passing (gnn_utils.py:5-74) over a destination-sorted CSR graph.
  * The reference's star (row 0 = destination, rows 1..N-1 = sources) is the CSR with

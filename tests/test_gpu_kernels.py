@@ -263,3 +263,35 @@ def test_adam_vs_oracle(ops):
         ops.adam(pd, cu(g), md, vd, 1e-3, step)
         P = opt.step(P, {"p": g.astype(np.float64)})
     np.testing.assert_allclose(pd.cpu().numpy(), P["p"], atol=1e-6)
+
+
+@pytest.mark.parametrize("B", [1, 5, 64, 300, 512, 1024, 4096])
+def test_transform_heads_fused_equals_unfused(ops, B):
+    """az_transform_heads_fwd (second GEMM's split-K reduction fused into the heads) is bit-
+    identical to az_gemm_f32 x2 + az_heads_fwd, and matches the oracle within 1e-5
+    (gnn_utils.py:115 then Connect4GNN.py:48-57, per row)."""
+    from oracle import nets as O
+    F, A = 3136, 8
+    g = torch.Generator().manual_seed(B)
+    x = torch.rand((B, F), generator=g) * 2 - 1
+    w0 = (torch.rand((F, F), generator=g) * 2 - 1) / F ** 0.5
+    w2 = (torch.rand((F, F), generator=g) * 2 - 1) / F ** 0.5
+    b0, b2 = (torch.rand((F,), generator=g) - 0.5) * 0.1, (torch.rand((F,), generator=g) - 0.5) * 0.1
+    wp = (torch.rand((A, F), generator=g) * 2 - 1) / F ** 0.5
+    wv = (torch.rand((1, F), generator=g) * 2 - 1) / F ** 0.5
+    bp, bv = torch.rand((A,), generator=g) - 0.5, torch.rand((1,), generator=g) - 0.5
+    c = [t.cuda() for t in (x, w0, b0, w2, b2, wp, bp, wv, bv)]
+    logp, pi, v, y, hid = ops.transform_heads(*c)
+    h_ref = ops.linear(c[0], c[1], c[2], act=ops.ACT_RELU)
+    y_ref = ops.linear(h_ref, c[3], c[4])
+    lp_ref, pi_ref, v_ref = ops.heads(y_ref, c[5], c[6], c[7], c[8])
+    torch.cuda.synchronize()
+    assert torch.equal(hid, h_ref) and torch.equal(y, y_ref)
+    assert torch.equal(logp, lp_ref) and torch.equal(pi, pi_ref) and torch.equal(v, v_ref)
+    G = {"output_transform.0.weight": w0.numpy(), "output_transform.0.bias": b0.numpy(),
+         "output_transform.2.weight": w2.numpy(), "output_transform.2.bias": b2.numpy()}
+    W = {"fc_policy.weight": wp.numpy(), "fc_policy.bias": bp.numpy(),
+         "fc_value.weight": wv.numpy(), "fc_value.bias": bv.numpy()}
+    olp, ov = O.c4_heads(O.policy_value_gnn_per_row(x.numpy(), G), W)
+    assert np.abs(logp.cpu().numpy() - olp).max() < 1e-5
+    assert np.abs(v.cpu().numpy() - ov).max() < 1e-5

@@ -49,10 +49,12 @@ def main(d, tag):
         """per az_gemm_f32 call: the tile kernel + the reduce that immediately follows it"""
         tile, red = [], []
         for i, (_, name, kb, _) in enumerate(rows):
-            if tile_pred(name):
+            nxt = rows[i + 1][1] if i + 1 < len(rows) else ""
+            # output_transform.0 = the tile kernel followed by its splitk_reduce_kernel (the
+            # second GEMM's slabs go to splitk_heads_partial_kernel instead)
+            if tile_pred(name) and "splitk_reduce" in nxt:
                 tile.append(kb)
-                nxt = rows[i + 1][1] if i + 1 < len(rows) else ""
-                red.append(rows[i + 1][2] if "splitk_reduce" in nxt else 0.0)
+                red.append(rows[i + 1][2])
         n = max(1, len(tile))
         return sum(tile) / n, sum(red) / n, len(tile)
 
@@ -71,7 +73,7 @@ def main(d, tag):
                   f"(tools/gpu_profile.sh {tag}); per-kernel averages over all dispatches; "
                   f"bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE reports "
                   f"half of wide reads, MI355X_MICROARCH.md HBM section)",
-        "gemm": {"kernel": "az_gemm_f32 output_transform call (gemm_f32_glds tile kernel + "
+        "gemm": {"kernel": "az_gemm_f32 output_transform.0 call (gemm_f32_glds tile kernel + "
                            "splitk_reduce_kernel)",
                  "dispatches": nf,
                  "hbm_bytes_per_launch": gemm_tile + gemm_red,
