@@ -37,6 +37,8 @@ struct GemmArgs {
   // the epilogue.
   int splits, kc;
   float* slab;
+  int ablate;   // timing experiments only (AZ_GEMM_ABLATE, glds2): 1 = no DMA after the first
+                // tile, 2 = no barrier in the k loop; results are then wrong
 };
 
 __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int col, float acc) {
@@ -185,6 +187,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][
   }
   const size_t plane = (size_t)p.M * p.N;
   float* slab = p.slab + (size_t)sp * plane;
+  const bool abl = (p.ablate & 4) != 0;
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -192,7 +195,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][
 #pragma unroll
       for (int r = 0; r < NACC; ++r) {
         const int row = row_of(i, r), col = c0 + j * MF + cl;
-        if (row < p.M && col < p.N) slab[(size_t)row * p.N + col] = acc[i][j][r];
+        if (row < p.M && col < p.N && (!abl || acc[i][j][r] != acc[i][j][r]))
+          slab[(size_t)row * p.N + col] = acc[i][j][r];
       }
 }
 
@@ -698,7 +702,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
+    const bool more = kt + 1 < nk && !(p.ablate & 1);
     if (!IL && more) issue(cur ^ 1, kbeg + (kt + 1) * BK);
     const float* S = smem + cur * (BM + BN) * BK;
     f32x4 a[NG][TI], b[NG][TJ];
@@ -754,7 +758,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
       __builtin_amdgcn_s_waitcnt(0);
       zero_tail(cur ^ 1, kbeg + (kt + 1) * BK);
     }
-    __syncthreads();
+    if (!(p.ablate & 2)) __syncthreads();
   }
 
   tile_epilogue<MF, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp);
@@ -1016,6 +1020,8 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
   a.C2 = d->C2; a.ldc2 = d->ldc2;
   a.slab = static_cast<float*>(d->ws);
   a.splits = 1; a.kc = d->K;
+  static const char* env_abl = getenv("AZ_GEMM_ABLATE");
+  a.ablate = env_abl ? atoi(env_abl) : 0;
 
   if (d->M <= 8 && akm && bkm && !d->C2 && d->act != AZ_ACT_DRELU) {
     launch_gemv(a, s);

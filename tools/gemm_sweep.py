@@ -76,10 +76,20 @@ if __name__ == "__main__":
                     print(json.dumps({"M": M, "cfg": cfg, "splits": sp or "auto", **res}),
                           flush=True)
         sys.exit(0)
-    if mode == "ablate":
-        for (M, N, K) in [(4096, 3136, 3136), (512, 3136, 3136)]:
-            for cfg in ("0", "1"):
-                for abl in ("0", "1", "2"):
+    if mode == "longk":        # steady state: K 10x longer, fixed splits (per-block overhead amortised)
+        for cfg in sys.argv[2].split(","):
+            for abl in sys.argv[3].split(","):
+                res = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_ABLATE": abl, "AZ_GEMM_SPLITS": "5"},
+                          512, 3136, 31360)
+                print(json.dumps({"M": 512, "K": 31360, "cfg": cfg, "ablate": abl, **res}),
+                      flush=True)
+        sys.exit(0)
+    if mode == "ablate":       # glds2 timing ablations (results wrong by design)
+        cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else ("15", "16")
+        abls = sys.argv[3].split(",") if len(sys.argv) > 3 else ("0", "1", "2", "3")
+        for (M, N, K) in [(512, 3136, 3136), (4096, 3136, 3136)]:
+            for cfg in cfgs:
+                for abl in abls:
                     res = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_ABLATE": abl}, M, N, K)
                     print(json.dumps({"M": M, "cfg": cfg, "ablate": abl, **res}), flush=True)
         sys.exit(0)
