@@ -858,6 +858,8 @@ struct TileCfg { int bm, bn, bk, wgm, wgn; };
 // mfma16  17: 128x64 mfma16  18: 128x64 mfma32  19: 128x128 mfma16 (8 waves 2x4)
 // v2 + DMA issue interleaved with the MFMAs: 20: 128x128 mfma32  21: 128x128 mfma16
 // 22: 128x64 mfma16
+// 8-wave 1-block-per-CU tiles (6 DMA pieces per 64 MFMAs instead of 8): 23: 256x128 (glds)
+// 24: 256x128 (v2, mfma16)  25: 128x256 (v2, mfma16)
 static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 64, 64, 2, 2},
                                 {128, 64, 32, 2, 2}, {128, 128, 32, 2, 4}, {256, 128, 32, 4, 2},
                                 {128, 128, 32, 2, 2}, {64, 64, 32, 2, 2},  {128, 64, 32, 2, 2},
@@ -865,8 +867,9 @@ static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 
                                 {128, 64, 32, 2, 2},  {128, 128, 16, 2, 2}, {128, 64, 16, 2, 2},
                                 {128, 128, 32, 2, 2}, {128, 128, 32, 2, 2}, {128, 64, 32, 2, 2},
                                 {128, 64, 32, 2, 2},  {128, 128, 32, 2, 4}, {128, 128, 32, 2, 2},
-                                {128, 128, 32, 2, 2}, {128, 64, 32, 2, 2}};
-constexpr int kNumCfgs = 23;
+                                {128, 128, 32, 2, 2}, {128, 64, 32, 2, 2},  {256, 128, 32, 4, 2},
+                                {256, 128, 32, 4, 2}, {128, 256, 32, 2, 4}};
+constexpr int kNumCfgs = 26;
 
 template <int BM, int BN, int BK, int WGM, int WGN>
 static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
@@ -904,6 +907,9 @@ static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream
     case 17: launch_glds2<128, 64, 2, 2, 16>(a, s); break;
     case 18: launch_glds2<128, 64, 2, 2, 32>(a, s); break;
     case 19: launch_glds2<128, 128, 2, 4, 16>(a, s); break;
+    case 23: launch_glds<256, 128, 4, 2>(a, s); break;
+    case 24: launch_glds2<256, 128, 4, 2, 16>(a, s); break;
+    case 25: launch_glds2<128, 256, 2, 4, 16>(a, s); break;
     case 20: launch_glds2<128, 128, 2, 2, 32, true>(a, s); break;
     case 21: launch_glds2<128, 128, 2, 2, 16, true>(a, s); break;
     case 22: launch_glds2<128, 64, 2, 2, 16, true>(a, s); break;
@@ -981,6 +987,18 @@ static int glds_splits(const GemmArgs& a, long tiles, size_t ws_bytes) {
   return best;
 }
 
+// Split factor for the 256x128 8-wave tile (96 KB of LDS: one block per CU): the largest S with
+// tiles * S <= 256 CUs, used only when that grid fills >= 90 % of the CUs, each split keeps
+// >= 8 k-tiles and the S slabs fit the workspace; 0 = do not use this tile.
+static int splits_256x128(int M, int N, int K, size_t ws_bytes) {
+  const long tiles = (long)((M + 255) / 256) * ((N + 127) / 128);
+  if (tiles >= 256) return 0;
+  const int S = (int)std::min<long>(256 / tiles, 8);
+  if (tiles * S < 230) return 0;
+  if (S > 1 && ((long)K / S < 8 * 32 || (size_t)S * M * N * 4 > ws_bytes)) return 0;
+  return S;
+}
+
 // The GEMM without its split-K reduction: when the plan splits K, the raw partial sums are left
 // in d->ws as slabs [*splits_out][M][N] and C is NOT written (the caller reduces them, e.g.
 // fused with its consumer: az_transform_heads_fwd); otherwise C is written and *splits_out = 1.
@@ -1031,9 +1049,14 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
   static const char* env_cfg = getenv("AZ_GEMM_CFG");
   const bool glds_ok = akm && bkm && !d->A2 && !d->a_rows;
   int cfg = 0;
+  int s256 = 0;   // split factor when the 256x128 8-wave tile packs the chip (one block per CU)
   if (env_cfg) {
     cfg = std::min(std::max(atoi(env_cfg), 0), kNumCfgs - 1);
     if (cfg >= 6 && !glds_ok) cfg = 0;
+  } else if (glds_ok && d->M > 256 && (s256 = splits_256x128(d->M, d->N, d->K, d->ws_bytes)) > 0) {
+    // 256x128 tile, 8 waves, one block per CU, K split so the grid fills >= 90 % of the CUs
+    // (tools/gemm_sweep.py glds on MI355X, M = 512: 106 us vs 113 us for 128x128 x 5)
+    cfg = 24;
   } else if (glds_ok && d->M > 128) {
     // LDS-DMA tiles (tools/gemm_sweep.py glds on MI355X): 128x64 once the grid fills the chip,
     // 128x128 + split-K below that
@@ -1045,7 +1068,11 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
   const TileCfg& tc = kCfgs[cfg];
   plan(a, tc.bm, tc.bn, tc.bk, d->ws_bytes);
   const bool is128 = tc.bm == 128 && tc.bn == 128 && cfg >= 6;
-  if (is128 && !getenv("AZ_GEMM_SPLITS")) {
+  if (s256 > 0 && !getenv("AZ_GEMM_SPLITS")) {
+    a.splits = s256;
+    a.kc = s256 > 1 ? ((a.K + s256 - 1) / s256 + 31) / 32 * 32 : a.K;
+    if (s256 > 1) a.splits = (a.K + a.kc - 1) / a.kc;
+  } else if (is128 && !getenv("AZ_GEMM_SPLITS")) {
     const int S = glds_splits(a, (long)((a.M + 127) / 128) * ((a.N + 127) / 128), d->ws_bytes);
     a.splits = S;
     a.kc = S > 1 ? ((a.K + S - 1) / S + 31) / 32 * 32 : a.K;

@@ -73,7 +73,7 @@ def main(d, tag):
                   f"(tools/gpu_profile.sh {tag}); per-kernel averages over all dispatches; "
                   f"bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE reports "
                   f"half of wide reads, MI355X_MICROARCH.md HBM section)",
-        "gemm": {"kernel": "az_gemm_f32 output_transform.0 call (gemm_f32_glds tile kernel + "
+        "gemm": {"kernel": "az_gemm_f32 output_transform.0 call (gemm_f32_glds2 tile kernel + "
                            "splitk_reduce_kernel)",
                  "dispatches": nf,
                  "hbm_bytes_per_launch": gemm_tile + gemm_red,
