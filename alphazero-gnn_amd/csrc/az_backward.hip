@@ -336,6 +336,55 @@ __global__ __launch_bounds__(256) void gnn_agg_bwd_edges_kernel(
   }
 }
 
+// High in-degree form of gnn_agg_bwd_edges_kernel (the star: one destination, N-1 edges,
+// F = 3136), in two passes so the per-edge dot products run in parallel:
+//  1. one wave per edge: p_e = dagg[dst(e)] . x[src(e)]  -> dsc[e] (scratch)
+//  2. one wave per destination: S = sum alpha, swd = sum_e w_e p_e (wave reductions), then
+//     dsc[e] = (norm ? (p_e - swd) / S : p_e) * a (1 - a),  an[e] = norm ? a / S : a.
+__global__ __launch_bounds__(256) void gnn_agg_bwd_dots_kernel(
+    int E, const int* __restrict__ edge_dst, const int* __restrict__ dst_index,
+    const int* __restrict__ col, const float* __restrict__ x, int F,
+    const float* __restrict__ dc, float* __restrict__ pdot) {
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (e >= E) return;
+  const int d = edge_dst[e];
+  const int r = dst_index ? dst_index[d] : d;
+  const float* dagg = dc + (size_t)r * 2 * F + F;
+  const float* xs = x + (size_t)col[e] * F;
+  float p = 0.f;
+  for (int f = lane * 4; f < F; f += 256) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(dagg + f);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(xs + f);
+    p = fmaf(a[0], b[0], fmaf(a[1], b[1], fmaf(a[2], b[2], fmaf(a[3], b[3], p))));
+  }
+  p = wave_sum(p);
+  if (lane == 0) pdot[e] = p;
+}
+
+__global__ __launch_bounds__(256) void gnn_agg_bwd_finish_kernel(
+    int D, const int* __restrict__ rows, const int* __restrict__ rowptr,
+    const float* __restrict__ alpha, float* __restrict__ dsc, float* __restrict__ an) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= D) return;
+  const int d = rows ? rows[r] : r;
+  const int e0 = rowptr[d], e1 = rowptr[d + 1];
+  float S = 0.f;
+  for (int e = e0 + lane; e < e1; e += 64) S += alpha[e];
+  S = wave_sum(S);
+  const bool norm = S > 0.f;
+  float swd = 0.f;
+  for (int e = e0 + lane; e < e1; e += 64) swd = fmaf(norm ? alpha[e] / S : alpha[e], dsc[e], swd);
+  swd = wave_sum(swd);
+  for (int e = e0 + lane; e < e1; e += 64) {
+    const float a = alpha[e], pe = dsc[e];
+    const float da = norm ? (pe - swd) / S : pe;
+    dsc[e] = da * a * (1.f - a);
+    an[e] = norm ? a / S : a;
+  }
+}
+
 // One wave per node v:
 //   dP[v][2q]   = sum_{e: dst(e)=v} dpre_e[q]     dP[v][2q+1] = sum_{e: src(e)=v} dpre_e[q]
 //   dpre_e[q]   = dsc_e * w2[q] * (P[dst][2q] + P[src][2q+1] + b1[q] > 0)
@@ -648,7 +697,15 @@ extern "C" int az_gnn_layer_bwd(const az_graph* g, const float* x, int F, int H,
                      dx);
   if ((rc = check_launch("gnn_dc_scatter_kernel"))) return rc;
   // aggregation + attention backward
-  if (E > 0) {
+  if (E > 0 && E >= 16L * D) {
+    // few destinations with many in-edges (the training star): per-edge dots in parallel
+    hipLaunchKernelGGL(gnn_agg_bwd_dots_kernel, dim3((E + 3) / 4), dim3(256), 0, s, E,
+                       g->edge_dst, D == V ? nullptr : g->dst_index, g->col, x, F, L.dc, L.dsc);
+    if ((rc = check_launch("gnn_agg_bwd_dots_kernel"))) return rc;
+    hipLaunchKernelGGL(gnn_agg_bwd_finish_kernel, dim3((D + 3) / 4), dim3(256), 0, s, D, rows,
+                       g->rowptr, sv.alpha, L.dsc, L.an);
+    if ((rc = check_launch("gnn_agg_bwd_finish_kernel"))) return rc;
+  } else if (E > 0) {
     hipLaunchKernelGGL(gnn_agg_bwd_edges_kernel, dim3((D + 3) / 4), dim3(256), 0, s, D, rows,
                        g->rowptr, g->col, sv.alpha, x, F, L.dc, L.dsc, L.an);
     if ((rc = check_launch("gnn_agg_bwd_edges_kernel"))) return rc;

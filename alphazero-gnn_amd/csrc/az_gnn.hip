@@ -137,6 +137,68 @@ __global__ __launch_bounds__(256) void aggregate_lanes_kernel(
   }
 }
 
+// High in-degree form (the reference's star: one destination, N-1 sources, F = 3136): the
+// lanes kernel would give one destination to one wave walking all its edges serially.  Here
+// block (destination i, 256-column chunk c) splits the destination's edges over its 4 waves in
+// contiguous quarters; each wave keeps its quarter's weighted float4 sums, the quarters are
+// added in wave order through LDS (deterministic), and sum(alpha) comes from a wave reduction.
+__global__ __launch_bounds__(256) void aggregate_wide_kernel(
+    int identity, const int* __restrict__ dst_rows, const int* __restrict__ rowptr,
+    const int* __restrict__ col, const float* __restrict__ alpha, const float* __restrict__ x,
+    int ldx, int F, float* __restrict__ agg, int ldagg) {
+  __shared__ f32x4 part[4][64];
+  const int i = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int d = identity ? i : dst_rows[i];
+  const int e0 = rowptr[d], e1 = rowptr[d + 1];
+  const int deg = e1 - e0;
+  float S = 0.f;
+  for (int e = e0 + lane; e < e1; e += 64) S += alpha[e];
+  S = wave_sum(S);
+  const bool norm = S > 0.f;
+  const int f = blockIdx.y * 256 + lane * 4;
+  const int q = (deg + 3) / 4;
+  const int eb = e0 + wave * q, ee = min(e1, eb + q);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (f < F) {
+    int e = eb;
+    for (; e + 4 <= ee; e += 4) {
+      int sc[4];
+      float w[4];
+      f32x4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sc[j] = col[e + j];
+        w[j] = norm ? alpha[e + j] / S : alpha[e + j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const f32x4*>(x + (size_t)sc[j] * ldx + f);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = fmaf(w[j], v[j][c], acc[c]);
+    }
+    for (; e < ee; ++e) {
+      const float w = norm ? alpha[e] / S : alpha[e];
+      const f32x4 v = *reinterpret_cast<const f32x4*>(x + (size_t)col[e] * ldx + f);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = fmaf(w, v[c], acc[c]);
+    }
+  }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && f < F) {
+    f32x4 r = part[0][lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const f32x4 t = part[w][lane];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) r[c] += t[c];
+    }
+    *reinterpret_cast<f32x4*>(agg + (size_t)d * ldagg + f) = r;
+  }
+}
+
 template <int LPR, int NV>
 static void launch_aggregate(const az_graph* g, int identity, const float* x, int ldx, int F,
                              const float* alpha, float* agg, int ldagg, hipStream_t s) {
@@ -150,6 +212,13 @@ int aggregate(const az_graph* g, const float* x, int ldx, int F, const float* al
               int ldagg, hipStream_t s) {
   if (g->D == 0) return AZ_OK;
   const int identity = (g->D == g->V) ? 1 : 0;
+  // few destinations with many in-edges each (the star of a training batch): spread every
+  // destination's edges over a block instead of walking them in one wave
+  if ((long)g->D * F < 65536 && g->E >= 16L * g->D) {
+    hipLaunchKernelGGL(aggregate_wide_kernel, dim3(g->D, (F + 255) / 256), dim3(256), 0, s,
+                       identity, g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg, ldagg);
+    return check_launch("aggregate_wide_kernel");
+  }
   if (F <= 32) launch_aggregate<8, 1>(g, identity, x, ldx, F, alpha, agg, ldagg, s);
   else if (F <= 64) launch_aggregate<8, 2>(g, identity, x, ldx, F, alpha, agg, ldagg, s);
   else if (F <= 128) launch_aggregate<16, 2>(g, identity, x, ldx, F, alpha, agg, ldagg, s);
