@@ -7,6 +7,8 @@
 //   x'[d]  = x_d + sigmoid(Wg[x_d;agg_d]+bg) * (Wu2 relu(Wu1[x_d;agg_d]+bu1)+bu2)   3 GEMMs,
 //            the concatenation [x_d;agg_d] is never materialised (A/A2 K-split + row gather),
 //            the gated residual is the last GEMM's epilogue.
+#include <stdlib.h>
+
 #include "az_common.h"
 
 namespace az {
@@ -199,6 +201,77 @@ __global__ __launch_bounds__(256) void aggregate_wide_kernel(
   }
 }
 
+// Max in-degree <= 4 (the synthetic grid), F = 64: 8 lanes x 2 float4 per destination row; a lane
+// group owns DPT consecutive destinations and issues all their index loads, then all their
+// neighbour-row loads, before any math.  NT: agg written with non-temporal stores.
+template <int LPR, int NV, int DPT, bool NT>
+__global__ __launch_bounds__(256) void aggregate_small_kernel(
+    int D, int identity, const int* __restrict__ dst_rows, const int* __restrict__ rowptr,
+    const int* __restrict__ col, const float* __restrict__ alpha, const float* __restrict__ x,
+    int ldx, int F, float* __restrict__ agg, int ldagg) {
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = (blk * 256 + threadIdx.x) / LPR;
+  const int l = threadIdx.x % LPR;
+  const int i0 = grp * DPT;
+  if (i0 >= D) return;
+  int d[DPT], e0[DPT], deg[DPT];
+#pragma unroll
+  for (int t = 0; t < DPT; ++t) {
+    const int i = min(i0 + t, D - 1);
+    d[t] = identity ? i : dst_rows[i];
+    e0[t] = rowptr[d[t]];
+    deg[t] = rowptr[d[t] + 1] - e0[t];
+  }
+  int sc[DPT][4];
+  float a[DPT][4];
+#pragma unroll
+  for (int t = 0; t < DPT; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sc[t][j] = j < deg[t] ? col[e0[t] + j] : 0;
+      a[t][j] = j < deg[t] ? alpha[e0[t] + j] : 0.f;
+    }
+  f32x4 v[DPT][4][NV];
+#pragma unroll
+  for (int t = 0; t < DPT; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        const int f = l * 4 + q * LPR * 4;
+        v[t][j][q] = (j < deg[t] && f < F)
+                         ? *reinterpret_cast<const f32x4*>(x + (size_t)sc[t][j] * ldx + f)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+  for (int t = 0; t < DPT; ++t) {
+    if (i0 + t >= D) break;
+    float S = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < deg[t]) S += a[t][j];
+    const bool norm = S > 0.f;
+    float w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = norm ? a[t][j] / S : a[t][j];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int f = l * 4 + q * LPR * 4;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < deg[t])
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[c] = fmaf(w[j], v[t][j][q][c], acc[c]);
+      if (f < F) {
+        f32x4* dst = reinterpret_cast<f32x4*>(agg + (size_t)d[t] * ldagg + f);
+        if constexpr (NT) __builtin_nontemporal_store(acc, dst);
+        else *dst = acc;
+      }
+    }
+  }
+}
+
 template <int LPR, int NV>
 static void launch_aggregate(const az_graph* g, int identity, const float* x, int ldx, int F,
                              const float* alpha, float* agg, int ldagg, hipStream_t s) {
@@ -218,6 +291,25 @@ int aggregate(const az_graph* g, const float* x, int ldx, int F, const float* al
     hipLaunchKernelGGL(aggregate_wide_kernel, dim3(g->D, (F + 255) / 256), dim3(256), 0, s,
                        identity, g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg, ldagg);
     return check_launch("aggregate_wide_kernel");
+  }
+  static const char* env = getenv("AZ_AGG_CFG");   // tuning experiments only
+  const int cfg = env ? atoi(env) : 0;
+  if (g->max_deg > 0 && g->max_deg <= 4 && F == 64 && cfg != 9) {
+    // the grid: non-temporal agg stores keep the gathered x rows resident in L2 / Infinity
+    // Cache instead of the stream of outputs (tools/agg_sweep.py: 67 -> 42 us on the 512-grid
+    // shard, unchanged at 4096 grids where x alone exceeds the 256 MB cache)
+    const int dpt = cfg == 2 ? 2 : 1;
+    const long groups = ((long)g->D + dpt - 1) / dpt;
+    const int blocks = (int)((groups * 8 + 255) / 256);
+    if (dpt == 2)
+      hipLaunchKernelGGL((aggregate_small_kernel<8, 2, 2, true>), dim3(blocks), dim3(256), 0, s,
+                         g->D, identity, g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg,
+                         ldagg);
+    else
+      hipLaunchKernelGGL((aggregate_small_kernel<8, 2, 1, true>), dim3(blocks), dim3(256), 0, s,
+                         g->D, identity, g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg,
+                         ldagg);
+    return check_launch("aggregate_small_kernel");
   }
   if (F <= 32) launch_aggregate<8, 1>(g, identity, x, ldx, F, alpha, agg, ldagg, s);
   else if (F <= 64) launch_aggregate<8, 2>(g, identity, x, ldx, F, alpha, agg, ldagg, s);

@@ -76,10 +76,7 @@ def cpu_baseline(W, G, seconds, B):
                       f"output_transform -> heads, BLAS threads={threads}), {dt:.1f} s"}
 
 
-def aggregate_roofline(torch, ops, device, graphs=512):
-    """Config 5 per-GPU shard (4096 grids / 8 GPUs): 32x32 4-neighbour grids, F=64, CSR by
-    destination.  Times the scatter-aggregate kernel alone (HIP events)."""
-    h = w = 32
+def _grid_graph(ops, device, graphs, h=32, w=32):
     rp, cl = [0], []
     for r in range(h):
         for c in range(w):
@@ -89,30 +86,58 @@ def aggregate_roofline(torch, ops, device, graphs=512):
             rp.append(len(cl))
     rp, cl = np.array(rp, np.int64), np.array(cl, np.int64)
     V1, E1 = h * w, len(cl)
-    rowptr = np.concatenate([rp[:-1] + g * E1 for g in range(graphs)] + [[graphs * E1]])
-    col = np.concatenate([cl + g * V1 for g in range(graphs)])
-    g = ops.DeviceGraph(rowptr, col, device)
-    V, E, Fd = g.V, g.E, 64
-    gen = torch.Generator(device=device).manual_seed(0)
-    x = torch.rand((V, Fd), device=device, generator=gen) * 2 - 1
-    alpha = torch.rand((E,), device=device, generator=gen)
-    agg = torch.empty_like(x)
-    for _ in range(3):
-        ops.aggregate(g, x, alpha, agg)
-    reps = 20
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
-    for i in range(reps):
-        ev[2 * i].record()
-        ops.aggregate(g, x, alpha, agg)
-        ev[2 * i + 1].record()
-    torch.cuda.synchronize()
-    ms = float(np.mean([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps)]))
-    nbytes = V * Fd * 4 + E * 4 + E * 4 + (V + 1) * 4 + V * Fd * 4
-    gbs = nbytes / (ms * 1e-3) / 1e9
-    return {"kernel": "aggregate_lanes_kernel<8,2>", "bound": "hbm", "achieved": round(gbs, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-            "traffic": None, "avg_launch_us": round(ms * 1e3, 2),
-            "workload": f"{graphs} 32x32 grids, V={V}, E={E}, F=64 (config-5 shard per GPU)"}
+    g = np.arange(graphs, dtype=np.int64)
+    rowptr = np.concatenate([(rp[:-1][None, :] + (g * E1)[:, None]).ravel(), [graphs * E1]])
+    col = (cl[None, :] + (g * V1)[:, None]).ravel()
+    return ops.DeviceGraph(rowptr, col, device)
+
+
+def aggregate_roofline(torch, ops, device, graphs=512, full_graphs=4096):
+    """Config 5 per-GPU shard (4096 grids / 8 GPUs = 512): 32x32 4-neighbour grids, F=64, CSR by
+    destination.  Times the scatter-aggregate kernel alone (HIP events on the launch stream):
+      warm -- back-to-back launches (x, 134 MB, stays resident in the 256 MB Infinity Cache);
+      cold -- the Infinity Cache flushed (a 512 MB read) before every timed launch;
+      full -- the whole config (4096 grids, 1.07 GB of x) on this one GPU, back-to-back."""
+    def run(gr, flush=None, reps=20):
+        g = _grid_graph(ops, device, gr)
+        V, E, Fd = g.V, g.E, 64
+        gen = torch.Generator(device=device).manual_seed(0)
+        x = torch.rand((V, Fd), device=device, generator=gen) * 2 - 1
+        alpha = torch.rand((E,), device=device, generator=gen)
+        agg = torch.empty_like(x)
+        for _ in range(3):
+            ops.aggregate(g, x, alpha, agg)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+        for i in range(reps):
+            if flush is not None:
+                flush.sum()          # a 512 MB read evicts x without leaving dirty lines
+            ev[2 * i].record()
+            ops.aggregate(g, x, alpha, agg)
+            ev[2 * i + 1].record()
+        torch.cuda.synchronize()
+        ms = float(np.mean([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps)]))
+        nbytes = V * Fd * 4 + E * 4 + E * 4 + (V + 1) * 4 + V * Fd * 4   # SURVEY.md §8d config 5
+        return nbytes / (ms * 1e-3) / 1e9, ms * 1e3, V, E
+
+    gbs, us, V, E = run(graphs)
+    flush = torch.zeros((128 << 20,), dtype=torch.float32, device=device)
+    cold_gbs, cold_us, _, _ = run(graphs, flush)
+    del flush
+    out = {"kernel": "aggregate_small_kernel<8,2,1,NT>", "bound": "hbm",
+           "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_us": round(us, 2),
+           "workload": f"{graphs} 32x32 grids, V={V}, E={E}, F=64 (config-5 shard per GPU), "
+                       f"back-to-back launches",
+           "cold": {"achieved": round(cold_gbs, 1), "frac": round(cold_gbs / HBM_PEAK_GBS, 4),
+                    "avg_launch_us": round(cold_us, 2),
+                    "note": "Infinity Cache flushed before each launch"}}
+    if full_graphs:
+        fgbs, fus, fV, fE = run(full_graphs, reps=10)
+        out["full_config"] = {"achieved": round(fgbs, 1), "frac": round(fgbs / HBM_PEAK_GBS, 4),
+                              "avg_launch_us": round(fus, 2),
+                              "workload": f"{full_graphs} grids, V={fV}, E={fE} (all of config 5 "
+                                          f"on one GPU)"}
+    return out
 
 
 def selfplay_args(sims):

@@ -63,8 +63,10 @@ def main(d, tag):
     wt, wr, _ = call_bytes(write, is_fwd_gemm)
     gemm_tile = int((2 * ft + wt) * 1024)
     gemm_red = int((2 * fr + wr) * 1024)
-    agg = [kb for _, n, kb, _ in fetch if "aggregate_lanes_kernel<8, 2>" in n]
-    aggw = [kb for _, n, kb, _ in write if "aggregate_lanes_kernel<8, 2>" in n]
+    # the 512-grid shard launches (grid = V * 8 lanes); the 4096-grid full-config ones excluded
+    shard = 512 * 1024 * 8
+    agg = [kb for _, n, kb, gs in fetch if "aggregate_small_kernel" in n and gs == shard]
+    aggw = [kb for _, n, kb, gs in write if "aggregate_small_kernel" in n and gs == shard]
     B, F = 512, 3136
     res = {
         "round": 1, "tag": tag,
@@ -82,7 +84,7 @@ def main(d, tag):
     }
     if agg and aggw:
         V, E = 512 * 1024, 512 * 3968
-        res["aggregate"] = {"kernel": "aggregate_lanes_kernel<8,2> (512 32x32 grids, F=64)",
+        res["aggregate"] = {"kernel": "aggregate_small_kernel<8,2,1,NT> (512 32x32 grids, F=64)",
                             "hbm_bytes_per_launch": int((2 * sum(agg) / len(agg)
                                                          + sum(aggw) / len(aggw)) * 1024),
                             "algorithmic_bytes": V * 64 * 4 * 2 + E * 8 + (V + 1) * 4}
