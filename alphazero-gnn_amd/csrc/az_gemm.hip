@@ -859,7 +859,8 @@ struct TileCfg { int bm, bn, bk, wgm, wgn; };
 // v2 + DMA issue interleaved with the MFMAs: 20: 128x128 mfma32  21: 128x128 mfma16
 // 22: 128x64 mfma16
 // 8-wave 1-block-per-CU tiles (6 DMA pieces per 64 MFMAs instead of 8): 23: 256x128 (glds)
-// 24: 256x128 (v2, mfma16)  25: 128x256 (v2, mfma16)
+// 24: 256x128 (v2, mfma16)  25: 128x256 (v2, mfma16)  26/27: 256x128 interleaved DMA issue
+// (mfma16 / mfma32)  28: 256x128 (v2, mfma32)
 static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 64, 64, 2, 2},
                                 {128, 64, 32, 2, 2}, {128, 128, 32, 2, 4}, {256, 128, 32, 4, 2},
                                 {128, 128, 32, 2, 2}, {64, 64, 32, 2, 2},  {128, 64, 32, 2, 2},
@@ -868,8 +869,9 @@ static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 
                                 {128, 128, 32, 2, 2}, {128, 128, 32, 2, 2}, {128, 64, 32, 2, 2},
                                 {128, 64, 32, 2, 2},  {128, 128, 32, 2, 4}, {128, 128, 32, 2, 2},
                                 {128, 128, 32, 2, 2}, {128, 64, 32, 2, 2},  {256, 128, 32, 4, 2},
-                                {256, 128, 32, 4, 2}, {128, 256, 32, 2, 4}};
-constexpr int kNumCfgs = 26;
+                                {256, 128, 32, 4, 2}, {128, 256, 32, 2, 4}, {256, 128, 32, 4, 2},
+                                {256, 128, 32, 4, 2}, {256, 128, 32, 4, 2}};
+constexpr int kNumCfgs = 29;
 
 template <int BM, int BN, int BK, int WGM, int WGN>
 static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
@@ -910,6 +912,9 @@ static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream
     case 23: launch_glds<256, 128, 4, 2>(a, s); break;
     case 24: launch_glds2<256, 128, 4, 2, 16>(a, s); break;
     case 25: launch_glds2<128, 256, 2, 4, 16>(a, s); break;
+    case 26: launch_glds2<256, 128, 4, 2, 16, true>(a, s); break;
+    case 27: launch_glds2<256, 128, 4, 2, 32, true>(a, s); break;
+    case 28: launch_glds2<256, 128, 4, 2, 32>(a, s); break;
     case 20: launch_glds2<128, 128, 2, 2, 32, true>(a, s); break;
     case 21: launch_glds2<128, 128, 2, 2, 16, true>(a, s); break;
     case 22: launch_glds2<128, 64, 2, 2, 16, true>(a, s); break;

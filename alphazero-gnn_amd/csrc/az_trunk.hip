@@ -8,7 +8,10 @@
 //      (NB*49), cols = 64 output channels, K = 288 ordered (tap, ci) so that every A-fragment
 //      read is ONE ds_read_b32 at lane-base + compile-time offset.  Each wave owns a 16-channel
 //      column tile and keeps its 72 weight fragments in VGPRs for the whole launch.
-//   4. bias + ReLU epilogue straight to the NCHW-flattened feature rows in HBM.
+//   4. bias + ReLU epilogue into an LDS copy of the NB NCHW-flattened feature rows, written to
+//      HBM as contiguous float4 rows.
+#include <stdlib.h>
+
 #include <algorithm>
 #include "az_common.h"
 
@@ -26,8 +29,13 @@ __global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict_
   constexpr int P = 49, PP = 81, CI = 32;
   constexpr int ROWS = NB * P;
   constexpr int MT = (ROWS + 15) / 16;
+  // STAGE: the output tile is assembled in LDS in NCHW-flatten order and written as whole
+  // float4 rows (the MFMA layout puts 16 channels 49 floats apart on consecutive lanes, so
+  // direct stores scatter 4-byte writes); NB = 8 lacks the LDS for it
+  constexpr bool STAGE = NB <= 4;
   __shared__ float bd[NB * PP];
   __shared__ float c1[NB * CI * PP];
+  __shared__ __attribute__((aligned(16))) float ob[STAGE ? NB * 3136 : 4];
   const int tid = threadIdx.x;
   const int b0 = blockIdx.x * NB;
   const int nb = min(NB, B - b0);
@@ -90,9 +98,16 @@ __global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict_
       if (row < nb * P) {
         const int b = row / P, p = row % P;
         const float v = acc[r] + bias;
-        feat[(size_t)(b0 + b) * 3136 + co * P + p] = v > 0.f ? v : 0.f;
+        if constexpr (STAGE) ob[b * 3136 + co * P + p] = v > 0.f ? v : 0.f;
+        else feat[(size_t)(b0 + b) * 3136 + co * P + p] = v > 0.f ? v : 0.f;
       }
     }
+  }
+  if constexpr (STAGE) {
+    __syncthreads();
+    f32x4v* dst = reinterpret_cast<f32x4v*>(feat + (size_t)b0 * 3136);
+    const f32x4v* src = reinterpret_cast<const f32x4v*>(ob);
+    for (int i = tid; i < nb * 784; i += 512) dst[i] = src[i];
   }
 }
 
@@ -147,32 +162,34 @@ __global__ __launch_bounds__(256) void heads_partial_kernel(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int k = c * HEADS_KC + lane * 4;
   const bool kin = k < K;
-  const bool same = (hp == hv && ldhp == ldhv);
-  f32x4 w[AMAX + 1];
-#pragma unroll
-  for (int a = 0; a < AMAX; ++a)
-    w[a] = (a < A && kin) ? *reinterpret_cast<const f32x4*>(wp + (size_t)a * K + k)
-                          : f32x4{0.f, 0.f, 0.f, 0.f};
-  w[AMAX] = kin ? *reinterpret_cast<const f32x4*>(wv + k) : f32x4{0.f, 0.f, 0.f, 0.f};
-  // all of this wave's rows are loaded before any reduction, so the loads overlap
+  const int kc = kin ? k : 0;
+  // every load is unconditional (addresses clamped into valid memory) and issued before any
+  // value is masked: a select or branch next to a load makes hipcc drain vmcnt there, which
+  // serialised the weight / row round trips of this latency-bound kernel (hv == hp, as for
+  // Connect4, just re-reads the same lines from cache)
   constexpr int RPW = HEADS_ROWS / 4;
   f32x4 xs[RPW], ys[RPW];
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
-    const int row = r0 + wave + 4 * i;
-    const bool ok = kin && row < B;
-    xs[i] = ok ? *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + k)
-               : f32x4{0.f, 0.f, 0.f, 0.f};
-    ys[i] = same ? xs[i]
-                 : (ok ? *reinterpret_cast<const f32x4*>(hv + (size_t)row * ldhv + k)
-                       : f32x4{0.f, 0.f, 0.f, 0.f});
+    const int row = min(r0 + wave + 4 * i, B - 1);
+    xs[i] = *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + kc);
+    ys[i] = *reinterpret_cast<const f32x4*>(hv + (size_t)row * ldhv + kc);
   }
+  f32x4 w[AMAX + 1];
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a)
+    w[a] = *reinterpret_cast<const f32x4*>(wp + (size_t)min(a, A - 1) * K + kc);
+  w[AMAX] = *reinterpret_cast<const f32x4*>(wv + kc);
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) w[a] = (a < A && kin) ? w[a] : z;
+  w[AMAX] = kin ? w[AMAX] : z;
   constexpr int LOGV = AMAX == 8 ? 3 : (AMAX == 16 ? 4 : 5);
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
     const int row = r0 + wave + 4 * i;
     if (row >= B) break;
-    const f32x4 x = xs[i], y = ys[i];
+    const f32x4 x = kin ? xs[i] : z, y = kin ? ys[i] : z;
     float* out = part + ((size_t)c * B + row) * (A + 1);
     float pv[AMAX];
 #pragma unroll
@@ -203,24 +220,28 @@ __global__ __launch_bounds__(256) void splitk_heads_partial_kernel(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int k = c * HEADS_KC + lane * 4;
   const bool kin = k < K;
+  const int kc = kin ? k : 0;
   const size_t plane = (size_t)B * K;
   constexpr int RPW = HEADS_ROWS / 4;
-  // slab loads first (S x RPW float4 in flight per lane), weights behind them
+  // all loads unconditional (clamped addresses) and issued before any masking, as in
+  // heads_partial_kernel: slabs (S x RPW float4 per lane), then weights and bias
   f32x4 sv[RPW][S];
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
-    const int row = r0 + wave + 4 * i;
-    const size_t off = (kin && row < B) ? (size_t)row * K + k : 0;
+    const size_t off = (size_t)min(r0 + wave + 4 * i, B - 1) * K + kc;
 #pragma unroll
     for (int q = 0; q < S; ++q) sv[i][q] = *reinterpret_cast<const f32x4*>(slab + q * plane + off);
   }
   f32x4 w[AMAX + 1];
 #pragma unroll
   for (int a = 0; a < AMAX; ++a)
-    w[a] = (a < A && kin) ? *reinterpret_cast<const f32x4*>(wp + (size_t)a * K + k)
-                          : f32x4{0.f, 0.f, 0.f, 0.f};
-  w[AMAX] = kin ? *reinterpret_cast<const f32x4*>(wv + k) : f32x4{0.f, 0.f, 0.f, 0.f};
-  const f32x4 bb = kin ? *reinterpret_cast<const f32x4*>(bias + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    w[a] = *reinterpret_cast<const f32x4*>(wp + (size_t)min(a, A - 1) * K + kc);
+  w[AMAX] = *reinterpret_cast<const f32x4*>(wv + kc);
+  const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + kc);
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) w[a] = (a < A && kin) ? w[a] : z;
+  w[AMAX] = kin ? w[AMAX] : z;
   constexpr int LOGV = AMAX == 8 ? 3 : (AMAX == 16 ? 4 : 5);
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
@@ -317,18 +338,25 @@ extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w
   AZ_REQUIRE(boards && conv1_w && conv1_b && conv2_w && conv2_b && feat, AZ_EINVAL,
              "az_c4_trunk_fwd: null pointer");
   hipStream_t s = as_stream(stream);
-  if (B >= 4096) {
-    hipLaunchKernelGGL(c4_trunk_kernel<8>, dim3((B + 7) / 8), dim3(512), 0, s, boards, B,
-                       conv1_w, conv1_b, conv2_w, conv2_b, feat);
-  } else if (B >= 2048) {
-    hipLaunchKernelGGL(c4_trunk_kernel<4>, dim3((B + 3) / 4), dim3(512), 0, s, boards, B,
-                       conv1_w, conv1_b, conv2_w, conv2_b, feat);
-  } else if (B >= 256) {
-    hipLaunchKernelGGL(c4_trunk_kernel<2>, dim3((B + 1) / 2), dim3(512), 0, s, boards, B,
-                       conv1_w, conv1_b, conv2_w, conv2_b, feat);
-  } else {
-    hipLaunchKernelGGL(c4_trunk_kernel<1>, dim3(B), dim3(512), 0, s, boards, B, conv1_w,
-                       conv1_b, conv2_w, conv2_b, feat);
+  static const char* env = getenv("AZ_TRUNK_NB");   // tuning experiments only
+  int nbk = B >= 4096 ? 8 : (B >= 2048 ? 4 : (B >= 256 ? 2 : 1));
+  if (env) nbk = atoi(env);
+  switch (nbk) {
+    case 8:
+      hipLaunchKernelGGL(c4_trunk_kernel<8>, dim3((B + 7) / 8), dim3(512), 0, s, boards, B,
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+      break;
+    case 4:
+      hipLaunchKernelGGL(c4_trunk_kernel<4>, dim3((B + 3) / 4), dim3(512), 0, s, boards, B,
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+      break;
+    case 2:
+      hipLaunchKernelGGL(c4_trunk_kernel<2>, dim3((B + 1) / 2), dim3(512), 0, s, boards, B,
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+      break;
+    default:
+      hipLaunchKernelGGL(c4_trunk_kernel<1>, dim3(B), dim3(512), 0, s, boards, B, conv1_w,
+                         conv1_b, conv2_w, conv2_b, feat);
   }
   return check_launch("c4_trunk_kernel");
 }

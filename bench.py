@@ -40,6 +40,8 @@ def parse():
                     help="bounded CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-aggregate", action="store_true")
+    ap.add_argument("--no-agg-extra", action="store_true",
+                    help="aggregate leg: only the warm 512-grid shard (profiling passes)")
     ap.add_argument("--no-selfplay", action="store_true")
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--sp-games", type=int, default=2048,
@@ -92,7 +94,7 @@ def _grid_graph(ops, device, graphs, h=32, w=32):
     return ops.DeviceGraph(rowptr, col, device)
 
 
-def aggregate_roofline(torch, ops, device, graphs=512, full_graphs=4096):
+def aggregate_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True):
     """Config 5 per-GPU shard (4096 grids / 8 GPUs = 512): 32x32 4-neighbour grids, F=64, CSR by
     destination.  Times the scatter-aggregate kernel alone (HIP events on the launch stream):
       warm -- back-to-back launches (x, 134 MB, stays resident in the 256 MB Infinity Cache);
@@ -120,17 +122,19 @@ def aggregate_roofline(torch, ops, device, graphs=512, full_graphs=4096):
         return nbytes / (ms * 1e-3) / 1e9, ms * 1e3, V, E
 
     gbs, us, V, E = run(graphs)
-    flush = torch.zeros((128 << 20,), dtype=torch.float32, device=device)
-    cold_gbs, cold_us, _, _ = run(graphs, flush)
-    del flush
     out = {"kernel": "aggregate_small_kernel<8,2,1,NT>", "bound": "hbm",
            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_us": round(us, 2),
            "workload": f"{graphs} 32x32 grids, V={V}, E={E}, F=64 (config-5 shard per GPU), "
-                       f"back-to-back launches",
-           "cold": {"achieved": round(cold_gbs, 1), "frac": round(cold_gbs / HBM_PEAK_GBS, 4),
-                    "avg_launch_us": round(cold_us, 2),
-                    "note": "Infinity Cache flushed before each launch"}}
+                       f"back-to-back launches"}
+    if not extra:
+        return out
+    flush = torch.zeros((128 << 20,), dtype=torch.float32, device=device)
+    cold_gbs, cold_us, _, _ = run(graphs, flush)
+    del flush
+    out["cold"] = {"achieved": round(cold_gbs, 1), "frac": round(cold_gbs / HBM_PEAK_GBS, 4),
+                   "avg_launch_us": round(cold_us, 2),
+                   "note": "Infinity Cache flushed (512 MB read) before each launch"}
     if full_graphs:
         fgbs, fus, fV, fE = run(full_graphs, reps=10)
         out["full_config"] = {"achieved": round(fgbs, 1), "frac": round(fgbs / HBM_PEAK_GBS, 4),
@@ -365,7 +369,7 @@ def main():
 
     agg = None
     if not args.no_aggregate:
-        agg = aggregate_roofline(torch, ops, device)
+        agg = aggregate_roofline(torch, ops, device, extra=not args.no_agg_extra)
 
     traffic = pmc_traffic("gemm")
     if agg is not None:
