@@ -169,18 +169,30 @@ class Coach:
                 self.nnet.save_checkpoint(folder=self.args.checkpoint, filename=temp)
             self._barrier()
             self.pnet.load_checkpoint(folder=self.args.checkpoint, filename=temp)
-            pmcts = MCTS(self.game, self.pnet, self.args)
+            native_arena = (_flag(self.args, "selfplay_engine", "native") == "native"
+                            and _native_ok(self.game))
+            if native_arena:
+                from mcts_native import ArenaPlayer
+                pplayer = ArenaPlayer(self.game, self.pnet, self.args)
+            else:
+                pmcts = MCTS(self.game, self.pnet, self.args)
+                pplayer = lambda x: np.argmax(pmcts.getActionProb(x, temp=0))  # noqa: E731
             if use_gnn and gnnExamples:
                 log.info(f"Training with {len(trainExamples)} standard examples and "
                          f"{len(gnnExamples)} GNN examples")
                 self.nnet.train(trainExamples, gnnExamples)
             else:
                 self.nnet.train(trainExamples)
-            nmcts = MCTS(self.game, self.nnet, self.args)
+            if native_arena:
+                nplayer = ArenaPlayer(self.game, self.nnet, self.args)
+            else:
+                nmcts = MCTS(self.game, self.nnet, self.args)
+                nplayer = lambda x: np.argmax(nmcts.getActionProb(x, temp=0))  # noqa: E731
 
             log.info("PITTING AGAINST PREVIOUS VERSION")
-            arena = Arena(lambda x: np.argmax(pmcts.getActionProb(x, temp=0)),
-                          lambda x: np.argmax(nmcts.getActionProb(x, temp=0)), self.game)
+            # Arena.py:249-291 with the reference's per-iteration MCTS objects (one tree per
+            # player for all games); the native players run the same searches in C++
+            arena = Arena(pplayer, nplayer, self.game)
             pwins, nwins, draws = arena.playGames(self.args.arenaCompare)
             log.info("NEW/PREV WINS : %d / %d ; DRAWS : %d" % (nwins, pwins, draws))
             if i == 1:

@@ -1,5 +1,6 @@
 """Tensor-level wrappers over the C-ABI.  Tensors are torch CUDA(HIP) tensors used purely as
 device memory; every FLOP runs in libaz_hip.so on the current torch stream."""
+import contextlib
 import ctypes
 
 import torch
@@ -27,15 +28,38 @@ def _need(t, dtype=torch.float32, name="tensor"):
 
 
 _WS = {}
+_WS_PINNED = {}
 
 
 def workspace(device, nbytes=96 << 20):
-    """Per-device split-K workspace (kept for the process lifetime; grows on demand)."""
+    """Per-device split-K workspace (kept for the process lifetime; grows on demand, which
+    frees the previous buffer -- so a captured hipGraph must not reference it: see
+    `pinned_workspace`)."""
     key = str(device)
+    t = _WS_PINNED.get(key)
+    if t is not None:
+        return t
     t = _WS.get(key)
     if t is None or t.numel() < nbytes:
         t = _WS[key] = torch.empty((nbytes,), dtype=torch.uint8, device=device)
     return t
+
+
+@contextlib.contextmanager
+def pinned_workspace(device, t):
+    """Every op on `device` uses the caller-owned workspace `t` inside the block (a graph
+    capture keeps `t` alive with the graph, so its kernels never point at a buffer the growing
+    shared workspace has freed).  The entry points check that it is large enough."""
+    key = str(device)
+    prev = _WS_PINNED.get(key)
+    _WS_PINNED[key] = t
+    try:
+        yield t
+    finally:
+        if prev is None:
+            _WS_PINNED.pop(key, None)
+        else:
+            _WS_PINNED[key] = prev
 
 
 def gemm(desc, device=None):

@@ -56,6 +56,65 @@ class _PinnedRing:
         self.i += 1
 
 
+class _Batch1Graph:
+    """The whole batch-1 evaluation captured as ONE hipGraph: pinned host board -> H2D ->
+    trunk -> heads [-> GNN tail] -> packed outputs -> D2H into pinned host memory.  MCTS asks
+    for one leaf at a time wherever simulations depend on each other (the reference's
+    MCTS.search, the arena's per-iteration trees), so this path is launch- and copy-latency
+    bound; one replay replaces ~8 launches and two synchronous copies.  The kernels are the
+    eager path's, so the outputs are bit-identical.  Parameters are updated in place (train,
+    load_state_dict, restore), so the captured pointers stay valid.
+
+    kind: "std" -> [pi, v], "gnn" -> [gnn_pi, gnn_v], "both" -> [pi, v, gnn_pi, gnn_v]."""
+
+    def __init__(self, w, kind):
+        dev = w.device
+        A = w.action_size
+        width = {"std": A + 1, "gnn": A + 1, "both": 2 * A + 2}[kind]
+        self.h_in = torch.zeros((1, w.board_x, w.board_y), dtype=torch.int8, pin_memory=True)
+        self.d_in = torch.zeros((1, w.board_x, w.board_y), dtype=torch.int8, device=dev)
+        self.h_out = torch.zeros((1, width), dtype=torch.float32, pin_memory=True)
+        self.d_out = torch.zeros((1, width), dtype=torch.float32, device=dev)
+
+        def body():
+            self.d_in.copy_(self.h_in, non_blocking=True)
+            f = w.nnet.features(self.d_in)
+            parts = []
+            if kind in ("std", "both"):
+                _, pi, v = w.nnet.heads(f)
+                parts += [pi, v[:, None]]
+            if kind in ("gnn", "both"):
+                _, gpi, gv = nets.gnn_per_row_heads(w.nnet, w.gnn, f)
+                parts += [gpi, gv[:, None]]
+            torch.cat(parts, dim=1, out=self.d_out)
+            self.h_out.copy_(self.d_out, non_blocking=True)
+
+        # the graph owns its workspace: the shared one is re-allocated when a large batch needs
+        # more, which would leave a captured kernel pointing at freed memory
+        self.ws = torch.empty((16 << 20,), dtype=torch.uint8, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with ops.pinned_workspace(dev, self.ws):
+            with torch.cuda.stream(side):
+                body()                   # eager warm-up on the same buffers
+            torch.cuda.current_stream(dev).wait_stream(side)
+            torch.cuda.synchronize(dev)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                body()
+        self.dev = dev
+
+    def run(self, board):
+        self.h_in.numpy()[0] = board
+        self.graph.replay()
+        torch.cuda.current_stream(self.dev).synchronize()
+        return self.h_out.numpy()[0].copy()
+
+
+def _graphs_enabled():
+    return os.environ.get("AZ_NO_GRAPH", "0") in ("", "0")
+
+
 class NetWrapper:
     """Common body; subclasses choose the board network class and whether a GNN exists."""
 
@@ -76,6 +135,20 @@ class NetWrapper:
         self.train_seed = 0
 
     # -- evaluation ------------------------------------------------------------------------
+    def _graph1(self, kind):
+        """The batch-1 graph of `kind`, captured on first use (None when disabled)."""
+        if not _graphs_enabled():
+            return None
+        g = getattr(self, "_g1", None)
+        if g is None:
+            g = self._g1 = {}
+        if kind not in g:
+            self.nnet.eval()
+            if self.has_gnn:
+                self.gnn.eval()
+            g[kind] = _Batch1Graph(self, kind)
+        return g[kind]
+
     def _eval(self, boards, gnn):
         b = boards_to_device(boards, self.device)
         if b.dim() == 2:
@@ -92,6 +165,10 @@ class NetWrapper:
         (Connect4GNN.py:59-84; `neighbor_states` is accepted and unused as in
         Connect4Net.py:110)."""
         self.nnet.eval()
+        g = self._graph1("std")
+        if g is not None:
+            out = g.run(board)
+            return out[:-1], out[-1]
         pi, v = self._eval(board, False)
         out = torch.cat([pi[0], v]).cpu().numpy()
         return out[:-1], out[-1]
@@ -99,6 +176,9 @@ class NetWrapper:
     def predict_batch(self, boards):
         """Row-wise predict for [B,n,n] boards -> (pi float32[B,A], v float32[B])."""
         self.nnet.eval()
+        if len(boards) == 1 and (g := self._graph1("std")) is not None:
+            out = g.run(boards[0])
+            return out[None, :-1], out[-1:]
         pi, v = self._eval(boards, False)
         return pi.cpu().numpy(), v.cpu().numpy()
 
@@ -253,6 +333,10 @@ class GNNWrapperMixin:
         identity (gnn_utils.py:35-36) and only output_transform runs before the heads."""
         self.nnet.eval()
         self.gnn.eval()
+        g = self._graph1("gnn")
+        if g is not None:
+            out = g.run(board)
+            return out[:-1], out[-1]
         pi, v = self._eval(board, True)
         out = torch.cat([pi[0], v]).cpu().numpy()
         return out[:-1], out[-1]
@@ -268,12 +352,15 @@ class GNNWrapperMixin:
         for every new leaf, MCTS.py:169-174) -> (pi, v, gnn_pi, gnn_v), one host copy."""
         self.nnet.eval()
         self.gnn.eval()
+        A = self.action_size
+        if len(boards) == 1 and (g := self._graph1("both")) is not None:
+            out = g.run(boards[0])[None]
+            return out[:, :A], out[:, A], out[:, A + 1:2 * A + 1], out[:, 2 * A + 1]
         b = boards_to_device(boards, self.device)
         f = self.nnet.features(b)
         _, pi, v = self.nnet.heads(f)
         _, gpi, gv = nets.gnn_per_row_heads(self.nnet, self.gnn, f)
         out = torch.cat([pi, v[:, None], gpi, gv[:, None]], dim=1).cpu().numpy()
-        A = self.action_size
         return out[:, :A], out[:, A], out[:, A + 1:2 * A + 1], out[:, 2 * A + 1]
 
     def predict_both_async(self, boards):

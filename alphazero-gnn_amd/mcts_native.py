@@ -354,3 +354,52 @@ class NativeMCTS:
         res = expand_result(A, initial_counts, initial_value, nsa, q, tag, self.game,
                             canonicalBoard)
         return {s: res}
+
+
+class ArenaPlayer:
+    """An Arena action function, the reference's `lambda x: np.argmax(mcts.getActionProb(x,
+    temp=0))` (Coach.py:140-142), with the searches in a one-slot native engine.  The tree
+    persists across moves and games exactly like the reference's MCTS object, which is created
+    once per iteration and reused for the whole arena -- so arena games depend on each other
+    and are played one after the other; what moves native is the per-simulation search and
+    rules work (MCTS.py:151-240).  Leaves go to the network one at a time (`predict_both` on
+    one board when use_gnn, else `predict_batch`), as the reference's batch-1 calls."""
+
+    def __init__(self, game, nnet, args):
+        get = (lambda k, d=None: args.get(k, d)) if isinstance(args, dict) else \
+            (lambda k, d=None: getattr(args, k, d))
+        self.use_gnn = bool(get("use_gnn", False))
+        self.nnet, self.args = nnet, args
+        self.eng = Engine(game, 1, float(get("cpuct", 1.0)), self.use_gnn)
+        self.mcts = NativeMCTS(self.eng, 0, game, args)
+
+    def _search(self, board, sims):
+        from selfplay import _net_call
+        self.eng.begin(0, board, sims)
+        idle = 0
+        while self.eng.remaining(0) > 0:
+            k = self.eng.collect(1)
+            if k == 0:
+                idle += 1
+                if idle > 4:
+                    raise RuntimeError("native arena search made no progress")
+                continue
+            idle = 0
+            try:
+                pi, v, gpi, gv = _net_call(self.nnet, self.eng.leaf_boards[:k], self.use_gnn)
+            except Exception as ex:  # MCTS.py:195-200: uniform priors, value 0
+                import logging
+                logging.getLogger(__name__).error(f"Error in neural network prediction: {ex}")
+                self.eng.feed(k, failed=True)
+                continue
+            self.eng.feed(k, pi, v, gpi, gv)
+
+    def __call__(self, canonical):
+        gen = self.mcts.getActionProb_g(canonical, temp=0)
+        try:
+            req = next(gen)
+            while True:
+                self._search(req[1], req[2])
+                req = gen.send(None)
+        except StopIteration as stop:
+            return int(np.argmax(stop.value))

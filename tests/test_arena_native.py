@@ -1,0 +1,82 @@
+"""The arena (Coach.py:137-145 -> Arena.py:249-291) with native-engine players must play the
+same games as the reference-shaped Python MCTS players: same moves, same W/L/D, given the same
+network and np.random state.  The network here is a deterministic hash of the board (any
+function of the board works: both paths see identical float32 outputs)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from test_mcts_golden import Args
+
+
+class HashNet:
+    def __init__(self, A, salt):
+        self.A, self.salt = A, salt
+
+    def _out(self, board, kind):
+        b = np.ascontiguousarray(board, np.int8).tobytes()
+        h = hashlib.blake2b(b + bytes([self.salt, kind]), digest_size=8).digest()
+        r = np.random.default_rng(int.from_bytes(h, "little"))
+        p = (r.random(self.A) + 0.05).astype(np.float32)
+        return (p / p.sum()).astype(np.float32), np.float32(r.random() * 2 - 1)
+
+    def predict(self, board):
+        return self._out(board, 0)
+
+    def predict_with_gnn(self, board):
+        return self._out(board, 1)
+
+    def predict_batch(self, boards):
+        rows = [self.predict(b) for b in boards]
+        return np.stack([p for p, _ in rows]), np.array([v for _, v in rows], np.float32)
+
+    def predict_both(self, boards):
+        pi, v = self.predict_batch(boards)
+        rows = [self.predict_with_gnn(b) for b in boards]
+        return pi, v, np.stack([p for p, _ in rows]), np.array([x for _, x in rows], np.float32)
+
+
+def _games():
+    from connect4.Connect4Game import Connect4Game
+    from tictactoe.TicTacToeGame import TicTacToeGame
+    return {"ttt3": (lambda: TicTacToeGame(3), 10, 8), "c4": (lambda: Connect4Game(7), 6, 4)}
+
+
+class Recorder:
+    def __init__(self, fn):
+        self.fn, self.moves = fn, []
+
+    def __call__(self, x):
+        a = int(self.fn(x))
+        self.moves.append((np.asarray(x).tobytes(), a))
+        return a
+
+
+@pytest.mark.parametrize("name", ["ttt3", "c4"])
+@pytest.mark.parametrize("use_gnn", [False, True])
+def test_native_arena_equals_python_arena(name, use_gnn):
+    from Arena import Arena
+    from MCTS import MCTS
+    from mcts_native import ArenaPlayer
+    make, sims, games = _games()[name]
+    game = make()
+    A = game.getActionSize()
+    args = Args(numMCTSSims=sims, cpuct=1.0, use_gnn=use_gnn)
+    pnet, nnet = HashNet(A, 1), HashNet(A, 2)
+
+    results = []
+    for native in (False, True):
+        np.random.seed(123)
+        if native:
+            p1, p2 = ArenaPlayer(game, pnet, args), ArenaPlayer(game, nnet, args)
+        else:
+            pm, nm = MCTS(game, pnet, args), MCTS(game, nnet, args)
+            p1 = lambda x: np.argmax(pm.getActionProb(x, temp=0))  # noqa: E731
+            p2 = lambda x: np.argmax(nm.getActionProb(x, temp=0))  # noqa: E731
+        r1, r2 = Recorder(p1), Recorder(p2)
+        wld = Arena(r1, r2, game).playGames(games)
+        results.append((wld, r1.moves, r2.moves))
+    assert results[0][0] == results[1][0]
+    assert results[0][1] == results[1][1] and results[0][2] == results[1][2]
+    assert len(results[0][1]) > games          # several moves per game were really searched

@@ -244,3 +244,40 @@ def test_coach_learn_with_native_lockstep_selfplay(tmp_path):
     std, gnn = coach.trainExamplesHistory[0]
     assert len(std) > 8 * 5 * 8 // 2 and len(gnn) > 8 * 2
     assert "best_gnn.pth.tar" in os.listdir(folder)
+
+
+def test_batch1_graph_equals_eager(c4_wrapper, monkeypatch):
+    """The batch-1 hipGraph path (predict / predict_with_gnn / predict_both on one board) returns
+    the eager path's bits, also after the parameters change in place."""
+    z = golden("c4_gnn.npz")
+    boards = [z["boards"][i].astype(np.int64) for i in range(0, 64, 9)]
+
+    def run():
+        out = []
+        for b in boards:
+            out += list(c4_wrapper.predict(b)) + list(c4_wrapper.predict_with_gnn(b))
+            out += [x[0] for x in c4_wrapper.predict_both(b[None])]
+        return [np.asarray(x) for x in out]
+
+    from azhip import ops
+    monkeypatch.setenv("AZ_NO_GRAPH", "0")
+    g0 = run()
+    # the shared workspace grows (a large self-play batch); captured graphs must not care
+    ops.workspace(c4_wrapper.device, ops.workspace(c4_wrapper.device).numel() + (64 << 20))
+    torch.cuda.synchronize()
+    g1 = run()
+    assert all(np.array_equal(a, b) for a, b in zip(g0, g1))
+    monkeypatch.setenv("AZ_NO_GRAPH", "1")
+    e1 = run()
+    assert all(np.array_equal(a, b) for a, b in zip(g1, e1))
+    # in-place parameter update (what train / load_checkpoint do): the graph sees it
+    snap = c4_wrapper.snapshot()
+    c4_wrapper.nnet.params.flat.mul_(0.5)
+    c4_wrapper.gnn.params.flat.mul_(0.9)
+    monkeypatch.setenv("AZ_NO_GRAPH", "0")
+    g2 = run()
+    monkeypatch.setenv("AZ_NO_GRAPH", "1")
+    e2 = run()
+    c4_wrapper.restore(snap)
+    assert all(np.array_equal(a, b) for a, b in zip(g2, e2))
+    assert not all(np.array_equal(a, b) for a, b in zip(g1, g2))

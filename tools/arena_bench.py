@@ -1,0 +1,40 @@
+"""Arena gating speed (Coach.py:137-145): Connect4 7x7 GNN players, numMCTSSims 100, on the GPU;
+the reference-shaped Python MCTS players vs the native-engine players (same games)."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "alphazero-gnn_amd"))
+from types import SimpleNamespace  # noqa: E402
+
+from Arena import Arena  # noqa: E402
+from MCTS import MCTS  # noqa: E402
+from connect4.Connect4GNN import Connect4GNNWrapper  # noqa: E402
+from connect4.Connect4Game import Connect4Game  # noqa: E402
+from mcts_native import ArenaPlayer  # noqa: E402
+
+games = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+args = SimpleNamespace(numMCTSSims=100, cpuct=1.0, use_gnn=True, dropout=0.3, gnn_layers=2)
+game = Connect4Game(7)
+torch.manual_seed(0)
+pnet, nnet = Connect4GNNWrapper(game, args), Connect4GNNWrapper(game, args)
+out = {}
+for native in (True, False):
+    np.random.seed(7)
+    if native:
+        p1, p2 = ArenaPlayer(game, pnet, args), ArenaPlayer(game, nnet, args)
+    else:
+        pm, nm = MCTS(game, pnet, args), MCTS(game, nnet, args)
+        p1 = lambda x: np.argmax(pm.getActionProb(x, temp=0))  # noqa: E731
+        p2 = lambda x: np.argmax(nm.getActionProb(x, temp=0))  # noqa: E731
+    t0 = time.perf_counter()
+    wld = Arena(p1, p2, game).playGames(games)
+    dt = time.perf_counter() - t0
+    out["native" if native else "python"] = {"wld": wld, "seconds": round(dt, 2),
+                                             "games_per_s": round(games / dt, 3)}
+    print(json.dumps(out), flush=True)
