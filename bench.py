@@ -302,10 +302,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # AZ_BENCH_BACKEND=gloo rehearses the N-rank path on a box with fewer GPUs (ranks share
+    # devices round-robin); the driver's multi-GPU runs use nccl = RCCL, one GPU per rank
+    backend = os.environ.get("AZ_BENCH_BACKEND", "nccl")
     if world > 1:
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
+    red_dev = device if backend == "nccl" else torch.device("cpu")
     from azhip import ops
     from azhip.nets import C4Evaluator
     from azhip.weights import connect4_net_spec, gnn_spec, synthetic_state_dict
@@ -359,7 +367,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=red_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     gemm_ms = [e[0].elapsed_time(e[1]) for e in evs]       # output_transform.0: one az_gemm_f32
@@ -381,7 +389,7 @@ def main():
             dist.barrier()
         dt, sp = selfplay_leg(W, G, args, device, rank)
         if world > 1:
-            t = torch.tensor([dt], device=device, dtype=torch.float64)
+            t = torch.tensor([dt], device=red_dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         sp.update({"games_per_s": round(world * sp["games"] / dt, 3),
