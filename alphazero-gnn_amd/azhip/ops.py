@@ -71,7 +71,7 @@ def gemm(desc, device=None):
 
 
 def linear(x, w, b=None, act=ACT_NONE, out=None, x2=None, a_rows=None, R=None, G=None,
-           c_rows=None, beta=0.0, M=None):
+           c_rows=None, beta=0.0, M=None, C2=None):
     """out = act(cat(x, x2) @ w.T + b) (optionally gated residual R + G*(...)), nn.Linear layout.
     x: [M, K1] (row stride taken from the tensor), x2: [M, K2] or None, w: [N, K1+K2]."""
     _need(x, name="x")
@@ -101,6 +101,8 @@ def linear(x, w, b=None, act=ACT_NONE, out=None, x2=None, a_rows=None, R=None, G
     d.beta = beta
     d.C, d.ldc = out.data_ptr(), out.stride(0)
     d.c_rows = c_rows.data_ptr() if c_rows is not None else None
+    if C2 is not None:
+        d.C2, d.ldc2 = C2.data_ptr(), C2.stride(0)
     gemm(d, x.device)
     return out
 

@@ -77,6 +77,36 @@ def test_linear_split_gather_gated(ops):
         assert np.all(o.cpu().numpy()[untouched] == 0)
 
 
+@pytest.mark.parametrize("M,N,K,split,act", [(20007, 256, 64, False, 0), (16384, 64, 64, False, 1),
+                                             (33000, 64, 128, True, 2), (16385, 64, 64, False, 0)])
+def test_linear_tall_skinny(ops, M, N, K, split, act):
+    """gemm_f32_tall (M >= 16384, K <= 128: the grid GNN layers) incl. the [x; agg] concat,
+    the gathered-row and gated-residual epilogue, and a ragged last 32-row tile."""
+    g = torch.Generator().manual_seed(M + N + K)
+    K1 = K // 2 if split else K
+    x = torch.rand((M, K1), generator=g) * 2 - 1
+    x2 = torch.rand((M, K - K1), generator=g) * 2 - 1 if split else None
+    w = (torch.rand((N, K), generator=g) * 2 - 1) / K ** 0.5
+    b = torch.rand((N,), generator=g) - 0.5
+    a = torch.cat([x, x2], 1) if split else x
+    ref = a.double() @ w.double().T + b.double()
+    ref = [lambda t: t, torch.relu, torch.sigmoid][act](ref)
+    bound = (a.double().abs() @ w.double().abs().T + b.double().abs()).numpy()
+    y = ops.linear(x.cuda(), w.cuda(), b.cuda(), act=act,
+                   x2=x2.cuda() if split else None).cpu()
+    check_dot_error(y.numpy(), ref.numpy(), bound)
+    if N == 64 and not split:
+        # gated residual with the pre-gate copy (C2), as the GNN layer's last GEMM uses it
+        R = torch.rand((M, N), generator=g)
+        G = torch.rand((M, N), generator=g)
+        pre = torch.empty((M, N)).cuda()
+        o = ops.linear(x.cuda(), w.cuda(), b.cuda(), R=R.cuda(), G=G.cuda(), C2=pre)
+        lin = x.double() @ w.double().T + b.double()
+        check_dot_error(pre.cpu().numpy(), lin.numpy(), bound)
+        np.testing.assert_allclose(o.cpu().numpy(), (R.double() + G.double() * lin).numpy(),
+                                   atol=1e-5)
+
+
 @pytest.mark.parametrize("M,N,K", [(64, 3136, 64), (128, 256, 4096), (36, 20, 64)])
 def test_matmul_tn_nn(ops, M, N, K):
     g = torch.Generator().manual_seed(11)

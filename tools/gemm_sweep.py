@@ -76,6 +76,13 @@ if __name__ == "__main__":
                     print(json.dumps({"M": M, "cfg": cfg, "splits": sp or "auto", **res}),
                           flush=True)
         sys.exit(0)
+    if mode == "tall":         # config-5 GNN layer shapes: M = V of 512 grids, K <= 128
+        for (M, N, K) in [(524288, 256, 64), (524288, 64, 64), (524288, 64, 128)]:
+            for cfg in sys.argv[2].split(","):
+                env = {"AZ_GEMM_CFG": cfg} if cfg != "auto" else {}
+                res = run(env, M, N, K)
+                print(json.dumps({"M": M, "N": N, "K": K, "cfg": cfg, **res}), flush=True)
+        sys.exit(0)
     if mode == "longk":        # steady state: K 10x longer, fixed splits (per-block overhead amortised)
         for cfg in sys.argv[2].split(","):
             for abl in sys.argv[3].split(","):
