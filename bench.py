@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--no-agg-extra", action="store_true",
                     help="aggregate leg: only the warm 512-grid shard (profiling passes)")
     ap.add_argument("--no-selfplay", action="store_true")
+    ap.add_argument("--no-grid", action="store_true", help="skip the config-5 forward leg")
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--sp-games", type=int, default=2048,
                     help="self-play leg: games per GPU, all played in lock step")
@@ -78,7 +79,7 @@ def cpu_baseline(W, G, seconds, B):
                       f"output_transform -> heads, BLAS threads={threads}), {dt:.1f} s"}
 
 
-def _grid_graph(ops, device, graphs, h=32, w=32):
+def _grid_graph(ops, device, graphs, h=32, w=32, build=True):
     rp, cl = [0], []
     for r in range(h):
         for c in range(w):
@@ -91,6 +92,8 @@ def _grid_graph(ops, device, graphs, h=32, w=32):
     g = np.arange(graphs, dtype=np.int64)
     rowptr = np.concatenate([(rp[:-1][None, :] + (g * E1)[:, None]).ravel(), [graphs * E1]])
     col = (cl[None, :] + (g * V1)[:, None]).ravel()
+    if not build:
+        return rowptr, col
     return ops.DeviceGraph(rowptr, col, device)
 
 
@@ -141,6 +144,66 @@ def aggregate_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=T
                               "avg_launch_us": round(fus, 2),
                               "workload": f"{full_graphs} grids, V={fV}, E={fE} (all of config 5 "
                                           f"on one GPU)"}
+    return out
+
+
+def grid_forward_leg(torch, ops, device, graphs=512, cpu_seconds=0.0):
+    """Config 5 end to end: PolicyValueGNN(64, 2 layers) forward over `graphs`
+    32x32 grids (the per-destination generalisation of gnn_utils.py:34-117: factored attention
+    GEMM, per-edge scores, CSR aggregate, gate/update GEMMs with the gated residual, then
+    output_transform), random-init weights of the reference's shapes.  node-updates/s =
+    V x layers / forward time (HIP events on the launch stream).  The first grid's output is
+    checked against the oracle (grids are independent) before timing."""
+    from azhip.nets import PolicyValueGNN
+    from azhip.weights import gnn_spec, synthetic_state_dict
+    from oracle import nets as O
+    Gw = synthetic_state_dict(gnn_spec(64, 2), 3)
+    g = _grid_graph(ops, device, graphs)
+    net = PolicyValueGNN(64, 2, device=device, init=Gw).eval()
+    x = torch.rand((g.V, 64), device=device,
+                   generator=torch.Generator(device=device).manual_seed(0)) * 2 - 1
+    y = net.forward_graph(x, g)
+    one = _grid_graph(ops, "cpu", 1, build=False)
+    ref = O.policy_value_gnn_csr(x[:1024].cpu().double().numpy(), one[0], one[1], Gw)
+    err = float(np.abs(y[:1024].cpu().double().numpy() - ref).max())
+    assert err < 1e-4, err
+    for _ in range(2):
+        net.forward_graph(x, g)
+    reps = 10
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        net.forward_graph(x, g)
+    ev[1].record()
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    # SURVEY §8d: 73,728 FLOP/node/layer + 640 FLOP/edge/layer + 16,384 FLOP/node output
+    flop = 2 * (73728 * g.V + 640 * g.E) + 16384 * g.V
+    out = {"workload": f"{graphs} 32x32 grids, V={g.V}, E={g.E}, F=64, 2 layers "
+                       f"(config-5 shard per GPU)",
+           "ms_per_forward": round(ms, 3), "node_updates_per_s": round(2 * g.V / (ms * 1e-3), 1),
+           "unit": "node-updates/s", "gflop_per_forward": round(flop / 1e9, 2),
+           "tflops": round(flop / (ms * 1e-3) / 1e12, 2), "max_abs_err_vs_oracle_grid0": err}
+    if cpu_seconds > 0:
+        n_g = 8
+        xs = x[:1024 * n_g].cpu().numpy()
+        cg = _grid_graph(ops, "cpu", n_g, build=False)
+        G32 = {k: np.asarray(v, np.float32) for k, v in Gw.items()}
+        O.policy_value_gnn_csr(xs, cg[0], cg[1], G32, dtype=np.float32)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < cpu_seconds:
+            O.policy_value_gnn_csr(xs, cg[0], cg[1], G32, dtype=np.float32)
+            n += 1
+        dt = time.perf_counter() - t0
+        try:
+            from threadpoolctl import threadpool_info
+            threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+        except Exception:  # pragma: no cover
+            threads = os.cpu_count()
+        out["cpu_baseline"] = {"value": round(n * 2 * 1024 * n_g / dt, 1),
+                               "unit": "node-updates/s", "cores": int(threads), "kind": "port",
+                               "sample": f"{n} forwards of {n_g} grids (numpy fp32 oracle, "
+                                         f"vectorised CSR restatement), {dt:.1f} s"}
     return out
 
 
@@ -379,6 +442,17 @@ def main():
     if not args.no_aggregate:
         agg = aggregate_roofline(torch, ops, device, extra=not args.no_agg_extra)
 
+    grid = None
+    if not args.no_grid:
+        grid = grid_forward_leg(torch, ops, device,
+                                cpu_seconds=(5.0 if (rank == 0 and world == 1 and not args.no_cpu)
+                                             else 0.0))
+        if world > 1:
+            t = torch.tensor([grid["ms_per_forward"]], device=red_dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            grid["node_updates_per_s"] = round(world * 2 * 524288 / (float(t.item()) * 1e-3), 1)
+            grid["n_gpus"] = world
+
     traffic = pmc_traffic("gemm")
     if agg is not None:
         agg["traffic"] = pmc_traffic("aggregate")
@@ -441,6 +515,7 @@ def main():
                          "avg_launch_us": round(avg_gemm_s * 1e6, 2),
                          "flop_per_launch": flop},
             "aggregate_roofline": agg,
+            "grid_forward": grid,
             "selfplay": sp,
             "train": tr,
             "cpu_baseline": cpu,
