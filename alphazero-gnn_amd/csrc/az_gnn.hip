@@ -272,6 +272,91 @@ __global__ __launch_bounds__(256) void aggregate_small_kernel(
   }
 }
 
+// Attention scores AND the aggregation of one destination in one pass, for the grid (in-degree
+// <= 4, F = 64, H = 128): 16 lanes per destination.  The destination's P row (its target
+// halves) is read once for all its edges instead of once per edge, the scores never round-trip
+// through HBM before the aggregation reads them, and one launch replaces two.  Every
+// arithmetic step is attn_score_kernel's (lane l owns hidden pairs m = l, l+16, l+32, l+48,
+// the same fmaf order and 16-lane xor reduction) and aggregate_small_kernel's (sum of alpha and
+// the weighted sum in edge order), so alpha and agg are bit-identical to the two-kernel path.
+__global__ __launch_bounds__(256) void attn_aggregate_small_kernel(
+    int D, int identity, const int* __restrict__ dst_rows, const int* __restrict__ rowptr,
+    const int* __restrict__ col, const float* __restrict__ P, int ldp,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    const float* __restrict__ x, int ldx, float* __restrict__ alpha, float* __restrict__ agg,
+    int ldagg) {
+  constexpr int H = 128, F = 64;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int i = (blk * 256 + threadIdx.x) >> 4;
+  const int l = threadIdx.x & 15;
+  if (i >= D) return;  // whole 16-lane groups exit together
+  const int d = identity ? i : dst_rows[i];
+  const int e0 = rowptr[d];
+  const int deg = rowptr[d + 1] - e0;
+  int sc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sc[j] = j < deg ? col[e0 + j] : d;
+  // every load issued before any math: target chunks, neighbour chunks, neighbour x rows
+  f32x4 t[4], u[4][4], xv[4];
+  const float* pd = P + (size_t)d * ldp;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = *reinterpret_cast<const f32x4*>(pd + 4 * (l + 16 * k));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float* ps = P + (size_t)sc[j] * ldp;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[j][k] = *reinterpret_cast<const f32x4*>(ps + 4 * (l + 16 * k));
+    xv[j] = *reinterpret_cast<const f32x4*>(x + (size_t)sc[j] * ldx + 4 * l);
+  }
+  float bb[8], ww[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int m = l + 16 * k;
+    bb[2 * k] = b1[2 * m];
+    bb[2 * k + 1] = b1[2 * m + 1];
+    ww[2 * k] = w2[2 * m];
+    ww[2 * k + 1] = w2[2 * m + 1];
+  }
+  const float bias2 = b2[0];
+  float a[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float h0 = t[k][0] + u[j][k][1] + bb[2 * k];
+      float h1 = t[k][2] + u[j][k][3] + bb[2 * k + 1];
+      h0 = h0 > 0.f ? h0 : 0.f;
+      h1 = h1 > 0.f ? h1 : 0.f;
+      acc = fmaf(h0, ww[2 * k], acc);
+      acc = fmaf(h1, ww[2 * k + 1], acc);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
+    a[j] = sigmoidf_ref(acc + bias2);
+  }
+  if (l < deg) {   // lane j writes edge j's score (deg <= 4 < 16)
+    const float aj = l == 0 ? a[0] : (l == 1 ? a[1] : (l == 2 ? a[2] : a[3]));
+    alpha[e0 + l] = aj;
+  }
+  float S = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < deg) S += a[j];
+  const bool norm = S > 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < deg) {
+      const float w = norm ? a[j] / S : a[j];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = fmaf(w, xv[j][c], acc[c]);
+    }
+  (void)H;
+  (void)F;
+  __builtin_nontemporal_store(acc, reinterpret_cast<f32x4*>(agg + (size_t)d * ldagg + 4 * l));
+}
+
 template <int LPR, int NV>
 static void launch_aggregate(const az_graph* g, int identity, const float* x, int ldx, int F,
                              const float* alpha, float* agg, int ldagg, hipStream_t s) {
@@ -421,9 +506,20 @@ extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
   d.C = L.P; d.ldc = 2 * H;
   d.ws = L.split; d.ws_bytes = kSplitWsBytes;
   if ((rc = gemm_f32(&d, s))) return rc;
-  // 2. per-edge attention weights, 3. normalised aggregation
-  if ((rc = attn_score(g, L.P, 2 * H, H, w->att_b1, w->att_w2, w->att_b2, L.alpha, s))) return rc;
-  if ((rc = aggregate(g, x, F, F, L.alpha, L.agg, F, s))) return rc;
+  // 2. per-edge attention weights, 3. normalised aggregation (one fused pass on the grid)
+  static const bool no_fuse = getenv("AZ_GNN_NOFUSE") != nullptr;   // A/B experiments
+  if (!no_fuse && g->max_deg > 0 && g->max_deg <= 4 && F == 64 && H == 128) {
+    const int identity = (g->D == g->V) ? 1 : 0;
+    const int blocks = (int)(((long)g->D * 16 + 255) / 256);
+    hipLaunchKernelGGL(attn_aggregate_small_kernel, dim3(blocks), dim3(256), 0, s, g->D, identity,
+                       g->dst_rows, g->rowptr, g->col, L.P, 2 * H, w->att_b1, w->att_w2,
+                       w->att_b2, x, F, L.alpha, L.agg, F);
+    if ((rc = check_launch("attn_aggregate_small_kernel"))) return rc;
+  } else {
+    if ((rc = attn_score(g, L.P, 2 * H, H, w->att_b1, w->att_w2, w->att_b2, L.alpha, s)))
+      return rc;
+    if ((rc = aggregate(g, x, F, F, L.alpha, L.agg, F, s))) return rc;
+  }
   // 4. gate = sigmoid(Wg [x_d; agg_d] + bg), u1 = relu(Wu1 [x_d; agg_d] + bu1)
   az_gemm_desc c = {};
   c.M = g->D; c.N = F; c.K = 2 * F;

@@ -5,6 +5,9 @@ import pytest
 
 from conftest import golden, split_weights
 
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
@@ -216,6 +219,36 @@ def test_grid_attention_and_aggregate_vs_oracle(ops):
     ref_agg = np.zeros((1024, 64))
     np.add.at(ref_agg, dst, x0[z["col"]] * (ref_a / s[dst])[:, None])
     np.testing.assert_allclose(agg, ref_agg, atol=2e-6)
+
+
+def test_fused_grid_attention_aggregate_bit_identical(ops):
+    """az_gnn_layer_fwd on a grid runs attention + aggregation as ONE kernel
+    (attn_aggregate_small_kernel); the alpha and agg it leaves in the layer workspace equal the
+    separate az_gnn_attn_score_fwd + az_gnn_aggregate_fwd bit for bit (8 grids, ragged CSR
+    degrees 2..4)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    z, G, _ = _synth()
+    g = bench._grid_graph(ops, "cuda", 8)
+    gen = torch.Generator().manual_seed(11)
+    x = (torch.rand((g.V, 64), generator=gen) * 2 - 1).cuda()
+    Gd = {k: cu(v) for k, v in G.items()}
+    Wl = {k[len("layers.0."):]: v for k, v in Gd.items() if k.startswith("layers.0.")}
+    out, ws = ops.gnn_layer(g, x, Wl)
+    V, E, H = g.V, g.E, 128
+    a256 = lambda b: (b + 255) // 256 * 256                                  # noqa: E731
+    P = ws[:V * 2 * H * 4].view(torch.float32).view(V, 2 * H)
+    o_alpha = a256(V * 2 * H * 4)
+    alpha_f = ws[o_alpha:o_alpha + E * 4].view(torch.float32)
+    o_agg = o_alpha + a256(E * 4)
+    agg_f = ws[o_agg:o_agg + V * 64 * 4].view(torch.float32).view(V, 64)
+    alpha = ops.attn_score(g, P, H, Wl["attention.0.bias"], Wl["attention.2.weight"],
+                           Wl["attention.2.bias"])
+    agg = ops.aggregate(g, x, alpha)
+    torch.cuda.synchronize()
+    assert torch.equal(alpha, alpha_f)
+    assert torch.equal(agg, agg_f)
 
 
 def test_grid_layers_vs_golden(ops):
