@@ -37,6 +37,8 @@ struct GemmArgs {
   // the epilogue.
   int splits, kc;
   float* slab;
+  int vec_epi;  // host-checked: N, every leading dimension % 4 == 0 and 16-B aligned C/C2/R/G,
+                // so whole float4 rows can leave through epilogue_store4
   int ablate;   // timing experiments only (AZ_GEMM_ABLATE, glds2): 1 = no DMA after the first
                 // tile, 2 = no barrier in the k loop; results are then wrong
 };
@@ -54,6 +56,41 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int c
   if (p.R) v = p.R[(size_t)cr * p.ldr + col] + (p.G ? p.G[(size_t)row * p.ldg + col] : 1.f) * v;
   float* dst = p.C + (size_t)cr * p.ldc + col;
   if (p.beta != 0.f) v += p.beta * *dst;
+  *dst = v;
+}
+
+// epilogue_store for 4 consecutive columns (col % 4 == 0, col + 4 <= N, p.vec_epi): one float4
+// load / store per operand instead of four scalar ones.
+__device__ __forceinline__ void epilogue_store4(const GemmArgs& p, int row, int col, f32x4 v) {
+  if (row >= p.M || col >= p.N) return;
+  if (p.bias) {
+    const f32x4 b = *reinterpret_cast<const f32x4*>(p.bias + col);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] += b[c];
+  }
+  if (p.act == AZ_ACT_DRELU) {
+    const f32x4 g = *reinterpret_cast<const f32x4*>(p.G + (size_t)row * p.ldg + col);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = g[c] > 0.f ? v[c] : 0.f;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = apply_act(v[c], p.act);
+  }
+  if (p.C2) *reinterpret_cast<f32x4*>(p.C2 + (size_t)row * p.ldc2 + col) = v;
+  const int cr = p.c_rows ? p.c_rows[row] : row;
+  if (p.R) {
+    const f32x4 r = *reinterpret_cast<const f32x4*>(p.R + (size_t)cr * p.ldr + col);
+    f32x4 g = {1.f, 1.f, 1.f, 1.f};
+    if (p.G) g = *reinterpret_cast<const f32x4*>(p.G + (size_t)row * p.ldg + col);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = r[c] + g[c] * v[c];
+  }
+  f32x4* dst = reinterpret_cast<f32x4*>(p.C + (size_t)cr * p.ldc + col);
+  if (p.beta != 0.f) {
+    const f32x4 o = *dst;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] += p.beta * o[c];
+  }
   *dst = v;
 }
 
@@ -168,34 +205,68 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
 // cdna_hip_programming.md §5 "In-launch split-K reduction".)
 template <int MF, int TI, int TJ, class Acc>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][TJ], int r0,
-                                              int c0, int sp) {
+                                              int c0, int sp, float* stage = nullptr) {
   constexpr int NACC = MF == 32 ? 16 : 4;
+  constexpr int WM = TI * MF, WN = TJ * MF;
   const int lane = threadIdx.x & 63;
-  auto row_of = [&](int i, int r) {
-    return r0 + i * MF +
-           (MF == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : 4 * (lane >> 4) + r);
+  auto row_in = [&](int i, int r) {
+    return i * MF + (MF == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : 4 * (lane >> 4) + r);
   };
   const int cl = lane & (MF - 1);
-  if (p.splits <= 1) {
+  const bool skip = (p.ablate & 4) != 0;
+  const size_t plane = (size_t)p.M * p.N;
+  float* slab = p.splits > 1 ? p.slab + (size_t)sp * plane : nullptr;
+  if (stage != nullptr && p.vec_epi && WN % 32 == 0) {
+    // Row-contiguous stores through the wave's LDS region (the MFMA layout scatters 4-byte
+    // stores over 2-4 rows per instruction): each 32-column chunk of the wave tile is written
+    // to LDS [WM][36] and read back as float4 rows, 8 lanes per 128-B row segment.
+    constexpr int LD = 36, CH = 32 / MF;   // MFMA column tiles per 32-column chunk
+    __syncthreads();                        // the k loop's last LDS reads are done everywhere
+#pragma unroll
+    for (int cc = 0; cc < WN / 32; ++cc) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int jj = 0; jj < CH; ++jj)
+#pragma unroll
+          for (int r = 0; r < NACC; ++r)
+            stage[row_in(i, r) * LD + jj * MF + cl] = acc[i][cc * CH + jj][r];
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < WM / 8; ++it) {
+        const int idx = it * 64 + lane, rl = idx >> 3, c4 = (idx & 7) * 4;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(stage + rl * LD + c4);
+        const int row = r0 + rl, col = c0 + cc * 32 + c4;
+        if (skip && v[0] == v[0]) continue;
+        if (slab) {
+          if (row < p.M && col < p.N) *reinterpret_cast<f32x4*>(slab + (size_t)row * p.N + col) = v;
+        } else {
+          epilogue_store4(p, row, col, v);
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  if (!slab) {
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int r = 0; r < NACC; ++r) epilogue_store(p, row_of(i, r), c0 + j * MF + cl, acc[i][j][r]);
+        for (int r = 0; r < NACC; ++r)
+          if (!skip || acc[i][j][r] != acc[i][j][r])
+            epilogue_store(p, r0 + row_in(i, r), c0 + j * MF + cl, acc[i][j][r]);
     return;
   }
-  const size_t plane = (size_t)p.M * p.N;
-  float* slab = p.slab + (size_t)sp * plane;
-  const bool abl = (p.ablate & 4) != 0;
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < NACC; ++r) {
-        const int row = row_of(i, r), col = c0 + j * MF + cl;
-        if (row < p.M && col < p.N && (!abl || acc[i][j][r] != acc[i][j][r]))
+        const int row = r0 + row_in(i, r), col = c0 + j * MF + cl;
+        if (row < p.M && col < p.N && (!skip || acc[i][j][r] != acc[i][j][r]))
           slab[(size_t)row * p.N + col] = acc[i][j][r];
       }
 }
@@ -420,7 +491,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds(GemmArgs p) {
     __syncthreads();
   }
 
-  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp);
+  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
+                            (NW * WM * 36 <= (int)(sizeof(smem) / 4)) ? smem + wave * (WM * 36)
+                                                                       : nullptr);
 }
 
 // Multi-stage LDS-DMA tile: NBUF buffers, tile t+NBUF-1 is issued while tile t is consumed, so
@@ -570,7 +643,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds_pipe(GemmArgs p)
     }
   }
 
-  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp);
+  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
+                            (NW * WM * 36 <= (int)(sizeof(smem) / 4)) ? smem + wave * (WM * 36)
+                                                                       : nullptr);
 }
 
 // LDS-DMA tile, v2: the same LDS image and DMA schedule as gemm_f32_glds, but every wave reads
@@ -761,7 +836,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
     if (!(p.ablate & 2)) __syncthreads();
   }
 
-  tile_epilogue<MF, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp);
+  tile_epilogue<MF, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
+                            (NW * WM * 36 <= (int)(sizeof(smem) / 4)) ? smem + wave * (WM * 36)
+                                                                       : nullptr);
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
@@ -1045,6 +1122,11 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
   a.splits = 1; a.kc = d->K;
   static const char* env_abl = getenv("AZ_GEMM_ABLATE");
   a.ablate = env_abl ? atoi(env_abl) : 0;
+  static const bool no_vec = getenv("AZ_GEMM_NOVEC") != nullptr;   // A/B experiments
+  a.vec_epi = !no_vec && d->N % 4 == 0 && d->ldc % 4 == 0 && aligned16(d->C) &&
+              (!d->C2 || (d->ldc2 % 4 == 0 && aligned16(d->C2))) &&
+              (!d->R || (d->ldr % 4 == 0 && aligned16(d->R))) &&
+              (!d->G || (d->ldg % 4 == 0 && aligned16(d->G))) && (!d->bias || aligned16(d->bias));
 
   if (d->M <= 8 && akm && bkm && !d->C2 && d->act != AZ_ACT_DRELU) {
     launch_gemv(a, s);

@@ -83,6 +83,14 @@ if __name__ == "__main__":
                 res = run(env, M, N, K)
                 print(json.dumps({"M": M, "N": N, "K": K, "cfg": cfg, **res}), flush=True)
         sys.exit(0)
+    if mode == "tallabl":      # epilogue-store ablation on the tall shapes (results wrong by design)
+        for (M, N, K) in [(524288, 256, 64), (524288, 64, 64)]:
+            for cfg in sys.argv[2].split(","):
+                for abl in ("0", "4"):
+                    res = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_ABLATE": abl}, M, N, K)
+                    print(json.dumps({"M": M, "N": N, "K": K, "cfg": cfg, "ablate": abl, **res}),
+                          flush=True)
+        sys.exit(0)
     if mode == "longk":        # steady state: K 10x longer, fixed splits (per-block overhead amortised)
         for cfg in sys.argv[2].split(","):
             for abl in sys.argv[3].split(","):
