@@ -313,10 +313,12 @@ def test_c4_star_forward_vs_golden(ops, c4_gnn_weights):
     np.testing.assert_allclose(v.cpu().numpy(), z["v_gnn_b1"], atol=1e-5)
 
 
-def test_adam_vs_oracle(ops):
+@pytest.mark.parametrize("n", [1, 3, 4, 1023, 10007, 262147])
+def test_adam_vs_oracle(ops, n):
+    """Every size class of the unrolled kernel: tail only (n < 4), one partial block, several
+    blocks with a ragged last one."""
     from oracle.nets import Adam
-    rng = np.random.default_rng(0)
-    n = 10007
+    rng = np.random.default_rng(n)
     p = rng.standard_normal(n).astype(np.float32)
     P = {"p": p.astype(np.float64)}
     opt = Adam(P, lr=1e-3)
