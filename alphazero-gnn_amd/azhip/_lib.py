@@ -57,17 +57,36 @@ class LayerGrads(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in LAYER_FIELDS]
 
 
+class C4Eval(ctypes.Structure):
+    """az_c4_eval (include/az_hip.h)."""
+    _fields_ = [("conv1_w", c_void_p), ("conv1_b", c_void_p), ("conv2_w", c_void_p),
+                ("conv2_b", c_void_p), ("fc_policy_w", c_void_p), ("fc_policy_b", c_void_p),
+                ("fc_value_w", c_void_p), ("fc_value_b", c_void_p), ("A", c_int),
+                ("ot0_w", c_void_p), ("ot0_b", c_void_p), ("ot2_w", c_void_p),
+                ("ot2_b", c_void_p), ("max_B", c_int), ("feat", c_void_p), ("hidden", c_void_p),
+                ("y", c_void_p), ("logp", c_void_p), ("glogp", c_void_p), ("ws", c_void_p),
+                ("ws_bytes", c_size_t)]
+
+
 # name -> (restype, argtypes); every symbol here must be declared in include/az_hip.h
 SIGNATURES = {
     "az_abi_version": (c_int, []),
     "az_last_error": (c_char_p, []),
     "az_check_device": (c_int, []),
+    "az_host_alloc": (c_void_p, [c_size_t]),
+    "az_host_free": (c_int, [c_void_p]),
     "az_gemm_f32": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "az_c4_trunk_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p]),
     "az_conv3x3_relu_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "az_heads_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "az_c4_eval_fwd": (c_int, [ctypes.POINTER(C4Eval), c_void_p, c_int, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p]),
+    "az_c4_trunk_heads_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                      c_void_p]),
     "az_heads_fwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p,
                              c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_size_t, c_void_p]),

@@ -86,11 +86,19 @@ class Connect4Net(_Net):
         s = ops.conv3x3_relu(s, W["conv2.weight"], W["conv2.bias"], 1)
         return s.view(s.shape[0], -1)
 
-    def heads(self, feat, want_pi=True):
-        """Connect4GNN.py:48-57."""
+    def features_heads(self, b, pi=None, v=None):
+        """features(b) and heads of them -> (feat, logp, pi, v); one launch for small B on the
+        7x7 board (ops.c4_trunk_heads), bit-identical to the two calls."""
+        if self.n != 7:
+            f = self.features(b)
+            return (f,) + self.heads(f, pi=pi, v=v)
+        return ops.c4_trunk_heads(b, self.params, pi=pi, v=v)
+
+    def heads(self, feat, want_pi=True, pi=None, v=None):
+        """Connect4GNN.py:48-57 (pi / v: optional output buffers, e.g. HostBuffer views)."""
         W = self.params
         return ops.heads(feat, W["fc_policy.weight"], W["fc_policy.bias"], W["fc_value.weight"],
-                         W["fc_value.bias"], want_pi=want_pi)
+                         W["fc_value.bias"], want_pi=want_pi, pi=pi, v=v)
 
     def __call__(self, b):
         logp, _, v = self.heads(self.features(b), want_pi=False)
@@ -124,12 +132,12 @@ class TicTacToeNet(_Net):
         h2 = ops.linear(feat, W["fc2.weight"], W["fc2.bias"], act=ops.ACT_RELU)
         return h1, h2
 
-    def heads(self, feat, want_pi=True):
+    def heads(self, feat, want_pi=True, pi=None, v=None):
         """TicTacToeGNN.py:36-45."""
         W = self.params
         h1, h2 = self.hidden(feat)
         return ops.heads(h1, W["fc_policy.weight"], W["fc_policy.bias"], W["fc_value.weight"],
-                         W["fc_value.bias"], hv=h2, want_pi=want_pi)
+                         W["fc_value.bias"], hv=h2, want_pi=want_pi, pi=pi, v=v)
 
     def __call__(self, b):
         logp, _, v = self.heads(self.features(b), want_pi=False)
@@ -196,7 +204,7 @@ class PolicyValueGNN(_Net):
         return self.output_transform(self.run_layers(x, graph))
 
 
-def gnn_per_row_heads(nnet, gnn, feat, want_pi=True):
+def gnn_per_row_heads(nnet, gnn, feat, want_pi=True, pi=None, v=None):
     """Batched predict_with_gnn after extract_features (Connect4GNN.py:108-114 applied per row:
     the layers are the identity on a 1-row input, gnn_utils.py:35-36) -> (logp, pi, v).
     Connect4 heads read the transform output directly, so the whole tail is one
@@ -206,9 +214,10 @@ def gnn_per_row_heads(nnet, gnn, feat, want_pi=True):
         logp, pi, v, _, _ = ops.transform_heads(
             feat, G["output_transform.0.weight"], G["output_transform.0.bias"],
             G["output_transform.2.weight"], G["output_transform.2.bias"], W["fc_policy.weight"],
-            W["fc_policy.bias"], W["fc_value.weight"], W["fc_value.bias"], want_pi=want_pi)
+            W["fc_policy.bias"], W["fc_value.weight"], W["fc_value.bias"], want_pi=want_pi,
+            pi=pi, v=v)
         return logp, pi, v
-    return nnet.heads(gnn.forward_per_row(feat), want_pi=want_pi)
+    return nnet.heads(gnn.forward_per_row(feat), want_pi=want_pi, pi=pi, v=v)
 
 
 class C4Evaluator:

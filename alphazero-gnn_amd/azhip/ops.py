@@ -18,13 +18,64 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def _dev(t):
+    """Device for the outputs of an op whose input is `t` (a HostBuffer view -> current GPU)."""
+    return t.device if t.is_cuda else torch.device("cuda", torch.cuda.current_device())
+
+
 def _need(t, dtype=torch.float32, name="tensor"):
     if t is None:
         return
-    if not t.is_cuda:
+    if not t.is_cuda and not _zero_copy(t):
         raise ValueError(f"{name} must live on the GPU (got {t.device})")
     if t.dtype != dtype:
         raise ValueError(f"{name} must be {dtype} (got {t.dtype})")
+
+
+_ZC_RANGES = {}   # start address -> end of each live HostBuffer
+
+
+def _zero_copy(t):
+    """True when CPU tensor `t` lies inside a HostBuffer (device-mapped host memory)."""
+    a = t.data_ptr()
+    return any(s <= a < e for s, e in _ZC_RANGES.items())
+
+
+class HostBuffer:
+    """Zero-copy host staging (az_host_alloc): fine-grained pinned host memory the kernels read
+    and write in place, exposed as CPU tensors.  The ops accept views of it wherever they take
+    a device input or output, so a batch-1 evaluation needs no copy launches: the host writes
+    the board, the graph runs, and after the stream synchronises the host reads the outputs."""
+
+    def __init__(self, nbytes):
+        L = _lib.lib()
+        p = L.az_host_alloc(nbytes)
+        if not p:
+            raise RuntimeError(f"az_host_alloc: {L.az_last_error().decode()}")
+        self.ptr, self.nbytes = int(p), int(nbytes)
+        self._arr = (ctypes.c_uint8 * self.nbytes).from_address(self.ptr)
+        self.bytes = torch.frombuffer(self._arr, dtype=torch.uint8)
+        _ZC_RANGES[self.ptr] = self.ptr + self.nbytes
+
+    def view(self, offset, dtype, shape):
+        """CPU tensor of `shape` over bytes [offset, offset + its size) of the buffer."""
+        n = torch.Size(shape).numel() * torch.empty((), dtype=dtype).element_size()
+        if offset % 16 or offset + n > self.nbytes:
+            raise ValueError("HostBuffer.view: misaligned or out of range")
+        return self.bytes[offset:offset + n].view(dtype).view(shape)
+
+    def close(self):
+        if self.ptr:
+            _ZC_RANGES.pop(self.ptr, None)
+            self.bytes = self._arr = None
+            _lib.lib().az_host_free(ctypes.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # interpreter shutdown
+            pass
 
 
 _WS = {}
@@ -136,7 +187,7 @@ def c4_trunk(boards_i8, W, out=None):
     _need(boards_i8, torch.int8, "boards")
     B = boards_i8.shape[0]
     if out is None:
-        out = torch.empty((B, 3136), device=boards_i8.device, dtype=torch.float32)
+        out = torch.empty((B, 3136), device=_dev(boards_i8), dtype=torch.float32)
     L = _lib.lib()
     _lib.check(L.az_c4_trunk_fwd(_p(boards_i8), B, _p(W["conv1.weight"]), _p(W["conv1.bias"]),
                                  _p(W["conv2.weight"]), _p(W["conv2.bias"]), _p(out), _stream()),
@@ -144,10 +195,32 @@ def c4_trunk(boards_i8, W, out=None):
     return out
 
 
+def c4_trunk_heads(boards_i8, W, feat=None, logp=None, pi=None, v=None, want_pi=True):
+    """Trunk + policy/value heads (Connect4Net.py:42-60) -> (feat, logp, pi, v); one launch
+    for B <= 32, bit-identical to c4_trunk then heads."""
+    _need(boards_i8, torch.int8, "boards")
+    B = boards_i8.shape[0]
+    dev = _dev(boards_i8)
+    A = W["fc_policy.weight"].shape[0]
+    feat = torch.empty((B, 3136), device=dev) if feat is None else feat
+    logp = torch.empty((B, A), device=dev) if logp is None else logp
+    pi = (torch.empty((B, A), device=dev) if pi is None else pi) if want_pi else None
+    v = torch.empty((B,), device=dev) if v is None else v
+    L = _lib.lib()
+    ws = workspace(dev, max(int(L.az_heads_ws_bytes(B, 3136, A)), 64 << 20))
+    _lib.check(L.az_c4_trunk_heads_fwd(
+        _p(boards_i8), B, _p(W["conv1.weight"]), _p(W["conv1.bias"]), _p(W["conv2.weight"]),
+        _p(W["conv2.bias"]), _p(W["fc_policy.weight"]), _p(W["fc_policy.bias"]), A,
+        _p(W["fc_value.weight"]), _p(W["fc_value.bias"]), _p(feat), _p(logp), _p(pi), _p(v),
+        _p(ws), ctypes.c_size_t(ws.numel()), _stream()), "az_c4_trunk_heads_fwd")
+    return feat, logp, pi, v
+
+
 def conv3x3_relu(x, w, b, pad, out=None):
     """x: int8 [B,H,W] (Cin=1) or fp32 [B,Cin,H,W] -> fp32 [B,Cout,Ho,Wo]."""
     is_i8 = x.dtype == torch.int8
     if is_i8:
+        _need(x, torch.int8, "x")
         B, H, Wd = x.shape
         Cin = 1
     else:
@@ -156,7 +229,7 @@ def conv3x3_relu(x, w, b, pad, out=None):
     Cout = w.shape[0]
     Ho, Wo = H + 2 * pad - 2, Wd + 2 * pad - 2
     if out is None:
-        out = torch.empty((B, Cout, Ho, Wo), device=x.device, dtype=torch.float32)
+        out = torch.empty((B, Cout, Ho, Wo), device=_dev(x), dtype=torch.float32)
     L = _lib.lib()
     _lib.check(L.az_conv3x3_relu_fwd(_p(x), int(is_i8), B, Cin, H, Wd, _p(w), _p(b), Cout, pad,
                                      _p(out), _stream()), "az_conv3x3_relu_fwd")
@@ -391,6 +464,7 @@ def nchw_drelu_to_pm(dy, y, B, C, HW, mask=None, scale=1.0, out=None):
 def im2col3x3(x, pad, ldc=None):
     is_i8 = x.dtype == torch.int8
     if is_i8:
+        _need(x, torch.int8, "x")
         B, H, W = x.shape
         C = 1
     else:

@@ -7,12 +7,13 @@ predict_batch_with_gnn, predict_both) for lock-step self-play.  Checkpoints are 
 torch.save dict ({'state_dict': ..., 'gnn': ...}) with the same keys, so files move freely
 between the reference and this implementation.
 """
+import ctypes
 import os
 
 import numpy as np
 import torch
 
-from . import nets, ops, train as T
+from . import _lib, nets, ops, train as T
 from .nets import boards_to_device
 
 
@@ -71,12 +72,39 @@ class _Batch1Graph:
         dev = w.device
         A = w.action_size
         width = {"std": A + 1, "gnn": A + 1, "both": 2 * A + 2}[kind]
-        self.h_in = torch.zeros((1, w.board_x, w.board_y), dtype=torch.int8, pin_memory=True)
-        self.d_in = torch.zeros((1, w.board_x, w.board_y), dtype=torch.int8, device=dev)
-        self.h_out = torch.zeros((1, width), dtype=torch.float32, pin_memory=True)
-        self.d_out = torch.zeros((1, width), dtype=torch.float32, device=dev)
+        # zero-copy staging (ops.HostBuffer): the trunk reads the board and the heads write
+        # their pi / v straight from / into mapped host memory, so the graph has no copy
+        # nodes; AZ_NO_ZEROCOPY=1 keeps the pinned-buffer + H2D / D2H copies instead
+        self.host = None
+        if os.environ.get("AZ_NO_ZEROCOPY", "0") in ("", "0"):
+            try:
+                self.host = ops.HostBuffer(256 + 4 * width)
+            except RuntimeError:
+                self.host = None
+        if self.host is not None:
+            self.h_in = self.host.view(0, torch.int8, (1, w.board_x, w.board_y))
+            self.h_out = self.host.view(256, torch.float32, (1, width))
+        else:
+            self.h_in = torch.zeros((1, w.board_x, w.board_y), dtype=torch.int8, pin_memory=True)
+            self.d_in = torch.zeros((1, w.board_x, w.board_y), dtype=torch.int8, device=dev)
+            self.h_out = torch.zeros((1, width), dtype=torch.float32, pin_memory=True)
+            self.d_out = torch.zeros((1, width), dtype=torch.float32, device=dev)
+        zc = self.host is not None
 
         def body():
+            if zc:
+                o = self.h_out
+                if kind in ("std", "both") and hasattr(w.nnet, "features_heads"):
+                    f, _, _, _ = w.nnet.features_heads(self.h_in, pi=o[:, :A], v=o[:, A])
+                elif kind in ("std", "both"):
+                    f = w.nnet.features(self.h_in)
+                    w.nnet.heads(f, pi=o[:, :A], v=o[:, A])
+                else:
+                    f = w.nnet.features(self.h_in)
+                if kind in ("gnn", "both"):
+                    c = 0 if kind == "gnn" else A + 1
+                    nets.gnn_per_row_heads(w.nnet, w.gnn, f, pi=o[:, c:c + A], v=o[:, c + A])
+                return
             self.d_in.copy_(self.h_in, non_blocking=True)
             f = w.nnet.features(self.d_in)
             parts = []
@@ -109,6 +137,74 @@ class _Batch1Graph:
         self.graph.replay()
         torch.cuda.current_stream(self.dev).synchronize()
         return self.h_out.numpy()[0].copy()
+
+
+class _Batch1Direct:
+    """Connect4 batch-1 evaluation as ONE C call (az_c4_eval_fwd: 1 + 3 direct launches) with
+    zero-copy staging: the board is read and pi / v written in place in mapped host memory.
+    Measured on MI355X, a hipGraph replay costs ~14 us of host time before its first kernel
+    runs, more than these launches, which overlap the GPU work they queue.  Same kernels as the
+    eager path (bit-identical outputs); parameters are read through the pointers fixed here,
+    which stay valid because every update is in place.  kind as _Batch1Graph."""
+
+    def __init__(self, w, kind):
+        dev = w.device
+        A = w.action_size
+        self.kind, self.A = kind, A
+        width = {"std": A + 1, "gnn": A + 1, "both": 2 * A + 2}[kind]
+        self.host = ops.HostBuffer(256 + 4 * width)
+        self.h_in = self.host.view(0, torch.int8, (1, w.board_x, w.board_y))
+        self.h_out = self.host.view(256, torch.float32, (1, width))
+        F = 3136
+        gnn = kind in ("gnn", "both")
+        self.feat = torch.empty((1, F), device=dev)
+        self.hidden = torch.empty((1, F), device=dev) if gnn else None
+        self.y = torch.empty((1, F), device=dev) if gnn else None
+        self.logp = torch.empty((1, A), device=dev)
+        self.glogp = torch.empty((1, A), device=dev)
+        self.ws = torch.empty((16 << 20,), dtype=torch.uint8, device=dev)
+        W = w.nnet.params
+        G = w.gnn.params if gnn else None
+        P = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        self.desc = _lib.C4Eval(
+            P(W["conv1.weight"]), P(W["conv1.bias"]), P(W["conv2.weight"]), P(W["conv2.bias"]),
+            P(W["fc_policy.weight"]), P(W["fc_policy.bias"]), P(W["fc_value.weight"]),
+            P(W["fc_value.bias"]), A,
+            P(G["output_transform.0.weight"]) if gnn else None,
+            P(G["output_transform.0.bias"]) if gnn else None,
+            P(G["output_transform.2.weight"]) if gnn else None,
+            P(G["output_transform.2.bias"]) if gnn else None,
+            1, P(self.feat), P(self.hidden), P(self.y), P(self.logp), P(self.glogp),
+            P(self.ws), self.ws.numel())
+        assert int(_lib.lib().az_transform_heads_ws_bytes(1, F, A)) <= self.ws.numel()
+        o = self.h_out.data_ptr()
+        std = kind in ("std", "both")
+        g0 = 0 if kind == "gnn" else A + 1
+        self.args = (ctypes.byref(self.desc), ctypes.c_void_p(self.h_in.data_ptr()), 1,
+                     ctypes.c_void_p(o) if std else None,
+                     ctypes.c_void_p(o + 4 * A) if std else None,
+                     ctypes.c_void_p(o + 4 * g0) if gnn else None,
+                     ctypes.c_void_p(o + 4 * (g0 + A)) if gnn else None)
+        self.fn = _lib.lib().az_c4_eval_fwd
+        self.dev = dev
+        # keep the parameter tensors alive with the pointers taken above
+        self._keep = (W, G)
+
+    def run(self, board):
+        self.h_in.numpy()[0] = board
+        s = torch.cuda.current_stream(self.dev)
+        rc = self.fn(*self.args, ctypes.c_void_p(s.cuda_stream))
+        if rc:
+            _lib.check(rc, "az_c4_eval_fwd")
+        s.synchronize()
+        return self.h_out.numpy()[0].copy()
+
+
+def _direct_ok(w):
+    """az_c4_eval_fwd covers the 7x7 Connect4Net (+ PolicyValueGNN output_transform)."""
+    return (os.environ.get("AZ_B1_MODE", "direct") == "direct"
+            and isinstance(w.nnet, nets.Connect4Net) and w.nnet.n == 7
+            and os.environ.get("AZ_NO_ZEROCOPY", "0") in ("", "0"))
 
 
 def _graphs_enabled():
@@ -146,7 +242,7 @@ class NetWrapper:
             self.nnet.eval()
             if self.has_gnn:
                 self.gnn.eval()
-            g[kind] = _Batch1Graph(self, kind)
+            g[kind] = _Batch1Direct(self, kind) if _direct_ok(self) else _Batch1Graph(self, kind)
         return g[kind]
 
     def _eval(self, boards, gnn):

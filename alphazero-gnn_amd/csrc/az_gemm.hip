@@ -924,6 +924,69 @@ __global__ __launch_bounds__(256) void gemv_f32(GemmArgs p) {
   }
 }
 
+// Whole-K GEMV for K <= 256*S (the batch-1 predict shapes): A's MR rows are staged in LDS once
+// (zero-padded to 256*S), then each wave issues ALL S float4 loads of its R weight rows before
+// the first FMA -- one HBM round trip per wave instead of one per KC chunk.  Loads past K
+// re-read the row start and meet zeros in the staged A; rows past N are clamped to row 0 and
+// never stored.
+template <int MR, int S, int R>
+__global__ __launch_bounds__(256) void gemv_full(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) float As[MR * S * 256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n_base = (blockIdx.x * 4 + wave) * R;
+  f32x4 w[R][S];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = n_base + r < p.N ? n_base + r : 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int k4 = (lane + 64 * s) * 4;
+      w[r][s] = *reinterpret_cast<const f32x4*>(p.B + (size_t)n * p.ldb + (k4 < p.K ? k4 : 0));
+    }
+  }
+  for (int idx = threadIdx.x; idx < MR * S * 64; idx += 256) {
+    const int m = idx / (S * 64), k = (idx % (S * 64)) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (m < p.M && k < p.K) {
+      const int ar = p.a_rows ? p.a_rows[m] : m;
+      const float* src = (p.A2 && k >= p.K0) ? p.A2 + (size_t)ar * p.lda2 + (k - p.K0)
+                                             : p.A + (size_t)ar * p.lda + k;
+      v = *reinterpret_cast<const f32x4*>(src);
+    }
+    *reinterpret_cast<f32x4*>(&As[m * S * 256 + k]) = v;
+  }
+  __syncthreads();
+  float acc[MR][R];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[m][r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int k4 = (lane + 64 * s) * 4;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(&As[m * S * 256 + k4]);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        acc[m][r] = fmaf(a[0], w[r][s][0], fmaf(a[1], w[r][s][1],
+                    fmaf(a[2], w[r][s][2], fmaf(a[3], w[r][s][3], acc[m][r]))));
+    }
+  }
+  float mine = 0.f;  // lane m*R + r keeps the reduced sum of output (m, n_base + r)
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float t = wave_sum(acc[m][r]);
+      if (lane == m * R + r) mine = t;
+    }
+  if (lane < MR * R) {
+    const int m = lane / R, r = lane % R;
+    if (m < p.M && n_base + r < p.N) epilogue_store(p, m, n_base + r, mine);
+  }
+}
+
 struct TileCfg { int bm, bn, bk, wgm, wgn; };
 // register-staged: 0: 64x64x32 (4 waves 2x2)   1: 128x128x32 (4 waves 2x2)   2: 64x64x64
 // 3: 128x64x32 (4 waves 2x2)  4: 128x128x32 (8 waves 2x4)   5: 256x128x32 (8 waves 4x2)
@@ -1013,7 +1076,43 @@ static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream
   }
 }
 
+template <int MR, int S, int R>
+static bool try_gemv_full(const GemmArgs& a, hipStream_t s) {
+  if constexpr (MR * S <= 32) {
+    if (a.K > 256 * S) return false;
+    const int nblk = (a.N + 4 * R - 1) / (4 * R);
+    hipLaunchKernelGGL((gemv_full<MR, S, R>), dim3(nblk), dim3(256), 0, s, a);
+    return true;
+  }
+  return false;
+}
+
+// whole-K kernel when A's rows fit 32 KB of LDS (S = ceil(K/256) rounded up to an
+// instantiated width); AZ_GEMV_R=1 selects one weight row per wave instead of two
+template <int MR>
+static bool launch_gemv_full(const GemmArgs& a, hipStream_t s) {
+  static const bool r1 = [] { const char* e = getenv("AZ_GEMV_R"); return e && atoi(e) == 1; }();
+  if (r1)
+    return try_gemv_full<MR, 1, 1>(a, s) || try_gemv_full<MR, 2, 1>(a, s) ||
+           try_gemv_full<MR, 4, 1>(a, s) || try_gemv_full<MR, 8, 1>(a, s) ||
+           try_gemv_full<MR, 13, 1>(a, s) || try_gemv_full<MR, 16, 1>(a, s);
+  return try_gemv_full<MR, 1, 2>(a, s) || try_gemv_full<MR, 2, 2>(a, s) ||
+         try_gemv_full<MR, 4, 2>(a, s) || try_gemv_full<MR, 8, 2>(a, s) ||
+         try_gemv_full<MR, 13, 2>(a, s) || try_gemv_full<MR, 16, 2>(a, s);
+}
+
 static void launch_gemv(const GemmArgs& a, hipStream_t s) {
+  static const bool chunked = getenv("AZ_GEMV_CHUNKED") != nullptr;   // A/B experiments
+  if (!chunked) {
+    bool done = false;
+    switch (a.M) {
+      case 1: done = launch_gemv_full<1>(a, s); break;
+      case 2: done = launch_gemv_full<2>(a, s); break;
+      case 3: case 4: done = launch_gemv_full<4>(a, s); break;
+      default: done = launch_gemv_full<8>(a, s); break;
+    }
+    if (done) return;
+  }
   const int nblk = (a.N + 4 * GV_ROWS - 1) / (4 * GV_ROWS);
   switch (a.M) {
     case 1: hipLaunchKernelGGL(gemv_f32<1>, dim3(nblk), dim3(256), 0, s, a); break;

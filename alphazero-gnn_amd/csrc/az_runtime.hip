@@ -48,3 +48,33 @@ extern "C" int az_check_device(void) {
   }
   return AZ_OK;
 }
+
+// Host staging the device reads and writes in place (zero-copy): fine-grained (coherent) pinned
+// memory mapped into the device's address space, so a kernel's loads see the host's latest
+// stores and its stores are visible to the host once the stream has synchronised -- with no
+// copy launch on either side.  Used by the batch-1 evaluation graph (one board in, one row of
+// policy/value out per MCTS leaf).
+extern "C" void* az_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (bytes == 0) bytes = 1;
+  if (hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+    az::set_error("az_host_alloc: hipHostMalloc(%zu) failed", bytes);
+    return nullptr;
+  }
+  void* dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || dp != p) {
+    az::set_error("az_host_alloc: host buffer is not mapped at the same device address");
+    (void)hipHostFree(p);
+    return nullptr;
+  }
+  memset(p, 0, bytes);
+  return p;
+}
+
+extern "C" int az_host_free(void* p) {
+  if (p && hipHostFree(p) != hipSuccess) {
+    az::set_error("az_host_free: hipHostFree failed");
+    return AZ_EDEVICE;
+  }
+  return AZ_OK;
+}

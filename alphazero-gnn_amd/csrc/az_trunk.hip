@@ -19,13 +19,32 @@ namespace az {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
+// conv2's weights in LDS: row co at stride W2S_STRIDE floats.  Stride = 2 (mod 32) makes the
+// conv2 fragment reads (lane: co = 16 consecutive rows, ci = 2 values 9 floats apart per 32-lane
+// half) hit 32 distinct ds_read_b32 banks.
+constexpr int W2S_STRIDE = 290;
+constexpr int W2S_FLOATS = 64 * W2S_STRIDE;
+
+// LDS the kernel hands to c4_trunk_tile: conv2's weights while they are read into registers,
+// then (NB <= 4) the NB*3136-float output staging tile
 template <int NB>
-__global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict__ boards, int B,
-                                                      const float* __restrict__ w1,
-                                                      const float* __restrict__ b1,
-                                                      const float* __restrict__ w2,
-                                                      const float* __restrict__ b2,
-                                                      float* __restrict__ feat) {
+constexpr int trunk_union_floats() {
+  return W2S_FLOATS > (NB <= 4 ? NB * 3136 : 0) ? W2S_FLOATS : NB * 3136;
+}
+
+// The trunk of one 512-thread block (boards blockIdx.x*NB ...).  `un` is LDS of
+// trunk_union_floats<NB>() floats: conv2's weights are staged there with coalesced float4 loads
+// (each lane then reads its 72 fragments from LDS -- one pass over the 74 KB per block instead of
+// 72 scattered 4-byte loads per lane in all 8 waves), and with NB <= 4 the feature rows are then
+// assembled in it (still there on return).
+template <int NB>
+__device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards, int B,
+                                              const float* __restrict__ w1,
+                                              const float* __restrict__ b1,
+                                              const float* __restrict__ w2,
+                                              const float* __restrict__ b2,
+                                              float* __restrict__ feat, float* un) {
+  float* const ob = un;
   constexpr int P = 49, PP = 81, CI = 32;
   constexpr int ROWS = NB * P;
   constexpr int MT = (ROWS + 15) / 16;
@@ -35,10 +54,21 @@ __global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict_
   constexpr bool STAGE = NB <= 4;
   __shared__ float bd[NB * PP];
   __shared__ float c1[NB * CI * PP];
-  __shared__ __attribute__((aligned(16))) float ob[STAGE ? NB * 3136 : 4];
+  __shared__ float w1s[CI * 9 + CI];   // conv1 weights then bias: one round trip, then LDS only
   const int tid = threadIdx.x;
   const int b0 = blockIdx.x * NB;
   const int nb = min(NB, B - b0);
+  const int lane = tid & 63, wave = tid >> 6;
+  const int nt = wave & 3, mh = wave >> 2;
+  const int h = lane >> 4, c16 = lane & 15;
+  const int co = nt * 16 + c16;
+  // conv2's weights -> LDS (row co = 288 floats = 72 float4, so no float4 crosses a row)
+  for (int i = tid; i < 64 * 72; i += 512) {
+    const f32x4v w = reinterpret_cast<const f32x4v*>(w2)[i];
+    float* d = un + (i / 72) * W2S_STRIDE + (i % 72) * 4;
+    d[0] = w[0]; d[1] = w[1]; d[2] = w[2]; d[3] = w[3];
+  }
+  const float bias = b2[co];
 
   for (int i = tid; i < NB * PP; i += 512) {
     const int b = i / PP, pp = i % PP, px = pp / 9, py = pp % 9;
@@ -47,7 +77,14 @@ __global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict_
       v = (float)boards[(size_t)(b0 + b) * P + (px - 1) * 7 + (py - 1)];
     bd[i] = v;
   }
+  if (tid < CI * 9 + CI) w1s[tid] = tid < CI * 9 ? w1[tid] : b1[tid - CI * 9];
   __syncthreads();
+  float breg[72];
+#pragma unroll
+  for (int s = 0; s < 72; ++s) {
+    const int tap = s >> 3, ci = 4 * (s & 7) + h;
+    breg[s] = un[co * W2S_STRIDE + ci * 9 + (tap / 3) * 3 + (tap % 3)];
+  }
   for (int i = tid; i < NB * CI * PP; i += 512) {
     const int b = i / (CI * PP), rem = i % (CI * PP), ci = rem / PP, pp = rem % PP;
     const int px = pp / 9, py = pp % 9;
@@ -58,40 +95,27 @@ __global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict_
       for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw)
-          s = fmaf(w1[ci * 9 + kh * 3 + kw], bd[b * PP + (px - 1 + kh) * 9 + (py - 1 + kw)], s);
-      s += b1[ci];
+          s = fmaf(w1s[ci * 9 + kh * 3 + kw], bd[b * PP + (px - 1 + kh) * 9 + (py - 1 + kw)], s);
+      s += w1s[CI * 9 + ci];
       v = s > 0.f ? s : 0.f;
     }
     c1[i] = v;
   }
   __syncthreads();
 
-  const int lane = tid & 63, wave = tid >> 6;
-  const int nt = wave & 3, mh = wave >> 2;
-  const int h = lane >> 4, c16 = lane & 15;
-  const int co = nt * 16 + c16;
-  float breg[72];
-#pragma unroll
-  for (int s = 0; s < 72; ++s) {
-    const int tap = s >> 3, ci = 4 * (s & 7) + h;
-    breg[s] = w2[co * 288 + ci * 9 + (tap / 3) * 3 + (tap % 3)];
-  }
-  const float bias = b2[co];
-  for (int mt = mh; mt < MT; mt += 2) {
+  // the wave's m-tiles go in pairs (mt, mt + 2) with their two MFMA chains interleaved: each
+  // chain keeps its own k order (same sums as one tile at a time), but the pipeline now has two
+  // independent accumulators to alternate between instead of stalling on one
+  auto a_base = [&](int mt) {
     const int i = mt * 16 + c16;
     int base = 0;
-    if (i < ROWS) {
+    if (mt < MT && i < ROWS) {
       const int b = i / P, p = i % P;
       base = b * CI * PP + h * PP + (p / 7) * 9 + (p % 7);
     }
-    const float* a_ptr = c1 + base;
-    f32x4v acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 72; ++s) {
-      const int tap = s >> 3;
-      const int off = 4 * (s & 7) * PP + (tap / 3) * 9 + (tap % 3);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a_ptr[off], breg[s], acc, 0, 0, 0);
-    }
+    return c1 + base;
+  };
+  auto store_tile = [&](int mt, const f32x4v& acc) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = mt * 16 + h * 4 + r;
@@ -102,6 +126,20 @@ __global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict_
         else feat[(size_t)(b0 + b) * 3136 + co * P + p] = v > 0.f ? v : 0.f;
       }
     }
+  };
+  for (int mt = mh; mt < MT; mt += 4) {
+    const float* a0 = a_base(mt);
+    const float* a1 = a_base(mt + 2);
+    f32x4v acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 72; ++s) {
+      const int tap = s >> 3;
+      const int off = 4 * (s & 7) * PP + (tap / 3) * 9 + (tap % 3);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[off], breg[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[off], breg[s], acc1, 0, 0, 0);
+    }
+    store_tile(mt, acc0);
+    if (mt + 2 < MT) store_tile(mt + 2, acc1);
   }
   if constexpr (STAGE) {
     __syncthreads();
@@ -109,6 +147,17 @@ __global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict_
     const f32x4v* src = reinterpret_cast<const f32x4v*>(ob);
     for (int i = tid; i < nb * 784; i += 512) dst[i] = src[i];
   }
+}
+
+template <int NB>
+__global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict__ boards, int B,
+                                                      const float* __restrict__ w1,
+                                                      const float* __restrict__ b1,
+                                                      const float* __restrict__ w2,
+                                                      const float* __restrict__ b2,
+                                                      float* __restrict__ feat) {
+  __shared__ __attribute__((aligned(16))) float un[trunk_union_floats<NB>()];
+  c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, un);
 }
 
 // Generic 3x3 conv + ReLU, one thread per output (TicTacToe trunks: tiny, latency-bound).
@@ -326,6 +375,134 @@ __global__ __launch_bounds__(256) void heads_finalize_kernel(const float* __rest
   v[row] = tanhf(sm[r][A] + bv[0]);
 }
 
+// Small batches (B <= HEADS_ROWS_MAXB, the batch-1 MCTS leaf): both passes in ONE launch, one
+// 512-thread block per row.  Wave w forms the chunk partials of chunks w, w+8, ... with exactly
+// heads_partial_kernel's arithmetic (two chunks' loads issued together), parks them in LDS, and
+// the finalize arithmetic of heads_finalize_kernel follows in the same block -- so logp, pi and v
+// are bit-identical to the two-launch path, minus one launch and the partials' HBM round trip.
+constexpr int HEADS_ROWS_MAXB = 32;
+constexpr int HEADS_ROWS_MAXC = 64;   // K <= 16384
+
+// One row's heads with all 512 threads of the block: xr / yr may point into LDS (the fused
+// trunk) or HBM; part is [HEADS_ROWS_MAXC][AMAX+1] and sm [AMAX+1] floats of LDS.  Ends with a
+// barrier, so the caller may reuse part / sm for the next row.
+template <int AMAX>
+__device__ __forceinline__ void heads_row_block(const float* xr, const float* yr, int K,
+                                                const float* __restrict__ wp, int A,
+                                                const float* __restrict__ wv,
+                                                const float* __restrict__ bp,
+                                                const float* __restrict__ bv, int row,
+                                                float* __restrict__ logp, float* __restrict__ pi,
+                                                float* __restrict__ v, float* part, float* sm) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nchunks = (K + HEADS_KC - 1) / HEADS_KC;
+  constexpr int LOGV = AMAX == 8 ? 3 : (AMAX == 16 ? 4 : 5);
+  constexpr int PW = AMAX + 1;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = wave; c0 < nchunks; c0 += 16) {
+    f32x4 xs[2], ys[2], w[2][AMAX + 1];
+    bool kin[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = min(c0 + 8 * j, nchunks - 1);
+      const int k = c * HEADS_KC + lane * 4;
+      kin[j] = k < K;
+      const int kc = kin[j] ? k : 0;
+      xs[j] = *reinterpret_cast<const f32x4*>(xr + kc);
+      ys[j] = *reinterpret_cast<const f32x4*>(yr + kc);
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a)
+        w[j][a] = *reinterpret_cast<const f32x4*>(wp + (size_t)min(a, A - 1) * K + kc);
+      w[j][AMAX] = *reinterpret_cast<const f32x4*>(wv + kc);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = c0 + 8 * j;
+      if (c >= nchunks) break;
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a) w[j][a] = (a < A && kin[j]) ? w[j][a] : z;
+      w[j][AMAX] = kin[j] ? w[j][AMAX] : z;
+      const f32x4 x = kin[j] ? xs[j] : z, y = kin[j] ? ys[j] : z;
+      float pv[AMAX];
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a)
+        pv[a] = fmaf(x[3], w[j][a][3], fmaf(x[2], w[j][a][2], fmaf(x[1], w[j][a][1], x[0] * w[j][a][0])));
+      const float ps = wave_multi_sum<AMAX>(pv);
+      const float vs = wave_sum(fmaf(y[3], w[j][AMAX][3], fmaf(y[2], w[j][AMAX][2],
+                                fmaf(y[1], w[j][AMAX][1], y[0] * w[j][AMAX][0]))));
+      const int a = lane >> (6 - LOGV);
+      if ((lane & ((1 << (6 - LOGV)) - 1)) == 0 && a < A) part[c * PW + a] = ps;
+      if (lane == 0) part[c * PW + A] = vs;
+    }
+  }
+  __syncthreads();
+  const int W = A + 1;
+  if (threadIdx.x < W) {
+    float s = 0.f;
+    for (int c = 0; c < nchunks; ++c) s += part[c * PW + threadIdx.x];
+    sm[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float l[AMAX];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a)
+      if (a < A) {
+        l[a] = sm[a] + bp[a];
+        mx = fmaxf(mx, l[a]);
+      }
+    float se = 0.f;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a)
+      if (a < A) se += expf(l[a] - mx);
+    const float lse = logf(se);
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a)
+      if (a < A) {
+        const float o = (l[a] - mx) - lse;
+        logp[(size_t)row * A + a] = o;
+        if (pi) pi[(size_t)row * A + a] = expf(o);
+      }
+    v[row] = tanhf(sm[A] + bv[0]);
+  }
+  __syncthreads();
+}
+
+template <int AMAX>
+__global__ __launch_bounds__(512) void heads_rows_kernel(
+    const float* __restrict__ hp, int ldhp, const float* __restrict__ hv, int ldhv, int K,
+    const float* __restrict__ wp, int A, const float* __restrict__ wv,
+    const float* __restrict__ bp, const float* __restrict__ bv, float* __restrict__ logp,
+    float* __restrict__ pi, float* __restrict__ v) {
+  __shared__ float part[HEADS_ROWS_MAXC * (AMAX + 1)];
+  __shared__ float sm[AMAX + 1];
+  const int row = blockIdx.x;
+  heads_row_block<AMAX>(hp + (size_t)row * ldhp, hv + (size_t)row * ldhv, K, wp, A, wv, bp, bv,
+                        row, logp, pi, v, part, sm);
+}
+
+// Connect4 trunk + policy/value heads in ONE launch for small batches (the batch-1 MCTS leaf):
+// c4_trunk_kernel's body, then each of the block's boards runs heads_row_block on its feature
+// row straight from the LDS staging tile -- same values and arithmetic as az_c4_trunk_fwd +
+// az_heads_fwd, so every output is bit-identical to that pair.
+template <int NB>
+__global__ __launch_bounds__(512) void c4_trunk_heads_kernel(
+    const int8_t* __restrict__ boards, int B, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    float* __restrict__ feat, const float* __restrict__ wp, const float* __restrict__ bp, int A,
+    const float* __restrict__ wv, const float* __restrict__ bv, float* __restrict__ logp,
+    float* __restrict__ pi, float* __restrict__ v) {
+  __shared__ __attribute__((aligned(16))) float ob[trunk_union_floats<NB>()];
+  __shared__ float part[HEADS_ROWS_MAXC * 9];
+  __shared__ float sm[9];
+  c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, ob);
+  const int b0 = blockIdx.x * NB, nb = min(NB, B - b0);
+  for (int b = 0; b < nb; ++b)
+    heads_row_block<8>(ob + b * 3136, ob + b * 3136, 3136, wp, A, wv, bp, bv, b0 + b, logp, pi, v,
+                       part, sm);
+}
+
 }  // namespace az
 
 using namespace az;
@@ -398,6 +575,12 @@ static void launch_heads(const float* hp, int ldhp, const float* hv, int ldhv, i
                          const float* bv, float* logp, float* pi, float* v, float* part,
                          hipStream_t s) {
   const int nchunks = (K + HEADS_KC - 1) / HEADS_KC;
+  static const bool two_pass = getenv("AZ_HEADS_TWOPASS") != nullptr;   // A/B experiments
+  if (B <= HEADS_ROWS_MAXB && nchunks <= HEADS_ROWS_MAXC && !two_pass) {
+    hipLaunchKernelGGL(heads_rows_kernel<AMAX>, dim3(B), dim3(512), 0, s, hp, ldhp, hv, ldhv, K,
+                       wp, A, wv, bp, bv, logp, pi, v);
+    return;
+  }
   dim3 g(nchunks, (B + HEADS_ROWS - 1) / HEADS_ROWS);
   hipLaunchKernelGGL(heads_partial_kernel<AMAX>, g, dim3(256), 0, s, hp, ldhp, hv, ldhv, B, K, wp,
                      A, wv, part);
@@ -426,6 +609,32 @@ extern "C" int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv
   else
     launch_heads<32>(hp, ldhp, hv, ldhv, B, K, wp, bp, A, wv, bv, logp, pi, v, part, s);
   return check_launch("heads_kernels");
+}
+
+extern "C" int az_c4_trunk_heads_fwd(const int8_t* boards, int B, const float* conv1_w,
+                                     const float* conv1_b, const float* conv2_w,
+                                     const float* conv2_b, const float* wp, const float* bp, int A,
+                                     const float* wv, const float* bv, float* feat, float* logp,
+                                     float* pi, float* v, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  AZ_REQUIRE(B >= 0 && A > 0 && A <= 32, AZ_EINVAL, "az_c4_trunk_heads_fwd: B=%d A=%d", B, A);
+  if (B == 0) return AZ_OK;
+  AZ_REQUIRE(boards && conv1_w && conv1_b && conv2_w && conv2_b && wp && bp && wv && bv && feat &&
+                 logp && v,
+             AZ_EINVAL, "az_c4_trunk_heads_fwd: null pointer");
+  AZ_REQUIRE(aligned16(feat) && aligned16(wp) && aligned16(wv), AZ_EINVAL,
+             "az_c4_trunk_heads_fwd: operands need 16B alignment");
+  static const bool split = getenv("AZ_TRUNK_HEADS_SPLIT") != nullptr;   // A/B experiments
+  if (B <= HEADS_ROWS_MAXB && A <= 8 && !split) {
+    hipLaunchKernelGGL(c4_trunk_heads_kernel<1>, dim3(B), dim3(512), 0, as_stream(stream), boards,
+                       B, conv1_w, conv1_b, conv2_w, conv2_b, feat, wp, bp, A, wv, bv, logp, pi,
+                       v);
+    return check_launch("c4_trunk_heads_kernel");
+  }
+  int rc = az_c4_trunk_fwd(boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, stream);
+  if (rc) return rc;
+  return az_heads_fwd(feat, 3136, feat, 3136, B, 3136, wp, bp, A, wv, bv, logp, pi, v, ws,
+                      ws_bytes, stream);
 }
 
 static size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -517,4 +726,28 @@ extern "C" int az_transform_heads_fwd(const float* x, int B, int F, const float*
   // y = hidden W2^T + b2 (output_transform.2) and the heads
   return az_linear_heads_fwd(hidden, B, F, w2, b2, wp, bp, A, wv, bv, y, logp, pi, v, ws,
                              ws_bytes, stream);
+}
+
+extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi,
+                              float* v, float* gpi, float* gv, void* stream) {
+  AZ_REQUIRE(e && B >= 0 && B <= e->max_B, AZ_EINVAL, "az_c4_eval_fwd: B=%d max_B=%d", B,
+             e ? e->max_B : 0);
+  if (B == 0) return AZ_OK;
+  AZ_REQUIRE(boards && e->feat, AZ_EINVAL, "az_c4_eval_fwd: null boards / feat");
+  int rc;
+  if (v) {
+    rc = az_c4_trunk_heads_fwd(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b,
+                               e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,
+                               e->feat, e->logp, pi, v, e->ws, e->ws_bytes, stream);
+  } else {
+    rc = az_c4_trunk_fwd(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b, e->feat,
+                         stream);
+  }
+  if (rc || !gv) return rc;
+  AZ_REQUIRE(e->ot0_w && e->ot0_b && e->ot2_w && e->ot2_b && e->hidden && e->y && e->glogp,
+             AZ_EINVAL, "az_c4_eval_fwd: GNN tail requested without its weights / scratch");
+  return az_transform_heads_fwd(e->feat, B, 3136, e->ot0_w, e->ot0_b, e->ot2_w, e->ot2_b,
+                                e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w,
+                                e->fc_value_b, e->hidden, e->y, e->glogp, gpi, gv, e->ws,
+                                e->ws_bytes, stream);
 }

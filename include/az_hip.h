@@ -45,6 +45,13 @@ int az_abi_version(void);
 const char* az_last_error(void);
 /* Checks that the current HIP device is a gfx950 (MI355X); returns AZ_OK or AZ_EDEVICE. */
 int az_check_device(void);
+/* Zero-copy host staging: fine-grained pinned host memory mapped at the same address on the
+ * device (a kernel may read / write it directly; host sees device stores after a stream
+ * synchronise).  Returns NULL on failure (az_last_error says why).  No reference counterpart:
+ * it replaces the .cpu() / torch.FloatTensor round trips of the batch-1 predict
+ * (connect4/Connect4GNN.py:59-84) with in-place reads and writes by the kernels. */
+void* az_host_alloc(size_t bytes);
+int az_host_free(void* p);
 
 /* ---------------------------------------------------------------------------------
  * Dense fp32 GEMM with fused epilogue:  C = epi(op(A) . op(B))     (MFMA 32x32x2 f32;
@@ -117,6 +124,39 @@ size_t az_heads_ws_bytes(int B, int K, int A);
 int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv, int B, int K,
                  const float* wp, const float* bp, int A, const float* wv, const float* bv,
                  float* logp, float* pi, float* v, void* ws, size_t ws_bytes, void* stream);
+
+/* Connect4 trunk and policy/value heads in one call: az_c4_trunk_fwd then az_heads_fwd on the
+ * feature rows (Connect4Net.py:42-60; Connect4GNN.py:48-57), bit-identical to that pair.  For
+ * B <= 32 and A <= 8 it is ONE launch (the heads read the features from the trunk's LDS tile);
+ * otherwise the two launches, with ws >= az_heads_ws_bytes(B, 3136, A).  feat [B][3136] is
+ * written either way; boards may be az_host_alloc memory (read in place). */
+int az_c4_trunk_heads_fwd(const int8_t* boards, int B, const float* conv1_w, const float* conv1_b,
+                          const float* conv2_w, const float* conv2_b, const float* wp,
+                          const float* bp, int A, const float* wv, const float* bv, float* feat,
+                          float* logp, float* pi, float* v, void* ws, size_t ws_bytes,
+                          void* stream);
+
+/* The whole Connect4 leaf evaluation of MCTS.search (MCTS.py:169-174 via Connect4GNN.py:59-120:
+ * predict and predict_with_gnn of the same boards) as ONE host call with direct launches:
+ * trunk + standard heads (az_c4_trunk_heads_fwd), then output_transform + heads on the same
+ * features (az_transform_heads_fwd).  Outputs are bit-identical to those calls.  Built for the
+ * batch-1 path, where a hipGraph replay costs more host time than these 4 launches. */
+typedef struct az_c4_eval {
+  const float* conv1_w; const float* conv1_b; const float* conv2_w; const float* conv2_b;
+  const float* fc_policy_w; const float* fc_policy_b; const float* fc_value_w;
+  const float* fc_value_b;
+  int A;                                   /* actions (fc_policy rows) */
+  const float* ot0_w; const float* ot0_b;  /* output_transform.0 [3136][3136], [3136] */
+  const float* ot2_w; const float* ot2_b;  /* output_transform.2; all four NULL: no GNN tail */
+  int max_B;                               /* capacity of the scratch below */
+  float* feat; float* hidden; float* y;    /* device [max_B][3136] each (hidden/y: GNN only) */
+  float* logp; float* glogp;               /* device [max_B][A] */
+  void* ws; size_t ws_bytes;               /* >= az_transform_heads_ws_bytes(max_B, 3136, A) */
+} az_c4_eval;
+/* v != NULL: standard heads into pi [B][A] (may be NULL) and v [B];  gv != NULL: the GNN tail
+ * into gpi / gv.  boards, pi, v, gpi, gv may be az_host_alloc memory. */
+int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, float* v,
+                   float* gpi, float* gv, void* stream);
 
 /* Per-row GNN evaluation tail: output_transform then the heads, i.e. gnn_utils.py:115 (in the
  * 1-row form of Connect4GNN.py:108-111, where the layers are the identity, gnn_utils.py:35-36)

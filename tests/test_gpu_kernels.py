@@ -43,7 +43,8 @@ def check_dot_error(got, ref, bound, tol=1e-6):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 3136, 3136), (3, 37, 64), (8, 128, 6272), (64, 128, 3136),
-                                   (512, 3136, 3136), (130, 70, 48), (4096, 256, 64)])
+                                   (512, 3136, 3136), (130, 70, 48), (4096, 256, 64),
+                                   (1, 7, 4096), (2, 1001, 260), (5, 300, 1024), (1, 33, 4100)])
 @pytest.mark.parametrize("act", [0, 1, 2])
 def test_linear_vs_torch(ops, M, N, K, act):
     g = torch.Generator().manual_seed(M * 7 + N + K + act)
@@ -145,6 +146,27 @@ def test_c4_trunk_and_heads_vs_oracle(ops):
     # golden reference outputs directly (batch-1 predict of the reference)
     np.testing.assert_allclose(pi.cpu().numpy()[:256], z["pi_b1"], atol=1e-5)
     np.testing.assert_allclose(v.cpu().numpy()[:256], z["v_b1"], atol=1e-5)
+
+
+@pytest.mark.parametrize("B", [1, 3, 32, 33, 100])
+def test_c4_trunk_heads_fused_bit_identical(ops, B):
+    """az_c4_trunk_heads_fwd (one launch for B <= 32) == az_c4_trunk_fwd + az_heads_fwd bit for
+    bit, and the oracle within 1e-5 (Connect4Net.py:42-60)."""
+    from oracle import nets as O
+    z = golden("c4_net.npz")
+    W = split_weights(z, "w/")
+    Wd = {k: cu(v) for k, v in W.items()}
+    boards = np.concatenate([z["boards"]] * 2)[:B]
+    f0 = ops.c4_trunk(cu(boards), Wd)
+    ref = ops.heads(f0, Wd["fc_policy.weight"], Wd["fc_policy.bias"], Wd["fc_value.weight"],
+                    Wd["fc_value.bias"])
+    f1, lp, pi, v = ops.c4_trunk_heads(cu(boards), Wd)
+    assert torch.equal(f0, f1)
+    for a, r in zip((lp, pi, v), ref):
+        assert torch.equal(a, r)
+    rlp, rv = O.c4_heads(O.c4_features(boards, W), W)
+    np.testing.assert_allclose(lp.cpu().numpy(), rlp, atol=1e-5)
+    np.testing.assert_allclose(v.cpu().numpy(), np.asarray(rv).reshape(-1), atol=1e-5)
 
 
 def test_c4_trunk_large_batches(ops):
@@ -360,3 +382,25 @@ def test_transform_heads_fused_equals_unfused(ops, B):
     olp, ov = O.c4_heads(O.policy_value_gnn_per_row(x.numpy(), G), W)
     assert np.abs(logp.cpu().numpy() - olp).max() < 1e-5
     assert np.abs(v.cpu().numpy() - ov).max() < 1e-5
+
+
+@pytest.mark.parametrize("A,K", [(8, 3136), (9, 512), (7, 256), (20, 1000)])
+def test_heads_small_batch_bit_identical(ops, A, K):
+    """B <= 32 runs the one-launch heads_rows_kernel; every row equals the two-launch path's
+    (the same rows inside a B = 64 batch) bit for bit, and the fp64 heads within 1e-5
+    (Connect4GNN.py:48-57)."""
+    g = torch.Generator().manual_seed(A * K)
+    x, y = torch.rand((64, K), generator=g) - 0.5, torch.rand((64, K), generator=g) - 0.5
+    wp, bp = (torch.rand((A, K), generator=g) - 0.5) / 8, torch.rand((A,), generator=g) - 0.5
+    wv, bv = (torch.rand((1, K), generator=g) - 0.5) / 8, torch.rand((1,), generator=g) - 0.5
+    args = [cu(t) for t in (wp, bp, wv, bv)]
+    ref = ops.heads(cu(x), *args, hv=cu(y))
+    lg = x.double() @ wp.double().T + bp.double()
+    lp64 = torch.log_softmax(lg, 1)
+    v64 = torch.tanh(y.double() @ wv.double().T + bv.double())[:, 0]
+    for B in (1, 5, 32):
+        got = ops.heads(cu(x[:B]), *args, hv=cu(y[:B]))
+        for a, r in zip(got, ref):
+            assert torch.equal(a, r[:B])
+        np.testing.assert_allclose(got[0].cpu().numpy(), lp64[:B].numpy(), atol=1e-5)
+        np.testing.assert_allclose(got[2].cpu().numpy(), v64[:B].numpy(), atol=1e-5)

@@ -89,8 +89,13 @@ def test_ttt3_all_positions_match_reference():
     np.testing.assert_allclose(v, z["v"], atol=TOL)
     np.testing.assert_allclose(gpi, z["pi_gnn"], atol=TOL)
     np.testing.assert_allclose(gv, z["v_gnn"], atol=TOL)
-    p1, v1 = w.predict_with_gnn(z["boards"][7].astype(np.int64))
-    np.testing.assert_allclose(p1, z["pi_gnn"][7], atol=TOL)
+    for i in (7, 100, 2500, 5477):      # batch-1 graph path (zero-copy host staging)
+        p1, v1 = w.predict_with_gnn(z["boards"][i].astype(np.int64))
+        np.testing.assert_allclose(p1, z["pi_gnn"][i], atol=TOL)
+        assert abs(float(v1) - float(z["v_gnn"][i])) <= TOL
+        p2, v2 = w.predict(z["boards"][i].astype(np.int64))
+        np.testing.assert_allclose(p2, z["pi"][i], atol=TOL)
+        assert abs(float(v2) - float(z["v"][i])) <= TOL
 
 
 def test_checkpoint_roundtrip_and_format(tmp_path, c4_wrapper):
@@ -281,3 +286,39 @@ def test_batch1_graph_equals_eager(c4_wrapper, monkeypatch):
     c4_wrapper.restore(snap)
     assert all(np.array_equal(a, b) for a, b in zip(g2, e2))
     assert not all(np.array_equal(a, b) for a, b in zip(g1, g2))
+
+
+def test_batch1_graph_zero_copy_equals_copy_path(c4_wrapper, monkeypatch):
+    """The zero-copy batch-1 graph (kernels read the board from / write pi, v into mapped host
+    memory) returns the bits of the H2D / D2H-copy graph, board after board (no stale reads),
+    and the reference's values."""
+    from azhip.wrappers import _Batch1Graph
+    z = golden("c4_gnn.npz")
+    monkeypatch.setenv("AZ_NO_ZEROCOPY", "0")
+    gz = _Batch1Graph(c4_wrapper, "both")
+    assert gz.host is not None
+    monkeypatch.setenv("AZ_NO_ZEROCOPY", "1")
+    gc = _Batch1Graph(c4_wrapper, "both")
+    assert gc.host is None
+    for i in list(range(0, 64, 3)) + [5, 5, 6, 5]:
+        b = z["boards"][i].astype(np.int64)
+        a, c = gz.run(b), gc.run(b)
+        assert np.array_equal(a, c), i
+        np.testing.assert_allclose(a[9:17], z["pi_gnn_b1"][i], atol=TOL)
+        assert abs(float(a[17]) - float(z["v_gnn_b1"][i])) <= TOL
+
+
+@pytest.mark.parametrize("kind", ["std", "gnn", "both"])
+def test_batch1_direct_equals_graph(c4_wrapper, kind):
+    """The one-call batch-1 path (az_c4_eval_fwd, zero-copy) returns the hipGraph path's bits
+    for every output kind, board after board."""
+    from azhip.wrappers import _Batch1Direct, _Batch1Graph
+    z = golden("c4_gnn.npz")
+    d, g = _Batch1Direct(c4_wrapper, kind), _Batch1Graph(c4_wrapper, kind)
+    for i in list(range(0, 64, 7)) + [3, 3, 4]:
+        b = z["boards"][i].astype(np.int64)
+        a, c = d.run(b), g.run(b)
+        assert np.array_equal(a, c), (kind, i)
+        if kind != "std":
+            k = 0 if kind == "gnn" else 9
+            np.testing.assert_allclose(a[k:k + 8], z["pi_gnn_b1"][i], atol=TOL)

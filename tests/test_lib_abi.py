@@ -53,7 +53,8 @@ def test_struct_layouts_match_header(built, tmp_path):
     cc = shutil.which("gcc") or shutil.which("cc")
     if cc is None:
         pytest.skip("no C compiler")
-    structs = {"az_gemm_desc": _lib.GemmDesc, "az_graph": _lib.Graph, "az_gnn_layer_w": _lib.LayerW}
+    structs = {"az_gemm_desc": _lib.GemmDesc, "az_graph": _lib.Graph, "az_gnn_layer_w": _lib.LayerW,
+               "az_c4_eval": _lib.C4Eval}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(){"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
