@@ -1,6 +1,5 @@
-"""c4_trunk GPU time at B = 1 / 512 / 4096 (50 launches in one hipGraph, event-timed); run
-under AZ_TRUNK_ABL=<bits> to time ablated variants (1 no conv2-weight loads, 2 no conv1,
-4 no conv2 MFMAs, 8 no feature store; results then wrong).  One JSON line."""
+"""c4_trunk GPU time at B = 1 / 512 / 4096 (50 launches in one hipGraph, event-timed).
+One JSON line."""
 import json
 import os
 import sys
@@ -14,7 +13,7 @@ from azhip import ops  # noqa: E402
 from azhip.weights import connect4_net_spec, synthetic_state_dict  # noqa: E402
 
 W = {k: torch.from_numpy(v).cuda() for k, v in synthetic_state_dict(connect4_net_spec(7), 1).items()}
-out = {"abl": os.environ.get("AZ_TRUNK_ABL", "0")}
+out = {}
 R = 50
 for B in (1, 512, 4096):
     boards = torch.from_numpy(np.random.default_rng(0).integers(-1, 2, (B, 7, 7)).astype(np.int8)).cuda()
