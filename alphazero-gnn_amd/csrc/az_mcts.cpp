@@ -329,6 +329,8 @@ struct Tree {
   std::vector<int32_t> N;
   std::vector<Val> Q;
   std::vector<uint8_t> V;
+  std::vector<int32_t> C;       // child node of each edge once known (-1): a descent follows
+                                // these instead of re-deriving and hashing every next state
   int32_t edges = 0;
   int32_t epoch = 1;
   // search state
@@ -348,6 +350,7 @@ struct Tree {
     N.clear();
     Q.clear();
     V.clear();
+    C.clear();
     edges = 0;
     epoch = 1;
     remaining = 0;
@@ -410,6 +413,7 @@ struct Tree {
     N.resize(N.size() + A, 0);
     Q.resize(Q.size() + A, Val{0.0, T_NONE});
     V.resize(V.size() + A, 0);
+    C.resize(C.size() + A, -1);
     R.valids(nd.key, &V[(size_t)nd.edge * A]);
   }
 };
@@ -479,10 +483,9 @@ void backup(az_mcts* m, Tree& t, Val v) {
 int advance(az_mcts* m, Tree& t) {
   while (t.remaining > 0 && t.pending_leaf < 0) {
     t.path.clear();
-    Key k = t.root;
+    int32_t id = t.find_or_add(t.root, m->R);
     Val v;
     for (;;) {
-      int32_t id = t.find_or_add(k, m->R);
       Node& nd = t.nodes[id];
       if (nd.es.x != 0.0) {                      // terminal (MCTS.py:152-157)
         v = nd.es;
@@ -499,9 +502,15 @@ int advance(az_mcts* m, Tree& t) {
         break;
       }
       t.path.emplace_back(id, a);
-      Key nk;
-      m->R.next(t.nodes[id].key, a, &nk);
-      k = nk;
+      const size_t e = (size_t)nd.edge * m->R.A + a;
+      int32_t child = t.C[e];
+      if (child < 0) {
+        Key nk;
+        m->R.next(nd.key, a, &nk);
+        child = t.find_or_add(nk, m->R);       // may grow t.nodes: nd is not used after this
+        t.C[e] = child;
+      }
+      id = child;
     }
     backup(m, t, v);
     t.remaining -= 1;
@@ -782,6 +791,65 @@ int az_mcts_episode_record(const az_mcts* m, int slot, int8_t* boards, int8_t* c
   std::memcpy(exp_tag, E.exp_tag.data(), n * A);
   *result_tag = E.result.tag == T_INT ? AZM_TAG_INT : AZM_TAG_FLOAT;
   *result = E.result.x;
+  return AZM_OK;
+}
+
+int az_mcts_episode_targets(const az_mcts* m, int slot, double* init_policy, double* exp_policy,
+                            int8_t* exp_value_tag, double* exp_value) {
+  if (!slot_ok(m, slot) || !init_policy || !exp_policy || !exp_value_tag || !exp_value)
+    return fail(AZM_EINVAL, "az_mcts_episode_targets: bad args");
+  const Episode& E = m->trees[slot].ep;
+  const int A = m->R.A;
+  std::vector<uint8_t> valid(A);
+  for (size_t i = 0; i < E.curs.size(); ++i) {
+    double* ip = init_policy + i * A;
+    double* xp = exp_policy + i * A;
+    const int32_t* inn = &E.init_nsa[i * A];
+    const int8_t* ih = &E.init_has[i * A];
+    const int32_t* xn = &E.exp_nsa[i * A];
+    const int8_t* xt = &E.exp_tag[i * A];
+    const double* xq = &E.exp_q[i * A];
+    // counts are integers: their float64 sums are exact in any order (np.sum's pairwise too)
+    double isum = 0.0;
+    for (int a = 0; a < A; ++a) {
+      ip[a] = ih[a] != AZM_TAG_NONE ? (double)inn[a] : 0.0;
+      isum += ip[a];
+    }
+    if (isum > 0) {
+      for (int a = 0; a < A; ++a) ip[a] /= isum;
+    } else {                                   // valids / np.sum(valids)
+      m->R.valids(E.boards[i], valid.data());
+      double vs = 0.0;
+      for (int a = 0; a < A; ++a) vs += valid[a];
+      for (int a = 0; a < A; ++a) ip[a] = (double)valid[a] / vs;
+    }
+    double esum = 0.0;
+    for (int a = 0; a < A; ++a) {
+      xp[a] = xt[a] != AZM_TAG_NONE ? (double)xn[a] : 0.0;
+      esum += xp[a];
+    }
+    if (esum > 0) {
+      for (int a = 0; a < A; ++a) xp[a] /= esum;
+    } else {
+      for (int a = 0; a < A; ++a) xp[a] = ip[a];
+    }
+    // expanded_value = sum(typed Q * N) / sum(N) over visited edges, else the root's value
+    Val ev = vint(0);
+    long cnt = 0;
+    for (int a = 0; a < A; ++a) {
+      if (xt[a] == AZM_TAG_NONE || xn[a] <= 0) continue;
+      const Val q{xq[a], xt[a] == AZM_TAG_INT ? T_INT : (xt[a] == AZM_TAG_FLOAT ? T_F64 : T_F32)};
+      ev = add(ev, mul_n(xn[a], q));
+      cnt += xn[a];
+    }
+    if (cnt > 0) {
+      ev = div_n(ev, cnt);
+    } else {
+      ev = {(double)E.std_v[i], T_F32};
+    }
+    exp_value_tag[i] = ev.tag == T_INT ? AZM_TAG_INT : (ev.tag == T_F64 ? AZM_TAG_FLOAT : AZM_TAG_F32);
+    exp_value[i] = ev.x;
+  }
   return AZM_OK;
 }
 

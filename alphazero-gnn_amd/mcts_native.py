@@ -55,6 +55,7 @@ _SIGS = {
     "az_mcts_episode_finished": (ctypes.c_int, [_P, _P, ctypes.c_int]),
     "az_mcts_episode_moves": (ctypes.c_int, [_P, ctypes.c_int]),
     "az_mcts_episode_record": (ctypes.c_int, [_P, ctypes.c_int] + [_P] * 13),
+    "az_mcts_episode_targets": (ctypes.c_int, [_P, ctypes.c_int] + [_P] * 4),
     "az_rng_test": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int,
                                    _P]),
     "az_rng_doubles": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, _P]),
@@ -77,7 +78,8 @@ def lib():
 
 
 def _ptr(a):
-    return a.ctypes.data        # a plain int is accepted for a c_void_p argument
+    # a plain int is accepted for a c_void_p argument (cheaper than a.ctypes.data)
+    return a.__array_interface__["data"][0]
 
 
 def _check(rc, what):
@@ -219,6 +221,15 @@ class Engine:
                                             ctypes.byref(tag), ctypes.byref(val)),
                "az_mcts_episode_record")
         r["result"] = int(val.value) if tag.value == TAG_INT else float(val.value)
+        if self.use_gnn:                 # expand_tree's targets per move, computed natively
+            t = {"init_policy": np.zeros((n, A), np.float64),
+                 "exp_policy": np.zeros((n, A), np.float64),
+                 "exp_value_tag": np.zeros(n, np.int8), "exp_value": np.zeros(n, np.float64)}
+            _check(lib().az_mcts_episode_targets(
+                self.h, slot, *[_ptr(t[k]) for k in ("init_policy", "exp_policy",
+                                                     "exp_value_tag", "exp_value")]),
+                "az_mcts_episode_targets")
+            r.update(t)
         return r
 
     def tree_stats(self, slot):
@@ -259,11 +270,45 @@ def expand_result(A, init_counts, initial_value, nsa, q, tag, game=None, board=N
     return initial_policy, initial_value, expanded_policy, expanded_value
 
 
+def _assemble_connect4(game, use_gnn, rec):
+    """assemble_episode for Connect4Game with whole-episode array operations.  The objects are
+    the generic path's: getSymmetries' identity comes first, so the GNN example's board is the
+    canonical board itself; the mirror is np.fliplr (a view) and mirror_pi np.copy of the pi
+    list (int64 for a temp-0 one-hot, float64 otherwise) with its first n entries reversed."""
+    n = game.board_size
+    boards = rec["boards"].astype(np.int64)
+    flips = boards[:, :, ::-1]
+    pis = rec["pi"]
+    one_hot = rec["temp"] == 0
+    mirror_f = pis.copy()
+    mirror_f[:, :n] = pis[:, n - 1::-1]
+    mirror_i = mirror_f.astype(np.int64)
+    curs = rec["cur"].tolist()
+    r = rec["result"]
+    last = -int(curs[-1])
+    std, gnn = [], []
+    for i, cur in enumerate(curs):
+        sg = r * ((-1) ** (cur != last))
+        if one_hot[i]:
+            pl, mp = pis[i].astype(np.int64).tolist(), mirror_i[i]
+        else:
+            pl, mp = pis[i].tolist(), mirror_f[i]
+        std.append((boards[i], pl, sg))
+        std.append((flips[i], mp, sg))
+        if use_gnn:
+            gnn.append((boards[i], cur, rec["init_policy"][i].copy(), np.float32(rec["std_v"][i]),
+                        rec["exp_policy"][i].copy(),
+                        typed_q(int(rec["exp_value_tag"][i]), rec["exp_value"][i]), sg))
+    return std, gnn
+
+
 def assemble_episode(game, args, rec):
     """Coach.executeEpisode's examples (Coach.py:27-79, the same steps as Coach.episode_g)
     from an engine episode record."""
     use_gnn = bool(args.get("use_gnn", False) if isinstance(args, dict)
                    else getattr(args, "use_gnn", False))
+    if type(game).__name__ == "Connect4Game" and (not use_gnn or "init_policy" in rec):
+        return _assemble_connect4(game, use_gnn, rec)
     A = game.getActionSize()
     examples, gnn_examples = [], []
     for i in range(len(rec["cur"])):
@@ -277,11 +322,16 @@ def assemble_episode(game, args, rec):
         examples.extend([b, cur, p, None] for b, p in sym)
         if use_gnn:
             s = game.stringRepresentation(canonical)
-            init_counts = {a: int(rec["init_nsa"][i][a]) for a in range(A)
-                           if rec["init_has"][i][a] != TAG_NONE}
-            res = expand_result(A, init_counts, np.float32(rec["std_v"][i]),
-                                rec["exp_nsa"][i].tolist(), rec["exp_q"][i].tolist(),
-                                rec["exp_tag"][i].tolist(), game, canonical)
+            if "init_policy" in rec:     # az_mcts_episode_targets (same values and types)
+                res = (rec["init_policy"][i].copy(), np.float32(rec["std_v"][i]),
+                       rec["exp_policy"][i].copy(),
+                       typed_q(int(rec["exp_value_tag"][i]), rec["exp_value"][i]))
+            else:
+                init_counts = {a: int(rec["init_nsa"][i][a]) for a in range(A)
+                               if rec["init_has"][i][a] != TAG_NONE}
+                res = expand_result(A, init_counts, np.float32(rec["std_v"][i]),
+                                    rec["exp_nsa"][i].tolist(), rec["exp_q"][i].tolist(),
+                                    rec["exp_tag"][i].tolist(), game, canonical)
             for b, _ in sym:
                 if game.stringRepresentation(b) == s:
                     gnn_examples.append([b, cur, *res, None])

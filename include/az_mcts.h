@@ -104,6 +104,13 @@ int az_mcts_episode_record(const az_mcts* m, int slot, int8_t* boards, int8_t* c
                            int8_t* temps, int32_t* actions, double* pi, int32_t* init_nsa,
                            int8_t* init_has, float* std_v, int32_t* exp_nsa, double* exp_q,
                            int8_t* exp_tag, int* result_tag, double* result);
+/* expand_tree's training targets of every recorded move of a finished episode (MCTS.py:115-146,
+ * what Coach keeps as a GNN example): initial_policy and expanded_policy [n][A] (float64), and
+ * expanded_value with its Python/NumPy type (AZM_TAG_INT / _FLOAT / _F32; the running sum and
+ * the division follow the same NEP 50 promotions as the search's Q update).  A move whose root
+ * had no visits before expansion gets valids / sum(valids). */
+int az_mcts_episode_targets(const az_mcts* m, int slot, double* init_policy, double* exp_policy,
+                            int8_t* exp_value_tag, double* exp_value);
 /* np.random.RandomState emulation, for tests: op 0 = n raw uint32 draws, 1 = n x randint(0, np_),
  * 2 = n x choice(np_, p=p); az_rng_doubles = n x random_sample(). */
 int az_rng_test(uint32_t seed, int op, int n, const double* p, int np_, int64_t* out);
