@@ -38,6 +38,101 @@ class PendingPrediction:
         return out[:, :A], out[:, A], None, None
 
 
+class _PendingDirect:
+    """A batched Connect4 prediction queued by _DirectBatch: the kernels write pi / v straight
+    into mapped host memory; result() waits for the event and copies them out."""
+
+    def __init__(self, entry, views, event, n):
+        # entry: the ring entry (its HostBuffer stays alive and reserved until result())
+        self.entry, self.views, self.event, self.n = entry, views, event, n
+        entry["busy"] = True
+
+    def result(self):
+        self.event.synchronize()
+        n = self.n
+        pi, v, gpi, gv = (None if a is None else a.numpy()[:n].copy() for a in self.views)
+        self.entry["busy"] = False
+        return pi, v, gpi, gv
+
+    def __del__(self):
+        # dropped unread: the entry is free again once the device is done with it
+        if self.entry.get("busy"):
+            self.event.synchronize()
+            self.entry["busy"] = False
+
+
+class _DirectBatch:
+    """Batched predict_both / predict_batch for the 7x7 Connect4Net as ONE az_c4_eval_fwd call
+    per batch (trunk + heads [+ output_transform + heads]): boards are read from and outputs
+    written to mapped host memory (ops.HostBuffer, a ring of `depth` so that several batches can
+    be in flight), device scratch is shared (the stream orders the batches).  Replaces ~10
+    torch-level launches, a pinned H2D and a D2H copy per lock-step round."""
+
+    def __init__(self, w):
+        self.w, self.cap, self.ring = w, 0, []
+        self.fn = _lib.lib().az_c4_eval_fwd
+
+    def _grow(self, n):
+        w, dev, A, F = self.w, self.w.device, self.w.action_size, 3136
+        cap = max(1024, 1 << (int(n) - 1).bit_length())
+        torch.cuda.synchronize(dev)               # in-flight batches may use the old scratch
+        self.feat = torch.empty((cap, F), device=dev)
+        self.hidden = torch.empty((cap, F), device=dev)
+        self.y = torch.empty((cap, F), device=dev)
+        self.logp = torch.empty((cap, A), device=dev)
+        self.glogp = torch.empty((cap, A), device=dev)
+        L = _lib.lib()
+        nb = max(int(L.az_transform_heads_ws_bytes(cap, F, A)), int(L.az_heads_ws_bytes(cap, F, A)))
+        self.ws = torch.empty((nb,), dtype=torch.uint8, device=dev)
+        W, G = w.nnet.params, w.gnn.params
+        P = lambda t: t.data_ptr()  # noqa: E731
+        self.desc = _lib.C4Eval(
+            P(W["conv1.weight"]), P(W["conv1.bias"]), P(W["conv2.weight"]), P(W["conv2.bias"]),
+            P(W["fc_policy.weight"]), P(W["fc_policy.bias"]), P(W["fc_value.weight"]),
+            P(W["fc_value.bias"]), A, P(G["output_transform.0.weight"]),
+            P(G["output_transform.0.bias"]), P(G["output_transform.2.weight"]),
+            P(G["output_transform.2.bias"]), cap, P(self.feat), P(self.hidden), P(self.y),
+            P(self.logp), P(self.glogp), P(self.ws), self.ws.numel())
+        self.ring = []        # entries still held by unread predictions keep their buffers
+        self.cap = cap
+
+    def _entry(self):
+        """A host staging set no unread prediction holds (a new one when all are held)."""
+        for e in self.ring:
+            if not e["busy"]:
+                return e
+        w, cap, A = self.w, self.cap, self.w.action_size
+        off = [0, (cap * w.board_x * w.board_y + 255) // 256 * 256]
+        for k in (A, 1, A, 1):
+            off.append(off[-1] + (4 * cap * k + 255) // 256 * 256)
+        hb = ops.HostBuffer(off[-1])
+        e = {"busy": False, "hb": hb,
+             "in": hb.view(0, torch.int8, (cap, w.board_x, w.board_y)),
+             "out": [hb.view(off[1 + j], torch.float32, (cap, k) if k > 1 else (cap,))
+                     for j, k in enumerate((A, 1, A, 1))]}
+        self.ring.append(e)
+        return e
+
+    def launch(self, boards, both):
+        boards = np.asarray(boards)
+        n = boards.shape[0]
+        if n > self.cap:
+            self._grow(n)
+        e = self._entry()
+        hin, outs = e["in"], e["out"]
+        hin.numpy()[:n] = boards
+        pi, v, gpi, gv = outs if both else (outs[0], outs[1], None, None)
+        s = torch.cuda.current_stream(self.w.device)
+        P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        rc = self.fn(ctypes.byref(self.desc), ctypes.c_void_p(hin.data_ptr()), n, P(pi), P(v),
+                     P(gpi), P(gv), ctypes.c_void_p(s.cuda_stream))
+        if rc:
+            _lib.check(rc, "az_c4_eval_fwd")
+        ev = torch.cuda.Event()
+        ev.record(s)
+        return _PendingDirect(e, (pi, v, gpi, gv), ev, n)
+
+
 class _PinnedRing:
     """Pinned host staging buffers reused round-robin (`depth` predictions in flight)."""
 
@@ -280,6 +375,12 @@ class NetWrapper:
 
     def _launch(self, boards, both):
         """Queue a batched prediction; returns a PendingPrediction (see predict_*_async)."""
+        if self.has_gnn and _direct_ok(self) and len(boards) > 0:
+            if getattr(self, "_direct", None) is None:
+                self._direct = _DirectBatch(self)
+            self.nnet.eval()
+            self.gnn.eval()
+            return self._direct.launch(boards, both)
         if not hasattr(self, "_ring"):
             self._ring = _PinnedRing()
         boards = np.asarray(boards)

@@ -322,3 +322,23 @@ def test_batch1_direct_equals_graph(c4_wrapper, kind):
         if kind != "std":
             k = 0 if kind == "gnn" else 9
             np.testing.assert_allclose(a[k:k + 8], z["pi_gnn_b1"][i], atol=TOL)
+
+
+def test_direct_batch_async_equals_predict_both(c4_wrapper):
+    """The lock-step rounds' batched call (predict_both_async -> az_c4_eval_fwd, zero-copy ring
+    of host buffers, scratch grown on demand) returns predict_both's bits, several batches in
+    flight at once, and predict_batch_async the standard half."""
+    z1, z2 = golden("c4_net.npz"), golden("c4_gnn.npz")
+    boards = np.concatenate([z1["boards"], z2["boards"]] * 8).astype(np.int64)   # 2560
+    pend = [(n, c4_wrapper.predict_both_async(boards[:n])) for n in (1, 33, 300, 2560, 7)]
+    pstd = c4_wrapper.predict_batch_async(boards[:300])
+    for n, p in pend:
+        ref = c4_wrapper.predict_both(boards[:n])
+        got = p.result()
+        for a, b in zip(got, ref):
+            assert np.array_equal(a, b), n
+    pi, v, gpi, gv = pstd.result()
+    assert gpi is None and gv is None
+    ref = c4_wrapper.predict_both(boards[:300])
+    assert np.array_equal(pi, ref[0]) and np.array_equal(v, ref[1])
+    np.testing.assert_allclose(pend[2][1].result()[2][256:], z2["pi_gnn_b1"][:44], atol=TOL)
