@@ -83,6 +83,8 @@ double pairwise(const double* a, long n) {
 }
 
 // ----------------------------------------------------------------------------- rules
+constexpr int kMaxA = 65;   // actions: n*n + 1 with n*n <= 64 cells
+
 struct Key {
   uint64_t p, q;   // bit i = cell i (i = x*n + y) holds +1 / -1
   bool operator==(const Key& o) const { return p == o.p && q == o.q; }
@@ -320,17 +322,23 @@ struct Node {
   uint8_t has_ns, expanded;
 };
 
+// One edge (s, a): prior, typed Q, visit count, child node, valid flag -- packed so that a
+// node's A edges are one contiguous run of cache lines (a descent touches them together).
+struct Edge {
+  double P;
+  double qx;       // Q value (qtag == T_NONE: no Qsa entry yet)
+  int32_t N;
+  int32_t C;       // child node once known (-1): a descent follows it instead of re-deriving
+                   // and hashing the next state
+  uint8_t qtag;
+  uint8_t V;       // valid move
+};
+
 struct Tree {
   std::vector<Node> nodes;
   std::vector<int32_t> table;   // open addressing, -1 = empty
   uint64_t mask = 0;
-  // edge pools, A entries per allocated node
-  std::vector<double> P;
-  std::vector<int32_t> N;
-  std::vector<Val> Q;
-  std::vector<uint8_t> V;
-  std::vector<int32_t> C;       // child node of each edge once known (-1): a descent follows
-                                // these instead of re-deriving and hashing every next state
+  std::vector<Edge> EP;         // edge pool, A entries per allocated node
   int32_t edges = 0;
   int32_t epoch = 1;
   // search state
@@ -346,11 +354,7 @@ struct Tree {
     nodes.clear();
     table.assign(1024, -1);
     mask = 1023;
-    P.clear();
-    N.clear();
-    Q.clear();
-    V.clear();
-    C.clear();
+    EP.clear();
     edges = 0;
     epoch = 1;
     remaining = 0;
@@ -409,12 +413,11 @@ struct Tree {
     if (nd.edge >= 0) return;
     nd.edge = edges++;
     size_t A = R.A;
-    P.resize(P.size() + A, 0.0);
-    N.resize(N.size() + A, 0);
-    Q.resize(Q.size() + A, Val{0.0, T_NONE});
-    V.resize(V.size() + A, 0);
-    C.resize(C.size() + A, -1);
-    R.valids(nd.key, &V[(size_t)nd.edge * A]);
+    EP.resize(EP.size() + A, Edge{0.0, 0.0, 0, -1, T_NONE, 0});
+    uint8_t v[kMaxA];
+    R.valids(nd.key, v);
+    Edge* e = &EP[(size_t)nd.edge * A];
+    for (size_t a = 0; a < A; ++a) e[a].V = v[a];
   }
 };
 
@@ -443,13 +446,13 @@ int select_action(const az_mcts* m, const Tree& t, const Node& nd) {
   double best = -INFINITY;
   int ba = -1;
   for (int a = 0; a < A; ++a) {
-    if (!t.V[o + a]) continue;
-    const Val& q = t.Q[o + a];
+    const Edge& ed = t.EP[o + a];
+    if (!ed.V) continue;
     double u;
-    if (q.tag != T_NONE)
-      u = q.x + m->cpuct * t.P[o + a] * sq / (double)(1 + t.N[o + a]);
+    if (ed.qtag != T_NONE)
+      u = ed.qx + m->cpuct * ed.P * sq / (double)(1 + ed.N);
     else
-      u = m->cpuct * t.P[o + a] * sq_eps;
+      u = m->cpuct * ed.P * sq_eps;
     if (u > best) {
       best = u;
       ba = a;
@@ -464,13 +467,16 @@ void backup(az_mcts* m, Tree& t, Val v) {
     Node& nd = t.nodes[t.path[i].first];
     int a = t.path[i].second;
     size_t e = (size_t)nd.edge * A + a;
-    Val& q = t.Q[e];
-    if (q.tag != T_NONE) {
-      q = div_n(add(mul_n(t.N[e], q), v), (long)t.N[e] + 1);
-      t.N[e] += 1;
+    Edge& ed = t.EP[e];
+    if (ed.qtag != T_NONE) {
+      const Val q = div_n(add(mul_n(ed.N, Val{ed.qx, ed.qtag}), v), (long)ed.N + 1);
+      ed.qx = q.x;
+      ed.qtag = q.tag;
+      ed.N += 1;
     } else {
-      q = v;
-      t.N[e] = 1;
+      ed.qx = v.x;
+      ed.qtag = v.tag;
+      ed.N = 1;
     }
     t.nsa_total += 1;
     nd.ns += 1;
@@ -503,12 +509,12 @@ int advance(az_mcts* m, Tree& t) {
       }
       t.path.emplace_back(id, a);
       const size_t e = (size_t)nd.edge * m->R.A + a;
-      int32_t child = t.C[e];
+      int32_t child = t.EP[e].C;
       if (child < 0) {
         Key nk;
         m->R.next(nd.key, a, &nk);
         child = t.find_or_add(nk, m->R);       // may grow t.nodes: nd is not used after this
-        t.C[e] = child;
+        t.EP[e].C = child;
       }
       id = child;
     }
@@ -523,9 +529,10 @@ void expand(az_mcts* m, Tree& t, const float* pi, float v_std, const float* gpi,
             bool failed) {
   const int A = m->R.A;
   Node& nd = t.nodes[t.pending_leaf];
-  const size_t o = (size_t)nd.edge * A;
-  double* P = &t.P[o];
-  const uint8_t* V = &t.V[o];
+  Edge* ed = &t.EP[(size_t)nd.edge * A];
+  double P[kMaxA];
+  uint8_t V[kMaxA];
+  for (int a = 0; a < A; ++a) V[a] = ed[a].V;
   Val v;
   auto uniform = [&]() {
     long cnt = 0;
@@ -548,6 +555,7 @@ void expand(az_mcts* m, Tree& t, const float* pi, float v_std, const float* gpi,
     }
     v = {(double)(m->use_gnn ? gv : v_std), T_F32};
   }
+  for (int a = 0; a < A; ++a) ed[a].P = P[a];
   nd.expanded = 1;
   nd.has_ns = 1;
   nd.ns = 0;
@@ -570,9 +578,10 @@ void root_snapshot(const az_mcts* m, const Tree& t, const Key& root, int32_t* ns
   if (id < 0 || t.nodes[id].edge < 0) return;
   const size_t o = (size_t)t.nodes[id].edge * A;
   for (int a = 0; a < A; ++a) {
-    const Val& v = t.Q[o + a];
-    if (v.tag == T_NONE) continue;
-    nsa[a] = t.N[o + a];
+    const Edge& ed = t.EP[o + a];
+    if (ed.qtag == T_NONE) continue;
+    const Val v{ed.qx, ed.qtag};
+    nsa[a] = ed.N;
     if (q) q[a] = v.x;
     tag[a] = v.tag == T_INT ? AZM_TAG_INT : (v.tag == T_F64 ? AZM_TAG_FLOAT : AZM_TAG_F32);
   }
@@ -985,11 +994,11 @@ int az_mcts_root_edges(const az_mcts* m, int slot, const int8_t* board, int32_t*
   if (id < 0 || t.nodes[id].edge < 0) return AZM_OK;
   size_t o = (size_t)t.nodes[id].edge * A;
   for (int a = 0; a < A; ++a) {
-    const Val& v = t.Q[o + a];
-    if (v.tag == T_NONE) continue;
-    nsa[a] = t.N[o + a];
-    q[a] = v.x;
-    qtag[a] = v.tag == T_INT ? AZM_TAG_INT : (v.tag == T_F64 ? AZM_TAG_FLOAT : AZM_TAG_F32);
+    const Edge& ed = t.EP[o + a];
+    if (ed.qtag == T_NONE) continue;
+    nsa[a] = ed.N;
+    q[a] = ed.qx;
+    qtag[a] = ed.qtag == T_INT ? AZM_TAG_INT : (ed.qtag == T_F64 ? AZM_TAG_FLOAT : AZM_TAG_F32);
   }
   return AZM_OK;
 }
