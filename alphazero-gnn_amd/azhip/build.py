@@ -36,7 +36,7 @@ def hipcc():
 def _compile(src):
     obj = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
     s = os.path.join(CSRC, src)
-    deps = [s, os.path.join(CSRC, "az_common.h"),
+    deps = [s, os.path.join(CSRC, "az_common.h"), os.path.join(CSRC, "az_heads.h"),
             os.path.join(os.path.dirname(PKG), "include", "az_hip.h")]
     if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj

@@ -15,6 +15,7 @@
 #include <type_traits>
 
 #include "az_common.h"
+#include "az_heads.h"
 
 namespace az {
 
@@ -930,10 +931,9 @@ __global__ __launch_bounds__(256) void gemv_f32(GemmArgs p) {
 // re-read the row start and meet zeros in the staged A; rows past N are clamped to row 0 and
 // never stored.
 template <int MR, int S, int R>
-__global__ __launch_bounds__(256) void gemv_full(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) float As[MR * S * 256];
+__device__ __forceinline__ void gemv_full_block(const GemmArgs& p, int bid, float* As) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n_base = (blockIdx.x * 4 + wave) * R;
+  const int n_base = (bid * 4 + wave) * R;
   f32x4 w[R][S];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -984,6 +984,29 @@ __global__ __launch_bounds__(256) void gemv_full(GemmArgs p) {
   if (lane < MR * R) {
     const int m = lane / R, r = lane % R;
     if (m < p.M && n_base + r < p.N) epilogue_store(p, m, n_base + r, mine);
+  }
+}
+
+template <int MR, int S, int R>
+__global__ __launch_bounds__(256) void gemv_full(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) float As[MR * S * 256];
+  gemv_full_block<MR, S, R>(p, blockIdx.x, As);
+}
+
+// gemv_full (M = 1) plus B extra blocks that run the policy/value heads of rows of `side.x` --
+// the batch-1 leaf's standard heads ride along with output_transform.0 instead of lengthening
+// the launch chain (they only need the trunk's features, which the GEMV reads too).
+template <int S, int R>
+__global__ __launch_bounds__(256) void gemv_side_heads(GemmArgs p, SideHeads h, int nblk) {
+  __shared__ __attribute__((aligned(16))) float As[S * 256];
+  __shared__ float part[HEADS_ROWS_MAXC * 9];
+  __shared__ float sm[9];
+  if ((int)blockIdx.x < nblk) {
+    gemv_full_block<1, S, R>(p, blockIdx.x, As);
+  } else {
+    const int row = blockIdx.x - nblk;
+    heads_row_block<8, 4>(h.x + (size_t)row * h.ldx, h.x + (size_t)row * h.ldx, h.K, h.wp, h.A,
+                          h.wv, h.bp, h.bv, row, h.logp, h.pi, h.v, part, sm);
   }
 }
 
@@ -1180,6 +1203,14 @@ static int splits_256x128(int M, int N, int K, size_t ws_bytes) {
   return S;
 }
 
+// True when the 256x128 grid is >= 4 rounds of one block per CU and its last round is >= 95 %
+// full (wave quantisation otherwise costs the 8-wave tile its edge: M = 8,192 / 16,384).
+static bool full_waves_256x128(int M, int N) {
+  const long tiles = (long)((M + 255) / 256) * ((N + 127) / 128);
+  const long rounds = (tiles + 255) / 256;
+  return rounds >= 4 && (double)tiles / (double)(rounds * 256) >= 0.95;
+}
+
 // The GEMM without its split-K reduction: when the plan splits K, the raw partial sums are left
 // in d->ws as slabs [*splits_out][M][N] and C is NOT written (the caller reduces them, e.g.
 // fused with its consumer: az_transform_heads_fwd); otherwise C is written and *splits_out = 1.
@@ -1243,6 +1274,10 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
     // 256x128 tile, 8 waves, one block per CU, K split so the grid fills >= 90 % of the CUs
     // (tools/gemm_sweep.py glds on MI355X, M = 512: 106 us vs 113 us for 128x128 x 5)
     cfg = 24;
+  } else if (glds_ok && d->N >= 1024 && d->K >= 1024 && full_waves_256x128(d->M, d->N)) {
+    // large M whose 256x128 grid is (nearly) whole rounds of 256 blocks: the 8-wave tile's
+    // steady state wins (tools/gemm_sweep.py bigm, M = 65,536: 130 vs 109 TFLOP/s for 128x64)
+    cfg = 24;
   } else if (glds_ok && d->M > 128) {
     // LDS-DMA tiles (tools/gemm_sweep.py glds on MI355X): 128x64 once the grid fills the chip,
     // 128x128 + split-K below that
@@ -1283,6 +1318,30 @@ int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s) {
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, a);
   return check_launch("splitk_reduce_kernel");
+}
+
+// gemv_side_heads for the batch-1 leaf: d must be M = 1 with K-major operands, a plain
+// bias/activation epilogue and 3072 < K <= 3328 (output_transform.0 at F = 3136), and h at most
+// 8 actions; returns 1 when launched, 0 when the shapes do not qualify (nothing launched), or
+// a negative AZ_E* code.
+int gemv1_with_side_heads(const az_gemm_desc* d, const SideHeads* h, hipStream_t s) {
+  if (!(d->M == 1 && d->a_kmajor && d->b_kmajor && !d->A2 && !d->a_rows && !d->C2 && !d->R &&
+        !d->G && d->act != AZ_ACT_DRELU && d->K > 3072 && d->K <= 3328 && d->K % 4 == 0 &&
+        d->lda % 4 == 0 && d->ldb % 4 == 0 && aligned16(d->A) && aligned16(d->B) &&
+        h->A >= 1 && h->A <= 8 && h->K % 4 == 0 && h->ldx % 4 == 0 &&
+        (h->K + HEADS_KC - 1) / HEADS_KC <= HEADS_ROWS_MAXC && aligned16(h->x) &&
+        aligned16(h->wp) && aligned16(h->wv)))
+    return 0;
+  GemmArgs a = {};
+  a.M = 1; a.N = d->N; a.K = d->K;
+  a.A = d->A; a.lda = d->lda; a.K0 = d->K;
+  a.B = d->B; a.ldb = d->ldb;
+  a.bias = d->bias; a.act = d->act; a.beta = d->beta; a.C = d->C; a.ldc = d->ldc;
+  a.splits = 1; a.kc = d->K;
+  const int nblk = (a.N + 4 * 2 - 1) / (4 * 2);
+  hipLaunchKernelGGL((gemv_side_heads<13, 2>), dim3(nblk + h->B), dim3(256), 0, s, a, *h, nblk);
+  const int rc = check_launch("gemv_side_heads");
+  return rc == AZ_OK ? 1 : rc;
 }
 
 int gemm_f32(const az_gemm_desc* d, hipStream_t s) {

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include "az_common.h"
+#include "az_heads.h"
 
 namespace az {
 
@@ -199,7 +200,6 @@ __global__ __launch_bounds__(256) void conv3x3_relu_kernel(const void* __restric
 //     one float4 column slice of the chunk and keeps the A+1 weight slices for it in VGPRs;
 //     every wave sweeps rows, reduces its 64 lanes and writes part[c][row][0..A].
 //  2. heads_finalize_kernel: sum the chunks in order, add biases, log_softmax / exp / tanh.
-constexpr int HEADS_KC = 256;        // K columns per chunk (64 lanes x float4)
 constexpr int HEADS_ROWS = 16;       // rows per block (4 per wave)
 
 template <int AMAX>
@@ -381,93 +381,6 @@ __global__ __launch_bounds__(256) void heads_finalize_kernel(const float* __rest
 // the finalize arithmetic of heads_finalize_kernel follows in the same block -- so logp, pi and v
 // are bit-identical to the two-launch path, minus one launch and the partials' HBM round trip.
 constexpr int HEADS_ROWS_MAXB = 32;
-constexpr int HEADS_ROWS_MAXC = 64;   // K <= 16384
-
-// One row's heads with all 512 threads of the block: xr / yr may point into LDS (the fused
-// trunk) or HBM; part is [HEADS_ROWS_MAXC][AMAX+1] and sm [AMAX+1] floats of LDS.  Ends with a
-// barrier, so the caller may reuse part / sm for the next row.
-template <int AMAX>
-__device__ __forceinline__ void heads_row_block(const float* xr, const float* yr, int K,
-                                                const float* __restrict__ wp, int A,
-                                                const float* __restrict__ wv,
-                                                const float* __restrict__ bp,
-                                                const float* __restrict__ bv, int row,
-                                                float* __restrict__ logp, float* __restrict__ pi,
-                                                float* __restrict__ v, float* part, float* sm) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nchunks = (K + HEADS_KC - 1) / HEADS_KC;
-  constexpr int LOGV = AMAX == 8 ? 3 : (AMAX == 16 ? 4 : 5);
-  constexpr int PW = AMAX + 1;
-  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  for (int c0 = wave; c0 < nchunks; c0 += 16) {
-    f32x4 xs[2], ys[2], w[2][AMAX + 1];
-    bool kin[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = min(c0 + 8 * j, nchunks - 1);
-      const int k = c * HEADS_KC + lane * 4;
-      kin[j] = k < K;
-      const int kc = kin[j] ? k : 0;
-      xs[j] = *reinterpret_cast<const f32x4*>(xr + kc);
-      ys[j] = *reinterpret_cast<const f32x4*>(yr + kc);
-#pragma unroll
-      for (int a = 0; a < AMAX; ++a)
-        w[j][a] = *reinterpret_cast<const f32x4*>(wp + (size_t)min(a, A - 1) * K + kc);
-      w[j][AMAX] = *reinterpret_cast<const f32x4*>(wv + kc);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = c0 + 8 * j;
-      if (c >= nchunks) break;
-#pragma unroll
-      for (int a = 0; a < AMAX; ++a) w[j][a] = (a < A && kin[j]) ? w[j][a] : z;
-      w[j][AMAX] = kin[j] ? w[j][AMAX] : z;
-      const f32x4 x = kin[j] ? xs[j] : z, y = kin[j] ? ys[j] : z;
-      float pv[AMAX];
-#pragma unroll
-      for (int a = 0; a < AMAX; ++a)
-        pv[a] = fmaf(x[3], w[j][a][3], fmaf(x[2], w[j][a][2], fmaf(x[1], w[j][a][1], x[0] * w[j][a][0])));
-      const float ps = wave_multi_sum<AMAX>(pv);
-      const float vs = wave_sum(fmaf(y[3], w[j][AMAX][3], fmaf(y[2], w[j][AMAX][2],
-                                fmaf(y[1], w[j][AMAX][1], y[0] * w[j][AMAX][0]))));
-      const int a = lane >> (6 - LOGV);
-      if ((lane & ((1 << (6 - LOGV)) - 1)) == 0 && a < A) part[c * PW + a] = ps;
-      if (lane == 0) part[c * PW + A] = vs;
-    }
-  }
-  __syncthreads();
-  const int W = A + 1;
-  if (threadIdx.x < W) {
-    float s = 0.f;
-    for (int c = 0; c < nchunks; ++c) s += part[c * PW + threadIdx.x];
-    sm[threadIdx.x] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float l[AMAX];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int a = 0; a < AMAX; ++a)
-      if (a < A) {
-        l[a] = sm[a] + bp[a];
-        mx = fmaxf(mx, l[a]);
-      }
-    float se = 0.f;
-#pragma unroll
-    for (int a = 0; a < AMAX; ++a)
-      if (a < A) se += expf(l[a] - mx);
-    const float lse = logf(se);
-#pragma unroll
-    for (int a = 0; a < AMAX; ++a)
-      if (a < A) {
-        const float o = (l[a] - mx) - lse;
-        logp[(size_t)row * A + a] = o;
-        if (pi) pi[(size_t)row * A + a] = expf(o);
-      }
-    v[row] = tanhf(sm[A] + bv[0]);
-  }
-  __syncthreads();
-}
 
 template <int AMAX>
 __global__ __launch_bounds__(512) void heads_rows_kernel(
@@ -478,7 +391,7 @@ __global__ __launch_bounds__(512) void heads_rows_kernel(
   __shared__ float part[HEADS_ROWS_MAXC * (AMAX + 1)];
   __shared__ float sm[AMAX + 1];
   const int row = blockIdx.x;
-  heads_row_block<AMAX>(hp + (size_t)row * ldhp, hv + (size_t)row * ldhv, K, wp, A, wv, bp, bv,
+  heads_row_block<AMAX, 8>(hp + (size_t)row * ldhp, hv + (size_t)row * ldhv, K, wp, A, wv, bp, bv,
                         row, logp, pi, v, part, sm);
 }
 
@@ -499,7 +412,7 @@ __global__ __launch_bounds__(512) void c4_trunk_heads_kernel(
   c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, ob);
   const int b0 = blockIdx.x * NB, nb = min(NB, B - b0);
   for (int b = 0; b < nb; ++b)
-    heads_row_block<8>(ob + b * 3136, ob + b * 3136, 3136, wp, A, wv, bp, bv, b0 + b, logp, pi, v,
+    heads_row_block<8, 8>(ob + b * 3136, ob + b * 3136, 3136, wp, A, wv, bp, bv, b0 + b, logp, pi, v,
                        part, sm);
 }
 
@@ -560,6 +473,7 @@ extern "C" int az_conv3x3_relu_fwd(const void* in, int in_int8, int B, int Cin, 
 }
 
 namespace az {
+int gemv1_with_side_heads(const az_gemm_desc* d, const SideHeads* h, hipStream_t s);
 int gemm_f32(const az_gemm_desc* d, hipStream_t s);
 int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out);
 int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s);
@@ -735,6 +649,28 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
   if (B == 0) return AZ_OK;
   AZ_REQUIRE(boards && e->feat, AZ_EINVAL, "az_c4_eval_fwd: null boards / feat");
   int rc;
+  static const bool side = getenv("AZ_EVAL_NO_SIDE") == nullptr;   // A/B experiments
+  if (B == 1 && v && gv && side && e->ot0_w && e->hidden && e->y && e->glogp) {
+    // batch 1: the standard heads ride along with output_transform.0 (extra blocks of the same
+    // launch, off the trunk -> GEMV -> GEMV -> heads chain); same kernels' arithmetic, same bits
+    if ((rc = az_c4_trunk_fwd(boards, 1, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b, e->feat,
+                              stream)))
+      return rc;
+    az_gemm_desc d = {};
+    d.M = 1; d.N = 3136; d.K = 3136;
+    d.A = e->feat; d.lda = 3136; d.a_kmajor = 1;
+    d.B = e->ot0_w; d.ldb = 3136; d.b_kmajor = 1; d.bias = e->ot0_b; d.act = AZ_ACT_RELU;
+    d.C = e->hidden; d.ldc = 3136;
+    const SideHeads h = {e->feat, 3136, 3136, 1, e->fc_policy_w, e->fc_policy_b, e->A,
+                         e->fc_value_w, e->fc_value_b, e->logp, pi, v};
+    rc = gemv1_with_side_heads(&d, &h, as_stream(stream));
+    if (rc < 0) return rc;
+    if (rc == 1)
+      return az_linear_heads_fwd(e->hidden, 1, 3136, e->ot2_w, e->ot2_b, e->fc_policy_w,
+                                 e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b, e->y,
+                                 e->glogp, gpi, gv, e->ws, e->ws_bytes, stream);
+    // shapes not covered: the general sequence below (re-runs the trunk, harmless)
+  }
   if (v) {
     rc = az_c4_trunk_heads_fwd(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b,
                                e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,

@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-selfplay", action="store_true")
     ap.add_argument("--no-grid", action="store_true", help="skip the config-5 forward leg")
     ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--large-batch", type=int, default=65536,
+                    help="extra leg at this batch (SURVEY §8d config 2); 0 = skip")
     ap.add_argument("--sp-games", type=int, default=2048,
                     help="self-play leg: games per GPU, all played in lock step")
     ap.add_argument("--sp-sims", type=int, default=100, help="numMCTSSims (SURVEY §8d config 3)")
@@ -205,6 +207,41 @@ def grid_forward_leg(torch, ops, device, graphs=512, cpu_seconds=0.0):
                                "sample": f"{n} forwards of {n_g} grids (numpy fp32 oracle, "
                                          f"vectorised CSR restatement), {dt:.1f} s"}
     return out
+
+
+def large_batch_leg(torch, ops, ev, device, B=65536, reps=5):
+    """SURVEY §8d config 2 at B = 65,536 (B = 512 is launch-latency sized): the product path
+    C4Evaluator.evaluate(gnn=True) (trunk -> az_transform_heads_fwd) per batch, and the
+    output_transform.0 GEMM alone (M = B) with HIP events."""
+    rng = np.random.default_rng(7)
+    boards = torch.from_numpy(rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int8)).to(device)
+    Gn = ev.gnn.params
+    x = torch.empty((B, F), device=device).uniform_(0, 1)
+    hid = torch.empty((B, F), device=device)
+    ev.evaluate(boards, gnn=True)
+    ops.linear(x, Gn["output_transform.0.weight"], Gn["output_transform.0.bias"],
+               act=ops.ACT_RELU, out=hid)
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    e[0].record()
+    for _ in range(reps):
+        ev.evaluate(boards, gnn=True)
+    e[1].record()
+    for _ in range(reps):
+        ops.linear(x, Gn["output_transform.0.weight"], Gn["output_transform.0.bias"],
+                   act=ops.ACT_RELU, out=hid)
+    e[2].record()
+    torch.cuda.synchronize()
+    ms = e[0].elapsed_time(e[1]) / reps
+    gemm_ms = e[1].elapsed_time(e[2]) / reps
+    tflops = 2.0 * B * F * F / (gemm_ms * 1e-3) / 1e12
+    del x, hid, boards
+    torch.cuda.empty_cache()
+    return {"batch": B, "ms_per_batch": round(ms, 3), "boards_per_s": round(B / (ms * 1e-3), 1),
+            "gemm": {"kernel": "az_gemm_f32 output_transform.0 at M = %d" % B,
+                     "ms": round(gemm_ms, 3), "achieved": round(tflops, 2),
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tflops / FP32_MFMA_PEAK_TFLOPS, 4)}}
 
 
 def selfplay_args(sims):
@@ -453,6 +490,10 @@ def main():
             grid["node_updates_per_s"] = round(world * 2 * 524288 / (float(t.item()) * 1e-3), 1)
             grid["n_gpus"] = world
 
+    large = None
+    if args.large_batch > 0:
+        large = large_batch_leg(torch, ops, ev, device, B=args.large_batch)
+
     traffic = pmc_traffic("gemm")
     if agg is not None:
         agg["traffic"] = pmc_traffic("aggregate")
@@ -515,6 +556,7 @@ def main():
                          "avg_launch_us": round(avg_gemm_s * 1e6, 2),
                          "flop_per_launch": flop},
             "aggregate_roofline": agg,
+            "large_batch": large,
             "grid_forward": grid,
             "selfplay": sp,
             "train": tr,

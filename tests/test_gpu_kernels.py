@@ -44,7 +44,8 @@ def check_dot_error(got, ref, bound, tol=1e-6):
 
 @pytest.mark.parametrize("M,N,K", [(1, 3136, 3136), (3, 37, 64), (8, 128, 6272), (64, 128, 3136),
                                    (512, 3136, 3136), (130, 70, 48), (4096, 256, 64),
-                                   (1, 7, 4096), (2, 1001, 260), (5, 300, 1024), (1, 33, 4100)])
+                                   (1, 7, 4096), (2, 1001, 260), (5, 300, 1024), (1, 33, 4100),
+                                   (32768, 1024, 1024)])
 @pytest.mark.parametrize("act", [0, 1, 2])
 def test_linear_vs_torch(ops, M, N, K, act):
     g = torch.Generator().manual_seed(M * 7 + N + K + act)

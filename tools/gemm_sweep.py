@@ -99,6 +99,12 @@ if __name__ == "__main__":
                 print(json.dumps({"M": 512, "K": 31360, "cfg": cfg, "ablate": abl, **res}),
                       flush=True)
         sys.exit(0)
+    if mode == "bigm":         # large-batch output_transform (also B = 65,536)
+        M = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
+        for cfg in sys.argv[2].split(","):
+            r = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_SPLITS": "1"}, M=M)
+            print(json.dumps({"M": M, "cfg": cfg, **r}), flush=True)
+        sys.exit(0)
     if mode == "ablate":       # glds2 timing ablations (results wrong by design)
         cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else ("15", "16")
         abls = sys.argv[3].split(",") if len(sys.argv) > 3 else ("0", "1", "2", "3")

@@ -11,6 +11,6 @@ rc=$?; echo "pytest rc=$rc" >> $OUT/tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit $?
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-selfplay --no-agg-extra > $OUT/stats.log 2>&1 || exit $?
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-selfplay --no-train --no-agg-extra > $OUT/fetch.log 2>&1 || exit $?
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-selfplay --no-train --no-agg-extra > $OUT/write.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-selfplay --no-train --no-agg-extra --large-batch 0 > $OUT/fetch.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-selfplay --no-train --no-agg-extra --large-batch 0 > $OUT/write.log 2>&1 || exit $?
 echo done > $OUT/done
