@@ -1192,13 +1192,13 @@ static int glds_splits(const GemmArgs& a, long tiles, size_t ws_bytes) {
 }
 
 // Split factor for the 256x128 8-wave tile (96 KB of LDS: one block per CU): the largest S with
-// tiles * S <= 256 CUs, used only when that grid fills >= 90 % of the CUs, each split keeps
+// tiles * S <= 256 CUs, used only when that grid fills >= 85 % of the CUs, each split keeps
 // >= 8 k-tiles and the S slabs fit the workspace; 0 = do not use this tile.
 static int splits_256x128(int M, int N, int K, size_t ws_bytes) {
   const long tiles = (long)((M + 255) / 256) * ((N + 127) / 128);
   if (tiles >= 256) return 0;
   const int S = (int)std::min<long>(256 / tiles, 8);
-  if (tiles * S < 230) return 0;
+  if (tiles * S < 218) return 0;   // >= 85 % of the CUs (M = 768: 225 blocks, 158 vs 178 us)
   if (S > 1 && ((long)K / S < 8 * 32 || (size_t)S * M * N * 4 > ws_bytes)) return 0;
   return S;
 }
@@ -1271,7 +1271,7 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
     cfg = std::min(std::max(atoi(env_cfg), 0), kNumCfgs - 1);
     if (cfg >= 6 && !glds_ok) cfg = 0;
   } else if (glds_ok && d->M > 256 && (s256 = splits_256x128(d->M, d->N, d->K, d->ws_bytes)) > 0) {
-    // 256x128 tile, 8 waves, one block per CU, K split so the grid fills >= 90 % of the CUs
+    // 256x128 tile, 8 waves, one block per CU, K split so the grid fills >= 85 % of the CUs
     // (tools/gemm_sweep.py glds on MI355X, M = 512: 106 us vs 113 us for 128x128 x 5)
     cfg = 24;
   } else if (glds_ok && d->N >= 1024 && d->K >= 1024 && full_waves_256x128(d->M, d->N)) {

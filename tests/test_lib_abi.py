@@ -80,3 +80,27 @@ def test_ops_fail_loudly_without_gpu(built):
     from azhip import _lib
     with pytest.raises(RuntimeError, match="no HIP device"):
         _lib.lib()
+
+
+def test_host_side_validation_without_gpu(built):
+    """Argument checks of the leaf-evaluation entry points run on the host before any HIP call:
+    B = 0 is a no-op, bad shapes / null pointers return AZ_EINVAL with a message (the
+    reference's exceptions become status codes at this boundary)."""
+    from azhip import _lib
+    L = _lib.load()
+    AZ_OK, AZ_EINVAL = 0, -1
+    d = _lib.C4Eval()
+    d.max_B = 4
+    assert L.az_c4_eval_fwd(ctypes.byref(d), None, 0, None, None, None, None, None) == AZ_OK
+    assert L.az_c4_eval_fwd(ctypes.byref(d), None, 5, None, None, None, None, None) == AZ_EINVAL
+    assert b"max_B" in L.az_last_error()
+    assert L.az_c4_eval_fwd(ctypes.byref(d), None, 1, None, None, None, None, None) == AZ_EINVAL
+    assert b"null" in L.az_last_error()
+    args = [None] * 6 + [None, None, 8, None, None] + [None] * 4 + [None, 0, None]
+    assert L.az_c4_trunk_heads_fwd(None, 0, *args[2:]) == AZ_OK
+    assert L.az_c4_trunk_heads_fwd(None, 3, *args[2:]) == AZ_EINVAL
+    bad_a = list(args[2:])
+    bad_a[6] = 40                                     # A > 32
+    assert L.az_c4_trunk_heads_fwd(None, 3, *bad_a) == AZ_EINVAL
+    assert b"A=40" in L.az_last_error()
+    assert L.az_host_free(None) == AZ_OK

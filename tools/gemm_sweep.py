@@ -99,6 +99,17 @@ if __name__ == "__main__":
                 print(json.dumps({"M": 512, "K": 31360, "cfg": cfg, "ablate": abl, **res}),
                       flush=True)
         sys.exit(0)
+    if mode == "mgrid":        # default dispatch vs cfg x split at given M (self-play batch sizes)
+        Ms = [int(x) for x in sys.argv[2].split(",")]
+        cfgs = sys.argv[3].split(",")
+        splits = sys.argv[4].split(",")
+        for M in Ms:
+            print(json.dumps({"M": M, "cfg": "default", **run({}, M=M)}), flush=True)
+            for cfg in cfgs:
+                for sp in splits:
+                    r = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_SPLITS": sp}, M=M)
+                    print(json.dumps({"M": M, "cfg": cfg, "splits": sp, **r}), flush=True)
+        sys.exit(0)
     if mode == "bigm":         # large-batch output_transform (also B = 65,536)
         M = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
         for cfg in sys.argv[2].split(","):
