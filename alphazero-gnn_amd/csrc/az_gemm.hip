@@ -1010,6 +1010,141 @@ __global__ __launch_bounds__(256) void gemv_side_heads(GemmArgs p, SideHeads h, 
   }
 }
 
+// ------------------------------------------------------------------------ tall-skinny GEMM
+// C[M][N] = epi(A[M][K] . W[N][K]^T) for the grid-graph layers: M ~ 10^5..10^6 rows, K in
+// {64, 128}, N in {64, 128, 256}.  A tile kernel with K <= 128 spends most of each block on its
+// prologue / epilogue (2 k-tiles of work per block; 2.2 TB/s on the 524288 x 256 x 64
+// projection).  Here each 256-thread block is persistent over 64-row strips:
+//   - W is resident in LDS, rows padded to K+1 floats (stride = 1 mod 32: the 16 columns x 2
+//     k-groups of one ds_read_b32 half-wave land on 32 distinct banks);
+//   - A goes straight from HBM to registers: the K axis is permuted so that lane group
+//     g = lane >> 4 owns k in [g*K/4, (g+1)*K/4) and MFMA step j (16x16x4 f32) takes k = g*K/4 + j,
+//     i.e. each lane reads K/4 CONTIGUOUS floats of its row (K/16 float4 loads, every row's
+//     K floats covered by the 4 groups: full lines);
+//   - the next strip's A is loaded while the current one is multiplied, and the outputs leave
+//     in the MFMA layout as 16-float (64 B) row segments per 16 lanes, the two halves of a
+//     128-B line coming from consecutive tiles of the same lanes.
+// Concatenated inputs [A | A2] need K0 = a multiple of K/4 (a whole k-group per source).
+// NW waves per block share one LDS copy of W (N = 256: W is 66.5 KB, so 8-wave blocks give
+// 16 waves per CU where 4-wave blocks gave 8); N is covered in NP column passes that reuse the
+// strip's A registers (NT/NP accumulator tiles live at a time: fewer VGPRs, more waves).
+template <int N, int K, int NW, int NP>
+__global__ __launch_bounds__(64 * NW) void gemm_tall(GemmArgs p, int nstrips) {
+  constexpr int KS = K + 1;            // padded W row (floats)
+  constexpr int KG = K / 4;            // k per lane group
+  constexpr int NT = N / 16 / NP;      // 16x16 output tiles per pass
+  constexpr int NV = KG / 4;           // float4 loads per lane per strip
+  constexpr int BM = 16 * NW;          // rows per strip
+  __shared__ float Ws[N * KS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  // W -> LDS (once per block)
+  for (int i = threadIdx.x; i < N * K / 4; i += 64 * NW) {
+    const int n = i / (K / 4), k = (i % (K / 4)) * 4;
+    const f32x4 w = *reinterpret_cast<const f32x4*>(p.B + (size_t)n * p.ldb + k);
+    float* d = Ws + n * KS + k;
+    d[0] = w[0]; d[1] = w[1]; d[2] = w[2]; d[3] = w[3];
+  }
+  // this lane's A source for a strip: row strip*BM + wave*16 + c, k in [g*KG, g*KG + KG)
+  const int kg0 = g * KG;
+  const bool from2 = p.A2 != nullptr && kg0 >= p.K0;
+  const float* abase = from2 ? p.A2 + (kg0 - p.K0) : p.A + kg0;
+  const int lda = from2 ? p.lda2 : p.lda;
+  auto load_a = [&](int strip, f32x4 (&a)[NV]) {
+    int row = strip * BM + wave * 16 + c;
+    row = row < p.M ? row : p.M - 1;              // clamped (never stored)
+    const f32x4* src = reinterpret_cast<const f32x4*>(abase + (size_t)row * lda);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) a[v] = src[v];
+  };
+  f32x4 acur[NV], anext[NV];
+  int strip = blockIdx.x;
+  if (strip < nstrips) load_a(strip, acur);
+  __syncthreads();
+  for (; strip < nstrips; strip += gridDim.x) {
+    const int nxt = strip + gridDim.x;
+    if (nxt < nstrips) load_a(nxt, anext);
+    const int rbase = strip * BM + wave * 16 + 4 * g;   // lane's rows: rbase + r, r = 0..3
+#pragma unroll 1
+    for (int h = 0; h < NP; ++h) {
+      f32x4 acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // B fragments of step j + 1 are read while step j's MFMAs run; the sched_barrier keeps
+      // the compiler from hoisting every step's LDS reads to the top (VGPR pressure)
+      const float* wcol = Ws + (h * NT * 16 + c) * KS + kg0;
+      float bcur[NT], bnext[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bcur[t] = wcol[t * 16 * KS];
+#pragma unroll
+      for (int j = 0; j < KG; ++j) {
+        if (j + 1 < KG) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) bnext[t] = wcol[t * 16 * KS + j + 1];
+        }
+        const float av = acur[j >> 2][j & 3];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bcur[t], acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bcur[t] = bnext[t];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (p.ablate & 4) {               // timing experiment: keep the sums live, no stores
+        float t0 = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) t0 += acc[t][0] + acc[t][1] + acc[t][2] + acc[t][3];
+        if (t0 == 1234.5f) p.C[0] = t0;
+        continue;
+      }
+      // epilogue: lane holds C[rbase + r][col], col = (h*NT + t)*16 + c; a row's tiles are
+      // stored back to back, so both 64-B halves of each 128-B line leave together
+      float bias[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bias[t] = p.bias ? p.bias[(h * NT + t) * 16 + c] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase + r;
+        if (row >= p.M) break;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int col = (h * NT + t) * 16 + c;
+          float v = apply_act(acc[t][r] + bias[t], p.act);
+          if (p.C2) p.C2[(size_t)row * p.ldc2 + col] = v;
+          if (p.R)
+            v = p.R[(size_t)row * p.ldr + col] + (p.G ? p.G[(size_t)row * p.ldg + col] : 1.f) * v;
+          float* dst = p.C + (size_t)row * p.ldc + col;
+          if (p.beta != 0.f) v += p.beta * *dst;
+          *dst = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acur[v] = anext[v];
+  }
+}
+
+// Launches gemm_tall when the shape is one it covers; false otherwise (nothing launched).
+static bool launch_tall(const GemmArgs& a, hipStream_t s) {
+  static const bool off = getenv("AZ_GEMM_NOTALL") != nullptr;   // A/B experiments
+  if (off || a.M < 16384 || a.a_rows || a.b_rows || a.c_rows || a.act == AZ_ACT_DRELU)
+    return false;
+  if (!((a.K == 64 || a.K == 128) && (a.N == 64 || a.N == 128 || a.N == 256))) return false;
+  if (a.A2 && (a.K0 % (a.K / 4) != 0 || a.lda2 % 4 != 0)) return false;
+  if (a.lda % 4 != 0 || a.ldb % 4 != 0) return false;
+#define AZ_TALL(NN, KK, NW, NP)                                                               \
+  if (a.N == NN && a.K == KK) {                                                              \
+    const int nstrips = (a.M + 16 * NW - 1) / (16 * NW);                                     \
+    hipLaunchKernelGGL((gemm_tall<NN, KK, NW, NP>), dim3(std::min(nstrips, 1024)),           \
+                       dim3(64 * NW), 0, s, a, nstrips);                                     \
+    return true;                                                                             \
+  }
+  AZ_TALL(64, 64, 4, 1) AZ_TALL(64, 128, 4, 1) AZ_TALL(128, 64, 8, 2) AZ_TALL(128, 128, 8, 2)
+  AZ_TALL(256, 64, 8, 2)
+#undef AZ_TALL
+  return false;
+}
+
 struct TileCfg { int bm, bn, bk, wgm, wgn; };
 // register-staged: 0: 64x64x32 (4 waves 2x2)   1: 128x128x32 (4 waves 2x2)   2: 64x64x64
 // 3: 128x64x32 (4 waves 2x2)  4: 128x128x32 (8 waves 2x4)   5: 256x128x32 (8 waves 4x2)
@@ -1262,6 +1397,7 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
     launch_gemv(a, s);
     return check_launch("gemv_f32");
   }
+  if (akm && bkm && launch_tall(a, s)) return check_launch("gemm_tall");
   // tile choice (tuning override for experiments: AZ_GEMM_CFG=<index into kCfgs>)
   static const char* env_cfg = getenv("AZ_GEMM_CFG");
   const bool glds_ok = akm && bkm && !d->A2 && !d->a_rows;

@@ -99,6 +99,14 @@ if __name__ == "__main__":
                 print(json.dumps({"M": 512, "K": 31360, "cfg": cfg, "ablate": abl, **res}),
                       flush=True)
         sys.exit(0)
+    if mode == "tallk":        # gemm_tall (default dispatch) vs the tile kernels (AZ_GEMM_NOTALL)
+        for (M, N, K) in [(524288, 256, 64), (524288, 64, 64), (524288, 64, 128),
+                          (524288, 128, 64), (20007, 64, 64)]:
+            for env in ({}, {"AZ_GEMM_NOTALL": "1"}, {"AZ_GEMM_ABLATE": "4"},
+                        {"AZ_GEMM_ABLATE": "8"}):
+                res = run(env, M, N, K)
+                print(json.dumps({"M": M, "N": N, "K": K, "env": env, **res}), flush=True)
+        sys.exit(0)
     if mode == "mgrid":        # default dispatch vs cfg x split at given M (self-play batch sizes)
         Ms = [int(x) for x in sys.argv[2].split(",")]
         cfgs = sys.argv[3].split(",")
