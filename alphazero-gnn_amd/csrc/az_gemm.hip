@@ -658,8 +658,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds_pipe(GemmArgs p)
 // Element t of the 4-k fragment feeds MFMA t, so the k order inside a group is permuted (only
 // the fp32 summation order changes).  The 16x16 shape is the lower-energy one per FLOP
 // (cdna_hip_programming.md §5.4 rule 28: the chip holds a higher clock on it).
-template <int BM, int BN, int WGM, int WGN, int MF, bool IL>
+//
+// NB = 3 (IL = false only): a three-buffer LDS ring.  Tile kt + 2 is issued right after the
+// barrier that retires tile kt, so each DMA has two k-tiles of MFMA time to land instead of
+// one, and the wait before a tile is a counted vmcnt (the next tile's pieces stay in flight);
+// one barrier per k-tile.  256x128: 144 KB of LDS, one block per CU.
+template <int BM, int BN, int WGM, int WGN, int MF, bool IL, int NB = 2>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
+  static_assert(NB == 2 || (NB == 3 && !IL), "three-buffer ring without interleaved issue");
   constexpr int BK = 32;
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -670,7 +676,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
   using acc_t = typename std::conditional<MF == 32, f32x16, f32x4>::type;
   constexpr int NACC = MF == 32 ? 16 : 4;
   static_assert(TI >= 1 && TJ >= 1 && APC >= 1 && BPC >= 1, "bad tile");
-  __shared__ __attribute__((aligned(1024))) float smem[2 * (BM + BN) * BK];
+  __shared__ __attribute__((aligned(1024))) float smem[NB * (BM + BN) * BK];
 
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
   const int nwg = mt_n * nt_n * p.splits;
@@ -770,6 +776,67 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
   }
 
   const int nk = (kend - kbeg + BK - 1) / BK;
+  if constexpr (NB == 3) {
+    constexpr int DPT = APC + BPC;                   // DMA pieces per lane per tile
+    if (nk > 0) issue(0, kbeg);
+    if (nk > 1) issue(1, kbeg + BK);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) wait_vm<DPT>();               // tile kt landed, tile kt + 1 in flight
+      else wait_vm<0>();
+      __syncthreads();                               // ... for every wave; tile kt - 1 retired
+      const int cur = kt % 3;
+      const int k0 = kbeg + kt * BK;
+      if (k0 + BK > kend) {                          // partial last tile: zero A's k >= kend
+        float* As = smem + cur * (BM + BN) * BK;
+        for (int idx = threadIdx.x; idx < BM * 8; idx += NT) {
+          const int r = idx >> 3, lc = idx & 7;
+          if (k0 + lc * 4 >= kend)
+            *reinterpret_cast<f32x4*>(As + r * BK + ((lc ^ ((r >> 1) & 7)) * 4)) =
+                f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        __syncthreads();
+      }
+      if (kt + 2 < nk) issue((kt + 2) % 3, k0 + 2 * BK);   // overwrites tile kt - 1's buffer
+      const float* S = smem + cur * (BM + BN) * BK;
+      f32x4 a[NG][TI], b[NG][TJ];
+      auto read = [&](int g) {
+        const int lc = g * (64 >> LSH) + (lane >> LSH);
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+          a[g][i] = *reinterpret_cast<const f32x4*>(S + aoff[i] + ((lc ^ akey[i]) * 4));
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          b[g][j] = *reinterpret_cast<const f32x4*>(S + boff[j] + ((lc ^ bkey[j]) * 4));
+      };
+      read(0);
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) {
+              if constexpr (MF == 32)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][i][t], b[g][j][t],
+                                                                 acc[i][j], 0, 0, 0);
+              else
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][i][t], b[g][j][t],
+                                                                 acc[i][j], 0, 0, 0);
+            }
+          if (t == 0 && g + 1 < NG) {
+            __builtin_amdgcn_sched_barrier(0);
+            read(g + 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+    }
+    __syncthreads();                                 // the epilogue reuses the LDS
+    tile_epilogue<MF, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
+                              (NW * WM * 36 <= (int)(sizeof(smem) / 4)) ? smem + wave * (WM * 36)
+                                                                         : nullptr);
+    return;
+  }
   if (nk > 0) {
     issue(0, kbeg);
     __builtin_amdgcn_s_waitcnt(0);
@@ -1168,8 +1235,9 @@ static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 
                                 {128, 64, 32, 2, 2},  {128, 128, 32, 2, 4}, {128, 128, 32, 2, 2},
                                 {128, 128, 32, 2, 2}, {128, 64, 32, 2, 2},  {256, 128, 32, 4, 2},
                                 {256, 128, 32, 4, 2}, {128, 256, 32, 2, 4}, {256, 128, 32, 4, 2},
-                                {256, 128, 32, 4, 2}, {256, 128, 32, 4, 2}};
-constexpr int kNumCfgs = 29;
+                                {256, 128, 32, 4, 2}, {256, 128, 32, 4, 2}, {256, 128, 32, 4, 2},
+                                {256, 128, 32, 4, 2}};
+constexpr int kNumCfgs = 31;
 
 template <int BM, int BN, int BK, int WGM, int WGN>
 static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
@@ -1193,11 +1261,11 @@ static void launch_pipe(const GemmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((gemm_f32_glds_pipe<BM, BN, BK, NBUF, 2, 2>), dim3(nwg), dim3(256), 0, s, a);
 }
 
-template <int BM, int BN, int WGM, int WGN, int MF, bool IL = false>
+template <int BM, int BN, int WGM, int WGN, int MF, bool IL = false, int NB = 2>
 static void launch_glds2(const GemmArgs& a, hipStream_t s) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
-  hipLaunchKernelGGL((gemm_f32_glds2<BM, BN, WGM, WGN, MF, IL>), dim3(nwg), dim3(64 * WGM * WGN), 0,
-                     s, a);
+  hipLaunchKernelGGL((gemm_f32_glds2<BM, BN, WGM, WGN, MF, IL, NB>), dim3(nwg),
+                     dim3(64 * WGM * WGN), 0, s, a);
 }
 
 static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
@@ -1213,6 +1281,8 @@ static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream
     case 26: launch_glds2<256, 128, 4, 2, 16, true>(a, s); break;
     case 27: launch_glds2<256, 128, 4, 2, 32, true>(a, s); break;
     case 28: launch_glds2<256, 128, 4, 2, 32>(a, s); break;
+    case 29: launch_glds2<256, 128, 4, 2, 16, false, 3>(a, s); break;
+    case 30: launch_glds2<256, 128, 4, 2, 32, false, 3>(a, s); break;
     case 20: launch_glds2<128, 128, 2, 2, 32, true>(a, s); break;
     case 21: launch_glds2<128, 128, 2, 2, 16, true>(a, s); break;
     case 22: launch_glds2<128, 64, 2, 2, 16, true>(a, s); break;
@@ -1422,6 +1492,8 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
   } else {
     cfg = 0;  // register-staged 64x64x32: gathered / concatenated operands, small M
   }
+  static const char* env_ring = getenv("AZ_GEMM_RING");   // experiment: 3-buffer 256x128
+  if (cfg == 24 && env_ring && atoi(env_ring) == 3) cfg = 29;
   const TileCfg& tc = kCfgs[cfg];
   plan(a, tc.bm, tc.bn, tc.bk, d->ws_bytes);
   const bool is128 = tc.bm == 128 && tc.bn == 128 && cfg >= 6;

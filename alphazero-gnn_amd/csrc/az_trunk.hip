@@ -259,19 +259,21 @@ __global__ __launch_bounds__(256) void heads_partial_kernel(
 // order and adds the bias -- the arithmetic of splitk_reduce_kernel -- stores y, and forms the
 // same per-chunk dot products, so y, logp, pi and v are bit-identical to the unfused path while
 // y is never re-read from HBM.
-template <int AMAX, int S>
+// ROWS rows per block (ROWS / 4 per wave): fewer rows per block = more blocks in flight for the
+// same bytes (the per-(chunk,row) arithmetic, hence the result, does not depend on ROWS).
+template <int AMAX, int S, int ROWS = HEADS_ROWS>
 __global__ __launch_bounds__(256) void splitk_heads_partial_kernel(
     const float* __restrict__ slab, int B, int K, const float* __restrict__ bias,
     float* __restrict__ y, const float* __restrict__ wp, int A, const float* __restrict__ wv,
     float* __restrict__ part) {
   const int c = blockIdx.x;
-  const int r0 = blockIdx.y * HEADS_ROWS;
+  const int r0 = blockIdx.y * ROWS;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int k = c * HEADS_KC + lane * 4;
   const bool kin = k < K;
   const int kc = kin ? k : 0;
   const size_t plane = (size_t)B * K;
-  constexpr int RPW = HEADS_ROWS / 4;
+  constexpr int RPW = ROWS / 4;
   // all loads unconditional (clamped addresses) and issued before any masking, as in
   // heads_partial_kernel: slabs (S x RPW float4 per lane), then weights and bias
   f32x4 sv[RPW][S];
@@ -562,6 +564,21 @@ template <int S>
 static void launch_splitk_heads(const float* slab, int B, int K, const float* bias, float* y,
                                 const float* wp, int A, const float* wv, float* part,
                                 hipStream_t s) {
+  // 4 rows per block (one per wave): 1,664 blocks at B = 512 instead of 416 with 16 rows, so
+  // 4x the slab loads in flight: 12.1 -> 9.0 us (tools/heads_rows_probe.sh on MI355X).
+  // AZ_SPLITK_HEADS_ROWS = 8 / 16 selects the other shapes for A/B runs.
+  static const char* env_rows = getenv("AZ_SPLITK_HEADS_ROWS");
+  const int rows = env_rows ? atoi(env_rows) : 4;
+  if (rows == 4 || rows == 8) {
+    dim3 g((K + HEADS_KC - 1) / HEADS_KC, (B + rows - 1) / rows);
+    if (rows == 4)
+      hipLaunchKernelGGL((splitk_heads_partial_kernel<8, S, 4>), g, dim3(256), 0, s, slab, B, K,
+                         bias, y, wp, A, wv, part);
+    else
+      hipLaunchKernelGGL((splitk_heads_partial_kernel<8, S, 8>), g, dim3(256), 0, s, slab, B, K,
+                         bias, y, wp, A, wv, part);
+    return;
+  }
   dim3 g((K + HEADS_KC - 1) / HEADS_KC, (B + HEADS_ROWS - 1) / HEADS_ROWS);
   hipLaunchKernelGGL((splitk_heads_partial_kernel<8, S>), g, dim3(256), 0, s, slab, B, K, bias, y,
                      wp, A, wv, part);
