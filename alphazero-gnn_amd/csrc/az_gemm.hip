@@ -663,9 +663,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds_pipe(GemmArgs p)
 // barrier that retires tile kt, so each DMA has two k-tiles of MFMA time to land instead of
 // one, and the wait before a tile is a counted vmcnt (the next tile's pieces stay in flight);
 // one barrier per k-tile.  256x128: 144 KB of LDS, one block per CU.
-template <int BM, int BN, int WGM, int WGN, int MF, bool IL, int NB = 2>
+template <int BM, int BN, int WGM, int WGN, int MF, bool IL, int NB = 2, bool ST = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
   static_assert(NB == 2 || (NB == 3 && !IL), "three-buffer ring without interleaved issue");
+  static_assert(!ST || NB == 3, "the stagger needs the three-buffer ring");
   constexpr int BK = 32;
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -778,12 +779,42 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
   const int nk = (kend - kbeg + BK - 1) / BK;
   if constexpr (NB == 3) {
     constexpr int DPT = APC + BPC;                   // DMA pieces per lane per tile
+    // ST: waves NW/2.. (the SIMD partners of waves 0..NW/2-1) run half a k-tile behind: they
+    // carry the fragments of the tile's last group across the barrier and start each tile with
+    // those MFMAs while their partners wait on their first LDS reads
+    // (MI355X_MICROARCH.md, "two waves that run the same program ... try a stagger").  The
+    // accumulation order of every wave is unchanged: results are bit-identical.
+    const bool hi = ST && wave >= NW / 2;
+    f32x4 a[NG][TI], b[NG][TJ];
+    auto read = [&](const float* S, int g) {
+      const int lc = g * (64 >> LSH) + (lane >> LSH);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+        a[g][i] = *reinterpret_cast<const f32x4*>(S + aoff[i] + ((lc ^ akey[i]) * 4));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        b[g][j] = *reinterpret_cast<const f32x4*>(S + boff[j] + ((lc ^ bkey[j]) * 4));
+    };
+    auto mfma = [&](int g, int t) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          if constexpr (MF == 32)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][i][t], b[g][j][t], acc[i][j],
+                                                             0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][i][t], b[g][j][t], acc[i][j],
+                                                             0, 0, 0);
+        }
+    };
     if (nk > 0) issue(0, kbeg);
     if (nk > 1) issue(1, kbeg + BK);
     for (int kt = 0; kt < nk; ++kt) {
+      // raw barriers only: __syncthreads()' fence would drain the next tile's DMA (vmcnt(0))
       if (kt + 1 < nk) wait_vm<DPT>();               // tile kt landed, tile kt + 1 in flight
       else wait_vm<0>();
-      __syncthreads();                               // ... for every wave; tile kt - 1 retired
+      lds_barrier();                                 // ... for every wave; tile kt - 1 retired
       const int cur = kt % 3;
       const int k0 = kbeg + kt * BK;
       if (k0 + BK > kend) {                          // partial last tile: zero A's k >= kend
@@ -794,44 +825,55 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
             *reinterpret_cast<f32x4*>(As + r * BK + ((lc ^ ((r >> 1) & 7)) * 4)) =
                 f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        __syncthreads();
+        lds_barrier();
       }
       if (kt + 2 < nk) issue((kt + 2) % 3, k0 + 2 * BK);   // overwrites tile kt - 1's buffer
       const float* S = smem + cur * (BM + BN) * BK;
-      f32x4 a[NG][TI], b[NG][TJ];
-      auto read = [&](int g) {
-        const int lc = g * (64 >> LSH) + (lane >> LSH);
+      if (!hi) {
+        read(S, 0);
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
-          a[g][i] = *reinterpret_cast<const f32x4*>(S + aoff[i] + ((lc ^ akey[i]) * 4));
+        for (int g = 0; g < NG; ++g)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          b[g][j] = *reinterpret_cast<const f32x4*>(S + boff[j] + ((lc ^ bkey[j]) * 4));
-      };
-      read(0);
-#pragma unroll
-      for (int g = 0; g < NG; ++g)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-#pragma unroll
-          for (int i = 0; i < TI; ++i)
-#pragma unroll
-            for (int j = 0; j < TJ; ++j) {
-              if constexpr (MF == 32)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][i][t], b[g][j][t],
-                                                                 acc[i][j], 0, 0, 0);
-              else
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][i][t], b[g][j][t],
-                                                                 acc[i][j], 0, 0, 0);
+          for (int t = 0; t < 4; ++t) {
+            mfma(g, t);
+            if (t == 0 && g + 1 < NG) {
+              __builtin_amdgcn_sched_barrier(0);
+              read(S, g + 1);
+              __builtin_amdgcn_sched_barrier(0);
             }
-          if (t == 0 && g + 1 < NG) {
-            __builtin_amdgcn_sched_barrier(0);
-            read(g + 1);
-            __builtin_amdgcn_sched_barrier(0);
           }
+      } else {
+        if (kt > 0) {                                // tile kt - 1's last group, from registers
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            mfma(NG - 1, t);
+            if (t == 0) {
+              __builtin_amdgcn_sched_barrier(0);
+              read(S, 0);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        } else {
+          read(S, 0);
         }
+#pragma unroll
+        for (int g = 0; g < NG - 1; ++g)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            mfma(g, t);
+            if (t == 0) {
+              __builtin_amdgcn_sched_barrier(0);
+              read(S, g + 1);                        // group NG - 1 rides across the barrier
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+      }
     }
-    __syncthreads();                                 // the epilogue reuses the LDS
+    if (hi && nk > 0) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) mfma(NG - 1, t);
+    }
+    lds_barrier();                                   // the epilogue reuses the LDS
     tile_epilogue<MF, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                               (NW * WM * 36 <= (int)(sizeof(smem) / 4)) ? smem + wave * (WM * 36)
                                                                          : nullptr);
@@ -1236,8 +1278,8 @@ static const TileCfg kCfgs[] = {{64, 64, 32, 2, 2},  {128, 128, 32, 2, 2}, {64, 
                                 {128, 128, 32, 2, 2}, {128, 64, 32, 2, 2},  {256, 128, 32, 4, 2},
                                 {256, 128, 32, 4, 2}, {128, 256, 32, 2, 4}, {256, 128, 32, 4, 2},
                                 {256, 128, 32, 4, 2}, {256, 128, 32, 4, 2}, {256, 128, 32, 4, 2},
-                                {256, 128, 32, 4, 2}};
-constexpr int kNumCfgs = 31;
+                                {256, 128, 32, 4, 2}, {256, 128, 32, 4, 2}, {256, 128, 32, 4, 2}};
+constexpr int kNumCfgs = 33;
 
 template <int BM, int BN, int BK, int WGM, int WGN>
 static void launch_tile(const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
@@ -1261,10 +1303,10 @@ static void launch_pipe(const GemmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((gemm_f32_glds_pipe<BM, BN, BK, NBUF, 2, 2>), dim3(nwg), dim3(256), 0, s, a);
 }
 
-template <int BM, int BN, int WGM, int WGN, int MF, bool IL = false, int NB = 2>
+template <int BM, int BN, int WGM, int WGN, int MF, bool IL = false, int NB = 2, bool ST = false>
 static void launch_glds2(const GemmArgs& a, hipStream_t s) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
-  hipLaunchKernelGGL((gemm_f32_glds2<BM, BN, WGM, WGN, MF, IL, NB>), dim3(nwg),
+  hipLaunchKernelGGL((gemm_f32_glds2<BM, BN, WGM, WGN, MF, IL, NB, ST>), dim3(nwg),
                      dim3(64 * WGM * WGN), 0, s, a);
 }
 
@@ -1283,6 +1325,8 @@ static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream
     case 28: launch_glds2<256, 128, 4, 2, 32>(a, s); break;
     case 29: launch_glds2<256, 128, 4, 2, 16, false, 3>(a, s); break;
     case 30: launch_glds2<256, 128, 4, 2, 32, false, 3>(a, s); break;
+    case 31: launch_glds2<256, 128, 4, 2, 16, false, 3, true>(a, s); break;
+    case 32: launch_glds2<256, 128, 4, 2, 32, false, 3, true>(a, s); break;
     case 20: launch_glds2<128, 128, 2, 2, 32, true>(a, s); break;
     case 21: launch_glds2<128, 128, 2, 2, 16, true>(a, s); break;
     case 22: launch_glds2<128, 64, 2, 2, 16, true>(a, s); break;
@@ -1493,7 +1537,10 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
     cfg = 0;  // register-staged 64x64x32: gathered / concatenated operands, small M
   }
   static const char* env_ring = getenv("AZ_GEMM_RING");   // experiment: 3-buffer 256x128
-  if (cfg == 24 && env_ring && atoi(env_ring) == 3) cfg = 29;
+  if (cfg == 24 && env_ring) {
+    const int r = atoi(env_ring);
+    cfg = r == 3 ? 29 : r == 4 ? 31 : r == 5 ? 30 : r == 6 ? 32 : 24;
+  }
   const TileCfg& tc = kCfgs[cfg];
   plan(a, tc.bm, tc.bn, tc.bk, d->ws_bytes);
   const bool is128 = tc.bm == 128 && tc.bn == 128 && cfg >= 6;

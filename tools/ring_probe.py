@@ -1,5 +1,6 @@
-"""A/B of the 256x128 LDS-DMA tile with a 2-buffer (default) vs 3-buffer LDS ring
-(AZ_GEMM_RING=3) on the output_transform shape at several M (each in its own subprocess).
+"""A/B of the 256x128 LDS-DMA tile variants on the output_transform shape (each run in its own
+subprocess): AZ_GEMM_RING = 2 (default 2-buffer), 3 (3-buffer ring), 4 (ring + stagger),
+5 / 6 (the same two with the 32x32x2 MFMA).
     python tools/ring_probe.py [M ...]"""
 import json
 import os
@@ -8,13 +9,14 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from gemm_sweep import run  # noqa: E402
 
-Ms = [int(a) for a in sys.argv[1:]] or [512, 768, 1024, 2048, 65536]
+Ms = [int(a) for a in sys.argv[1:]] or [512, 768, 1024, 65536]
+RINGS = os.environ.get("RINGS", "2,3,4,5,6").split(",")
 for M in Ms:
-    for ring in ("2", "3", "2", "3"):
-        env = {"AZ_GEMM_RING": ring}
-        r = run(env, M=M)
-        print(json.dumps({"M": M, "ring": ring, **r}), flush=True)
+    for rep in range(2):
+        for ring in RINGS:
+            r = run({"AZ_GEMM_RING": ring}, M=M)
+            print(json.dumps({"M": M, "ring": ring, **r}), flush=True)
 for K in (3100, 1000):                 # partial last k-tile of a split (A's tail zeroed)
-    for ring in ("2", "3"):
-        print(json.dumps({"M": 512, "K": K, "ring": ring, **run({"AZ_GEMM_RING": ring}, 512, 3136, K)}),
-              flush=True)
+    for ring in RINGS:
+        print(json.dumps({"M": 512, "K": K, "ring": ring,
+                          **run({"AZ_GEMM_RING": ring}, 512, 3136, K)}), flush=True)
