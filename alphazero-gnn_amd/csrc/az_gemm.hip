@@ -961,6 +961,27 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
   }
 }
 
+// splitk_reduce_kernel for p.vec_epi shapes: one float4 of the output per lane, its S slab
+// float4s loaded before the first add (S known at compile time), summed in slab order from 0.f
+// exactly as above, then epilogue_store4; one pass, no grid-stride loop.
+template <int S>
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmArgs p) {
+  const long i4 = blockIdx.x * 256L + threadIdx.x;
+  const long total4 = (long)p.M * p.N / 4;
+  if (i4 >= total4) return;
+  const size_t plane = (size_t)p.M * p.N;
+  f32x4 v[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) v[k] = *reinterpret_cast<const f32x4*>(p.slab + k * plane + i4 * 4);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < S; ++k)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s[c] += v[k][c];
+  const long e = i4 * 4;
+  epilogue_store4(p, (int)(e / p.N), (int)(e % p.N), s);
+}
+
 // ------------------------------------------------------------------------------ GEMV
 // C[M<=8][N] = epi(A[M][K] . W[N][K]^T): each wave owns GV_ROWS output columns and streams
 // their weight rows from HBM (float4, GV_ROWS*KC/256 loads in flight per lane); A is staged
@@ -1570,6 +1591,27 @@ int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s) {
   a.slab = static_cast<float*>(d->ws);
   a.splits = splits;
   const long total = (long)a.M * a.N;
+  static const bool no_vec = getenv("AZ_GEMM_NOVEC") != nullptr;   // A/B experiments
+  const bool vec = !no_vec && d->N % 4 == 0 && d->ldc % 4 == 0 && aligned16(d->C) &&
+                   (!d->C2 || (d->ldc2 % 4 == 0 && aligned16(d->C2))) &&
+                   (!d->R || (d->ldr % 4 == 0 && aligned16(d->R))) &&
+                   (!d->G || (d->ldg % 4 == 0 && aligned16(d->G))) &&
+                   (!d->bias || aligned16(d->bias)) && aligned16(d->ws);
+  if (vec && splits >= 2 && splits <= 8) {
+    // float4 per lane: 38.7 MB at M = 512, N = 3136, S = 5 in one pass (the scalar
+    // grid-stride kernel took 10.6 us for it)
+    const int blocks = (int)((total / 4 + 255) / 256);
+    switch (splits) {
+      case 2: hipLaunchKernelGGL(splitk_reduce4_kernel<2>, dim3(blocks), dim3(256), 0, s, a); break;
+      case 3: hipLaunchKernelGGL(splitk_reduce4_kernel<3>, dim3(blocks), dim3(256), 0, s, a); break;
+      case 4: hipLaunchKernelGGL(splitk_reduce4_kernel<4>, dim3(blocks), dim3(256), 0, s, a); break;
+      case 5: hipLaunchKernelGGL(splitk_reduce4_kernel<5>, dim3(blocks), dim3(256), 0, s, a); break;
+      case 6: hipLaunchKernelGGL(splitk_reduce4_kernel<6>, dim3(blocks), dim3(256), 0, s, a); break;
+      case 7: hipLaunchKernelGGL(splitk_reduce4_kernel<7>, dim3(blocks), dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL(splitk_reduce4_kernel<8>, dim3(blocks), dim3(256), 0, s, a); break;
+    }
+    return check_launch("splitk_reduce4_kernel");
+  }
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, a);
   return check_launch("splitk_reduce_kernel");
