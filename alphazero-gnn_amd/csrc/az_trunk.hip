@@ -397,6 +397,158 @@ __global__ __launch_bounds__(512) void heads_rows_kernel(
                         row, logp, pi, v, part, sm);
 }
 
+// output_transform.2's split-K slabs reduced and both head passes in ONE launch, one 512-thread
+// block per row: the row x = sum of the S slabs (in slab order, from 0.f) + bias -- the arithmetic
+// of splitk_heads_partial_kernel -- is staged in LDS (and stored as y), then heads_row_block forms
+// the chunk partials and the finalize as heads_rows_kernel does.  Bit-identical to
+// splitk_heads_partial_kernel + heads_finalize_kernel, minus that launch and the partials' round
+// trip.  K <= SPLITK_ROWS_MAXK.
+constexpr int SPLITK_ROWS_MAXK = 4096;
+
+template <int AMAX, int S>
+__global__ __launch_bounds__(512) void splitk_heads_rows_kernel(
+    const float* __restrict__ slab, int B, int K, const float* __restrict__ bias,
+    float* __restrict__ y, const float* __restrict__ wp, int A, const float* __restrict__ wv,
+    const float* __restrict__ bp, const float* __restrict__ bv, float* __restrict__ logp,
+    float* __restrict__ pi, float* __restrict__ v) {
+  __shared__ __attribute__((aligned(16))) float xr[SPLITK_ROWS_MAXK];
+  __shared__ float part[HEADS_ROWS_MAXC * (AMAX + 1)];
+  __shared__ float sm[AMAX + 1];
+  const int row = blockIdx.x;
+  const size_t plane = (size_t)B * K;
+  const float* src = slab + (size_t)row * K;
+  const int K4 = K / 4;
+  constexpr int IT = SPLITK_ROWS_MAXK / 4 / 512;
+  f32x4 sv[IT][S];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {                  // every slab load issued before the adds
+    const int k4 = min(it * 512 + (int)threadIdx.x, K4 - 1);
+#pragma unroll
+    for (int q = 0; q < S; ++q)
+      sv[it][q] = *reinterpret_cast<const f32x4*>(src + q * plane + (size_t)k4 * 4);
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int k4 = it * 512 + (int)threadIdx.x;
+    if (k4 >= K4) break;
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + (size_t)k4 * 4);
+    f32x4 x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < S; ++q) t += sv[it][q][e];
+      x[e] = t + bb[e];
+    }
+    *reinterpret_cast<f32x4*>(xr + k4 * 4) = x;
+    if (y) *reinterpret_cast<f32x4*>(y + (size_t)row * K + k4 * 4) = x;
+  }
+  __syncthreads();
+  heads_row_block<AMAX, 8>(xr, xr, K, wp, A, wv, bp, bv, row, logp, pi, v, part, sm);
+}
+
+// The same in one launch with R rows per block and one wave per 256-column chunk (blockDim =
+// 64 * nchunks <= 1024): wave c loads its chunk's head weights ONCE into registers and reuses
+// them for the block's R rows (the one-row-per-block kernel re-reads 113 KB of weights per row);
+// every slab load of the R rows is issued before the first add.  Per (row, chunk) arithmetic and
+// chunk-order finalize exactly as splitk_heads_partial_kernel + heads_finalize_kernel.
+template <int AMAX, int S, int R>
+__global__ __launch_bounds__(1024) void splitk_heads_rowsw_kernel(
+    const float* __restrict__ slab, int B, int K, const float* __restrict__ bias,
+    float* __restrict__ y, const float* __restrict__ wp, int A, const float* __restrict__ wv,
+    const float* __restrict__ bp, const float* __restrict__ bv, float* __restrict__ logp,
+    float* __restrict__ pi, float* __restrict__ v) {
+  constexpr int PW = AMAX + 1;
+  __shared__ float part[R][16][PW];
+  __shared__ float sm[R][PW];
+  const int lane = threadIdx.x & 63, c = threadIdx.x >> 6;
+  const int nchunks = blockDim.x >> 6;
+  const int r0 = blockIdx.x * R;
+  const int k = c * HEADS_KC + lane * 4;
+  const bool kin = k < K;
+  const int kc = kin ? k : 0;
+  const size_t plane = (size_t)B * K;
+  f32x4 sv[R][S];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const size_t off = (size_t)min(r0 + i, B - 1) * K + kc;
+#pragma unroll
+    for (int q = 0; q < S; ++q) sv[i][q] = *reinterpret_cast<const f32x4*>(slab + q * plane + off);
+  }
+  f32x4 w[AMAX + 1];
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a)
+    w[a] = *reinterpret_cast<const f32x4*>(wp + (size_t)min(a, A - 1) * K + kc);
+  w[AMAX] = *reinterpret_cast<const f32x4*>(wv + kc);
+  const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + kc);
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) w[a] = (a < A && kin) ? w[a] : z;
+  w[AMAX] = kin ? w[AMAX] : z;
+  constexpr int LOGV = AMAX == 8 ? 3 : (AMAX == 16 ? 4 : 5);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = r0 + i;
+    if (row >= B) break;
+    f32x4 x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < S; ++q) t += sv[i][q][e];
+      x[e] = kin ? t + bb[e] : 0.f;
+    }
+    if (kin) *reinterpret_cast<f32x4*>(y + (size_t)row * K + k) = x;
+    float pv[AMAX];
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a)
+      pv[a] = fmaf(x[3], w[a][3], fmaf(x[2], w[a][2], fmaf(x[1], w[a][1], x[0] * w[a][0])));
+    const float ps = wave_multi_sum<AMAX>(pv);
+    const float vs = wave_sum(
+        fmaf(x[3], w[AMAX][3], fmaf(x[2], w[AMAX][2], fmaf(x[1], w[AMAX][1], x[0] * w[AMAX][0]))));
+    const int a = lane >> (6 - LOGV);
+    if ((lane & ((1 << (6 - LOGV)) - 1)) == 0 && a < A) part[i][c][a] = ps;
+    if (lane == 0) part[i][c][A] = vs;
+  }
+  __syncthreads();
+  const int W = A + 1;
+  if (threadIdx.x < R * PW) {
+    const int i = threadIdx.x / PW, a = threadIdx.x % PW;
+    if (a < W) {
+      float s = 0.f;
+      for (int cc = 0; cc < nchunks; ++cc) s += part[i][cc][a];
+      sm[i][a] = s;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < R) {
+    const int i = threadIdx.x, row = r0 + i;
+    if (row < B) {
+      float l[AMAX];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a)
+        if (a < A) {
+          l[a] = sm[i][a] + bp[a];
+          mx = fmaxf(mx, l[a]);
+        }
+      float se = 0.f;
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a)
+        if (a < A) se += expf(l[a] - mx);
+      const float lse = logf(se);
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a)
+        if (a < A) {
+          const float o = (l[a] - mx) - lse;
+          logp[(size_t)row * A + a] = o;
+          if (pi) pi[(size_t)row * A + a] = expf(o);
+        }
+      v[row] = tanhf(sm[i][A] + bv[0]);
+    }
+  }
+}
+
 // Connect4 trunk + policy/value heads in ONE launch for small batches (the batch-1 MCTS leaf):
 // c4_trunk_kernel's body, then each of the block's boards runs heads_row_block on its feature
 // row straight from the LDS staging tile -- same values and arithmetic as az_c4_trunk_fwd +
@@ -612,6 +764,38 @@ extern "C" int az_linear_heads_fwd(const float* x, int B, int F, const float* w,
   int S = 1;
   if ((rc = gemm_f32_partial(&d, s, &S))) return rc;
   const float* sl = static_cast<const float*>(slabs);
+  // one launch: splitk_heads_rowsw_kernel (AZ_SPLITK_HEADS_MODE = rows / chunks select the
+  // one-row-per-block kernel / chunk partials + finalize for A/B runs)
+  static const char* env_mode = getenv("AZ_SPLITK_HEADS_MODE");
+  const char mode = env_mode ? env_mode[0] : 'w';   // w: rowsw, r: rows, c: chunks + finalize
+  const bool rows_mode = mode != 'c' && F <= SPLITK_ROWS_MAXK &&
+                         (F + HEADS_KC - 1) / HEADS_KC <= HEADS_ROWS_MAXC;
+  const int nch = (F + HEADS_KC - 1) / HEADS_KC;
+  static const char* env_r = getenv("AZ_SPLITK_HEADS_R");   // rows per block, A/B runs
+  const int R = env_r ? atoi(env_r) : 2;
+  if (S > 1 && A <= 8 && S <= 8 && rows_mode && mode == 'w' && nch <= 16 &&
+      (R == 1 || R == 2 || R == 4)) {
+    const dim3 g((B + R - 1) / R), blk(64 * nch);
+    switch (S * 8 + R) {
+#define AZ_SKW(SS, RR) case SS * 8 + RR: hipLaunchKernelGGL((splitk_heads_rowsw_kernel<8, SS, RR>), g, \
+                           blk, 0, s, sl, B, F, b, y, wp, A, wv, bp, bv, logp, pi, v); break;
+      AZ_SKW(2, 1) AZ_SKW(3, 1) AZ_SKW(4, 1) AZ_SKW(5, 1) AZ_SKW(6, 1) AZ_SKW(7, 1) AZ_SKW(8, 1)
+      AZ_SKW(2, 2) AZ_SKW(3, 2) AZ_SKW(4, 2) AZ_SKW(5, 2) AZ_SKW(6, 2) AZ_SKW(7, 2) AZ_SKW(8, 2)
+      AZ_SKW(2, 4) AZ_SKW(3, 4) AZ_SKW(4, 4) AZ_SKW(5, 4) AZ_SKW(6, 4) AZ_SKW(7, 4) AZ_SKW(8, 4)
+#undef AZ_SKW
+    }
+    return check_launch("splitk_heads_rowsw_kernel");
+  }
+  if (S > 1 && A <= 8 && S <= 8 && rows_mode) {
+    switch (S) {
+#define AZ_SKR(SS) case SS: hipLaunchKernelGGL((splitk_heads_rows_kernel<8, SS>), dim3(B), dim3(512), \
+                                              0, s, sl, B, F, b, y, wp, A, wv, bp, bv, logp, pi, v); break;
+      AZ_SKR(2) AZ_SKR(3) AZ_SKR(4) AZ_SKR(5) AZ_SKR(6) AZ_SKR(7)
+      default: AZ_SKR(8)
+#undef AZ_SKR
+    }
+    return check_launch("splitk_heads_rows_kernel");
+  }
   if (S > 1 && A <= 8 && S <= 8) {
     switch (S) {
       case 2: launch_splitk_heads<2>(sl, B, F, b, y, wp, A, wv, part, s); break;
