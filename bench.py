@@ -549,7 +549,7 @@ def main():
                        "global_batch": B * world, "batch_per_gpu": B, "feature_dim": F,
                        "parallelism": f"dp{world} (independent shards, no collective)"},
             "roofline": {"kernel": "az_gemm_f32 output_transform.0 (gemm_f32_glds2 256x128 "
-                                   "8-wave split-K 5 + splitk_reduce_kernel), Linear 3136x3136",
+                                   "8-wave split-K 5 + splitk_reduce4_kernel<5>), Linear 3136x3136",
                          "bound": "mfma", "achieved": round(achieved, 2),
                          "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,

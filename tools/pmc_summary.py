@@ -6,7 +6,7 @@ profiles/<tag>_pmc_hbm.csv and profiles/pmc.json (what bench.py reports as roofl
 HBM bytes per dispatch = (2 * FETCH_SIZE + WRITE_SIZE) KB * 1024: on gfx950 FETCH_SIZE counts
 half of the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section).  The bench's
 output_transform call is one az_gemm_f32 = the tile kernel plus, when split-K is used, the
-splitk_reduce_kernel dispatched right after it; both are charged to that call.
+split-K reduce kernel dispatched right after it; both are charged to that call.
 """
 import csv
 import collections
@@ -76,7 +76,7 @@ def main(d, tag):
                   f"bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE reports "
                   f"half of wide reads, MI355X_MICROARCH.md HBM section)",
         "gemm": {"kernel": "az_gemm_f32 output_transform.0 call (gemm_f32_glds2 tile kernel + "
-                           "splitk_reduce_kernel)",
+                           "splitk_reduce4_kernel)",
                  "dispatches": nf,
                  "hbm_bytes_per_launch": gemm_tile + gemm_red,
                  "gemm_kernel_bytes": gemm_tile, "reduce_kernel_bytes": gemm_red,
