@@ -452,12 +452,17 @@ __global__ __launch_bounds__(512) void splitk_heads_rows_kernel(
 // them for the block's R rows (the one-row-per-block kernel re-reads 113 KB of weights per row);
 // every slab load of the R rows is issued before the first add.  Per (row, chunk) arithmetic and
 // chunk-order finalize exactly as splitk_heads_partial_kernel + heads_finalize_kernel.
-template <int AMAX, int S, int R>
-__global__ __launch_bounds__(1024) void splitk_heads_rowsw_kernel(
-    const float* __restrict__ slab, int B, int K, const float* __restrict__ bias,
-    float* __restrict__ y, const float* __restrict__ wp, int A, const float* __restrict__ wv,
-    const float* __restrict__ bp, const float* __restrict__ bv, float* __restrict__ logp,
-    float* __restrict__ pi, float* __restrict__ v) {
+// Body of the R-rows-per-block heads kernels: wave c owns chunk c (blockDim = 64 * nchunks),
+// keeps that chunk's head weights in registers for the block's R rows, and gets the rows' x / y
+// float4s from load(i, kc, x, y) (all of them issued before the first FMA); then the chunk-order
+// finalize for the R rows.
+template <int AMAX, int R, typename Load>
+__device__ __forceinline__ void heads_rowsw_body(int B, int K, const float* __restrict__ wp,
+                                                 int A, const float* __restrict__ wv,
+                                                 const float* __restrict__ bp,
+                                                 const float* __restrict__ bv,
+                                                 float* __restrict__ logp, float* __restrict__ pi,
+                                                 float* __restrict__ v, Load load) {
   constexpr int PW = AMAX + 1;
   __shared__ float part[R][16][PW];
   __shared__ float sm[R][PW];
@@ -467,20 +472,13 @@ __global__ __launch_bounds__(1024) void splitk_heads_rowsw_kernel(
   const int k = c * HEADS_KC + lane * 4;
   const bool kin = k < K;
   const int kc = kin ? k : 0;
-  const size_t plane = (size_t)B * K;
-  f32x4 sv[R][S];
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const size_t off = (size_t)min(r0 + i, B - 1) * K + kc;
-#pragma unroll
-    for (int q = 0; q < S; ++q) sv[i][q] = *reinterpret_cast<const f32x4*>(slab + q * plane + off);
-  }
+  f32x4 xs[R], ys[R];
+  load(r0, kc, kin, k, xs, ys);
   f32x4 w[AMAX + 1];
 #pragma unroll
   for (int a = 0; a < AMAX; ++a)
     w[a] = *reinterpret_cast<const f32x4*>(wp + (size_t)min(a, A - 1) * K + kc);
   w[AMAX] = *reinterpret_cast<const f32x4*>(wv + kc);
-  const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + kc);
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int a = 0; a < AMAX; ++a) w[a] = (a < A && kin) ? w[a] : z;
@@ -490,22 +488,14 @@ __global__ __launch_bounds__(1024) void splitk_heads_rowsw_kernel(
   for (int i = 0; i < R; ++i) {
     const int row = r0 + i;
     if (row >= B) break;
-    f32x4 x;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float t = 0.f;
-#pragma unroll
-      for (int q = 0; q < S; ++q) t += sv[i][q][e];
-      x[e] = kin ? t + bb[e] : 0.f;
-    }
-    if (kin) *reinterpret_cast<f32x4*>(y + (size_t)row * K + k) = x;
+    const f32x4 x = kin ? xs[i] : z, y = kin ? ys[i] : z;
     float pv[AMAX];
 #pragma unroll
     for (int a = 0; a < AMAX; ++a)
       pv[a] = fmaf(x[3], w[a][3], fmaf(x[2], w[a][2], fmaf(x[1], w[a][1], x[0] * w[a][0])));
     const float ps = wave_multi_sum<AMAX>(pv);
     const float vs = wave_sum(
-        fmaf(x[3], w[AMAX][3], fmaf(x[2], w[AMAX][2], fmaf(x[1], w[AMAX][1], x[0] * w[AMAX][0]))));
+        fmaf(y[3], w[AMAX][3], fmaf(y[2], w[AMAX][2], fmaf(y[1], w[AMAX][1], y[0] * w[AMAX][0]))));
     const int a = lane >> (6 - LOGV);
     if ((lane & ((1 << (6 - LOGV)) - 1)) == 0 && a < A) part[i][c][a] = ps;
     if (lane == 0) part[i][c][A] = vs;
@@ -547,6 +537,58 @@ __global__ __launch_bounds__(1024) void splitk_heads_rowsw_kernel(
       v[row] = tanhf(sm[i][A] + bv[0]);
     }
   }
+}
+
+template <int AMAX, int S, int R>
+__global__ __launch_bounds__(1024) void splitk_heads_rowsw_kernel(
+    const float* __restrict__ slab, int B, int K, const float* __restrict__ bias,
+    float* __restrict__ y, const float* __restrict__ wp, int A, const float* __restrict__ wv,
+    const float* __restrict__ bp, const float* __restrict__ bv, float* __restrict__ logp,
+    float* __restrict__ pi, float* __restrict__ v) {
+  const size_t plane = (size_t)B * K;
+  heads_rowsw_body<AMAX, R>(B, K, wp, A, wv, bp, bv, logp, pi, v,
+                            [&](int r0, int kc, bool kin, int k, f32x4 (&xs)[R], f32x4 (&ys)[R]) {
+    f32x4 sv[R][S];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const size_t off = (size_t)min(r0 + i, B - 1) * K + kc;
+#pragma unroll
+      for (int q = 0; q < S; ++q) sv[i][q] = *reinterpret_cast<const f32x4*>(slab + q * plane + off);
+    }
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + kc);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      f32x4 x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < S; ++q) t += sv[i][q][e];
+        x[e] = kin ? t + bb[e] : 0.f;
+      }
+      if (kin && r0 + i < B) *reinterpret_cast<f32x4*>(y + (size_t)(r0 + i) * K + k) = x;
+      xs[i] = x;
+      ys[i] = x;
+    }
+  });
+}
+
+// Plain heads (x = hp rows, y = hv rows) with the same body: az_heads_fwd for B > 32, A <= 8.
+template <int AMAX, int R>
+__global__ __launch_bounds__(1024) void heads_rowsw_kernel(
+    const float* __restrict__ hp, int ldhp, const float* __restrict__ hv, int ldhv, int B, int K,
+    const float* __restrict__ wp, int A, const float* __restrict__ wv,
+    const float* __restrict__ bp, const float* __restrict__ bv, float* __restrict__ logp,
+    float* __restrict__ pi, float* __restrict__ v) {
+  heads_rowsw_body<AMAX, R>(B, K, wp, A, wv, bp, bv, logp, pi, v,
+                            [&](int r0, int kc, bool, int, f32x4 (&xs)[R], f32x4 (&ys)[R]) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = min(r0 + i, B - 1);
+      xs[i] = *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + kc);
+      ys[i] = *reinterpret_cast<const f32x4*>(hv + (size_t)row * ldhv + kc);
+    }
+  });
 }
 
 // Connect4 trunk + policy/value heads in ONE launch for small batches (the batch-1 MCTS leaf):
@@ -647,6 +689,12 @@ static void launch_heads(const float* hp, int ldhp, const float* hv, int ldhv, i
   if (B <= HEADS_ROWS_MAXB && nchunks <= HEADS_ROWS_MAXC && !two_pass) {
     hipLaunchKernelGGL(heads_rows_kernel<AMAX>, dim3(B), dim3(512), 0, s, hp, ldhp, hv, ldhv, K,
                        wp, A, wv, bp, bv, logp, pi, v);
+    return;
+  }
+  if (AMAX == 8 && nchunks <= 16 && !two_pass) {
+    // one launch, 2 rows per block, one wave per chunk (splitk_heads_rowsw_kernel's body)
+    hipLaunchKernelGGL((heads_rowsw_kernel<8, 2>), dim3((B + 1) / 2), dim3(64 * nchunks), 0, s,
+                       hp, ldhp, hv, ldhv, B, K, wp, A, wv, bp, bv, logp, pi, v);
     return;
   }
   dim3 g(nchunks, (B + HEADS_ROWS - 1) / HEADS_ROWS);
