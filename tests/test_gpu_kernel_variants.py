@@ -1,0 +1,80 @@
+"""The A/B kernel variants the C-ABI keeps behind environment switches compute the same bits as
+the default path (each switch is read once per process, so every variant runs in a child
+process of its own on the same inputs):
+  - heads: one launch with 2 rows per block (default) vs chunk partials + finalize
+    (AZ_HEADS_TWOPASS=1) -- Connect4GNN.py:48-57;
+  - the GNN tail's split-K heads: rowsw (default) vs one row per block
+    (AZ_SPLITK_HEADS_MODE=rows) vs chunk partials + finalize (=chunks) -- gnn_utils.py:115;
+  - the split-K reduce: float4 (default) vs scalar (AZ_GEMM_NOVEC=1);
+  - the 256x128 GEMM tile: 2-buffer (default) vs 3-buffer ring and its stagger
+    (AZ_GEMM_RING=3 / 4): the same k order, so the same sums."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1] + "/alphazero-gnn_amd")
+from azhip import ops
+out = {}
+F, A = 3136, 8
+for B in (33, 100, 512):
+    g = torch.Generator().manual_seed(B)
+    x = torch.rand((B, F), generator=g) * 2 - 1
+    w0 = (torch.rand((F, F), generator=g) * 2 - 1) / F ** 0.5
+    w2 = (torch.rand((F, F), generator=g) * 2 - 1) / F ** 0.5
+    b0 = (torch.rand((F,), generator=g) - 0.5) * 0.1
+    b2 = (torch.rand((F,), generator=g) - 0.5) * 0.1
+    wp = (torch.rand((A, F), generator=g) * 2 - 1) / F ** 0.5
+    wv = (torch.rand((1, F), generator=g) * 2 - 1) / F ** 0.5
+    bp, bv = torch.rand((A,), generator=g) - 0.5, torch.rand((1,), generator=g) - 0.5
+    c = [t.cuda() for t in (x, w0, b0, w2, b2, wp, bp, wv, bv)]
+    logp, pi, v, y, hid = ops.transform_heads(*c)
+    hl, hp_, hv_ = ops.heads(c[0], c[5], c[6], c[7], c[8])
+    for k, t in (("logp", logp), ("pi", pi), ("v", v), ("y", y), ("hid", hid),
+                 ("h_logp", hl), ("h_pi", hp_), ("h_v", hv_)):
+        out["%s_%d" % (k, B)] = t.cpu().numpy()
+np.savez(sys.argv[2], **out)
+print("ok")
+'''
+
+VARIANTS = {
+    "default": {},
+    "twopass_chunks": {"AZ_HEADS_TWOPASS": "1", "AZ_SPLITK_HEADS_MODE": "chunks"},
+    "rows": {"AZ_SPLITK_HEADS_MODE": "rows"},
+    "novec": {"AZ_GEMM_NOVEC": "1"},
+    "ring3": {"AZ_GEMM_RING": "3"},
+    "ring_stagger": {"AZ_GEMM_RING": "4"},
+}
+
+
+def _run(tmp_path, name, env_extra):
+    env = dict(os.environ)
+    for k in ("AZ_HEADS_TWOPASS", "AZ_SPLITK_HEADS_MODE", "AZ_GEMM_NOVEC", "AZ_GEMM_RING"):
+        env.pop(k, None)
+    env.update(env_extra)
+    path = str(tmp_path / f"{name}.npz")
+    r = subprocess.run([sys.executable, "-c", CHILD, ROOT, path], env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return dict(np.load(path))
+
+
+@pytest.mark.timeout(600)
+def test_kernel_variants_bit_identical(tmp_path):
+    ref = _run(tmp_path, "default", VARIANTS["default"])
+    for name, env in VARIANTS.items():
+        if name == "default":
+            continue
+        got = _run(tmp_path, name, env)
+        for k, a in ref.items():
+            assert np.array_equal(a, got[k]), f"{name}: {k} differs"
