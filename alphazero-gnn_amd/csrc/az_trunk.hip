@@ -691,8 +691,10 @@ static void launch_heads(const float* hp, int ldhp, const float* hv, int ldhv, i
                        wp, A, wv, bp, bv, logp, pi, v);
     return;
   }
-  if (AMAX == 8 && nchunks <= 16 && !two_pass) {
-    // one launch, 2 rows per block, one wave per chunk (splitk_heads_rowsw_kernel's body)
+  if (AMAX == 8 && nchunks <= 16 && !two_pass && B <= 2048) {
+    // one launch, 2 rows per block, one wave per chunk (splitk_heads_rowsw_kernel's body).
+    // Large B stays two-pass: its blocks reuse each weight slice for 16 rows, where rowsw
+    // re-reads all 113 KB of head weights every 2 rows (B = 65,536: 735 us vs ~0.3 ms)
     hipLaunchKernelGGL((heads_rowsw_kernel<8, 2>), dim3((B + 1) / 2), dim3(64 * nchunks), 0, s,
                        hp, ldhp, hv, ldhv, B, K, wp, A, wv, bp, bv, logp, pi, v);
     return;
