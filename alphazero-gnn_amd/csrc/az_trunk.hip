@@ -218,11 +218,20 @@ __global__ __launch_bounds__(256) void heads_partial_kernel(
   // Connect4, just re-reads the same lines from cache)
   constexpr int RPW = HEADS_ROWS / 4;
   f32x4 xs[RPW], ys[RPW];
+  if (hv == hp && ldhv == ldhp) {           // Connect4: both heads read the same rows (uniform)
 #pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const int row = min(r0 + wave + 4 * i, B - 1);
-    xs[i] = *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + kc);
-    ys[i] = *reinterpret_cast<const f32x4*>(hv + (size_t)row * ldhv + kc);
+    for (int i = 0; i < RPW; ++i) {
+      const int row = min(r0 + wave + 4 * i, B - 1);
+      xs[i] = *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + kc);
+      ys[i] = xs[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int row = min(r0 + wave + 4 * i, B - 1);
+      xs[i] = *reinterpret_cast<const f32x4*>(hp + (size_t)row * ldhp + kc);
+      ys[i] = *reinterpret_cast<const f32x4*>(hv + (size_t)row * ldhv + kc);
+    }
   }
   f32x4 w[AMAX + 1];
 #pragma unroll
