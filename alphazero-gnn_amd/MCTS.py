@@ -24,6 +24,8 @@ import math
 
 import numpy as np
 
+import nn_fallback
+
 EPS = 1e-8
 
 log = logging.getLogger(__name__)
@@ -203,8 +205,8 @@ class MCTS:
             if self._use_gnn() and s in self.gnn_predictions:
                 return self.gnn_predictions[s][1]
             return self.standard_predictions[s][1]
-        except Exception as e:  # the reference's silent degradation (MCTS.py:195-200)
-            log.error(f"Error in neural network prediction: {e}")
+        except Exception as e:  # the reference's degradation (MCTS.py:195-200), counted
+            nn_fallback.record("MCTS.search", e)
             self.Ps[s] = valids / np.sum(valids)
             self.Ns[s] = 0
             return 0

@@ -313,7 +313,15 @@ class NetWrapper:
     has_gnn = False
     makedirs_on_save = True
 
+    MAX_ACTIONS = 32      # the heads kernels keep a wave's A+1 weight chunks in registers
+
     def __init__(self, game, args):
+        A = game.getActionSize()
+        if A > self.MAX_ACTIONS:
+            # rejected up front: MCTS would otherwise swallow every predict's error and play
+            # a whole iteration on uniform priors before train() fails (MCTS.py:195-200)
+            raise ValueError(f"{type(self).__name__}: action size {A} > {self.MAX_ACTIONS} is "
+                             f"not supported by the HIP heads kernels (board {game.getBoardSize()})")
         self.device = nets.default_device()
         self.nnet = self.net_class(game, args, device=self.device)
         self.board_x, self.board_y = game.getBoardSize()

@@ -283,7 +283,7 @@ struct MT19937 {
 // the rules.  Every move is recorded; Python assembles the examples from the records with the
 // same code as the sequential path (mcts_native.assemble_episode).
 enum Phase : uint8_t { E_IDLE, E_START_MOVE, E_AP, E_EXP_CHECK, E_EXP_PRE, E_EXP_STD, E_EXP, E_MOVE,
-                       E_DONE };
+                       E_DONE, E_ABORTED };
 
 struct Episode {
   Phase phase = E_IDLE;
@@ -960,14 +960,21 @@ int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const f
       return fail(AZM_ESTATE, "az_mcts_feed: slot has no pending request");
   }
   // every leaf belongs to a different slot's tree: the expansions are independent
-#pragma omp parallel for schedule(dynamic, 8) num_threads(m->threads) if (count >= 32)
+  int aborted = 0;
+#pragma omp parallel for schedule(dynamic, 8) num_threads(m->threads) if (count >= 32) \
+    reduction(+ : aborted)
   for (int i = 0; i < count; ++i) {
     Tree& t = m->trees[m->last_order[i]];
     if (t.pending_std) {                        // expand_tree's root predict: v only
-      Node& nd = t.nodes[t.find_or_add(t.ep.board, m->R)];
-      nd.std_v = failed ? 0.f : v[i];
-      nd.std_epoch = t.epoch;
       t.pending_std = false;
+      if (failed) {                             // unguarded in the reference (MCTS.py:108-113)
+        t.ep.phase = E_ABORTED;
+        aborted += 1;
+        continue;
+      }
+      Node& nd = t.nodes[t.find_or_add(t.ep.board, m->R)];
+      nd.std_v = v[i];
+      nd.std_epoch = t.epoch;
       continue;
     }
     expand(m, t, failed ? nullptr : pi + (size_t)i * A, failed ? 0.f : v[i],
@@ -975,7 +982,7 @@ int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const f
            (failed || !m->use_gnn) ? 0.f : gv[i], failed != 0);
   }
   m->last_order.clear();
-  return AZM_OK;
+  return aborted;
 }
 
 int az_mcts_root_edges(const az_mcts* m, int slot, const int8_t* board, int32_t* nsa, double* q,

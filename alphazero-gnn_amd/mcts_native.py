@@ -19,6 +19,8 @@ import os
 
 import numpy as np
 
+import nn_fallback
+
 EPS = 1e-8
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "azhip", "libaz_mcts.so")
@@ -171,10 +173,27 @@ class Engine:
                                             int(threads)), "az_mcts_collect")
 
     def feed(self, k, pi=None, v=None, gpi=None, gv=None, failed=False):
-        arrs = [None if a is None else np.ascontiguousarray(a[:k], dtype=np.float32)
+        """Network outputs for the last collect's k leaves (or failed=True: the reference's
+        uniform-priors / v=0 path).  Returns the number of episode-mode slots whose expand_tree
+        root prediction was among the failed requests: those episodes are aborted (the
+        reference's root predict is unguarded, MCTS.py:108-113) and the caller must raise."""
+        k = int(k)
+        if not failed:
+            # the C side reads pi + i*A for i < k: check shapes here, before any pointer escapes
+            need = [("pi", pi, 2), ("v", v, 1)]
+            if self.use_gnn:
+                need += [("gpi", gpi, 2), ("gv", gv, 1)]
+            for name, a, nd in need:
+                if a is None:
+                    raise ValueError(f"Engine.feed: {name} missing")
+                a = np.asarray(a)
+                if a.ndim != nd or a.shape[0] < k or (nd == 2 and a.shape[1] != self.A):
+                    raise ValueError(f"Engine.feed: {name} has shape {a.shape}, need "
+                                     f"({'>=%d' % k}{', %d' % self.A if nd == 2 else ''})")
+        arrs = [None if (a is None or failed) else np.ascontiguousarray(a[:k], dtype=np.float32)
                 for a in (pi, v, gpi, gv)]
         ptrs = [None if a is None else _ptr(a) for a in arrs]
-        _check(lib().az_mcts_feed(self.h, int(k), *ptrs, int(bool(failed))), "az_mcts_feed")
+        return _check(lib().az_mcts_feed(self.h, k, *ptrs, int(bool(failed))), "az_mcts_feed")
 
     def root_edges(self, slot, board):
         """-> (nsa list[int], q list[float64], tags list[int])."""
@@ -437,9 +456,8 @@ class ArenaPlayer:
             idle = 0
             try:
                 pi, v, gpi, gv = _net_call(self.nnet, self.eng.leaf_boards[:k], self.use_gnn)
-            except Exception as ex:  # MCTS.py:195-200: uniform priors, value 0
-                import logging
-                logging.getLogger(__name__).error(f"Error in neural network prediction: {ex}")
+            except Exception as ex:  # MCTS.py:195-200: uniform priors, value 0 (counted)
+                nn_fallback.record("ArenaPlayer", ex, k)
                 self.eng.feed(k, failed=True)
                 continue
             self.eng.feed(k, pi, v, gpi, gv)

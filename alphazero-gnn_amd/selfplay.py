@@ -15,16 +15,23 @@ batch stays full until the last games drain.
 
 Determinism: game e draws from its own np.random.RandomState(seed(e)) for both the move
 choice (Coach.py:62) and MCTS's temp-0 tie-break (MCTS.py:39-44).  A lock-step game therefore
-plays exactly the episode the sequential reference plays after np.random.seed(seed(e)) given
-the same network outputs, independent of G and of how episodes are spread over ranks
-(tests/test_selfplay.py).  Network outputs for a row of a batch equal the batch-1 call within
-1e-5 (tests/test_gpu_kernels.py); they are not bit-identical, as the reference's own batch-1
-vs batch-B CPU GEMMs are not.
+plays exactly the episode the sequential reference plays after np.random.seed(seed(e)) GIVEN
+THE SAME NETWORK OUTPUTS PER BOARD, independent of G and of how episodes are spread over ranks
+(tests/test_selfplay.py, with recorded outputs).  On the GPU a row's outputs depend on the
+batch it rides in (the GEMM's split-K factor and tile are chosen by B): they equal the batch-1
+call within 1e-5 (tests/test_gpu_kernels.py) but not bit for bit, as the reference's own
+batch-1 vs batch-B CPU GEMMs are not.  A UCB near-tie can therefore resolve
+differently for different G or rank counts; tests/test_gpu_selfplay.py measures the action
+agreement and locates the first divergence.
+
+Network failures follow the reference (uniform priors, value 0 per leaf, MCTS.py:195-200) and
+are counted in nn_fallback; an expand_tree root predict that fails propagates (MCTS.py:108-113).
 """
 import os
 
 import numpy as np
 
+import nn_fallback
 from Coach import episode_g
 from MCTS import MCTS
 
@@ -53,6 +60,7 @@ class BatchEvaluator:
         try:
             out = fn(boards)
         except Exception as e:  # the reference degrades per leaf; a batch fails as a whole
+            # (each waiting leaf is degraded -- and counted -- in MCTS._evaluate_leaf_g)
             return [(None, None, e)] * n
         if want_gnn:
             pi, v, gpi, gv = out
@@ -240,6 +248,7 @@ class _Lane:
                 if err is None:
                     self.eng.feed(k, pi, v, gpi, gv)
                 else:
+                    nn_fallback.record("selfplay.native", err, k)
                     self.eng.feed(k, failed=True)
             for i, (slot, _) in enumerate(self.pred):
                 if err is None:
@@ -361,9 +370,15 @@ class _EpisodeLane:
         if pending is not None:
             try:
                 pi, v, gpi, gv = pending.result()
+            except Exception as err:  # the reference's per-leaf degradation (MCTS.py:195-200)
+                aborted = self.eng.feed(self.k, failed=True)
+                if aborted:
+                    # an expand_tree root predict was in the batch: unguarded in the reference
+                    # (MCTS.py:108-113), so the failure propagates out of the episode
+                    raise err
+                nn_fallback.record("selfplay.engine", err, self.k)
+            else:                     # engine errors (shapes, state) propagate as themselves
                 self.eng.feed(self.k, pi, v, gpi, gv)
-            except Exception:     # the reference's per-leaf degradation (MCTS.py:195-200)
-                self.eng.feed(self.k, failed=True)
         self.harvest()
 
     def live(self):

@@ -73,7 +73,11 @@ int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int thr
 /* Network outputs for the leaves of the last collect, same order: pi/gpi [count][A] float32
  * probabilities, v/gv [count] float32 (gpi/gv may be NULL when use_gnn == 0).  failed != 0
  * applies the reference's exception path to every leaf (uniform priors, value 0,
- * MCTS.py:195-200).  Expands each leaf and backs its value up the searched path. */
+ * MCTS.py:195-200).  Expands each leaf and backs its value up the searched path.
+ * A failed request that was an episode slot's expand_tree root prediction is NOT degraded:
+ * that predict is unguarded in the reference (MCTS.py:108-113), so the episode is aborted (it
+ * is never reported finished).  Returns the number of episodes aborted this way (>= 0; the
+ * caller raises the network's exception when it is non-zero) or an error code. */
 int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const float* gpi,
                  const float* gv, int failed);
 

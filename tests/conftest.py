@@ -15,6 +15,21 @@ for p in (ROOT, PKG):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP library)")
     config.addinivalue_line("markers", "slow: takes more than a few seconds on CPU")
+    config.addinivalue_line("markers", "nn_failures_expected: the test injects network "
+                                       "failures on purpose (skips the zero-fallback check)")
+
+
+@pytest.fixture(autouse=True)
+def _no_silent_nn_fallbacks(request):
+    """the reference silently degrades a failed network call to uniform priors
+    and v=0 (MCTS.py:195-200).  Every such event is counted (nn_fallback); a test that ends
+    with a non-zero count fails, so a broken kernel cannot pass as degraded play."""
+    import nn_fallback
+    nn_fallback.reset()
+    yield
+    if request.node.get_closest_marker("nn_failures_expected") is None:
+        assert nn_fallback.total() == 0, f"network fallbacks occurred: {nn_fallback.counts()}"
+    nn_fallback.reset()
 
 
 def golden(name):

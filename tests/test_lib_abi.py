@@ -104,3 +104,13 @@ def test_host_side_validation_without_gpu(built):
     assert L.az_c4_trunk_heads_fwd(None, 3, *bad_a) == AZ_EINVAL
     assert b"A=40" in L.az_last_error()
     assert L.az_host_free(None) == AZ_OK
+
+
+def test_unsupported_action_size_rejected_up_front():
+    """A board whose action size exceeds the heads kernels' limit (TicTacToe n >= 6: A = 37) is
+    rejected when the wrapper is built, with a clear error -- not per predict, where MCTS would
+    swallow it and play a whole iteration on uniform priors (MCTS.py:195-200)."""
+    from tictactoe.TicTacToeGNN import TicTacToeGNNWrapper
+    from tictactoe.TicTacToeGame import TicTacToeGame
+    with pytest.raises(ValueError, match="action size 37"):
+        TicTacToeGNNWrapper(TicTacToeGame(6), {"use_gnn": True, "gnn_layers": 2})

@@ -196,10 +196,12 @@ def test_native_matches_python_mcts_fuzz(gi, use_gnn):
         assert _norm_gnn(nat[e][1]) == _norm_gnn(py[e][1]), e
 
 
+@pytest.mark.nn_failures_expected
 def test_native_engine_errors_and_failed_batches():
+    import nn_fallback
     from connect4.Connect4Game import Connect4Game
     from mcts_native import Engine
-    from selfplay import play_episodes_native
+    from selfplay import play_episodes_engine, play_episodes_native
     eng = Engine(Connect4Game(7), 2, 1.0, False)
     b = np.zeros((7, 7), np.int8)
     eng.begin(0, b, 3)
@@ -211,14 +213,35 @@ def test_native_engine_errors_and_failed_batches():
     assert k == 1 and eng.leaf_slots[0] == 0
     with pytest.raises(RuntimeError):
         eng.feed(2, np.ones((2, 8), np.float32) / 8, np.zeros(2, np.float32))
+    # misshaped network outputs are rejected before any pointer reaches the C side
+    with pytest.raises(ValueError):
+        eng.feed(1, np.ones((1, 7), np.float32) / 7, np.zeros(1, np.float32))
+    with pytest.raises(ValueError):
+        eng.feed(1, np.ones((0, 8), np.float32), np.zeros(1, np.float32))
+    with pytest.raises(ValueError):
+        eng.feed(1, np.ones((1, 8), np.float32) / 8, None)
 
     class Broken:
         def predict_batch(self, boards):
             raise RuntimeError("device lost")
 
+        def predict_both(self, boards):
+            raise RuntimeError("device lost")
+
     args = Args(numMCTSSims=4, cpuct=1.0, tempThreshold=15, use_gnn=False)
     out = play_episodes_native(Connect4Game(7), Broken(), args, [0, 1], {0: 0, 1: 1}, 2)
     assert len(out) == 2 and all(len(std) > 0 for std, _ in out.values())
+    assert nn_fallback.counts().get("selfplay.native", 0) > 0
+    n0 = nn_fallback.total()
+    out = play_episodes_engine(Connect4Game(7), Broken(), args, [0, 1], {0: 0, 1: 1}, 2,
+                               threads=1)
+    assert len(out) == 2 and nn_fallback.counts().get("selfplay.engine", 0) > 0
+    assert nn_fallback.total() > n0
+    # with the GNN path, expand_tree's root predict is unguarded (MCTS.py:108-113): the
+    # engine aborts the episode and the driver re-raises the network's exception
+    gargs = Args(numMCTSSims=4, cpuct=1.0, tempThreshold=15, use_gnn=True, expand_by=2)
+    with pytest.raises(RuntimeError, match="device lost"):
+        play_episodes_engine(Connect4Game(7), Broken(), gargs, [0], {0: 0}, 1, threads=1)
 
 
 def test_rng_emulation_matches_numpy_randomstate(host_lib):

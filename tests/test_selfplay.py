@@ -70,9 +70,12 @@ def test_lockstep_games_equal_reference_episodes(case, parallel, batched):
         assert max(net.batches) > 1          # leaves really were evaluated together
 
 
-def test_lockstep_batch_failure_degrades_like_reference():
+@pytest.mark.nn_failures_expected
+def test_lockstep_batch_failure_degrades_like_reference(monkeypatch):
     """A failing batched call gives every waiting leaf uniform priors and value 0
-    (MCTS.py:195-200), and the games still finish."""
+    (MCTS.py:195-200), and the games still finish -- but every degraded leaf is counted, and
+    AZ_STRICT_NN=1 turns the degradation into an error."""
+    import nn_fallback
     from connect4.Connect4Game import Connect4Game
     from selfplay import play_episodes
 
@@ -84,3 +87,32 @@ def test_lockstep_batch_failure_degrades_like_reference():
     out = play_episodes(Connect4Game(7), Broken(), args, [0, 1], {0: 0, 1: 1},
                         parallel_games=2)
     assert len(out) == 2 and all(len(std) > 0 for std, _ in out.values())
+    moves = sum(len(std) // 2 for std, _ in out.values())
+    # every search hits exactly one new (failing) leaf or a terminal / known node
+    assert 0 < nn_fallback.counts()["MCTS.search"] <= moves * 4
+    monkeypatch.setenv("AZ_STRICT_NN", "1")
+    with pytest.raises(nn_fallback.NNFailure):
+        play_episodes(Connect4Game(7), Broken(), args, [0], {0: 0}, parallel_games=1)
+
+
+@pytest.mark.nn_failures_expected
+def test_gnn_root_predict_failure_propagates():
+    """expand_tree's root predict is unguarded in the reference (MCTS.py:108-113): a network
+    that fails there ends the episode with the exception instead of a v=0 training target."""
+    from connect4.Connect4Game import Connect4Game
+    from selfplay import play_episodes
+
+    class FailsOnRoot:
+        """Serves search leaves, fails on the standard-only root request of expand_tree."""
+
+        def predict_batch(self, boards):
+            raise RuntimeError("root predict failed")
+
+        def predict_both(self, boards):
+            n = len(boards)
+            return (np.full((n, 8), 0.125, np.float32), np.zeros(n, np.float32),
+                    np.full((n, 8), 0.125, np.float32), np.zeros(n, np.float32))
+
+    args = Args(numMCTSSims=3, cpuct=1.0, tempThreshold=15, use_gnn=True, expand_by=2)
+    with pytest.raises(RuntimeError, match="root predict failed"):
+        play_episodes(Connect4Game(7), FailsOnRoot(), args, [0], {0: 0}, parallel_games=1)
