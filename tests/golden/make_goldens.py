@@ -21,6 +21,8 @@ Fixtures:
   G6 mcts_c4.npz/json    Connect4 self-play episodes (sims 25, no GNN): per-move root counts/pi/choices,
                          every NN output the search requested, the examples
      mcts_ttt3.npz/json  TicTacToe 3x3 GNN self-play episodes with expand_tree
+     mcts_c4_gnn.npz/json  Connect4 GNN self-play at the north-star setting (sims 100, use_gnn,
+                         expand_tree; G1 CNN weights + G2 GNN weights), episodes 0-2
   G7 coach_ttt3.json     one full TicTacToe 3x3 GNN Coach iteration (seeds 0): counts, arena W/L/D
   G8 rules.npz           game rules on random-play positions (Connect4 n=7,5; TicTacToe n=3,4):
                          getGameEnded for both players, getValidMoves, every legal next state,
@@ -363,7 +365,7 @@ def _tag(x):
     return type(x).__name__
 
 
-def run_episodes(game, net, args, episodes, name, n):
+def run_episodes(game, net, args, episodes, name, n, compress=False):
     coach = ref_coach.Coach.__new__(ref_coach.Coach)  # skip pnet construction (Coach.py:21)
     coach.game, coach.args = game, args
     rec = Recorder(net)
@@ -419,7 +421,8 @@ def run_episodes(game, net, args, episodes, name, n):
         json.dump(dict(args=dict(args), moves=moves, episodes=results), f)
     std = list(rec.std.values())
     gnn = list(rec.gnn.values())
-    np.savez(out(name + ".npz"),
+    (np.savez_compressed if compress else np.savez)(
+             out(name + ".npz"),
              std_boards=np.stack([s[0] for s in std]).reshape(-1, n, n),
              std_pi=np.stack([s[1] for s in std]).astype(np.float32),
              std_v=np.array([s[2] for s in std], np.float32),
@@ -434,6 +437,25 @@ def g6(c4net, tttnet):
     run_episodes(Connect4Game(7), c4net, base_args(numMCTSSims=25), [0, 1], "mcts_c4", 7)
     run_episodes(TicTacToeGame(3), tttnet, base_args(numMCTSSims=10, use_gnn=True),
                  [0, 1, 2], "mcts_ttt3", 3)
+
+
+def g6b():
+    """Connect4 7x7, use_gnn, numMCTSSims 100 (the config-3 search, Coach.py:48-60 with
+    expand_tree): the network is the reference's Connect4GNNWrapper with the G1 CNN weights
+    (read back from c4_net.npz) and the G2 synthetic GNN weights (PCG64 seed 1234)."""
+    z = np.load(out("c4_net.npz"))
+    c4sd = {k[2:]: z[k] for k in z.files if k.startswith("w/")}
+    game = Connect4Game(7)
+    torch.manual_seed(0)
+    g = Connect4GNNWrapper(game, base_args(use_gnn=True))
+    g.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in c4sd.items()})
+    gsd = W.synthetic_state_dict(W.gnn_spec(3136, 2), GNN_C4_SEED)
+    g.gnn.load_state_dict({k: torch.from_numpy(v) for k, v in gsd.items()})
+    del gsd
+    t0 = time.time()
+    run_episodes(game, g, base_args(numMCTSSims=100, use_gnn=True), [0, 1, 2], "mcts_c4_gnn", 7,
+                 compress=True)
+    print(f"  G6b episodes {time.time() - t0:.1f}s")
 
 
 # ----------------------------------------------------------------------------------- G7
@@ -546,6 +568,10 @@ def main():
     if want == {"g8"}:
         g8()
         print(f"G8 done {time.time() - t0:.1f}s")
+        return
+    if want == {"g6b"}:
+        g6b()
+        print(f"G6b done {time.time() - t0:.1f}s")
         return
     c4net, c4b = g1()
     print(f"G1 done {time.time() - t0:.1f}s")

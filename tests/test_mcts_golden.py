@@ -106,6 +106,13 @@ def test_connect4_selfplay_matches_reference():
     run_golden("mcts_c4", Connect4Game(7), 7)
 
 
+def test_connect4_gnn_sims100_selfplay_matches_reference():
+    """The north-star search setting (config 3): Connect4, use_gnn, 100 simulations,
+    expand_tree targets (Coach.py:48-60, MCTS.py:60-149), three episodes."""
+    from connect4.Connect4Game import Connect4Game
+    run_golden("mcts_c4_gnn", Connect4Game(7), 7)
+
+
 def test_tictactoe_gnn_selfplay_with_expand_tree_matches_reference():
     from tictactoe.TicTacToeGame import TicTacToeGame
     run_golden("mcts_ttt3", TicTacToeGame(3), 3)

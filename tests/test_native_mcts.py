@@ -111,11 +111,11 @@ def _native_episodes(game, net, args, eps, seeds, parallel, threads=2, per_move=
             mcts_native.NativeMCTS.getActionProb_g = orig
 
 
-@pytest.mark.parametrize("case", ["mcts_c4", "mcts_ttt3"])
+@pytest.mark.parametrize("case", ["mcts_c4", "mcts_ttt3", "mcts_c4_gnn"])
 def test_native_episodes_equal_reference(case):
     from connect4.Connect4Game import Connect4Game
     from tictactoe.TicTacToeGame import TicTacToeGame
-    game = Connect4Game(7) if case == "mcts_c4" else TicTacToeGame(3)
+    game = TicTacToeGame(3) if case == "mcts_ttt3" else Connect4Game(7)
     meta = json.load(open(os.path.join(GOLDEN, case + ".json")))
     net = BatchedRecordedNet(golden(case + ".npz"), 0)
     eps = [ep["episode"] for ep in meta["episodes"]]
@@ -275,13 +275,13 @@ def test_rng_emulation_matches_numpy_randomstate(host_lib):
                 assert out.tolist() == [int(rs.choice(n, p=p)) for _ in range(200)], (seed, n)
 
 
-@pytest.mark.parametrize("case", ["mcts_c4", "mcts_ttt3"])
+@pytest.mark.parametrize("case", ["mcts_c4", "mcts_ttt3", "mcts_c4_gnn"])
 def test_engine_episodes_equal_reference(case):
     """Whole episodes in the engine (episode mode) reproduce the reference's examples."""
     from connect4.Connect4Game import Connect4Game
     from tictactoe.TicTacToeGame import TicTacToeGame
     from selfplay import play_episodes_engine
-    game = Connect4Game(7) if case == "mcts_c4" else TicTacToeGame(3)
+    game = TicTacToeGame(3) if case == "mcts_ttt3" else Connect4Game(7)
     meta = json.load(open(os.path.join(GOLDEN, case + ".json")))
     net = BatchedRecordedNet(golden(case + ".npz"), 0)
     eps = [ep["episode"] for ep in meta["episodes"]]
