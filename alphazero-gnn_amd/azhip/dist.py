@@ -7,13 +7,19 @@ torch.distributed with backend "nccl" (RCCL over xGMI) on the GPU box, "gloo" in
 * the global host RNG streams (`random`, `np.random`) are seeded identically on every rank at
   the start of Coach.learn, so shuffles, batch sampling (np.random.randint,
   Connect4GNN.py:142-143) and arena tie-breaks agree across ranks;
-* train: "replicas" (default) -- every rank runs the identical step, no collective: the
-  kernels are deterministic (no float atomics), so parameters stay bit-identical, which
-  `params_in_sync` checks with one scalar all-reduce; "allreduce" -- the CNN step's 64 rows are
-  split over ranks (loss normalised by the global batch) and the flat gradient buffer
-  (47,049 floats for Connect4) is summed with one all_reduce before the identical Adam step.
-  The GNN step couples all rows through the star's row 0 and its 478.6 MB gradient would cost
-  far more on xGMI than the ~20 µs of step compute, so it stays replicated.
+* train (args.train_parallel):
+  "replicas" (default) -- every rank runs the identical step, no collective: the kernels are
+  deterministic (no float atomics), so parameters stay bit-identical, which `params_in_sync`
+  checks with one scalar all-reduce;
+  "allreduce" -- data parallel over the sampled rows (azhip/train.py): the CNN step's rows are
+  split over ranks (loss normalised by the global batch) and the flat 188 KB gradient is summed
+  with one all_reduce; the GNN step uses SURVEY.md §8e's scheme (row-sharded trunk, gathered
+  features, the star's row-0 layer stack on every rank, own-row output_transform / heads / loss,
+  gradient all_reduce(SUM)) in one of two gradient-exchange forms (args.gnn_grad_sync):
+  "row0" (default) broadcasts d loss / d x_L[0] (12.5 KB) so every rank computes the identical
+  layer gradients itself and only output_transform's 78.7 MB is all-reduced; "flat" is the
+  literal one-bucket all_reduce of the whole 478.6 MB gradient (layer parts from row 0's owner).
+  DESIGN.md §5 says why "replicas" stays the default.
 """
 import random
 
@@ -83,6 +89,38 @@ def allreduce_sum_(t):
         import torch.distributed as dist
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
+
+
+def broadcast_(t, src=0):
+    if dist_ok():
+        import torch.distributed as dist
+        dist.broadcast(t, src=src)
+    return t
+
+
+def gather_rows(own, n, world, rank):
+    """The [n, F] matrix whose rows row_shard(n, world, r) are rank r's `own` rows, on every
+    rank.  RCCL: one all_gather_into_tensor of equal-size padded shards.  Other backends (gloo
+    cannot all-gather device tensors): an all_reduce(SUM) of a zero matrix holding only this
+    rank's rows -- exact, since every element is one rank's value plus zeros."""
+    r0, r1 = row_shard(n, world, rank)
+    F = own.shape[1]
+    if not dist_ok():
+        return own.contiguous()
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl":
+        m = -(-n // world)
+        pad = torch.zeros((m, F), dtype=own.dtype, device=own.device)
+        pad[:r1 - r0] = own
+        buf = torch.empty((world * m, F), dtype=own.dtype, device=own.device)
+        dist.all_gather_into_tensor(buf, pad)
+        parts = [buf[r * m:r * m + (row_shard(n, world, r)[1] - row_shard(n, world, r)[0])]
+                 for r in range(world)]
+        return torch.cat(parts)
+    full = torch.zeros((n, F), dtype=own.dtype, device=own.device)
+    full[r0:r1] = own
+    dist.all_reduce(full, op=dist.ReduceOp.SUM)
+    return full
 
 
 def params_in_sync(flat):

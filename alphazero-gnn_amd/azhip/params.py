@@ -37,6 +37,17 @@ class FlatParams:
     def __getitem__(self, k):
         return self.views[k]
 
+    def span(self, prefix):
+        """[start, end) of the flat buffer holding every tensor whose name starts with `prefix`
+        (contiguous: tensors are laid out in spec order), e.g. "output_transform."."""
+        hits = [(o, n) for k, (o, n, _) in self.offsets.items() if k.startswith(prefix)]
+        if not hits:
+            raise KeyError(prefix)
+        s, e = hits[0][0], _align4(hits[-1][0] + hits[-1][1])
+        if sum(_align4(n) for _, n in hits) != e - s:
+            raise ValueError(f"tensors under {prefix!r} are not contiguous")
+        return s, e
+
     def keys(self):
         return self.views.keys()
 

@@ -255,3 +255,113 @@ def gnn_step(net, gnn, boards, tpi, tv, lr, seed=0, drop_mask=None):
     loss = gnn_grads(net, gnn, boards, tpi, tv, seed, drop_mask)
     adam_step(gnn, lr)
     return loss
+
+
+# ------------------------------------------------------------------------------ data parallel
+def gnn_grads_dp(net, gnn, boards, tpi, tv, seed=0, grad_sync="row0"):
+    """The GNN step's gradient, data parallel over the ranks.  `boards`, `tpi`,
+    `tv` are the GLOBAL sampled batch (identical on every rank: the host RNGs are synchronised).
+
+    The batch is ONE star: row 0 aggregates every other row, and only row 0's path reaches the
+    layer parameters (gnn_utils.py:34-74; rows 1.. pass through unchanged).  So:
+      1. the conv trunk runs on this rank's rows only (row_shard), with the global batch's
+         dropout mask sliced to them (Connect4GNN.py:178 -> extract_features, dropout on);
+      2. the features are gathered ([B, F], 800 KB at B = 64, F = 3136);
+      3. every rank runs the star's layer stack (row 0 changes; rows 1.. are copies);
+      4. output_transform, heads and the loss run on this rank's rows, normalised by the global
+         B (Connect4GNN.py:187-193), giving output_transform's gradient over these rows;
+      5. d loss / d x_L[0] lives on row 0's owner (rank 0).  grad_sync "row0": it is broadcast
+         (12.5 KB) and every rank back-propagates the layer stack from it -- identical,
+         deterministic kernels, so identical layer gradients -- and only output_transform's
+         span of the flat gradient is all-reduced; "flat": only rank 0 back-propagates the
+         layers, the other ranks' layer gradients are zero, and the whole flat gradient is
+         all-reduced in one bucket (the literal §8e exchange).
+    The conv-trunk backward stays skipped (dead work, see gnn_step).  Returns (l_pi, l_v) summed
+    over ALL rows (each rank's own-row partial sums all-reduced)."""
+    from . import dist as D
+    world, rank = D.world_rank()
+    B = boards.shape[0]
+    r0, r1 = D.row_shard(B, world, rank)
+    GG = _grads(gnn)
+    F = net.feature_dim
+    if _kind(net) == "c4":
+        drop = float(net.dropout)
+        mask = ops.dropout_mask(B * F, drop, seed, boards.device) if drop > 0.0 else None
+        own = (C4Forward(net, boards[r0:r1], drop, seed, None if mask is None else
+                         mask[r0 * F:r1 * F]).s if r1 > r0
+               else torch.empty((0, F), device=boards.device))
+    else:
+        own = (TTTForward(net, boards[r0:r1]).s if r1 > r0
+               else torch.empty((0, F), device=boards.device))
+    x = D.gather_rows(own.contiguous(), B, world, rank)
+    xs, wss = [x], []
+    graph = gnn._star(B) if B > 1 else None
+    if graph is not None:
+        for layer in gnn.layers:
+            x, ws = ops.gnn_layer(graph, x, layer.weights())
+            xs.append(x)
+            wss.append(ws)
+    Wg = gnn.params.views
+    P = gnn.params
+    GG["output_transform.0.weight"].zero_()          # a rank without rows contributes zeros
+    GG["output_transform.0.bias"].zero_()
+    GG["output_transform.2.weight"].zero_()
+    GG["output_transform.2.bias"].zero_()
+    lrows = torch.zeros((B, 2), device=boards.device)
+    d0 = torch.zeros((1, F), device=boards.device)
+    if r1 > r0:
+        xo = xs[-1][r0:r1].contiguous()
+        y, hidden = ops.mlp2(xo, Wg["output_transform.0.weight"], Wg["output_transform.0.bias"],
+                             Wg["output_transform.2.weight"], Wg["output_transform.2.bias"])
+        if _kind(net) == "c4":
+            logp, v, saved = c4_heads_fwd(net, y)
+        else:
+            logp, v, saved = ttt_heads_fwd(net, y)
+        dl, dv = ops.heads_loss_bwd(logp, v, tpi[r0:r1], tv[r0:r1], B_norm=B,
+                                    loss_rows=lrows[r0:r1])
+        dy = (c4_heads_bwd if _kind(net) == "c4" else ttt_heads_bwd)(net, y, dl, dv, saved, None)
+        own_row0 = r0 == 0 and graph is not None
+        dxo = ops.mlp2_bwd(xo, Wg["output_transform.0.weight"], Wg["output_transform.2.weight"],
+                           hidden, dy, {"w0": GG["output_transform.0.weight"],
+                                        "b0": GG["output_transform.0.bias"],
+                                        "w2": GG["output_transform.2.weight"],
+                                        "b2": GG["output_transform.2.bias"]},
+                           want_dx=own_row0)
+        if own_row0:
+            d0.copy_(dxo[0:1])
+    layer_span = (0, P.span("output_transform.")[0])
+    if graph is None:
+        GG_flat = P.grad_flat
+        GG_flat[layer_span[0]:layer_span[1]].zero_()  # 1-row input: the layers are the identity
+    else:
+        run_layers = True
+        if grad_sync == "row0":
+            D.broadcast_(d0, src=0)
+        elif grad_sync == "flat":
+            run_layers = rank == 0
+        else:
+            raise ValueError(f"grad_sync must be 'row0' or 'flat', not {grad_sync!r}")
+        if run_layers:
+            dx = torch.zeros_like(xs[-1])
+            dx[0:1] = d0                             # only row 0 reaches the layer parameters
+            for li in range(len(gnn.layers) - 1, -1, -1):
+                layer = gnn.layers[li]
+                grads = {k[len(layer.prefix):]: g for k, g in GG.items()
+                         if k.startswith(layer.prefix)}
+                dx = ops.gnn_layer_bwd(graph, xs[li], layer.weights(), wss[li], dx, grads)
+        else:
+            P.grad_flat[layer_span[0]:layer_span[1]].zero_()
+    if grad_sync == "flat":
+        D.allreduce_sum_(P.grad_flat)
+    else:
+        s, e = P.span("output_transform.")
+        D.allreduce_sum_(P.grad_flat[s:e])
+    D.allreduce_sum_(lrows)
+    return lrows.sum(0)
+
+
+def gnn_step_dp(net, gnn, boards, tpi, tv, lr, seed=0, grad_sync="row0"):
+    """gnn_step, data parallel (gnn_grads_dp) then the identical Adam step on every rank."""
+    loss = gnn_grads_dp(net, gnn, boards, tpi, tv, seed, grad_sync)
+    adam_step(gnn, lr)
+    return loss

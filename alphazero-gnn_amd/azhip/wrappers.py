@@ -476,13 +476,18 @@ class NetWrapper:
             if self.has_gnn and gnn_examples and len(gnn_examples) > 0:
                 b, p, v = self._gnn_batch(gnn_examples)
                 self.train_seed += 1
-                T.gnn_step(self.nnet, self.gnn, b, p, v, lr, seed=self.train_seed)
+                if self._dp_world() > 1:
+                    T.gnn_step_dp(self.nnet, self.gnn, b, p, v, lr, seed=self.train_seed,
+                                  grad_sync=nets._args_get(self.args, "gnn_grad_sync", "row0"))
+                else:
+                    T.gnn_step(self.nnet, self.gnn, b, p, v, lr, seed=self.train_seed)
         torch.cuda.current_stream().synchronize()
 
 
     def _dp_world(self):
-        """>1 when the CNN step is data-parallel over ranks (args.train_parallel ==
-        "allreduce" under torch.distributed); "replicas" (default) runs it whole everywhere."""
+        """>1 when the train steps are data-parallel over ranks (args.train_parallel ==
+        "allreduce" under torch.distributed: CNN rows split + gradient all_reduce, the GNN step
+        as train.gnn_step_dp); "replicas" (default) runs them whole everywhere."""
         from . import dist as D
         if nets._args_get(self.args, "train_parallel", "replicas") != "allreduce":
             return 1

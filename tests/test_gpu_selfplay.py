@@ -1,0 +1,291 @@
+"""End-to-end search parity on the MI355X (BASELINE config 3): Connect4 7x7,
+use_gnn, 100 simulations, expand_tree targets -- the setting Coach.learn runs -- with the HIP
+network, against the reference's own trace of the same episodes (tests/golden G6b,
+mcts_c4_gnn: the reference's Connect4GNNWrapper, same weights, same per-episode seeds).
+
+* the network on every board the reference's search visited: within 1e-5;
+* the sequential reference loop (Coach.executeEpisode, batch-1 predict / predict_with_gnn) with
+  the HIP network: visit counts, pi and every np.random draw per move follow the reference
+  trace; a divergence is allowed only at a UCB near-tie, |u1 - u2| below what the 1e-5 network
+  tolerance can move (checked at the first differing selection), and the agreement is reported;
+* lock-step native engine episodes (one slot) == the sequential loop, example for example;
+  wider lock step (several games per batch) is reported as an agreement rate, since a row's
+  bits depend on the batch it rides in (selfplay.py);
+* one Coach.learn iteration (self-play on the engine, train, arena, checkpoints).
+
+AZ_REPORT_DIR=<dir> writes the agreement reports there as JSON.
+"""
+import json
+import math
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden, split_weights
+from test_mcts_golden import Args, _tag
+from test_selfplay import _norm_gnn, _norm_std
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+TOL = 1e-5
+CASE = "mcts_c4_gnn"
+
+
+def _report(name, obj):
+    d = os.environ.get("AZ_REPORT_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name + ".json"), "w") as f:
+            json.dump(obj, f, indent=1)
+
+
+@pytest.fixture(scope="module")
+def c4(c4_gnn_weights):
+    from connect4.Connect4GNN import Connect4GNNWrapper
+    from connect4.Connect4Game import Connect4Game
+    w = Connect4GNNWrapper(Connect4Game(7), SimpleNamespace(dropout=0.3, gnn_layers=2))
+    w.nnet.load_state_dict(split_weights(golden("c4_net.npz"), "w/"))
+    w.gnn.load_state_dict(c4_gnn_weights)
+    return w
+
+
+@pytest.fixture(scope="module")
+def meta():
+    return json.load(open(os.path.join(GOLDEN, CASE + ".json")))
+
+
+def test_hip_outputs_on_every_visited_board(c4):
+    """Every (board -> pi, v) the reference's search requested, standard and GNN, batched."""
+    z = golden(CASE + ".npz")
+    pi, v, _, _ = c4.predict_both(z["std_boards"].astype(np.int64))
+    np.testing.assert_allclose(pi, z["std_pi"], atol=TOL)
+    np.testing.assert_allclose(v, z["std_v"], atol=TOL)
+    _, _, gpi, gv = c4.predict_both(z["gnn_boards"].astype(np.int64))
+    np.testing.assert_allclose(gpi, z["gnn_pi"], atol=TOL)
+    np.testing.assert_allclose(gv, z["gnn_v"], atol=TOL)
+
+
+class _Recorded:
+    def __init__(self, z):
+        self.std = {np.asarray(b, np.int64).tobytes(): (p, v)
+                    for b, p, v in zip(z["std_boards"], z["std_pi"], z["std_v"])}
+        self.gnn = {np.asarray(b, np.int64).tobytes(): (p, v)
+                    for b, p, v in zip(z["gnn_boards"], z["gnn_pi"], z["gnn_v"])}
+
+    def predict(self, board):
+        p, v = self.std[board.tobytes()]
+        return np.array(p, np.float32), np.float32(v)
+
+    def predict_with_gnn(self, board):
+        p, v = self.gnn[board.tobytes()]
+        return np.array(p, np.float32), np.float32(v)
+
+
+def _sequential(game, net, args, e):
+    """Coach.executeEpisode after np.random.seed(e) (the reference loop), recording per move
+    the root counts / Q / pi, every np.random.choice draw, and every UCB selection with the gap
+    between its best and second-best scores."""
+    import Coach as C
+    import MCTS as M
+    coach = C.Coach.__new__(C.Coach)
+    coach.game, coach.args, coach.nnet = game, args, net
+    A = game.getActionSize()
+    moves, choices, selects = [], [], []
+    orig_choice, orig_select = np.random.choice, M.MCTS._select
+
+    def rec_choice(*a, **k):
+        r = orig_choice(*a, **k)
+        choices.append(int(r))
+        return r
+
+    def rec_select(self, s):
+        a = orig_select(self, s)
+        us = []
+        for b in range(A):
+            if not self.Vs[s][b]:
+                continue
+            P = self.Ps[s][b]
+            if (s, b) in self.Qsa:
+                u = self.Qsa[(s, b)] + args.cpuct * P * math.sqrt(self.Ns[s]) / (1 + self.Nsa[(s, b)])
+            else:
+                u = args.cpuct * P * math.sqrt(self.Ns[s] + M.EPS)
+            us.append(float(u))
+        us.sort(reverse=True)
+        selects.append((s, int(a), us[0] - us[1] if len(us) > 1 else math.inf, self.Ns[s]))
+        return a
+
+    np.random.choice, M.MCTS._select = rec_choice, rec_select
+    try:
+        np.random.seed(e)
+        coach.mcts = mc = M.MCTS(game, net, args)
+        orig = mc.getActionProb_g
+
+        def gap(board, temp=1):
+            pi = yield from orig(board, temp=temp)
+            s = game.stringRepresentation(board)
+            moves.append(dict(board=board.astype(np.int8).tolist(), temp=temp,
+                              counts=[int(mc.Nsa.get((s, a), 0)) for a in range(A)],
+                              q=[float(mc.Qsa[(s, a)]) if (s, a) in mc.Qsa else None
+                                 for a in range(A)],
+                              qtype=[_tag(mc.Qsa[(s, a)]) if (s, a) in mc.Qsa else None
+                                     for a in range(A)],
+                              pi=[float(x) for x in pi], choices=len(choices)))
+            return pi
+
+        mc.getActionProb_g = gap
+        std, gnn = coach.executeEpisode()
+    finally:
+        np.random.choice, M.MCTS._select = orig_choice, orig_select
+    return dict(moves=moves, choices=choices, selects=selects, std=std, gnn=gnn)
+
+
+_SEQ = {}
+
+
+def _hip_sequential(c4, meta, e):
+    from connect4.Connect4Game import Connect4Game
+    if e not in _SEQ:
+        _SEQ[e] = _sequential(Connect4Game(7), c4, Args(meta["args"]), e)
+    return _SEQ[e]
+
+
+def test_sequential_search_with_hip_net_follows_reference(c4, meta):
+    from connect4.Connect4Game import Connect4Game
+    args = Args(meta["args"])
+    rec = _Recorded(golden(CASE + ".npz"))
+    report = []
+    for ep, ref_moves in zip(meta["episodes"], meta["moves"]):
+        e = ep["episode"]
+        hip = _hip_sequential(c4, meta, e)
+        matched, first = 0, None
+        for i, ref in enumerate(ref_moves):
+            if i >= len(hip["moves"]):
+                first = first or {"move": i, "why": "episode ended early"}
+                break
+            got = hip["moves"][i]
+            same = all(got[k] == ref[k] for k in ("board", "temp", "counts", "pi")) and \
+                hip["choices"][:got["choices"]] == ep["choices"][:got["choices"]]
+            if not same:
+                first = {"move": i}
+                break
+            for a, b in zip(got["q"], ref["q"]):
+                assert (a is None) == (b is None) and (a is None or abs(a - b) <= TOL), (e, i)
+            matched += 1
+        entry = {"episode": e, "reference_moves": len(ref_moves), "hip_moves": len(hip["moves"]),
+                 "agreeing_moves": matched, "first_divergence": first}
+        if first is None:
+            assert len(hip["moves"]) == len(ref_moves)
+            assert _norm_std(hip["std"]) == [tuple(x) for x in ep["std_examples"]]
+            got = _norm_gnn(hip["gnn"])
+            assert len(got) == len(ep["gnn_examples"])
+            for a, b in zip(got, ep["gnn_examples"]):
+                assert (a[0], a[1], a[2], a[4], a[6]) == (b[0], b[1], b[2], b[4], b[6])
+                assert abs(a[3] - b[3]) <= TOL and abs(a[5] - b[5]) <= TOL    # values: 1e-5
+        else:
+            # locate the first UCB selection that differs and check it was a near-tie
+            ref_run = _sequential(Connect4Game(7), rec, args, e)
+            k = next(j for j, (x, y) in enumerate(zip(ref_run["selects"], hip["selects"]))
+                     if x[:2] != y[:2])
+            s, _, gap_ref, ns = ref_run["selects"][k]
+            bound = 2.0 * (TOL + 2.0 * TOL * args.cpuct * math.sqrt(ns + 1))
+            first.update(select_index=k, gap=gap_ref, bound=bound)
+            assert gap_ref <= bound, entry
+        report.append(entry)
+    total = sum(r["reference_moves"] for r in report)
+    agree = sum(r["agreeing_moves"] for r in report)
+    _report("c4_gnn_sims100_sequential_agreement",
+            {"case": CASE, "agreement": agree / total, "episodes": report})
+    assert agree > 0
+
+
+def test_engine_one_slot_equals_sequential_hip(c4, meta):
+    """Lock-step native engine episodes with one slot (every round a batch of one) produce the
+    sequential reference loop's examples exactly, with the same HIP network."""
+    from connect4.Connect4Game import Connect4Game
+    from selfplay import play_episodes_engine
+    eps = [ep["episode"] for ep in meta["episodes"]]
+    out = play_episodes_engine(Connect4Game(7), c4, Args(meta["args"]), eps, {e: e for e in eps},
+                               parallel_games=1, threads=2, lanes=1)
+    for e in eps:
+        hip = _hip_sequential(c4, meta, e)
+        assert _norm_std(out[e][0]) == _norm_std(hip["std"]), e
+        assert _norm_gnn(out[e][1]) == _norm_gnn(hip["gnn"]), e
+
+
+def test_wide_lockstep_agreement_report(c4, meta):
+    """Several games per batch (engine slots G = 3 and the Python lock-step driver): episodes
+    may leave the sequential loop only at UCB near-ties; report the example agreement."""
+    from connect4.Connect4Game import Connect4Game
+    from selfplay import play_episodes, play_episodes_engine
+    eps = [ep["episode"] for ep in meta["episodes"]]
+    args = Args(meta["args"])
+    rep = {}
+    for name, run in (("engine_G3", lambda: play_episodes_engine(
+            Connect4Game(7), c4, args, eps, {e: e for e in eps}, parallel_games=3, threads=3,
+            lanes=1)),
+                      ("python_G3", lambda: play_episodes(
+            Connect4Game(7), c4, args, eps, {e: e for e in eps}, parallel_games=3))):
+        out = run()
+        same = tot = 0
+        firsts = {}
+        for e in eps:
+            a, b = _norm_std(out[e][0]), _norm_std(_hip_sequential(c4, meta, e)["std"])
+            n = min(len(a), len(b))
+            k = next((i for i in range(n) if a[i] != b[i]), n)
+            firsts[e] = None if a == b else k // 2          # 2 examples (symmetries) per move
+            same += k
+            tot += len(b)
+        rep[name] = {"example_agreement": same / tot, "first_divergent_move": firsts}
+    _report("c4_gnn_sims100_lockstep_agreement", rep)
+    assert all(r["example_agreement"] > 0 for r in rep.values())
+
+
+def test_batch_row_bit_identity_report(c4):
+    """Which batch sizes give a row the batch-1 bits (the premise of exact lock-step parity):
+    rows always agree within 1e-5; bit identity is reported."""
+    z = golden("c4_gnn.npz")
+    boards = np.concatenate([z["boards"]] * 8).astype(np.int64)
+    ref = [np.concatenate([np.asarray(x).ravel() for x in c4.predict_both(boards[i:i + 1])])
+           for i in range(4)]
+    rep = {}
+    for B in (1, 2, 3, 4, 8, 16, 32, 64, 256, 512):
+        out = c4.predict_both(boards[:B])
+        rows = [np.concatenate([np.asarray(x[i]).ravel() for x in out]) for i in range(4)
+                if i < B]
+        for a, b in zip(rows, ref):
+            np.testing.assert_allclose(a, b, atol=TOL)
+        rep[B] = all(np.array_equal(a, b) for a, b in zip(rows, ref))
+    _report("batch_row_bit_identity", rep)
+    assert rep[1]
+
+
+def test_coach_learn_connect4_gnn_sims100(tmp_path):
+    """Config 3 end to end on the GPU: connect4/config.yaml + --use_gnn --numMCTSSims 100,
+    self-play on the native engine (lock step), train, arena, checkpoints; no network fallback
+    (checked by the autouse fixture in conftest.py)."""
+    import main as M
+    from Coach import Coach
+    from register import get_game
+    args = M.config_to_args(M.load_config(os.path.join(M.HERE, "connect4", "config.yaml")))
+    args.update(numIters=1, use_gnn=True, gnn_layers=2, game="connect4", load_model=False,
+                numEps=4, parallel_games=4, numMCTSSims=100, arenaCompare=2, epochs=2)
+    folder = str(tmp_path / "connect4")
+    os.makedirs(folder)
+    args.checkpoint, args.load_folder_file = folder, (folder, "best_gnn.pth.tar")
+    np.random.seed(3)
+    GameClass, NNet = get_game("connect4", use_gnn=True)
+    game = M.create_game_instance(GameClass, args)
+    coach = Coach(game, NNet(game, args), args)
+    coach.learn()
+    std, gnn = coach.trainExamplesHistory[0]
+    assert len(std) == 2 * len(gnn) and len(gnn) >= 4 * 7
+    for b, p, r in std:
+        assert b.shape == (7, 7) and abs(sum(p) - 1) < 1e-6 and abs(r) in (1, 1e-4)
+    for x in gnn:
+        assert len(x) == 7 and abs(np.sum(x[2]) - 1) < 1e-9 and abs(np.sum(x[4]) - 1) < 1e-9
+    files = sorted(os.listdir(folder))
+    assert {"best_gnn.pth.tar", "checkpoint_1_gnn.pth.tar", "checkpoint_0_gnn.pth.tar.examples",
+            "temp.pth.tar"} <= set(files), files
