@@ -136,7 +136,7 @@ class Coach:
         """Coach.py:87-176.  Under torch.distributed every rank runs this loop on identical
         data (host RNGs synchronised here); only rank 0 writes files."""
         use_gnn = _flag(self.args, "use_gnn")
-        if D.world_rank()[0] > 1:
+        if D.dist_ok():        # any process group, world size 1 included: same RNG use for any P
             D.sync_host_rngs()
         for i in range(1, self.args.numIters + 1):
             log.info(f"Starting Iter #{i} ...")
