@@ -95,6 +95,15 @@ SIGNATURES = {
     "az_gnn_aggregate_fwd": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int, c_void_p,
                                      c_void_p, c_int, c_void_p]),
     "az_gnn_layer_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "az_gnn_layer_infer_ws_bytes": (c_size_t, [ctypes.POINTER(Graph), c_int, c_int]),
+    "az_gnn_layer_infer": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int,
+                                   ctypes.POINTER(LayerW), c_void_p, c_void_p, c_size_t,
+                                   c_void_p]),
+    "az_gnn_source_proj_fwd": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int,
+                                       ctypes.POINTER(LayerW), c_void_p, c_void_p, c_size_t,
+                                       c_void_p]),
+    "az_gnn_layer_fused_fwd": (c_int, [ctypes.POINTER(Graph), c_void_p, c_void_p, c_int, c_int,
+                                       ctypes.POINTER(LayerW), c_void_p, c_void_p]),
     "az_gnn_layer_fwd": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int,
                                  ctypes.POINTER(LayerW), c_void_p, c_void_p, c_size_t, c_void_p]),
     "az_mlp2_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -21,8 +21,8 @@ HOST_SOURCES = ["az_mcts.cpp"]
 HOST_FLAGS = ["-O3", "-fPIC", "-shared", "-std=c++17", "-fopenmp", "-ffp-contract=off",
               "-Wall", "-Wl,-z,defs"]
 OBJ = os.path.join(CSRC, "build")
-SOURCES = ["az_runtime.hip", "az_gemm.hip", "az_trunk.hip", "az_gnn.hip", "az_optim.hip",
-           "az_backward.hip"]
+SOURCES = ["az_runtime.hip", "az_gemm.hip", "az_trunk.hip", "az_gnn.hip", "az_gnn_fused.hip",
+           "az_optim.hip", "az_backward.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wall",
          "-Wno-unused-function", "-fno-gpu-rdc"]
 

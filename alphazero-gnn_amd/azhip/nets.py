@@ -183,8 +183,11 @@ class PolicyValueGNN(_Net):
         return y
 
     def run_layers(self, x, graph):
+        """The layer stack; in eval mode nothing is kept for a backward pass
+        (az_gnn_layer_infer: one fused kernel per layer on grid-shaped graphs)."""
         for layer in self.layers:
-            x, self._ws = ops.gnn_layer(graph, x, layer.weights(), ws=self._ws)
+            x, self._ws = ops.gnn_layer(graph, x, layer.weights(), ws=self._ws,
+                                        save=self.training)
         return x
 
     def __call__(self, features):

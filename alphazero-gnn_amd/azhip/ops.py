@@ -326,18 +326,45 @@ def layer_ws_bytes(g, F, H=128):
     return int(_lib.load().az_gnn_layer_ws_bytes(g.V, g.E, g.D, F, H))
 
 
-def gnn_layer(g, x, Wl, out=None, ws=None, H=128):
+def gnn_layer(g, x, Wl, out=None, ws=None, H=128, save=True):
+    """One GNNLayer over graph g.  save=True (training): az_gnn_layer_fwd, which keeps the
+    activations az_gnn_layer_bwd reads in `ws`; save=False (eval): az_gnn_layer_infer (the fused
+    path on grid-shaped graphs).  Returns (x_out, ws)."""
     F = x.shape[1]
     out = torch.empty_like(x) if out is None else out
-    nbytes = layer_ws_bytes(g, F, H)
+    L = _lib.lib()
+    nbytes = layer_ws_bytes(g, F, H) if save else \
+        int(L.az_gnn_layer_infer_ws_bytes(ctypes.byref(g.c), F, H))
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty((nbytes,), dtype=torch.uint8, device=x.device)
     lw = layer_weights(Wl)
-    L = _lib.lib()
-    _lib.check(L.az_gnn_layer_fwd(ctypes.byref(g.c), _p(x), F, H, ctypes.byref(lw), _p(out),
-                                  _p(ws), ctypes.c_size_t(ws.numel()), _stream()),
-               "az_gnn_layer_fwd")
+    fn = L.az_gnn_layer_fwd if save else L.az_gnn_layer_infer
+    _lib.check(fn(ctypes.byref(g.c), _p(x), F, H, ctypes.byref(lw), _p(out), _p(ws),
+                  ctypes.c_size_t(ws.numel()), _stream()),
+               "az_gnn_layer_fwd" if save else "az_gnn_layer_infer")
     return out, ws
+
+
+def gnn_source_proj(g, x, Wl, Ps=None, H=128):
+    """Ps [V][H] = x W1[:, F:]^T (the fused layer path's first launch)."""
+    Ps = torch.empty((g.V, H), device=x.device) if Ps is None else Ps
+    L = _lib.lib()
+    ws = workspace(x.device)
+    _lib.check(L.az_gnn_source_proj_fwd(ctypes.byref(g.c), _p(x), x.shape[1], H,
+                                        ctypes.byref(layer_weights(Wl)), _p(Ps), _p(ws),
+                                        ctypes.c_size_t(ws.numel()), _stream()),
+               "az_gnn_source_proj_fwd")
+    return Ps
+
+
+def gnn_layer_fused(g, x, Ps, Wl, out=None, H=128):
+    """The fused layer kernel given Ps (the fused path's second launch)."""
+    out = torch.empty_like(x) if out is None else out
+    L = _lib.lib()
+    _lib.check(L.az_gnn_layer_fused_fwd(ctypes.byref(g.c), _p(x), _p(Ps), x.shape[1], H,
+                                        ctypes.byref(layer_weights(Wl)), _p(out), _stream()),
+               "az_gnn_layer_fused_fwd")
+    return out
 
 
 def mlp2(x, w0, b0, w2, b2, hidden=None, out=None):

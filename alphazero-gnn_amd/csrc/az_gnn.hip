@@ -13,6 +13,14 @@
 
 namespace az {
 int gemm_f32(const az_gemm_desc* d, hipStream_t s);
+bool gnn_layer_fusable(const az_graph* g, int F, int H);
+size_t gnn_layer_fused_ws_bytes(int V);
+int gnn_layer_fused(const az_graph* g, const float* x, const az_gnn_layer_w* w, float* x_out,
+                    void* ws, size_t ws_bytes, hipStream_t s);
+int gnn_layer_fused_kernel_launch(const az_graph* g, const float* x, const float* Ps,
+                                  const az_gnn_layer_w* w, float* x_out, hipStream_t s);
+int gnn_layer_source_projection(const az_graph* g, const float* x, const az_gnn_layer_w* w,
+                                float* Ps, void* ws, size_t ws_bytes, hipStream_t s);
 
 __device__ __forceinline__ int xcd_remap(int b, int n) {
   // give every XCD (blocks b, b+8, ...) one contiguous run of destinations so the
@@ -541,6 +549,68 @@ extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
   o.C = x_out; o.ldc = F; o.c_rows = (g->D == g->V) ? nullptr : g->dst_rows;
   o.ws = L.split; o.ws_bytes = kSplitWsBytes;
   return gemm_f32(&o, s);
+}
+
+extern "C" size_t az_gnn_layer_infer_ws_bytes(const az_graph* g, int F, int H) {
+  if (!g) return 0;
+  return gnn_layer_fusable(g, F, H) ? gnn_layer_fused_ws_bytes(g->V)
+                                    : az_gnn_layer_ws_bytes(g->V, g->E, g->D, F, H);
+}
+
+extern "C" int az_gnn_layer_infer(const az_graph* g, const float* x, int F, int H,
+                                  const az_gnn_layer_w* w, float* x_out, void* ws,
+                                  size_t ws_bytes, void* stream) {
+  int rc = check_graph(g);
+  if (rc) return rc;
+  if (!gnn_layer_fusable(g, F, H))
+    return az_gnn_layer_fwd(g, x, F, H, w, x_out, ws, ws_bytes, stream);
+  AZ_REQUIRE(x && x_out && w && ws && x != x_out, AZ_EINVAL, "az_gnn_layer_infer: bad pointers");
+  AZ_REQUIRE(aligned16(x) && aligned16(x_out) && aligned16(ws), AZ_EINVAL,
+             "az_gnn_layer_infer: x, x_out, ws need 16B alignment");
+  AZ_REQUIRE(w->att_w1 && w->att_b1 && w->att_w2 && w->att_b2 && w->upd_w1 && w->upd_b1 &&
+                 w->upd_w2 && w->upd_b2 && w->gate_w && w->gate_b,
+             AZ_EINVAL, "az_gnn_layer_infer: null weight");
+  AZ_REQUIRE(ws_bytes >= az_gnn_layer_infer_ws_bytes(g, F, H), AZ_EINVAL,
+             "az_gnn_layer_infer: workspace too small");
+  hipStream_t s = as_stream(stream);
+  if (g->D < g->V) {
+    if (hipMemcpyAsync(x_out, x, (size_t)g->V * F * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return check_launch("hipMemcpyAsync");
+  }
+  return gnn_layer_fused(g, x, w, x_out, ws, ws_bytes, s);
+}
+
+extern "C" int az_gnn_source_proj_fwd(const az_graph* g, const float* x, int F, int H,
+                                      const az_gnn_layer_w* w, float* Ps, void* ws,
+                                      size_t ws_bytes, void* stream) {
+  int rc = check_graph(g);
+  if (rc) return rc;
+  AZ_REQUIRE(gnn_layer_fusable(g, F, H), AZ_EINVAL,
+             "az_gnn_source_proj_fwd: only the fused shapes (F 64, H 128, in-degree <= 4)");
+  AZ_REQUIRE(x && w && w->att_w1 && Ps && aligned16(x) && aligned16(Ps), AZ_EINVAL,
+             "az_gnn_source_proj_fwd: bad pointers");
+  return gnn_layer_source_projection(g, x, w, Ps, ws, ws_bytes, as_stream(stream));
+}
+
+extern "C" int az_gnn_layer_fused_fwd(const az_graph* g, const float* x, const float* Ps, int F,
+                                      int H, const az_gnn_layer_w* w, float* x_out,
+                                      void* stream) {
+  int rc = check_graph(g);
+  if (rc) return rc;
+  AZ_REQUIRE(gnn_layer_fusable(g, F, H), AZ_EINVAL,
+             "az_gnn_layer_fused_fwd: only F 64, H 128, in-degree <= 4");
+  AZ_REQUIRE(x && Ps && x_out && w && x != x_out && aligned16(x) && aligned16(Ps) &&
+                 aligned16(x_out),
+             AZ_EINVAL, "az_gnn_layer_fused_fwd: bad pointers");
+  AZ_REQUIRE(w->att_w1 && w->att_b1 && w->att_w2 && w->att_b2 && w->upd_w1 && w->upd_b1 &&
+                 w->upd_w2 && w->upd_b2 && w->gate_w && w->gate_b,
+             AZ_EINVAL, "az_gnn_layer_fused_fwd: null weight");
+  hipStream_t s = as_stream(stream);
+  if (g->D < g->V) {
+    if (hipMemcpyAsync(x_out, x, (size_t)g->V * F * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return check_launch("hipMemcpyAsync");
+  }
+  return gnn_layer_fused_kernel_launch(g, x, Ps, w, x_out, s);
 }
 
 extern "C" int az_mlp2_fwd(const float* x, int M, int F, const float* w0, const float* b0,

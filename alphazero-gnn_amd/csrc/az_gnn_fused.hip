@@ -1,0 +1,386 @@
+// Inference form of one GNNLayer (gnn_utils.py:5-74) on a destination-sorted CSR graph, for the
+// shapes of the synthetic grid workload (F = 64 node features, H = 128 attention hidden units,
+// in-degree <= 4): two launches and nothing kept for a backward pass.
+//
+//   1. Ps[v] = W1[:, F:] x_v            (az_gemm_f32; the SOURCE half of the factored attention
+//                                        projection only, [V][H] planar -- gnn_utils.py:30-32,
+//                                        W1 [t; x] = W1[:, :F] t + W1[:, F:] x)
+//   2. gnn_layer_fused_kernel, per tile of 64 destinations, entirely in LDS / registers:
+//        Pt    = X_d W1[:, :F]^T                    MFMA 16x16x4 f32 (the TARGET half, never in HBM)
+//        alpha = sigmoid(w2 . relu(Pt[d] + Ps[s] + b1) + b2) per in-edge      (gnn_utils.py:48-52)
+//        agg_d = sum_e alpha_e / sum(alpha) x_s   (sum(alpha) > 0, else un-normalised, :55-65)
+//        [g|u1] = [x_d; agg_d] [Wg; Wu1]^T + b      MFMA, sigmoid / relu      (gnn_utils.py:67-70)
+//        x_out = x_d + g * (u1 Wu2^T + bu2)         MFMA + the gated residual (gnn_utils.py:71)
+//      The projection P's target half, alpha, agg, the gate and both update activations never
+//      reach HBM: per layer the traffic is x (once per destination, plus the gathered neighbour
+//      rows, mostly L2 hits), Ps (gathered), the CSR arrays and x_out.
+//
+// Block: 256 threads = 4 waves, two blocks per CU (72 KB LDS each), persistent over a
+// contiguous run of tiles so consecutive tiles' neighbour rows are warm in the XCD's L2.
+#include "az_common.h"
+
+namespace az {
+int gemm_f32(const az_gemm_desc* d, hipStream_t s);
+
+namespace {
+
+constexpr int FF = 64;        // node features
+constexpr int HH = 128;       // attention hidden units
+constexpr int TT = 64;        // destinations per tile
+constexpr int NT = 256;       // threads per block (4 waves); two blocks per CU
+constexpr int CS = 132;       // LDS row stride of [x_d | agg] and Pt: = 4 (mod 64), so a wave's
+                              // ds_read_b128 of 16 rows x 16 B is bank-conflict free
+constexpr int GS = 68;        // LDS row stride of the gate / u1 images (= 4 mod 64 as well)
+constexpr int MAXD = 4;       // in-degree bound of the fused path
+constexpr int LDS_C = TT * CS;                       // [x_d | agg]
+constexpr int LDS_R = (TT * CS > 2 * TT * GS) ? TT * CS : 2 * TT * GS;   // Pt, then gate + u1
+
+struct FusedW {
+  const float *w1, *b1, *w2, *b2, *gw, *gb, *uw1, *ub1, *uw2, *ub2;
+};
+
+__device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+
+// acc[mt][nt] += A[16 mt + i][k] . B[k][16 nt + j] over k < 16 KG on 16x16x4 f32 MFMAs, with the
+// k order permuted inside each group of 16: k-step t of group kg gives lane (lr, lg) the element
+// k = 16 kg + 4 lg + t.  A lane's A fragments for the 4 k-steps of a group are then ONE
+// ds_read_b128 (A[row lr][16 kg + 4 lg .. +3], row stride lda = 4 mod 64: conflict free) and its
+// B fragments ONE global dwordx4 (W[n][16 kg + 4 lg .. +3] of the nn.Linear weight, row stride
+// ldw; L2-resident).  Group kg + 1's operands load while group kg's 4 * MT * NTL MFMAs run.
+template <int MT, int NTL, int KG>
+__device__ __forceinline__ void mfma_tile(f32x4 (&acc)[MT][NTL], const float* A, int lda,
+                                          const float* const (&Wr)[NTL], int lr, int lg) {
+  const float* ab = A + lr * lda + 4 * lg;
+  f32x4 a[MT], an[MT], b[NTL], bn[NTL];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) a[mt] = *reinterpret_cast<const f32x4*>(ab + 16 * mt * lda);
+#pragma unroll
+  for (int nt = 0; nt < NTL; ++nt) b[nt] = *reinterpret_cast<const f32x4*>(Wr[nt] + 4 * lg);
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) {
+    if (kg + 1 < KG) {
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt)
+        bn[nt] = *reinterpret_cast<const f32x4*>(Wr[nt] + 16 * (kg + 1) + 4 * lg);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        an[mt] = *reinterpret_cast<const f32x4*>(ab + 16 * mt * lda + 16 * (kg + 1));
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NTL; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt][t], b[nt][t], acc[mt][nt],
+                                                              0, 0, 0);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) a[mt] = an[mt];
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) b[nt] = bn[nt];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// The gathered neighbour rows of one destination (16 lanes: lane j holds hidden units 8j..8j+7
+// of Ps and features 4j..4j+3 of x for each in-edge).
+struct Gather {
+  f32x4 ps[MAXD][2];
+  f32x4 xs[MAXD];
+};
+
+__device__ __forceinline__ void issue_gather(Gather& g, const int* idx, const float* __restrict__ Ps,
+                                             const float* __restrict__ x, int j) {
+#pragma unroll
+  for (int q = 0; q < MAXD; ++q) {
+    const int sq = idx[2 + q];
+    const float* pr = Ps + (size_t)sq * HH + 8 * j;
+    g.ps[q][0] = *reinterpret_cast<const f32x4*>(pr);
+    g.ps[q][1] = *reinterpret_cast<const f32x4*>(pr + 4);
+    g.xs[q] = *reinterpret_cast<const f32x4*>(x + (size_t)sq * FF + 4 * j);
+  }
+}
+
+// attention scores of one destination's in-edges and its normalised aggregation (gnn_utils.py:
+// 48-65): agg = sum_e alpha_e / S x_s, S = sum alpha (> 0; else un-normalised)
+__device__ __forceinline__ f32x4 edge_pass(const Gather& g, int deg, const float* pt,
+                                           const float* AB, float b2, int j) {
+  f32x4 agg = {0.f, 0.f, 0.f, 0.f};
+  if (deg <= 0) return agg;
+  const f32x4 pt0 = *reinterpret_cast<const f32x4*>(pt + 8 * j);
+  const f32x4 pt1 = *reinterpret_cast<const f32x4*>(pt + 8 * j + 4);
+  const f32x4 bb0 = *reinterpret_cast<const f32x4*>(AB + 8 * j);
+  const f32x4 bb1 = *reinterpret_cast<const f32x4*>(AB + 8 * j + 4);
+  const f32x4 ww0 = *reinterpret_cast<const f32x4*>(AB + HH + 8 * j);
+  const f32x4 ww1 = *reinterpret_cast<const f32x4*>(AB + HH + 8 * j + 4);
+  float a[MAXD];
+#pragma unroll
+  for (int q = 0; q < MAXD; ++q) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc = fmaf(relu(pt0[c] + g.ps[q][0][c] + bb0[c]), ww0[c], acc);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc = fmaf(relu(pt1[c] + g.ps[q][1][c] + bb1[c]), ww1[c], acc);
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
+    a[q] = sigmoidf_ref(acc + b2);
+  }
+  float S = 0.f;
+#pragma unroll
+  for (int q = 0; q < MAXD; ++q)
+    if (q < deg) S += a[q];
+  const bool norm = S > 0.f;
+#pragma unroll
+  for (int q = 0; q < MAXD; ++q)
+    if (q < deg) {
+      const float wq = norm ? a[q] / S : a[q];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) agg[c] = fmaf(wq, g.xs[q][c], agg[c]);
+    }
+  return agg;
+}
+
+}  // namespace
+
+// One block = 4 waves on a tile of 64 destinations, two blocks per CU, persistent over a
+// contiguous run of tiles.  The weights stream from L2 (112 KB, resident there) one 16-wide k
+// group ahead of the MFMAs; the next tile's CSR indices are fetched one tile ahead into LDS and
+// its x rows into registers; half of a tile's neighbour gathers are in flight during step 1's
+// MFMAs, the other half during the first half's edge arithmetic.
+__global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
+    int D, int identity, const int* __restrict__ dst_rows, const int* __restrict__ rowptr,
+    const int* __restrict__ col, const float* __restrict__ x, const float* __restrict__ Ps,
+    FusedW W, float* __restrict__ x_out, int ntiles, int tiles_per_block) {
+  __shared__ float C[LDS_C];
+  __shared__ float R[LDS_R];
+  __shared__ int IDX[2][TT][8];           // per destination: node, in-degree (-1: none), sources
+  __shared__ float AB[2 * HH];            // attention.0 bias, attention.2 weight
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, l = tid & 63, lr = l & 15, lg = l >> 4;
+
+  // weight rows this lane streams (nn.Linear layout [out][in])
+  const float* const w1r[2] = {W.w1 + (32 * wave + lr) * 2 * FF,          // step 1: W1[:, :F]
+                               W.w1 + (32 * wave + 16 + lr) * 2 * FF};
+  const int n3 = 32 * wave + lr;                                           // step 3: [Wg; Wu1]
+  const float* const wcr[2] = {n3 < FF ? W.gw + n3 * 2 * FF : W.uw1 + (n3 - FF) * 2 * FF,
+                               n3 + 16 < FF ? W.gw + (n3 + 16) * 2 * FF
+                                            : W.uw1 + (n3 + 16 - FF) * 2 * FF};
+  const float* const w4r[1] = {W.uw2 + (16 * wave + lr) * FF};            // step 4: Wu2
+  const float cbias0 = n3 < FF ? W.gb[n3] : W.ub1[n3 - FF];
+  const float cbias1 = n3 + 16 < FF ? W.gb[n3 + 16] : W.ub1[n3 + 16 - FF];
+  const float ubias = W.ub2[16 * wave + lr];
+  const float b2 = W.b2[0];
+  if (tid < HH) {
+    AB[tid] = W.b1[tid];
+    AB[HH + tid] = W.w2[tid];
+  }
+  const int j = tid & 15, grp = tid >> 4;          // step 2: 16 lanes per destination, 16 groups
+  const int im = tid >> 2, iq = tid & 3;           // index prefetch: 4 lanes per destination
+
+  const int t0 = blockIdx.x * tiles_per_block;
+  const int t1 = min(ntiles, t0 + tiles_per_block);
+  if (t0 >= t1) return;                   // uniform per block
+
+  // prologue: the first tile's indices and x rows
+  {
+    const int i = t0 * TT + im;
+    int d = 0, e0 = 0, deg = -1;
+    if (i < D) {
+      d = identity ? i : dst_rows[i];
+      e0 = rowptr[d];
+      deg = rowptr[d + 1] - e0;
+    }
+    IDX[0][im][2 + iq] = iq < deg ? col[e0 + iq] : d;
+    if (iq == 0) {
+      IDX[0][im][0] = d;
+      IDX[0][im][1] = deg;
+    }
+  }
+  f32x4 xnext[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int i = t0 * TT + p * 16 + (tid >> 4);
+    xnext[p] = i < D ? *reinterpret_cast<const f32x4*>(
+                           x + (size_t)(identity ? i : dst_rows[i]) * FF + (tid & 15) * 4)
+                     : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+
+  int cur = 0;
+  for (int tile = t0; tile < t1; ++tile, cur ^= 1) {
+    const int nxt = cur ^ 1;
+    const bool has_next = tile + 1 < t1;
+    // ---- step 0: x rows -> C[:, 0:64]; passes 0 and 1 of the neighbour gathers in flight
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      *reinterpret_cast<f32x4*>(&C[(p * 16 + (tid >> 4)) * CS + (tid & 15) * 4]) = xnext[p];
+    Gather g0, g1;
+    issue_gather(g0, IDX[cur][grp], Ps, x, j);
+    issue_gather(g1, IDX[cur][16 + grp], Ps, x, j);
+    // the next tile's index chain, link 1: its destination node
+    const int ni = (tile + 1) * TT + im;
+    const bool nvalid = has_next && ni < D;
+    int nd = 0, ne0 = 0, ndeg = -1;
+    if (nvalid) nd = identity ? ni : dst_rows[ni];
+    __syncthreads();
+
+    // ---- step 1: Pt = X_d W1[:, :F]^T -> R[m][n]   (wave: n in [32 wave, 32 wave + 32))
+    {
+      f32x4 acc[4][2];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_tile<4, 2, FF / 16>(acc, C, CS, w1r, lr, lg);
+      float* dst = R + 4 * lg * CS + 32 * wave + lr;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dst[(16 * mt + r) * CS] = acc[mt][0][r];
+          dst[(16 * mt + r) * CS + 16] = acc[mt][1][r];
+        }
+    }
+    // link 2: its CSR segment
+    if (nvalid) {
+      ne0 = rowptr[nd];
+      ndeg = rowptr[nd + 1] - ne0;
+    }
+    __syncthreads();
+
+    // ---- step 2: attention + normalised aggregation, four passes of 16 destinations
+    {
+      const int m0 = grp, m1 = 16 + grp, m2 = 32 + grp, m3 = 48 + grp;
+      *reinterpret_cast<f32x4*>(&C[m0 * CS + FF + 4 * j]) =
+          edge_pass(g0, IDX[cur][m0][1], &R[m0 * CS], AB, b2, j);
+      issue_gather(g0, IDX[cur][m2], Ps, x, j);
+      *reinterpret_cast<f32x4*>(&C[m1 * CS + FF + 4 * j]) =
+          edge_pass(g1, IDX[cur][m1][1], &R[m1 * CS], AB, b2, j);
+      issue_gather(g1, IDX[cur][m3], Ps, x, j);
+      *reinterpret_cast<f32x4*>(&C[m2 * CS + FF + 4 * j]) =
+          edge_pass(g0, IDX[cur][m2][1], &R[m2 * CS], AB, b2, j);
+      *reinterpret_cast<f32x4*>(&C[m3 * CS + FF + 4 * j]) =
+          edge_pass(g1, IDX[cur][m3][1], &R[m3 * CS], AB, b2, j);
+    }
+    // link 3: its sources
+    const int nsq = iq < ndeg ? col[ne0 + iq] : nd;
+    __syncthreads();
+
+    // ---- step 3: [gate | u1] = [x_d; agg] [Wg; Wu1]^T + b  (wave: n in [32 wave, 32 wave + 32))
+    {
+      f32x4 acc[4][2];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_tile<4, 2, 2 * FF / 16>(acc, C, CS, wcr, lr, lg);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {       // the next tile's x rows, in flight during the epilogue
+        const int i = (tile + 1) * TT + p * 16 + (tid >> 4);
+        if (has_next && i < D)
+          xnext[p] = *reinterpret_cast<const f32x4*>(
+              x + (size_t)(identity ? i : dst_rows[i]) * FF + (tid & 15) * 4);
+      }
+      // waves 0-1 hold gate columns, 2-3 u1 columns (wave-uniform)
+      if (wave < 2) {
+        float* dst = R + 4 * lg * GS + 32 * wave + lr;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dst[(16 * mt + r) * GS] = sigmoidf_ref(acc[mt][0][r] + cbias0);
+            dst[(16 * mt + r) * GS + 16] = sigmoidf_ref(acc[mt][1][r] + cbias1);
+          }
+      } else {
+        float* dst = R + TT * GS + 4 * lg * GS + 32 * (wave - 2) + lr;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dst[(16 * mt + r) * GS] = relu(acc[mt][0][r] + cbias0);
+            dst[(16 * mt + r) * GS + 16] = relu(acc[mt][1][r] + cbias1);
+          }
+      }
+    }
+    IDX[nxt][im][2 + iq] = nsq;
+    if (iq == 0) {
+      IDX[nxt][im][0] = nd;
+      IDX[nxt][im][1] = nvalid ? ndeg : -1;
+    }
+    __syncthreads();
+
+    // ---- step 4: x_out = x_d + gate * (u1 Wu2^T + bu2)   (wave: features [16 wave, +16))
+    {
+      const float* G = R;
+      const float* U = R + TT * GS;
+      f32x4 acc[4][1];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_tile<4, 1, FF / 16>(acc, U, GS, w4r, lr, lg);
+      const int f = 16 * wave + lr;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * mt + 4 * lg + r;
+          if (IDX[cur][row][1] >= 0)
+            x_out[(size_t)IDX[cur][row][0] * FF + f] =
+                C[row * CS + f] + G[row * GS + f] * (acc[mt][0][r] + ubias);
+        }
+    }
+    __syncthreads();                      // C / R / IDX[cur] are rewritten by the next tile
+  }
+}
+
+// Host side -----------------------------------------------------------------------------------
+bool gnn_layer_fusable(const az_graph* g, int F, int H) {
+  return F == FF && H == HH && g->max_deg >= 0 && g->max_deg <= MAXD && g->D > 0;
+}
+
+size_t gnn_layer_fused_ws_bytes(int V) {
+  return ((size_t)V * HH * 4 + 255) / 256 * 256 + (size_t(40) << 20);
+}
+
+int gnn_layer_fused_kernel_launch(const az_graph* g, const float* x, const float* Ps,
+                                  const az_gnn_layer_w* w, float* x_out, hipStream_t s) {
+  // persistent blocks (two per CU) over contiguous runs of 64-destination tiles
+  const int ntiles = (g->D + TT - 1) / TT;
+  static int cus = 0;                     // queried once per process
+  if (cus <= 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      cus = n;
+    else
+      cus = 256;
+  }
+  const int want = 2 * cus;
+  const int per = (ntiles + want - 1) / want;
+  const int blocks = (ntiles + per - 1) / per;
+  const FusedW fw = {w->att_w1, w->att_b1, w->att_w2, w->att_b2, w->gate_w, w->gate_b,
+                     w->upd_w1, w->upd_b1, w->upd_w2, w->upd_b2};
+  hipLaunchKernelGGL(gnn_layer_fused_kernel, dim3(blocks), dim3(NT), 0, s, g->D,
+                     g->D == g->V ? 1 : 0, g->dst_rows, g->rowptr, g->col, x, Ps, fw, x_out,
+                     ntiles, per);
+  return check_launch("gnn_layer_fused_kernel");
+}
+
+int gnn_layer_source_projection(const az_graph* g, const float* x, const az_gnn_layer_w* w,
+                                float* Ps, void* ws, size_t ws_bytes, hipStream_t s) {
+  // Ps = x W1[:, F:]^T (W1 [H][2F], row stride 2F): the source half of the attention projection
+  az_gemm_desc d = {};
+  d.M = g->V; d.N = HH; d.K = FF;
+  d.A = x; d.lda = FF; d.a_kmajor = 1;
+  d.B = w->att_w1 + FF; d.ldb = 2 * FF; d.b_kmajor = 1;
+  d.C = Ps; d.ldc = HH;
+  d.ws = ws; d.ws_bytes = ws ? ws_bytes : 0;
+  return gemm_f32(&d, s);
+}
+
+int gnn_layer_fused(const az_graph* g, const float* x, const az_gnn_layer_w* w, float* x_out,
+                    void* ws, size_t ws_bytes, hipStream_t s) {
+  float* Ps = static_cast<float*>(ws);
+  const size_t ps_bytes = ((size_t)g->V * HH * 4 + 255) / 256 * 256;
+  int rc = gnn_layer_source_projection(g, x, w, Ps, static_cast<char*>(ws) + ps_bytes,
+                                       ws_bytes - ps_bytes, s);
+  if (rc) return rc;
+  return gnn_layer_fused_kernel_launch(g, x, Ps, w, x_out, s);
+}
+
+}  // namespace az

@@ -100,11 +100,13 @@ def _grid_graph(ops, device, graphs, h=32, w=32, build=True):
 
 
 def aggregate_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True):
-    """Config 5 per-GPU shard (4096 grids / 8 GPUs = 512): 32x32 4-neighbour grids, F=64, CSR by
-    destination.  Times the scatter-aggregate kernel alone (HIP events on the launch stream):
-      warm -- back-to-back launches (x, 134 MB, stays resident in the 256 MB Infinity Cache);
-      cold -- the Infinity Cache flushed (a 512 MB read) before every timed launch;
-      full -- the whole config (4096 grids, 1.07 GB of x) on this one GPU, back-to-back."""
+    """The standalone scatter-aggregate kernel (az_gnn_aggregate_fwd) as TRAINING runs it: the
+    train-mode layer (az_gnn_layer_fwd) keeps alpha / agg for the backward pass.  Eval-mode
+    layers on grid graphs fuse it away (layer_roofline).  Config-5 shard per GPU (512 32x32
+    grids, F = 64, dst-sorted CSR), HIP events on the launch stream:
+      cold -- Infinity Cache flushed (a 512 MB read) before every timed launch (the headline);
+      warm -- back-to-back launches (x, 134 MB, stays in the 256 MB Infinity Cache);
+      full -- all of config 5 (4096 grids, 1.07 GB of x) on this one GPU, back-to-back."""
     def run(gr, flush=None, reps=20):
         g = _grid_graph(ops, device, gr)
         V, E, Fd = g.V, g.E, 64
@@ -126,26 +128,112 @@ def aggregate_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=T
         nbytes = V * Fd * 4 + E * 4 + E * 4 + (V + 1) * 4 + V * Fd * 4
         return nbytes / (ms * 1e-3) / 1e9, ms * 1e3, V, E
 
-    gbs, us, V, E = run(graphs)
-    out = {"kernel": "aggregate_small_kernel<8,2,1,NT>", "bound": "hbm",
-           "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    flush = torch.zeros((128 << 20,), dtype=torch.float32, device=device)
+    gbs, us, V, E = run(graphs, flush)
+    del flush
+    out = {"kernel": "aggregate_small_kernel<8,2,1,NT> (training-path layer, az_gnn_layer_fwd)",
+           "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_us": round(us, 2),
            "workload": f"{graphs} 32x32 grids, V={V}, E={E}, F=64 (config-5 shard per GPU), "
-                       f"back-to-back launches"}
+                       f"Infinity Cache flushed before each launch"}
     if not extra:
         return out
-    flush = torch.zeros((128 << 20,), dtype=torch.float32, device=device)
-    cold_gbs, cold_us, _, _ = run(graphs, flush)
-    del flush
-    out["cold"] = {"achieved": round(cold_gbs, 1), "frac": round(cold_gbs / HBM_PEAK_GBS, 4),
-                   "avg_launch_us": round(cold_us, 2),
-                   "note": "Infinity Cache flushed (512 MB read) before each launch"}
+    wgbs, wus, _, _ = run(graphs)
+    out["warm"] = {"achieved": round(wgbs, 1), "frac": round(wgbs / HBM_PEAK_GBS, 4),
+                   "avg_launch_us": round(wus, 2), "note": "back-to-back launches, x cache-warm"}
     if full_graphs:
         fgbs, fus, fV, fE = run(full_graphs, reps=10)
         out["full_config"] = {"achieved": round(fgbs, 1), "frac": round(fgbs / HBM_PEAK_GBS, 4),
                               "avg_launch_us": round(fus, 2),
                               "workload": f"{full_graphs} grids, V={fV}, E={fE} (all of config 5 "
                                           f"on one GPU)"}
+    return out
+
+
+def layer_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True):
+    """The eval-mode GNN layer exactly as az_gnn_layer_infer runs it on the config-5 grid (what
+    PolicyValueGNN.forward_graph launches): (1) the source-projection GEMM Ps = x W1[:, F:]^T,
+    (2) gnn_layer_fused_kernel (target projection, attention, normalised aggregation, gate /
+    update MLPs, gated residual; nothing else reaches HBM).  Each launch timed alone with HIP
+    events on the launch stream, Infinity Cache flushed before each (the headline) and
+    back-to-back.  Algorithmic work (per layer):
+      fused kernel: 57,344 FLOP per destination (73,728 minus the 16,384 of the source
+                    projection) + 640 FLOP per edge; bytes = x (V*256) + Ps (V*512) + col (4E)
+                    + rowptr (4(V+1)) + x_out (V*256)
+      projection:   16,384 FLOP per node; bytes = x (V*256) + Ps written (V*512)."""
+    from azhip.weights import gnn_spec, synthetic_state_dict
+    Gw = synthetic_state_dict(gnn_spec(64, 2), 3)
+    Wl = {k[len("layers.0."):]: torch.from_numpy(v).to(device) for k, v in Gw.items()
+          if k.startswith("layers.0.")}
+
+    def run(gr, flush=None, reps=20):
+        g = _grid_graph(ops, device, gr)
+        V, E = g.V, g.E
+        x = torch.rand((V, 64), device=device,
+                       generator=torch.Generator(device=device).manual_seed(0)) * 2 - 1
+        Ps = torch.empty((V, 128), device=device)
+        out = torch.empty_like(x)
+        for _ in range(2):
+            ops.gnn_source_proj(g, x, Wl, Ps)
+            ops.gnn_layer_fused(g, x, Ps, Wl, out)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4 * reps)]
+        for i in range(reps):
+            if flush is not None:
+                flush.sum()
+            ev[4 * i].record()
+            ops.gnn_source_proj(g, x, Wl, Ps)
+            ev[4 * i + 1].record()
+            if flush is not None:
+                flush.sum()
+            ev[4 * i + 2].record()
+            ops.gnn_layer_fused(g, x, Ps, Wl, out)
+            ev[4 * i + 3].record()
+        torch.cuda.synchronize()
+        proj_ms = float(np.mean([ev[4 * i].elapsed_time(ev[4 * i + 1]) for i in range(reps)]))
+        fused_ms = float(np.mean([ev[4 * i + 2].elapsed_time(ev[4 * i + 3]) for i in range(reps)]))
+        D = g.D
+        f_flop = 57344 * D + 640 * E
+        f_bytes = V * 256 + V * 512 + 4 * E + 4 * (V + 1) + D * 256
+        p_flop, p_bytes = 16384 * V, V * 256 + V * 512
+        del x, Ps, out
+        return {"V": V, "E": E, "fused_us": fused_ms * 1e3, "proj_us": proj_ms * 1e3,
+                "fused_tflops": f_flop / (fused_ms * 1e-3) / 1e12,
+                "fused_gbs": f_bytes / (fused_ms * 1e-3) / 1e9,
+                "proj_gbs": p_bytes / (proj_ms * 1e-3) / 1e9,
+                "proj_tflops": p_flop / (proj_ms * 1e-3) / 1e12,
+                "fused_flop": f_flop, "fused_bytes": f_bytes, "proj_bytes": p_bytes}
+
+    flush = torch.zeros((128 << 20,), dtype=torch.float32, device=device)
+    c = run(graphs, flush)
+    out = {"kernel": "gnn_layer_fused_kernel (az_gnn_layer_infer, eval-mode GNNLayer)",
+           "bound": "mfma", "achieved": round(c["fused_tflops"], 2),
+           "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(c["fused_tflops"] / FP32_MFMA_PEAK_TFLOPS, 4),
+           "traffic": pmc_traffic("gnn_layer_fused"), "avg_launch_us": round(c["fused_us"], 2),
+           "flop_per_launch": c["fused_flop"], "algorithmic_bytes": c["fused_bytes"],
+           "hbm_gbs_algorithmic": round(c["fused_gbs"], 1),
+           "workload": f"{graphs} 32x32 grids, V={c['V']}, E={c['E']}, F=64, H=128 (config-5 "
+                       f"shard per GPU), Infinity Cache flushed before each launch",
+           "source_projection": {"kernel": "az_gemm_f32 Ps = x W1[:, F:]^T (M=V, N=128, K=64)",
+                                 "bound": "hbm", "avg_launch_us": round(c["proj_us"], 2),
+                                 "achieved": round(c["proj_gbs"], 1), "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": round(c["proj_gbs"] / HBM_PEAK_GBS, 4),
+                                 "traffic": pmc_traffic("gnn_source_proj")},
+           "layer_us": round(c["fused_us"] + c["proj_us"], 2)}
+    del flush
+    if extra:
+        w = run(graphs)
+        out["warm"] = {"fused_us": round(w["fused_us"], 2), "proj_us": round(w["proj_us"], 2),
+                       "fused_tflops": round(w["fused_tflops"], 2),
+                       "note": "back-to-back launches, x cache-warm"}
+        if full_graphs:
+            f = run(full_graphs, reps=5)
+            out["full_config"] = {"fused_us": round(f["fused_us"], 2),
+                                  "proj_us": round(f["proj_us"], 2),
+                                  "fused_tflops": round(f["fused_tflops"], 2),
+                                  "fused_frac": round(f["fused_tflops"] / FP32_MFMA_PEAK_TFLOPS, 4),
+                                  "workload": f"{full_graphs} grids, V={f['V']} (all of config 5 "
+                                              f"on one GPU)"}
     return out
 
 
@@ -475,8 +563,9 @@ def main():
     flop = 2.0 * B * F * F
     achieved = flop / avg_gemm_s / 1e12
 
-    agg = None
+    agg = layer = None
     if not args.no_aggregate:
+        layer = layer_roofline(torch, ops, device, extra=not args.no_agg_extra)
         agg = aggregate_roofline(torch, ops, device, extra=not args.no_agg_extra)
 
     grid = None
@@ -555,6 +644,7 @@ def main():
                          "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                          "avg_launch_us": round(avg_gemm_s * 1e6, 2),
                          "flop_per_launch": flop},
+            "layer_roofline": layer,
             "aggregate_roofline": agg,
             "large_batch": large,
             "grid_forward": grid,

@@ -240,6 +240,25 @@ size_t az_gnn_layer_ws_bytes(int V, int E, int D, int F, int H);
 int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H, const az_gnn_layer_w* w,
                      float* x_out, void* ws, size_t ws_bytes, void* stream);
 
+/* Inference form of az_gnn_layer_fwd (eval mode: same function, nothing kept for a backward
+ * pass).  When F == 64, H == 128 and g->max_deg <= 4 (the synthetic grid, config 5; the graph's
+ * max_deg must be its true maximum in-degree) the layer runs as ONE source-projection GEMM
+ * (Ps = x W1[:, F:]^T, [V][H] in ws) plus ONE fused kernel per 64-destination tile: the target
+ * projection, attention scores, normalised aggregation, gate / update MLPs and the gated residual
+ * stay in LDS / registers (gnn_utils.py:30-74).  Other shapes run az_gnn_layer_fwd.
+ * ws >= az_gnn_layer_infer_ws_bytes(g, F, H). */
+size_t az_gnn_layer_infer_ws_bytes(const az_graph* g, int F, int H);
+int az_gnn_layer_infer(const az_graph* g, const float* x, int F, int H, const az_gnn_layer_w* w,
+                       float* x_out, void* ws, size_t ws_bytes, void* stream);
+/* The two launches of the fused path, separately (profiling / callers that keep Ps):
+ * Ps [V][H] = x W1[:, F:]^T, then the fused layer kernel given Ps (copies non-destination rows
+ * of x to x_out first when D < V).  Fused shapes only (AZ_EINVAL otherwise). */
+int az_gnn_source_proj_fwd(const az_graph* g, const float* x, int F, int H,
+                           const az_gnn_layer_w* w, float* Ps, void* ws, size_t ws_bytes,
+                           void* stream);
+int az_gnn_layer_fused_fwd(const az_graph* g, const float* x, const float* Ps, int F, int H,
+                           const az_gnn_layer_w* w, float* x_out, void* stream);
+
 /* output_transform, gnn_utils.py:101-105,115: y = W2 relu(W0 x + b0) + b2 on M rows.
  * hidden: [M][F] scratch (kept for the backward pass); ws: optional split-K workspace. */
 int az_mlp2_fwd(const float* x, int M, int F, const float* w0, const float* b0,

@@ -291,6 +291,66 @@ def test_grid_layers_vs_golden(ops):
     np.testing.assert_allclose(y.cpu().numpy(), z["grid_out"], atol=1e-5)
 
 
+def test_grid_layers_infer_vs_golden(ops):
+    """Eval-mode layers (az_gnn_layer_infer: the source-projection GEMM + ONE fused kernel per
+    layer, nothing saved) on the reference's 32x32 grid (G3): within 1e-5 of the reference."""
+    z, G, x0 = _synth()
+    g = ops.DeviceGraph(z["rowptr"], z["col"])
+    Gd = {k: cu(v) for k, v in G.items()}
+    x = cu(x0)
+    for i, key in enumerate(("grid_x1", "grid_x2")):
+        Wl = {k[len(f"layers.{i}."):]: v for k, v in Gd.items() if k.startswith(f"layers.{i}.")}
+        x, _ = ops.gnn_layer(g, x, Wl, save=False)
+        np.testing.assert_allclose(x.cpu().numpy(), z[key], atol=1e-5)
+
+
+def _random_graph(V, maxdeg, seed, p_empty=0.1, local=True):
+    rng = np.random.default_rng(seed)
+    deg = rng.integers(1, maxdeg + 1, V)
+    deg[rng.random(V) < p_empty] = 0
+    rowptr = np.concatenate([[0], np.cumsum(deg)])
+    if local:       # mostly nearby sources (grid-like), some far ones
+        col = (np.repeat(np.arange(V), deg) + rng.integers(-40, 41, rowptr[-1])) % V
+        far = rng.random(rowptr[-1]) < 0.05
+        col[far] = rng.integers(0, V, far.sum())
+    else:
+        col = rng.integers(0, V, rowptr[-1])
+    for d in range(V):                   # sorted, distinct sources per destination (as a CSR)
+        seg = col[rowptr[d]:rowptr[d + 1]]
+        col[rowptr[d]:rowptr[d + 1]] = np.sort(seg)
+    return rowptr, col
+
+
+@pytest.mark.parametrize("V,maxdeg,local", [(1000, 4, True), (4099, 4, False), (70001, 4, True),
+                                            (3000, 6, True)])
+def test_fused_layer_equals_training_path(ops, V, maxdeg, local):
+    """az_gnn_layer_infer == az_gnn_layer_fwd (the unfused kernels the backward relies on) on
+    random CSR graphs: ragged in-degrees 0..maxdeg (destination subsets, D < V, so untouched rows
+    are copies), partial last tiles, arbitrary gathers; maxdeg > 4 takes the unfused path
+    (bit-identical).  Small graphs are also checked against the oracle (gnn_utils.py:34-74)."""
+    from oracle import nets as O
+    _, G, _ = _synth()
+    rowptr, col = _random_graph(V, maxdeg, seed=V)
+    g = ops.DeviceGraph(rowptr, col)
+    assert g.D < V
+    Gd = {k: cu(v) for k, v in G.items()}
+    x0 = (np.random.default_rng(V + 1).random((V, 64), dtype=np.float32) * 2 - 1)
+    x = cu(x0)
+    Wl = {k[len("layers.1."):]: v for k, v in Gd.items() if k.startswith("layers.1.")}
+    a, _ = ops.gnn_layer(g, x, Wl, save=True)
+    b, _ = ops.gnn_layer(g, x, Wl, save=False)
+    a, b = a.cpu().numpy(), b.cpu().numpy()
+    if maxdeg > 4:
+        np.testing.assert_array_equal(a, b)
+    else:
+        np.testing.assert_allclose(b, a, atol=2e-6, rtol=1e-6)
+    empty = np.diff(rowptr) == 0
+    np.testing.assert_array_equal(b[empty], x0[empty])
+    if V <= 4099:
+        ref = O.gnn_layer_csr(x0.astype(np.float64), rowptr, col, G, 1)
+        np.testing.assert_allclose(b, ref, atol=1e-5)
+
+
 def test_star_literal_n4096(ops):
     z, G, _ = _synth()
     Gd = {k: cu(v) for k, v in G.items()}
