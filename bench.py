@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--no-selfplay", action="store_true")
     ap.add_argument("--no-grid", action="store_true", help="skip the config-5 forward leg")
     ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--no-b1", action="store_true", help="skip the as-called batch-1 leg")
     ap.add_argument("--large-batch", type=int, default=65536,
                     help="extra leg at this batch (SURVEY §8d config 2); 0 = skip")
     ap.add_argument("--sp-games", type=int, default=2048,
@@ -56,29 +57,104 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(W, G, seconds, B):
-    """The oracle (numpy restatement, fp32, BLAS threads) on the same workload: per-board GNN
-    forward of 512-board batches, repeated for ~`seconds`."""
-    from oracle import nets as O
+CALIBRATION = "profiles/r02_cpu_calibration.json"   # tools/cpu_calibration.py, build container
+CPU_THREADS = 8        # the thread count of the reference measurements
+
+
+def _calibration():
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        threads = os.cpu_count()
+        return json.load(open(os.path.join(ROOT, CALIBRATION)))
+    except (OSError, ValueError):
+        return {}
+
+
+def cpu_baseline(W, G, seconds, B):
+    """The reference CPU path's workload on this host: the per-board GNN forward of B-board
+    batches (extract_features -> output_transform -> heads, Connect4GNN.py:31-57 +
+    gnn_utils.py:115) as oracle/torch_ref.py's restatement -- the same torch CPU ops as the
+    reference, fp32, eval, no_grad, CPU_THREADS torch threads -- repeated for ~`seconds`.
+    profiles/r02_cpu_calibration.json records its time against the imported reference's on
+    identical inputs and threads in the build container (ratio within a few %)."""
+    import torch
+    from oracle import torch_ref as TR
+    torch.set_num_threads(CPU_THREADS)
     rng = np.random.default_rng(1)
-    boards = rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int8)
-    W32 = {k: np.asarray(v, np.float32) for k, v in W.items()}
-    G32 = {k: np.asarray(v, np.float32) for k, v in G.items() if k.startswith("output_transform")}
-    f = np.float32
-    O.c4_heads(O.policy_value_gnn_per_row(O.c4_features(boards, W32, f), G32, f), W32, f)
+    boards = torch.from_numpy(rng.integers(-1, 2, size=(B, 7, 7)).astype(np.float32))
+    Wt = TR.params(W, torch.float32, requires_grad=False)
+    Gt = TR.params({k: v for k, v in G.items() if k.startswith("output_transform")},
+                   torch.float32, requires_grad=False)
+
+    def run():
+        with torch.no_grad():
+            return TR.c4_heads(TR.output_transform(TR.c4_features(boards, Wt), Gt), Wt)
+    run()
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        O.c4_heads(O.policy_value_gnn_per_row(O.c4_features(boards, W32, f), G32, f), W32, f)
+        run()
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": n * B / dt, "unit": "board evals/s", "cores": int(threads), "kind": "port",
-            "sample": f"{n} batches x {B} random boards (numpy fp32 oracle: c4_features -> "
-                      f"output_transform -> heads, BLAS threads={threads}), {dt:.1f} s"}
+    cal = _calibration().get("gnn_b512", {})
+    return {"value": n * B / dt, "unit": "board evals/s", "cores": CPU_THREADS, "kind": "port",
+            "sample": f"{n} batches x {B} random boards, {dt:.1f} s: oracle/torch_ref.py "
+                      f"(the reference's torch CPU ops: c4_features -> output_transform -> heads), "
+                      f"fp32, {CPU_THREADS} threads; calibration {CALIBRATION}: port / reference "
+                      f"time = {cal.get('ratio_port_torch_over_reference')} on the build "
+                      f"container"}
+
+
+def cnn_b512_leg(torch, ev, device, B=512, reps=50):
+    """SURVEY.md §8d config 2, the CNN half: Net.predict (Connect4Net.forward,
+    Connect4Net.py:30-60) on a batch of B random boards resident in HBM, trunk + heads."""
+    rng = np.random.default_rng(11)
+    boards = torch.from_numpy(rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int8)).to(device)
+    for _ in range(5):
+        ev.evaluate(boards, gnn=False)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    e[0].record()
+    for _ in range(reps):
+        ev.evaluate(boards, gnn=False)
+    e[1].record()
+    torch.cuda.synchronize()
+    ms = e[0].elapsed_time(e[1]) / reps
+    cal = _calibration().get("cnn_b512", {})
+    return {"batch": B, "ms_per_batch": round(ms, 4), "boards_per_s": round(B / (ms * 1e-3), 1),
+            "flop_per_board": 1891008,
+            "tflops": round(1891008 * B / (ms * 1e-3) / 1e12, 2),
+            "reference_cpu_boards_per_s": cal.get("reference_boards_per_s"),
+            "note": "trunk (c4_trunk_kernel) + heads; reference figure from " + CALIBRATION}
+
+
+def as_called_b1_leg(W, G, leaves=2000):
+    """The reference's calling pattern (MCTS.py:169-174): every new leaf is a batch-1 predict
+    AND a batch-1 predict_with_gnn on a host numpy int64 board, results back in host numpy --
+    host<->device traffic and launch latency included (Connect4GNN.py:59-120).  Also the
+    one-call form the native search uses (predict_both on one board)."""
+    import torch
+    from connect4.Connect4GNN import Connect4GNNWrapper
+    from connect4.Connect4Game import Connect4Game
+    net = Connect4GNNWrapper(Connect4Game(7), selfplay_args(2))
+    net.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()})
+    net.gnn.load_state_dict({k: torch.from_numpy(v) for k, v in G.items()})
+    boards = np.random.default_rng(5).integers(-1, 2, size=(leaves, 7, 7)).astype(np.int64)
+    for b in boards[:50]:
+        net.predict(b)
+        net.predict_with_gnn(b)
+        net.predict_both(b[None])
+    t0 = time.perf_counter()
+    for b in boards:
+        net.predict(b)
+        net.predict_with_gnn(b)
+    t_pair = (time.perf_counter() - t0) / leaves
+    t0 = time.perf_counter()
+    for b in boards:
+        net.predict_both(b[None])
+    t_both = (time.perf_counter() - t0) / leaves
+    return {"leaves": leaves, "us_per_leaf_predict_and_predict_with_gnn": round(t_pair * 1e6, 2),
+            "leaf_evals_per_s": round(1.0 / t_pair, 1),
+            "us_per_leaf_predict_both": round(t_both * 1e6, 2),
+            "note": "host numpy board in, numpy (pi, v) out per call (perf_counter around the "
+                    "calls, no batching); the reference on 8 CPU threads: 153 us (predict) + "
+                    "1.01 ms (predict_with_gnn) per leaf, SURVEY.md §6"}
 
 
 def _grid_graph(ops, device, graphs, h=32, w=32, build=True):
@@ -355,13 +431,19 @@ def selfplay_leg(W, G, args, device, rank):
     lanes = getattr(args, "sp_lanes", 2)
     play_episodes_engine(Connect4Game(7), net, selfplay_args(2), eps[:8], seeds, 8,
                          threads=args.sp_threads, lanes=lanes)          # warm-up
+    import nn_fallback
+    nn_fallback.reset()
     st = {}
     t0 = time.perf_counter()
     out = play_episodes_engine(Connect4Game(7), net, sa, eps, seeds, args.sp_games,
                                threads=args.sp_threads, stats=st, lanes=lanes)
     dt = time.perf_counter() - t0
+    failures = nn_fallback.total()
+    if failures:     # degraded play (uniform priors, v = 0) is not a throughput to report
+        raise RuntimeError(f"self-play leg: {failures} network fallbacks {nn_fallback.counts()}")
     moves = sum(len(std) // 2 for std, _ in out.values())
     return dt, {"games": len(out), "moves": moves, "evals": st["rows"], "rounds": st["rounds"],
+                "nn_failures": failures,
                 "net_wait_s": round(st["net_s"], 3), "host_s": round(st["host_s"], 3),
                 "assemble_s": round(st.get("assemble_s", 0.0), 3)}
 
@@ -420,33 +502,41 @@ def train_leg(W, G, device):
 
 
 def selfplay_cpu_baseline(W, G, sims, seconds):
-    """The reference's sequential loop (Coach.executeEpisode over the Python MCTS, batch-1
-    predict + predict_with_gnn per new leaf) with the numpy fp32 oracle as the network, on
-    the host: games/s from the games (and the fraction of one) finished in `seconds`."""
+    """The reference's sequential loop on the host: Coach.executeEpisode over this repo's Python
+    MCTS (bit-exact with the reference's, tests/test_mcts_golden.py) with oracle/torch_ref.py as
+    the network behind the reference's batch-1 predict plumbing (Connect4GNN.py:59-120), torch
+    on CPU_THREADS threads (the reference measurement's count): moves finished in `seconds`.
+    tools/cpu_calibration.py measured this loop against the imported reference's loop on the
+    same episode (profiles/r02_cpu_calibration.json: selfplay)."""
+    import torch
     import Coach as C
     import MCTS as M
     from connect4.Connect4Game import Connect4Game
-    from oracle import nets as O
-    f = np.float32
-    W32 = {k: np.asarray(v, f) for k, v in W.items()}
-    G32 = {k: np.asarray(v, f) for k, v in G.items() if k.startswith("output_transform")}
+    from oracle import torch_ref as TR
+    torch.set_num_threads(CPU_THREADS)
+    Wt = TR.params(W, torch.float32, requires_grad=False)
+    Gt = TR.params({k: v for k, v in G.items() if k.startswith("output_transform")},
+                   torch.float32, requires_grad=False)
 
-    class OracleNet:
+    class PortNet:
+        def _run(self, board, gnn):
+            b = torch.FloatTensor(np.asarray(board).astype(np.float64)).contiguous().view(1, 7, 7)
+            with torch.no_grad():
+                f = TR.c4_features(b, Wt)
+                lp, v = TR.c4_heads(TR.output_transform(f, Gt) if gnn else f, Wt)
+            return torch.exp(lp).data.cpu().numpy()[0], v.data.cpu().numpy()[0]
+
         def predict(self, b):
-            lp, v = O.c4_heads(O.c4_features(np.asarray(b)[None], W32, f), W32, f)
-            return np.exp(lp[0]).astype(f), f(v[0])
+            return self._run(b, False)
 
         def predict_with_gnn(self, b):
-            x = O.policy_value_gnn_per_row(O.c4_features(np.asarray(b)[None], W32, f), G32, f)
-            lp, v = O.c4_heads(x, W32, f)
-            return np.exp(lp[0]).astype(f), f(v[0])
+            return self._run(b, True)
 
     game = Connect4Game(7)
     sa = selfplay_args(sims)
     moves = 0
     t0 = time.perf_counter()
     done = 0
-    est = None
 
     class Counting(M.MCTS):
         def getActionProb_g(self, board, temp=1):
@@ -458,7 +548,7 @@ def selfplay_cpu_baseline(W, G, sims, seconds):
             return pi
 
     coach = C.Coach.__new__(C.Coach)
-    coach.game, coach.args, coach.nnet = game, sa, OracleNet()
+    coach.game, coach.args, coach.nnet = game, sa, PortNet()
     try:
         while True:
             np.random.seed(done)
@@ -468,9 +558,7 @@ def selfplay_cpu_baseline(W, G, sims, seconds):
     except TimeoutError:
         pass
     dt = time.perf_counter() - t0
-    # a partial game counts by its moves at the mean game length of the GPU leg (set later)
-    est = {"games_done": done, "moves": moves, "seconds": round(dt, 1)}
-    return est
+    return {"games_done": done, "moves": moves, "seconds": round(dt, 1)}
 
 
 def pmc_traffic(key):
@@ -579,6 +667,16 @@ def main():
             grid["node_updates_per_s"] = round(world * 2 * 524288 / (float(t.item()) * 1e-3), 1)
             grid["n_gpus"] = world
 
+    cnn = cnn_b512_leg(torch, ev, device, B=B)
+    if world > 1:
+        t = torch.tensor([cnn["ms_per_batch"]], device=red_dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        cnn["boards_per_s"] = round(world * B / (float(t.item()) * 1e-3), 1)
+
+    b1 = None
+    if rank == 0 and not args.no_b1:
+        b1 = as_called_b1_leg(W, G)
+
     large = None
     if args.large_batch > 0:
         large = large_batch_leg(torch, ops, ev, device, B=args.large_batch)
@@ -615,13 +713,18 @@ def main():
             b = selfplay_cpu_baseline(W, G, args.sp_sims, args.cpu_seconds)
             mean_moves = sp["moves"] / max(1, sp["games"])
             games = b["moves"] / mean_moves
+            ratio = _calibration().get("selfplay", {}).get("ratio_port_over_reference_time")
+            rate = games / b["seconds"]
             sp["cpu_baseline"] = {
-                "value": round(games / b["seconds"], 4), "unit": "games/s", "cores": 1,
-                "kind": "port",
-                "sample": f"reference sequential loop (Python MCTS, batch-1 predict + "
-                          f"predict_with_gnn) with the numpy fp32 oracle as the network: "
+                "value": round(rate, 4), "unit": "games/s", "cores": CPU_THREADS, "kind": "port",
+                "reference_equivalent": round(rate * ratio, 4) if ratio else None,
+                "sample": f"reference sequential loop (this repo's bit-exact Python MCTS, batch-1 "
+                          f"predict + predict_with_gnn through oracle/torch_ref.py with the "
+                          f"reference's predict plumbing, {CPU_THREADS} torch threads): "
                           f"{b['moves']} moves in {b['seconds']} s = {games:.2f} games at the "
-                          f"GPU leg's mean {mean_moves:.1f} moves/game"}
+                          f"GPU leg's mean {mean_moves:.1f} moves/game; {CALIBRATION}: this loop "
+                          f"takes {ratio} of the imported reference loop's time on the same "
+                          f"episode -> reference_equivalent"}
 
     if rank == 0:
         value = world * B * args.steps / elapsed
@@ -645,6 +748,8 @@ def main():
                          "avg_launch_us": round(avg_gemm_s * 1e6, 2),
                          "flop_per_launch": flop},
             "layer_roofline": layer,
+            "cnn_b512": cnn,
+            "as_called_b1": b1,
             "aggregate_roofline": agg,
             "large_batch": large,
             "grid_forward": grid,

@@ -112,13 +112,17 @@ def main():
     assert float((lp_r - lp_p).abs().max()) < 1e-4 and float((v_r.view(-1) - v_p).abs().max()) < 1e-4
     out = {"threads": THREADS, "container": "8-core build container (torch CPU)",
            "torch": torch.__version__}
-    t_ref, t_port, t_np = med_times(ref_gnn, port_gnn, numpy_gnn)
+    t_ref, t_port = med_times(ref_gnn, port_gnn)
+    t_cnn_ref, t_cnn_port = med_times(ref_cnn, port_cnn)
+    # numpy last and alone: OpenBLAS worker threads spin after each call and would steal the
+    # cores from torch's pool if the legs were interleaved
+    t_np, = med_times(numpy_gnn)
     out["gnn_b512"] = {"reference_ms": round(t_ref * 1e3, 2), "port_torch_ms": round(t_port * 1e3, 2),
                        "port_numpy_ms": round(t_np * 1e3, 2),
                        "ratio_port_torch_over_reference": round(t_port / t_ref, 3),
                        "ratio_port_numpy_over_reference": round(t_np / t_ref, 3),
                        "reference_boards_per_s": round(512 / t_ref, 1)}
-    t_ref, t_port = med_times(ref_cnn, port_cnn)
+    t_ref, t_port = t_cnn_ref, t_cnn_port
     out["cnn_b512"] = {"reference_ms": round(t_ref * 1e3, 2), "port_torch_ms": round(t_port * 1e3, 2),
                        "ratio_port_torch_over_reference": round(t_port / t_ref, 3),
                        "reference_boards_per_s": round(512 / t_ref, 1)}
@@ -178,17 +182,21 @@ def main():
     assert my_mcts.__file__.startswith(ROOT)
 
     class PortNet:
-        def predict(self, b):
-            with torch.no_grad():
-                lp, v = TR.c4_heads(TR.c4_features(torch.from_numpy(
-                    np.asarray(b, np.float32)[None]), Wt), Wt)
-            return torch.exp(lp)[0].numpy(), np.float32(v[0])
+        """The torch_ref network behind the reference's batch-1 predict plumbing
+        (Connect4GNN.py:59-120: float64 -> FloatTensor, view, no_grad, exp, .cpu().numpy())."""
 
-        def predict_with_gnn(self, b):
+        def _run(self, board, gnn):
+            b = torch.FloatTensor(np.asarray(board).astype(np.float64)).contiguous().view(1, 7, 7)
             with torch.no_grad():
-                f = TR.c4_features(torch.from_numpy(np.asarray(b, np.float32)[None]), Wt)
-                lp, v = TR.c4_heads(TR.output_transform(f, Gt), Wt)
-            return torch.exp(lp)[0].numpy(), np.float32(v[0])
+                f = TR.c4_features(b, Wt)
+                lp, v = TR.c4_heads(TR.output_transform(f, Gt) if gnn else f, Wt)
+            return torch.exp(lp).data.cpu().numpy()[0], v.data.cpu().numpy()[0]
+
+        def predict(self, board):
+            return self._run(board, False)
+
+        def predict_with_gnn(self, board):
+            return self._run(board, True)
 
     port_rate = episode_rate(my_coach, my_mcts, PortNet(), generator=True)
     port_rate = max(port_rate, episode_rate(my_coach, my_mcts, PortNet(), generator=True))

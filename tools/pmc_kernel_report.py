@@ -29,7 +29,7 @@ for k, cs in vals.items():
     wc = a.get("SQ_WAVE_CYCLES")
     if ns and "GRBM_GUI_ACTIVE" in a:
         gui = a["GRBM_GUI_ACTIVE"]
-        out.append(f"clk_GHz={gui / ns:.3f}")
+        out.append(f"clk_GHz={gui / 8 / ns:.3f}")
         if "SQ_VALU_MFMA_BUSY_CYCLES" in a:
             out.append(f"mfma_busy={a['SQ_VALU_MFMA_BUSY_CYCLES'] / (gui / 8 * 1024):.3f}")
     if wc:
