@@ -9,7 +9,10 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libaz_hip.so")
+# AZ_TUNING_LIB=1 selects the tuning build (A/B-experiment switches + slower variants; tools/
+# and the kernel-variant test only)
+LIB_PATH = os.path.join(HERE, "libaz_hip_tuning.so" if os.environ.get("AZ_TUNING_LIB") == "1"
+                        else "libaz_hip.so")
 
 c_int, c_float, c_double, c_void_p, c_int64, c_size_t = (
     ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_void_p, ctypes.c_int64, ctypes.c_size_t)

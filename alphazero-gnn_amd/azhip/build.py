@@ -1,9 +1,15 @@
-"""Build the two in-tree libraries (no torch involved in either build):
+"""Build the in-tree libraries (no torch involved in any build):
 
-    libaz_hip.so   hipcc --offload-arch=gfx950   the device kernels + C-ABI (include/az_hip.h)
-    libaz_mcts.so  g++ -fopenmp                  the native MCTS engine (include/az_mcts.h)
+    libaz_hip.so          hipcc --offload-arch=gfx950   the device kernels + C-ABI (include/az_hip.h)
+    libaz_hip_tuning.so   the same with -DAZ_TUNING: the A/B-experiment switches and the measured-
+                          slower kernel variants (tools/ and tests/test_gpu_kernel_variants.py load
+                          it with AZ_TUNING_LIB=1; the product library has neither)
+    libaz_mcts.so         g++ -fopenmp                  the native MCTS engine (include/az_mcts.h)
 
-    python -m azhip.build          # from alphazero-gnn_amd/
+    python -m azhip.build [--force]     # from alphazero-gnn_amd/
+
+force=True recompiles every object from source (the driver's build() does); BUILD_INFO.json
+beside the libraries records the compiler, flags and a hash of every source.
 """
 import concurrent.futures as cf
 import os
@@ -14,6 +20,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(HERE, "libaz_hip.so")
+TUNING_OUT = os.path.join(HERE, "libaz_hip_tuning.so")
+INFO = os.path.join(HERE, "BUILD_INFO.json")
 HOST_OUT = os.path.join(HERE, "libaz_mcts.so")
 HOST_SOURCES = ["az_mcts.cpp"]
 # -ffp-contract=off: no FMA contraction, so the float64/float32 search arithmetic rounds
@@ -33,41 +41,76 @@ def hipcc():
             return c
 
 
-def _compile(src):
-    obj = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+def _compile(src, force=False, tuning=False):
+    odir = os.path.join(OBJ, "tuning") if tuning else OBJ
+    obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
     s = os.path.join(CSRC, src)
     deps = [s, os.path.join(CSRC, "az_common.h"), os.path.join(CSRC, "az_heads.h"),
             os.path.join(os.path.dirname(PKG), "include", "az_hip.h")]
-    if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
+    if not force and os.path.exists(obj) and \
+            all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj
-    cmd = [hipcc()] + FLAGS + ["-c", s, "-o", obj]
+    cmd = [hipcc()] + FLAGS + (["-DAZ_TUNING"] if tuning else []) + ["-c", s, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
     return obj
 
 
-def build(verbose=True):
-    os.makedirs(OBJ, exist_ok=True)
-    srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
-    if os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(o) for o in objs):
-        return OUT
-    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-Wl,-z,defs", "-o", OUT] + objs
+def _link(objs, out, force):
+    if not force and os.path.exists(out) and \
+            all(os.path.getmtime(out) >= os.path.getmtime(o) for o in objs):
+        return False
+    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-Wl,-z,defs", "-o", out] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
-    if verbose:
-        print(f"built {OUT}")
+    return True
+
+
+def _build_info():
+    import hashlib
+    import json
+    import time
+    ver = subprocess.run([hipcc(), "--version"], capture_output=True, text=True).stdout
+    srcs = {}
+    for f in sorted(os.listdir(CSRC)):
+        p = os.path.join(CSRC, f)
+        if os.path.isfile(p):
+            srcs[f] = hashlib.sha256(open(p, "rb").read()).hexdigest()[:16]
+    hdr = os.path.join(os.path.dirname(PKG), "include")
+    for f in sorted(os.listdir(hdr)):
+        srcs["include/" + f] = hashlib.sha256(open(os.path.join(hdr, f), "rb").read()).hexdigest()[:16]
+    info = {"built_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+            "hipcc": [l for l in ver.splitlines() if l.strip()][:2], "flags": FLAGS,
+            "host_flags": HOST_FLAGS, "sources_sha256_16": srcs}
+    with open(INFO, "w") as f:
+        json.dump(info, f, indent=1)
+
+
+def build(verbose=True, force=False, tuning=True):
+    """Compile libaz_hip.so (and libaz_hip_tuning.so unless tuning=False) for gfx950."""
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(os.path.join(OBJ, "tuning"), exist_ok=True)
+    srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    jobs = [(s, False) for s in srcs] + ([(s, True) for s in srcs] if tuning else [])
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
+        objs = list(ex.map(lambda j: _compile(j[0], force, j[1]), jobs))
+    changed = _link(objs[:len(srcs)], OUT, force)
+    if tuning:
+        changed |= _link(objs[len(srcs):], TUNING_OUT, force)
+    if changed or force or not os.path.exists(INFO):
+        _build_info()
+    if verbose and changed:
+        print(f"built {OUT}" + (f" and {os.path.basename(TUNING_OUT)}" if tuning else ""))
     return OUT
 
 
-def build_host(verbose=True):
+def build_host(verbose=True, force=False):
     srcs = [os.path.join(CSRC, f) for f in HOST_SOURCES]
     deps = srcs + [os.path.join(os.path.dirname(PKG), "include", "az_mcts.h")]
-    if os.path.exists(HOST_OUT) and all(os.path.getmtime(HOST_OUT) >= os.path.getmtime(d)
-                                        for d in deps):
+    if not force and os.path.exists(HOST_OUT) and \
+            all(os.path.getmtime(HOST_OUT) >= os.path.getmtime(d) for d in deps):
         return HOST_OUT
     cmd = ["g++"] + HOST_FLAGS + srcs + ["-o", HOST_OUT]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -79,6 +122,7 @@ def build_host(verbose=True):
 
 
 if __name__ == "__main__":
-    build_host()
-    build()
+    f = "--force" in sys.argv
+    build_host(force=f)
+    build(force=f)
     sys.exit(0)

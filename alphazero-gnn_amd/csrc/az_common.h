@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "../../include/az_hip.h"
 
@@ -71,6 +72,15 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// A/B-experiment switches (AZ_GEMM_CFG, AZ_SPLITK_HEADS_MODE, ...) are read only by the tuning
+// build (-DAZ_TUNING -> libaz_hip_tuning.so, used by tools/ and the kernel-variant test): the
+// product library never consults the environment and runs its fixed, measured dispatch.
+#ifdef AZ_TUNING
+inline const char* tuning_env(const char* name) { return getenv(name); }
+#else
+inline const char* tuning_env(const char*) { return nullptr; }
+#endif
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -1256,7 +1256,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_tall(GemmArgs p, int nstrips) {
 
 // Launches gemm_tall when the shape is one it covers; false otherwise (nothing launched).
 static bool launch_tall(const GemmArgs& a, hipStream_t s) {
-  static const bool off = getenv("AZ_GEMM_NOTALL") != nullptr;   // A/B experiments
+  static const bool off = tuning_env("AZ_GEMM_NOTALL") != nullptr;   // A/B experiments
   if (off || a.M < 16384 || a.a_rows || a.b_rows || a.c_rows || a.act == AZ_ACT_DRELU)
     return false;
   if (!((a.K == 64 || a.K == 128) && (a.N == 64 || a.N == 128 || a.N == 256))) return false;
@@ -1332,14 +1332,19 @@ static void launch_glds2(const GemmArgs& a, hipStream_t s) {
 }
 
 static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream_t s) {
+  // the product dispatch uses configs 0, 6, 8 and 24 (gemm_f32_partial); every other tile is a
+  // measured-slower experiment, compiled only into the tuning build
   switch (cfg) {
+    case 24: launch_glds2<256, 128, 4, 2, 16>(a, s); break;
+    case 6: launch_glds<128, 128, 2, 2>(a, s); break;
+    case 8: launch_glds<128, 64, 2, 2>(a, s); break;
+#ifdef AZ_TUNING
     case 15: launch_glds2<128, 128, 2, 2, 32>(a, s); break;
     case 16: launch_glds2<128, 128, 2, 2, 16>(a, s); break;
     case 17: launch_glds2<128, 64, 2, 2, 16>(a, s); break;
     case 18: launch_glds2<128, 64, 2, 2, 32>(a, s); break;
     case 19: launch_glds2<128, 128, 2, 4, 16>(a, s); break;
     case 23: launch_glds<256, 128, 4, 2>(a, s); break;
-    case 24: launch_glds2<256, 128, 4, 2, 16>(a, s); break;
     case 25: launch_glds2<128, 256, 2, 4, 16>(a, s); break;
     case 26: launch_glds2<256, 128, 4, 2, 16, true>(a, s); break;
     case 27: launch_glds2<256, 128, 4, 2, 32, true>(a, s); break;
@@ -1356,15 +1361,14 @@ static void launch_cfg(int cfg, const GemmArgs& a, bool akm, bool bkm, hipStream
     case 12: launch_pipe<128, 64, 32, 3>(a, s); break;
     case 13: launch_pipe<128, 128, 16, 3>(a, s); break;
     case 14: launch_pipe<128, 64, 16, 4>(a, s); break;
-    case 6: launch_glds<128, 128, 2, 2>(a, s); break;
     case 7: launch_glds<64, 64, 2, 2>(a, s); break;
-    case 8: launch_glds<128, 64, 2, 2>(a, s); break;
     case 9: launch_glds<128, 128, 2, 4>(a, s); break;
     case 1: launch_tile<128, 128, 32, 2, 2>(a, akm, bkm, s); break;
     case 2: launch_tile<64, 64, 64, 2, 2>(a, akm, bkm, s); break;
     case 3: launch_tile<128, 64, 32, 2, 2>(a, akm, bkm, s); break;
     case 4: launch_tile<128, 128, 32, 2, 4>(a, akm, bkm, s); break;
     case 5: launch_tile<256, 128, 32, 4, 2>(a, akm, bkm, s); break;
+#endif
     default: launch_tile<64, 64, 32, 2, 2>(a, akm, bkm, s); break;
   }
 }
@@ -1384,18 +1388,20 @@ static bool try_gemv_full(const GemmArgs& a, hipStream_t s) {
 // instantiated width); AZ_GEMV_R=1 selects one weight row per wave instead of two
 template <int MR>
 static bool launch_gemv_full(const GemmArgs& a, hipStream_t s) {
-  static const bool r1 = [] { const char* e = getenv("AZ_GEMV_R"); return e && atoi(e) == 1; }();
+#ifdef AZ_TUNING
+  static const bool r1 = [] { const char* e = tuning_env("AZ_GEMV_R"); return e && atoi(e) == 1; }();
   if (r1)
     return try_gemv_full<MR, 1, 1>(a, s) || try_gemv_full<MR, 2, 1>(a, s) ||
            try_gemv_full<MR, 4, 1>(a, s) || try_gemv_full<MR, 8, 1>(a, s) ||
            try_gemv_full<MR, 13, 1>(a, s) || try_gemv_full<MR, 16, 1>(a, s);
+#endif
   return try_gemv_full<MR, 1, 2>(a, s) || try_gemv_full<MR, 2, 2>(a, s) ||
          try_gemv_full<MR, 4, 2>(a, s) || try_gemv_full<MR, 8, 2>(a, s) ||
          try_gemv_full<MR, 13, 2>(a, s) || try_gemv_full<MR, 16, 2>(a, s);
 }
 
 static void launch_gemv(const GemmArgs& a, hipStream_t s) {
-  static const bool chunked = getenv("AZ_GEMV_CHUNKED") != nullptr;   // A/B experiments
+  static const bool chunked = tuning_env("AZ_GEMV_CHUNKED") != nullptr;   // A/B experiments
   if (!chunked) {
     bool done = false;
     switch (a.M) {
@@ -1420,7 +1426,7 @@ static void launch_gemv(const GemmArgs& a, hipStream_t s) {
 static void plan(GemmArgs& a, int bm, int bn, int bk, size_t ws_bytes) {
   const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
   int S = 1;
-  static const char* env_split = getenv("AZ_GEMM_SPLITS");
+  static const char* env_split = tuning_env("AZ_GEMM_SPLITS");
   if (env_split && a.slab) {
     S = std::max(1, atoi(env_split));
   } else if (tiles < 1024 && a.slab) {
@@ -1520,9 +1526,9 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
   a.C2 = d->C2; a.ldc2 = d->ldc2;
   a.slab = static_cast<float*>(d->ws);
   a.splits = 1; a.kc = d->K;
-  static const char* env_abl = getenv("AZ_GEMM_ABLATE");
+  static const char* env_abl = tuning_env("AZ_GEMM_ABLATE");
   a.ablate = env_abl ? atoi(env_abl) : 0;
-  static const bool no_vec = getenv("AZ_GEMM_NOVEC") != nullptr;   // A/B experiments
+  static const bool no_vec = tuning_env("AZ_GEMM_NOVEC") != nullptr;   // A/B experiments
   a.vec_epi = !no_vec && d->N % 4 == 0 && d->ldc % 4 == 0 && aligned16(d->C) &&
               (!d->C2 || (d->ldc2 % 4 == 0 && aligned16(d->C2))) &&
               (!d->R || (d->ldr % 4 == 0 && aligned16(d->R))) &&
@@ -1534,7 +1540,7 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
   }
   if (akm && bkm && launch_tall(a, s)) return check_launch("gemm_tall");
   // tile choice (tuning override for experiments: AZ_GEMM_CFG=<index into kCfgs>)
-  static const char* env_cfg = getenv("AZ_GEMM_CFG");
+  static const char* env_cfg = tuning_env("AZ_GEMM_CFG");
   const bool glds_ok = akm && bkm && !d->A2 && !d->a_rows;
   int cfg = 0;
   int s256 = 0;   // split factor when the 256x128 8-wave tile packs the chip (one block per CU)
@@ -1557,7 +1563,7 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
   } else {
     cfg = 0;  // register-staged 64x64x32: gathered / concatenated operands, small M
   }
-  static const char* env_ring = getenv("AZ_GEMM_RING");   // experiment: 3-buffer 256x128
+  static const char* env_ring = tuning_env("AZ_GEMM_RING");   // experiment: 3-buffer 256x128
   if (cfg == 24 && env_ring) {
     const int r = atoi(env_ring);
     cfg = r == 3 ? 29 : r == 4 ? 31 : r == 5 ? 30 : r == 6 ? 32 : 24;
@@ -1565,11 +1571,11 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
   const TileCfg& tc = kCfgs[cfg];
   plan(a, tc.bm, tc.bn, tc.bk, d->ws_bytes);
   const bool is128 = tc.bm == 128 && tc.bn == 128 && cfg >= 6;
-  if (s256 > 0 && !getenv("AZ_GEMM_SPLITS")) {
+  if (s256 > 0 && !tuning_env("AZ_GEMM_SPLITS")) {
     a.splits = s256;
     a.kc = s256 > 1 ? ((a.K + s256 - 1) / s256 + 31) / 32 * 32 : a.K;
     if (s256 > 1) a.splits = (a.K + a.kc - 1) / a.kc;
-  } else if (is128 && !getenv("AZ_GEMM_SPLITS")) {
+  } else if (is128 && !tuning_env("AZ_GEMM_SPLITS")) {
     const int S = glds_splits(a, (long)((a.M + 127) / 128) * ((a.N + 127) / 128), d->ws_bytes);
     a.splits = S;
     a.kc = S > 1 ? ((a.K + S - 1) / S + 31) / 32 * 32 : a.K;
@@ -1591,7 +1597,7 @@ int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s) {
   a.slab = static_cast<float*>(d->ws);
   a.splits = splits;
   const long total = (long)a.M * a.N;
-  static const bool no_vec = getenv("AZ_GEMM_NOVEC") != nullptr;   // A/B experiments
+  static const bool no_vec = tuning_env("AZ_GEMM_NOVEC") != nullptr;   // A/B experiments
   const bool vec = !no_vec && d->N % 4 == 0 && d->ldc % 4 == 0 && aligned16(d->C) &&
                    (!d->C2 || (d->ldc2 % 4 == 0 && aligned16(d->C2))) &&
                    (!d->R || (d->ldr % 4 == 0 && aligned16(d->R))) &&

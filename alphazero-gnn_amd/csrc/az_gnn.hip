@@ -385,7 +385,7 @@ int aggregate(const az_graph* g, const float* x, int ldx, int F, const float* al
                        identity, g->dst_rows, g->rowptr, g->col, alpha, x, ldx, F, agg, ldagg);
     return check_launch("aggregate_wide_kernel");
   }
-  static const char* env = getenv("AZ_AGG_CFG");   // tuning experiments only
+  static const char* env = tuning_env("AZ_AGG_CFG");   // tuning experiments only
   const int cfg = env ? atoi(env) : 0;
   if (g->max_deg > 0 && g->max_deg <= 4 && F == 64 && cfg != 9) {
     // the grid: non-temporal agg stores keep the gathered x rows resident in L2 / Infinity
@@ -515,7 +515,7 @@ extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
   d.ws = L.split; d.ws_bytes = kSplitWsBytes;
   if ((rc = gemm_f32(&d, s))) return rc;
   // 2. per-edge attention weights, 3. normalised aggregation (one fused pass on the grid)
-  static const bool no_fuse = getenv("AZ_GNN_NOFUSE") != nullptr;   // A/B experiments
+  static const bool no_fuse = tuning_env("AZ_GNN_NOFUSE") != nullptr;   // A/B experiments
   if (!no_fuse && g->max_deg > 0 && g->max_deg <= 4 && F == 64 && H == 128) {
     const int identity = (g->D == g->V) ? 1 : 0;
     const int blocks = (int)(((long)g->D * 16 + 255) / 256);

@@ -78,7 +78,7 @@ extern "C" int az_adam_f32(float* p, const float* g, float* m, float* v, int64_t
   const double bc2_sqrt = sqrt(bc2);
   const long n4 = n / 4;
   static const int env_u = [] {
-    const char* e = getenv("AZ_ADAM_U");
+    const char* e = tuning_env("AZ_ADAM_U");
     return e ? atoi(e) : 0;
   }();
   const int U = env_u == 1 || env_u == 2 || env_u == 4 || env_u == 8 ? env_u : 4;

@@ -633,7 +633,7 @@ extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w
   AZ_REQUIRE(boards && conv1_w && conv1_b && conv2_w && conv2_b && feat, AZ_EINVAL,
              "az_c4_trunk_fwd: null pointer");
   hipStream_t s = as_stream(stream);
-  static const char* env = getenv("AZ_TRUNK_NB");   // tuning experiments only
+  static const char* env = tuning_env("AZ_TRUNK_NB");   // tuning experiments only
   int nbk = B >= 4096 ? 8 : (B >= 2048 ? 4 : (B >= 256 ? 2 : 1));
   if (env) nbk = atoi(env);
   switch (nbk) {
@@ -694,7 +694,7 @@ static void launch_heads(const float* hp, int ldhp, const float* hv, int ldhv, i
                          const float* bv, float* logp, float* pi, float* v, float* part,
                          hipStream_t s) {
   const int nchunks = (K + HEADS_KC - 1) / HEADS_KC;
-  static const bool two_pass = getenv("AZ_HEADS_TWOPASS") != nullptr;   // A/B experiments
+  static const bool two_pass = tuning_env("AZ_HEADS_TWOPASS") != nullptr;   // A/B experiments
   if (B <= HEADS_ROWS_MAXB && nchunks <= HEADS_ROWS_MAXC && !two_pass) {
     hipLaunchKernelGGL(heads_rows_kernel<AMAX>, dim3(B), dim3(512), 0, s, hp, ldhp, hv, ldhv, K,
                        wp, A, wv, bp, bv, logp, pi, v);
@@ -751,7 +751,7 @@ extern "C" int az_c4_trunk_heads_fwd(const int8_t* boards, int B, const float* c
              AZ_EINVAL, "az_c4_trunk_heads_fwd: null pointer");
   AZ_REQUIRE(aligned16(feat) && aligned16(wp) && aligned16(wv), AZ_EINVAL,
              "az_c4_trunk_heads_fwd: operands need 16B alignment");
-  static const bool split = getenv("AZ_TRUNK_HEADS_SPLIT") != nullptr;   // A/B experiments
+  static const bool split = tuning_env("AZ_TRUNK_HEADS_SPLIT") != nullptr;   // A/B experiments
   if (B <= HEADS_ROWS_MAXB && A <= 8 && !split) {
     hipLaunchKernelGGL(c4_trunk_heads_kernel<1>, dim3(B), dim3(512), 0, as_stream(stream), boards,
                        B, conv1_w, conv1_b, conv2_w, conv2_b, feat, wp, bp, A, wv, bv, logp, pi,
@@ -778,7 +778,7 @@ static void launch_splitk_heads(const float* slab, int B, int K, const float* bi
   // 4 rows per block (one per wave): 1,664 blocks at B = 512 instead of 416 with 16 rows, so
   // 4x the slab loads in flight: 12.1 -> 9.0 us (tools/heads_rows_probe.sh on MI355X).
   // AZ_SPLITK_HEADS_ROWS = 8 / 16 selects the other shapes for A/B runs.
-  static const char* env_rows = getenv("AZ_SPLITK_HEADS_ROWS");
+  static const char* env_rows = tuning_env("AZ_SPLITK_HEADS_ROWS");
   const int rows = env_rows ? atoi(env_rows) : 4;
   if (rows == 4 || rows == 8) {
     dim3 g((K + HEADS_KC - 1) / HEADS_KC, (B + rows - 1) / rows);
@@ -825,12 +825,12 @@ extern "C" int az_linear_heads_fwd(const float* x, int B, int F, const float* w,
   const float* sl = static_cast<const float*>(slabs);
   // one launch: splitk_heads_rowsw_kernel (AZ_SPLITK_HEADS_MODE = rows / chunks select the
   // one-row-per-block kernel / chunk partials + finalize for A/B runs)
-  static const char* env_mode = getenv("AZ_SPLITK_HEADS_MODE");
+  static const char* env_mode = tuning_env("AZ_SPLITK_HEADS_MODE");
   const char mode = env_mode ? env_mode[0] : 'w';   // w: rowsw, r: rows, c: chunks + finalize
   const bool rows_mode = mode != 'c' && F <= SPLITK_ROWS_MAXK &&
                          (F + HEADS_KC - 1) / HEADS_KC <= HEADS_ROWS_MAXC;
   const int nch = (F + HEADS_KC - 1) / HEADS_KC;
-  static const char* env_r = getenv("AZ_SPLITK_HEADS_R");   // rows per block, A/B runs
+  static const char* env_r = tuning_env("AZ_SPLITK_HEADS_R");   // rows per block, A/B runs
   const int R = env_r ? atoi(env_r) : 2;
   if (S > 1 && A <= 8 && S <= 8 && rows_mode && mode == 'w' && nch <= 16 &&
       (R == 1 || R == 2 || R == 4)) {
@@ -838,9 +838,11 @@ extern "C" int az_linear_heads_fwd(const float* x, int B, int F, const float* w,
     switch (S * 8 + R) {
 #define AZ_SKW(SS, RR) case SS * 8 + RR: hipLaunchKernelGGL((splitk_heads_rowsw_kernel<8, SS, RR>), g, \
                            blk, 0, s, sl, B, F, b, y, wp, A, wv, bp, bv, logp, pi, v); break;
-      AZ_SKW(2, 1) AZ_SKW(3, 1) AZ_SKW(4, 1) AZ_SKW(5, 1) AZ_SKW(6, 1) AZ_SKW(7, 1) AZ_SKW(8, 1)
       AZ_SKW(2, 2) AZ_SKW(3, 2) AZ_SKW(4, 2) AZ_SKW(5, 2) AZ_SKW(6, 2) AZ_SKW(7, 2) AZ_SKW(8, 2)
+#ifdef AZ_TUNING   // 1 and 4 rows per block: measured slower than 2 (AZ_SPLITK_HEADS_R)
+      AZ_SKW(2, 1) AZ_SKW(3, 1) AZ_SKW(4, 1) AZ_SKW(5, 1) AZ_SKW(6, 1) AZ_SKW(7, 1) AZ_SKW(8, 1)
       AZ_SKW(2, 4) AZ_SKW(3, 4) AZ_SKW(4, 4) AZ_SKW(5, 4) AZ_SKW(6, 4) AZ_SKW(7, 4) AZ_SKW(8, 4)
+#endif
 #undef AZ_SKW
     }
     return check_launch("splitk_heads_rowsw_kernel");
@@ -909,7 +911,7 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
   if (B == 0) return AZ_OK;
   AZ_REQUIRE(boards && e->feat, AZ_EINVAL, "az_c4_eval_fwd: null boards / feat");
   int rc;
-  static const bool side = getenv("AZ_EVAL_NO_SIDE") == nullptr;   // A/B experiments
+  static const bool side = tuning_env("AZ_EVAL_NO_SIDE") == nullptr;   // A/B experiments
   if (B == 1 && v && gv && side && e->ot0_w && e->hidden && e->y && e->glogp) {
     // batch 1: the standard heads ride along with output_transform.0 (extra blocks of the same
     // launch, off the trunk -> GEMV -> GEMV -> heads chain); same kernels' arithmetic, same bits

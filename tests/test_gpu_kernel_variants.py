@@ -1,6 +1,7 @@
-"""The A/B kernel variants the C-ABI keeps behind environment switches compute the same bits as
-the default path (each switch is read once per process, so every variant runs in a child
-process of its own on the same inputs):
+"""The A/B kernel variants compute the same bits as the default path.  The switches exist only in
+the tuning build (libaz_hip_tuning.so, AZ_TUNING_LIB=1; the product library ignores the
+environment); each switch is read once per process, so every variant runs in a child process of
+its own on the same inputs, and the product library's default run is compared too:
   - heads: one launch with 2 rows per block (default) vs chunk partials + finalize
     (AZ_HEADS_TWOPASS=1) -- Connect4GNN.py:48-57;
   - the GNN tail's split-K heads: rowsw (default) vs one row per block
@@ -57,8 +58,11 @@ VARIANTS = {
 }
 
 
-def _run(tmp_path, name, env_extra):
+def _run(tmp_path, name, env_extra, tuning=True):
     env = dict(os.environ)
+    env.pop("AZ_TUNING_LIB", None)
+    if tuning:
+        env["AZ_TUNING_LIB"] = "1"
     for k in ("AZ_HEADS_TWOPASS", "AZ_SPLITK_HEADS_MODE", "AZ_GEMM_NOVEC", "AZ_GEMM_RING"):
         env.pop(k, None)
     env.update(env_extra)
@@ -72,6 +76,9 @@ def _run(tmp_path, name, env_extra):
 @pytest.mark.timeout(600)
 def test_kernel_variants_bit_identical(tmp_path):
     ref = _run(tmp_path, "default", VARIANTS["default"])
+    prod = _run(tmp_path, "product", {}, tuning=False)
+    for k, a in ref.items():
+        assert np.array_equal(a, prod[k]), f"product library: {k} differs"
     for name, env in VARIANTS.items():
         if name == "default":
             continue

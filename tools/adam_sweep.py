@@ -1,3 +1,5 @@
+import os
+os.environ.setdefault("AZ_TUNING_LIB", "1")   # A/B switches live in the tuning build
 import os, sys, time, json, torch
 sys.path.insert(0, "/root/repo/alphazero-gnn_amd")
 from azhip import ops

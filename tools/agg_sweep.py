@@ -2,6 +2,7 @@
 AZ_AGG_CFG tuning variants (each in its own process: the override is read once)."""
 import json
 import os
+os.environ.setdefault("AZ_TUNING_LIB", "1")   # A/B switches live in the tuning build
 import subprocess
 import sys
 

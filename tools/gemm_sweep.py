@@ -2,6 +2,7 @@
 tile/split overrides (each variant in its own subprocess since the overrides are read once)."""
 import json
 import os
+os.environ.setdefault("AZ_TUNING_LIB", "1")   # A/B switches live in the tuning build
 import subprocess
 import sys
 

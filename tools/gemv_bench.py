@@ -2,6 +2,7 @@
 predict_both hipGraph replay (H2D, trunk, two GEMVs, heads, D2H, sync).  One JSON line."""
 import json
 import os
+os.environ.setdefault("AZ_TUNING_LIB", "1")   # A/B switches live in the tuning build
 import sys
 import time
 

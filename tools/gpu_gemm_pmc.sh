@@ -1,5 +1,6 @@
 # GPU-box: SQ / GRBM / TCC counters of az_gemm_f32 for a list of tile configs at one shape.
 #   bash tools/gpu_gemm_pmc.sh TAG "6 16" M [N K]   ("auto" = the dispatcher's own choice)
+export AZ_TUNING_LIB=1   # A/B switches live in the tuning build
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

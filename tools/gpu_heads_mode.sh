@@ -1,5 +1,6 @@
 # GPU-box: GPU tests + smoke, then A/B of the split-K heads tail: one launch per row (default)
 # with R = 1/2/4 rows per block vs one row per block vs chunk partials + finalize, B = 512 step.
+export AZ_TUNING_LIB=1   # A/B switches live in the tuning build
 set -u
 cd "$GRAFT_REPO_ROOT"
 bash tools/gpu_check.sh hm || exit $?

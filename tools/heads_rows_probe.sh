@@ -1,5 +1,6 @@
 # GPU-box A/B of splitk_heads_partial_kernel rows per block (AZ_SPLITK_HEADS_ROWS = 16 / 8 / 4):
 # bench main step only, plus a kernel-trace pass per setting.   bash tools/heads_rows_probe.sh
+export AZ_TUNING_LIB=1   # A/B switches live in the tuning build
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

@@ -4,6 +4,7 @@ subprocess): AZ_GEMM_RING = 2 (default 2-buffer), 3 (3-buffer ring), 4 (ring + s
     python tools/ring_probe.py [M ...]"""
 import json
 import os
+os.environ.setdefault("AZ_TUNING_LIB", "1")   # A/B switches live in the tuning build
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
