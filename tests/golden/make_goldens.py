@@ -27,6 +27,10 @@ Fixtures:
   G8 rules.npz           game rules on random-play positions (Connect4 n=7,5; TicTacToe n=3,4):
                          getGameEnded for both players, getValidMoves, every legal next state,
                          getSymmetries boards and policies
+  G9 resume_ttt3/        --load_model resume (main.py:259-280, Coach.py:187-201): the checkpoint
+                         (best_gnn.pth.tar) and example history (best_gnn.pth.tar.examples) the
+                         reference wrote after one TicTacToe 3x3 GNN iteration (G7's run), and
+                         resume_ttt3.json: what the reference's resumed iteration did (seeds 1)
 """
 import argparse
 import importlib.util
@@ -510,6 +514,72 @@ def g7():
     print("  G7", res)
 
 
+# ----------------------------------------------------------------------------------- G9
+def _ttt3_args(folder, numIters=1):
+    """main.py:30-43,209-236 wiring for --game tictactoe --board_size 3 --use_gnn."""
+    import yaml
+    with open(os.path.join(REF, "tictactoe", "config.yaml")) as f:
+        config = yaml.safe_load(f)
+    args = dotdict({})
+    for section in config:
+        for k, v in config[section].items():
+            args[k] = v
+    args.update(board_size=3, numIters=numIters, use_gnn=True, gnn_layers=2, game="tictactoe",
+                load_model=False, checkpoint=folder, load_folder_file=(folder, "best_gnn.pth.tar"))
+    return args
+
+
+def g9():
+    tmp = tempfile.mkdtemp(prefix="az_g9_")
+    first = os.path.join(tmp, "first")
+    os.makedirs(first)
+    random.seed(0)
+    np.random.seed(0)
+    torch.manual_seed(0)
+    game = TicTacToeGame(n=3)
+    args = _ttt3_args(first)
+    nnet = TicTacToeGNNWrapper(game, args)
+    ref_coach.Coach(game, nnet, args).learn()
+    fix = os.path.join(HERE, "resume_ttt3")
+    os.makedirs(fix, exist_ok=True)
+    shutil.copy(os.path.join(first, "best_gnn.pth.tar"), os.path.join(fix, "best_gnn.pth.tar"))
+    shutil.copy(os.path.join(first, "checkpoint_0_gnn.pth.tar.examples"),
+                os.path.join(fix, "best_gnn.pth.tar.examples"))
+    # the resumed iteration, exactly as main.py runs it with --load_model (seeds 1)
+    second = os.path.join(tmp, "second")
+    shutil.copytree(fix, second)
+    random.seed(1)
+    np.random.seed(1)
+    torch.manual_seed(1)
+    args = _ttt3_args(second)
+    args.load_model = True
+    nnet = TicTacToeGNNWrapper(game, args)
+    nnet.load_checkpoint(args.load_folder_file[0], args.load_folder_file[1])
+    coach = ref_coach.Coach(game, nnet, args)
+    coach.loadTrainExamples()
+    arena_res = []
+    orig = ref_arena.Arena.playGames
+
+    def pg(self, num, verbose=False):
+        r = orig(self, num, verbose)
+        arena_res.append([int(x) for x in r])
+        return r
+
+    ref_arena.Arena.playGames = pg
+    try:
+        coach.learn()
+    finally:
+        ref_arena.Arena.playGames = orig
+    std_ex, gnn_ex = coach.trainExamplesHistory[0]
+    res = dict(seeds=1, loaded_history=len(coach.trainExamplesHistory), n_std=len(std_ex),
+               n_gnn=len(gnn_ex), skip_first_selfplay=bool(coach.skipFirstSelfPlay),
+               arena_pwins_nwins_draws=arena_res[0], files=sorted(os.listdir(second)))
+    shutil.rmtree(tmp)
+    with open(out("resume_ttt3.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print("  G9", res)
+
+
 # ----------------------------------------------------------------------------------- G8
 def g8():
     """Connect4Game.py:116-219 / TicTacToeGame.py on positions reached by seeded random play
@@ -572,6 +642,10 @@ def main():
     if want == {"g6b"}:
         g6b()
         print(f"G6b done {time.time() - t0:.1f}s")
+        return
+    if want == {"g9"}:
+        g9()
+        print(f"G9 done {time.time() - t0:.1f}s")
         return
     c4net, c4b = g1()
     print(f"G1 done {time.time() - t0:.1f}s")
