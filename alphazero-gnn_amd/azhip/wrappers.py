@@ -535,6 +535,13 @@ class GNNWrapperMixin:
 
     has_gnn = True
 
+    @property
+    def batch_invariant_rows(self):
+        """Largest batch whose predict_both rows are bit-identical to batch-1 calls: the 7x7
+        Connect4 evaluator (az_c4_eval_fwd) computes every row of a batch of <= 8 with the
+        batch-1 arithmetic (tests/test_gpu_selfplay.py); 0 = no such guarantee."""
+        return 8 if _direct_ok(self) else 0
+
     def predict(self, board):
         return NetWrapper.predict(self, board)
 

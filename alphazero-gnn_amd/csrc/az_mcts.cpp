@@ -1074,6 +1074,23 @@ int az_game_next_canonical(int game, int n, const int8_t* board, int action, int
   return AZM_OK;
 }
 
+int az_game_children(int game, int n, const int8_t* board, int cap, int8_t* out) {
+  Rules R;
+  Key k, nk;
+  if (!R.init(game, n) || !R.from_board(board, &k) || cap < 0 || (cap > 0 && !out))
+    return fail(AZM_EINVAL, "az_game_children: bad args");
+  if (R.ended(k).x != 0.0) return 0;            // terminal: the search never expands it
+  std::vector<uint8_t> v(R.A);
+  R.valids(k, v.data());
+  int cnt = 0;
+  for (int a = 0; a < R.A && cnt < cap; ++a) {
+    if (!v[a] || !R.next(k, a, &nk)) continue;
+    R.to_board(nk, out + (size_t)cnt * R.cells);
+    ++cnt;
+  }
+  return cnt;
+}
+
 double az_np_pairwise_sum(const double* a, int n) { return pairwise(a, n); }
 
 }  // extern "C"

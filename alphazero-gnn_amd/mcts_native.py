@@ -51,6 +51,7 @@ _SIGS = {
     "az_game_ended": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _P, _P]),
     "az_game_valids": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _P]),
     "az_game_next_canonical": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, _P]),
+    "az_game_children": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, _P]),
     "az_np_pairwise_sum": (ctypes.c_double, [_P, ctypes.c_int]),
     "az_mcts_episode_begin": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int]),
@@ -432,18 +433,53 @@ class ArenaPlayer:
     once per iteration and reused for the whole arena -- so arena games depend on each other
     and are played one after the other; what moves native is the per-simulation search and
     rules work (MCTS.py:151-240).  Leaves go to the network one at a time (`predict_both` on
-    one board when use_gnn, else `predict_batch`), as the reference's batch-1 calls."""
+    one board when use_gnn, else `predict_batch`), as the reference's batch-1 calls.
 
-    def __init__(self, game, nnet, args):
+    Speculative leaf batches (nets whose rows are batch-invariant, `batch_invariant_rows`): a
+    leaf the search asks for is evaluated together with the boards one move below it (at most
+    batch_invariant_rows - 1 of them) and every row is cached by board bytes, so the next
+    simulation that reaches one of those children finds it without a network round trip.  The
+    rows of such a batch are bit-identical to batch-1 evaluations of the same boards
+    (tests/test_gpu_selfplay.py), so the search -- and every arena game -- is unchanged; only the
+    number of launches drops.  The cache lives as long as the player (one arena: the network
+    does not change)."""
+
+    def __init__(self, game, nnet, args, prefetch=True):
         get = (lambda k, d=None: args.get(k, d)) if isinstance(args, dict) else \
             (lambda k, d=None: getattr(args, k, d))
         self.use_gnn = bool(get("use_gnn", False))
         self.nnet, self.args = nnet, args
         self.eng = Engine(game, 1, float(get("cpuct", 1.0)), self.use_gnn)
         self.mcts = NativeMCTS(self.eng, 0, game, args)
+        rows = int(getattr(nnet, "batch_invariant_rows", 0) or 0) if prefetch else 0
+        self.spec = rows if rows >= 2 else 0
+        self.cache = {}
+        self.calls = self.hits = 0
+        if self.spec:
+            self._kids = np.zeros((self.spec - 1, self.eng.n, self.eng.n), np.int8)
+
+    def _evaluate(self, boards):
+        """pi, v, gpi, gv for the k leaf boards (k = 1 in the arena)."""
+        from selfplay import _net_call
+        if not self.spec:
+            self.calls += 1
+            return _net_call(self.nnet, boards, self.use_gnn)
+        key = boards[0].tobytes()
+        row = self.cache.get(key)
+        if row is None:
+            nk = lib().az_game_children(self.eng.kind, self.eng.n, _ptr(np.ascontiguousarray(
+                boards[0])), self.spec - 1, _ptr(self._kids))
+            batch = np.concatenate([boards[:1], self._kids[:max(0, nk)]])
+            self.calls += 1
+            out = _net_call(self.nnet, batch, self.use_gnn)
+            for i in range(len(batch)):
+                self.cache[batch[i].tobytes()] = tuple(None if a is None else a[i] for a in out)
+            row = self.cache[key]
+        else:
+            self.hits += 1
+        return tuple(None if a is None else np.asarray(a)[None] for a in row)
 
     def _search(self, board, sims):
-        from selfplay import _net_call
         self.eng.begin(0, board, sims)
         idle = 0
         while self.eng.remaining(0) > 0:
@@ -455,7 +491,7 @@ class ArenaPlayer:
                 continue
             idle = 0
             try:
-                pi, v, gpi, gv = _net_call(self.nnet, self.eng.leaf_boards[:k], self.use_gnn)
+                pi, v, gpi, gv = self._evaluate(self.eng.leaf_boards[:k])
             except Exception as ex:  # MCTS.py:195-200: uniform priors, value 0 (counted)
                 nn_fallback.record("ArenaPlayer", ex, k)
                 self.eng.feed(k, failed=True)

@@ -80,3 +80,51 @@ def test_native_arena_equals_python_arena(name, use_gnn):
     assert results[0][0] == results[1][0]
     assert results[0][1] == results[1][1] and results[0][2] == results[1][2]
     assert len(results[0][1]) > games          # several moves per game were really searched
+
+
+class SpecHashNet(HashNet):
+    """HashNet whose rows do not depend on the batch: ArenaPlayer may batch a leaf with its
+    children (speculative leaf batches)."""
+    batch_invariant_rows = 8
+
+    def __init__(self, A, salt):
+        super().__init__(A, salt)
+        self.batches = []
+
+    def predict_batch(self, boards):
+        self.batches.append(len(boards))
+        return super().predict_batch(boards)
+
+    def predict_both(self, boards):
+        self.batches.append(len(boards))
+        pi, v = HashNet.predict_batch(self, boards)
+        rows = [self.predict_with_gnn(b) for b in boards]
+        return pi, v, np.stack([p for p, _ in rows]), np.array([x for _, x in rows], np.float32)
+
+
+@pytest.mark.parametrize("name", ["ttt3", "c4"])
+@pytest.mark.parametrize("use_gnn", [False, True])
+def test_speculative_leaf_batches_play_the_same_games(name, use_gnn):
+    """A leaf evaluated together with its children (rows cached by board) leaves every search,
+    move and W/L/D of the arena unchanged, with fewer network calls."""
+    from Arena import Arena
+    from mcts_native import ArenaPlayer
+    make, sims, games = _games()[name]
+    game = make()
+    A = game.getActionSize()
+    args = Args(numMCTSSims=sims, cpuct=1.0, use_gnn=use_gnn)
+    results, calls = [], []
+    for prefetch in (False, True):
+        pnet, nnet = SpecHashNet(A, 1), SpecHashNet(A, 2)
+        np.random.seed(321)
+        p1 = ArenaPlayer(game, pnet, args, prefetch=prefetch)
+        p2 = ArenaPlayer(game, nnet, args, prefetch=prefetch)
+        r1, r2 = Recorder(p1), Recorder(p2)
+        wld = Arena(r1, r2, game).playGames(games)
+        results.append((wld, r1.moves, r2.moves))
+        calls.append((p1.calls + p2.calls, p1.hits + p2.hits,
+                      max(pnet.batches + nnet.batches)))
+    assert results[0] == results[1]
+    (c0, h0, b0), (c1, h1, b1) = calls
+    assert h0 == 0 and b0 == 1 and h1 > 0 and b1 <= 8
+    assert c1 + h1 == c0 and c1 < c0

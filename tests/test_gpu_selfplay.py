@@ -262,6 +262,62 @@ def test_batch_row_bit_identity_report(c4):
     assert rep[1]
 
 
+def test_batch_rows_up_to_8_are_batch1_bits(c4):
+    """The premise of the arena's speculative leaf batches (mcts_native.ArenaPlayer,
+    c4.batch_invariant_rows == 8): in any batch of <= 8 boards every row of predict_both --
+    pi, v, gnn_pi, gnn_v -- is bit-identical (torch.equal) to the batch-1 evaluation of that
+    board, whatever the other rows are and wherever the row sits."""
+    z = golden(CASE + ".npz")
+    boards = z["std_boards"].astype(np.int64)
+    rng = np.random.default_rng(5)
+    pick = rng.choice(len(boards), size=48, replace=False)
+    one = {int(i): [torch.from_numpy(np.ascontiguousarray(np.asarray(x).reshape(-1)))
+                    for x in c4.predict_both(boards[i:i + 1])] for i in pick}
+    assert c4.batch_invariant_rows == 8
+    for B in range(1, 9):
+        for t in range(6):
+            idx = rng.choice(pick, size=B, replace=False)
+            out = c4.predict_both(boards[idx])
+            for r, i in enumerate(idx):
+                for k, x in enumerate(out):
+                    row = torch.from_numpy(np.ascontiguousarray(np.asarray(x[r]).reshape(-1)))
+                    assert torch.equal(row, one[int(i)][k]), (B, t, r, k)
+
+
+def test_arena_speculative_batches_equal_batch1(c4):
+    """Arena gating (Coach.py:137-145) with the HIP GNN players, config 3 search (sims 100):
+    speculative leaf batches (leaf + children, rows cached) play exactly the games of batch-1
+    leaves -- same moves, same W/L/D -- with about half the network calls."""
+    from Arena import Arena
+    from connect4.Connect4Game import Connect4Game
+    from connect4.Connect4GNN import Connect4GNNWrapper
+    from mcts_native import ArenaPlayer
+    game = Connect4Game(7)
+    args = SimpleNamespace(numMCTSSims=100, cpuct=1.0, use_gnn=True, dropout=0.3, gnn_layers=2)
+    torch.manual_seed(11)
+    other = Connect4GNNWrapper(game, args)
+    res, calls = [], []
+    for prefetch in (False, True):
+        np.random.seed(7)
+        p1 = ArenaPlayer(game, c4, args, prefetch=prefetch)
+        p2 = ArenaPlayer(game, other, args, prefetch=prefetch)
+        moves = []
+
+        def rec(p):
+            def f(x):
+                a = p(x)
+                moves.append((np.asarray(x).tobytes(), a))
+                return a
+            return f
+        wld = Arena(rec(p1), rec(p2), game).playGames(2)
+        res.append((wld, moves))
+        calls.append((p1.calls + p2.calls, p1.hits + p2.hits))
+    _report("arena_speculative_calls", {"batch1": calls[0], "speculative": calls[1],
+                                        "wld": list(res[0][0])})
+    assert res[0] == res[1]
+    assert calls[1][0] < 0.7 * calls[0][0] and calls[1][0] + calls[1][1] == calls[0][0]
+
+
 def test_coach_learn_connect4_gnn_sims100(tmp_path):
     """Config 3 end to end on the GPU: connect4/config.yaml + --use_gnn --numMCTSSims 100,
     self-play on the native engine (lock step), train, arena, checkpoints; no network fallback

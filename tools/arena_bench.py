@@ -18,16 +18,20 @@ from connect4.Connect4GNN import Connect4GNNWrapper  # noqa: E402
 from connect4.Connect4Game import Connect4Game  # noqa: E402
 from mcts_native import ArenaPlayer  # noqa: E402
 
-games = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+games = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 4
 args = SimpleNamespace(numMCTSSims=100, cpuct=1.0, use_gnn=True, dropout=0.3, gnn_layers=2)
 game = Connect4Game(7)
 torch.manual_seed(0)
 pnet, nnet = Connect4GNNWrapper(game, args), Connect4GNNWrapper(game, args)
 out = {}
-for native in (True, False):
+legs = ["native_speculative", "native_batch1"] + (["python"] if "--python" in sys.argv else [])
+for leg in legs:
     np.random.seed(7)
+    native = leg != "python"
     if native:
-        p1, p2 = ArenaPlayer(game, pnet, args), ArenaPlayer(game, nnet, args)
+        pf = leg == "native_speculative"
+        p1 = ArenaPlayer(game, pnet, args, prefetch=pf)
+        p2 = ArenaPlayer(game, nnet, args, prefetch=pf)
     else:
         pm, nm = MCTS(game, pnet, args), MCTS(game, nnet, args)
         p1 = lambda x: np.argmax(pm.getActionProb(x, temp=0))  # noqa: E731
@@ -35,6 +39,7 @@ for native in (True, False):
     t0 = time.perf_counter()
     wld = Arena(p1, p2, game).playGames(games)
     dt = time.perf_counter() - t0
-    out["native" if native else "python"] = {"wld": wld, "seconds": round(dt, 2),
-                                             "games_per_s": round(games / dt, 3)}
+    out[leg] = {"wld": wld, "seconds": round(dt, 2), "games_per_s": round(games / dt, 3)}
+    if native:
+        out[leg].update(calls=p1.calls + p2.calls, hits=p1.hits + p2.hits)
     print(json.dumps(out), flush=True)
