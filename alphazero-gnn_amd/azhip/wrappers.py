@@ -235,28 +235,34 @@ class _Batch1Graph:
 
 
 class _Batch1Direct:
-    """Connect4 batch-1 evaluation as ONE C call (az_c4_eval_fwd: 1 + 3 direct launches) with
-    zero-copy staging: the board is read and pi / v written in place in mapped host memory.
-    Measured on MI355X, a hipGraph replay costs ~14 us of host time before its first kernel
-    runs, more than these launches, which overlap the GPU work they queue.  Same kernels as the
-    eager path (bit-identical outputs); parameters are read through the pointers fixed here,
-    which stay valid because every update is in place.  kind as _Batch1Graph."""
+    """Connect4 evaluation of up to `cap` boards as ONE C call (az_c4_eval_fwd: 1 + 3 direct
+    launches) with zero-copy staging: the boards are read and pi / v written in place in mapped
+    host memory.  Measured on MI355X, a hipGraph replay costs ~14 us of host time before its
+    first kernel runs, more than these launches, which overlap the GPU work they queue.  Same
+    kernels as the eager path (bit-identical outputs); parameters are read through the pointers
+    fixed here, which stay valid because every update is in place.  kind as _Batch1Graph.
 
-    def __init__(self, w, kind):
+    Output layout in the host buffer: pi [cap][A], v [cap] (kind std/both), then gpi [cap][A],
+    gv [cap] (kind gnn/both); with cap = 1 that is the packed [pi, v(, gpi, gv)] row run()
+    returns.  cap = 8 serves the arena's speculative leaf batches (rows <= 8 take the same
+    GEMV arithmetic as one row: mcts_native.ArenaPlayer, tests/test_gpu_selfplay.py)."""
+
+    def __init__(self, w, kind, cap=1):
         dev = w.device
         A = w.action_size
-        self.kind, self.A = kind, A
-        width = {"std": A + 1, "gnn": A + 1, "both": 2 * A + 2}[kind]
-        self.host = ops.HostBuffer(256 + 4 * width)
-        self.h_in = self.host.view(0, torch.int8, (1, w.board_x, w.board_y))
-        self.h_out = self.host.view(256, torch.float32, (1, width))
-        F = 3136
+        self.kind, self.A, self.cap = kind, A, cap
+        std = kind in ("std", "both")
         gnn = kind in ("gnn", "both")
-        self.feat = torch.empty((1, F), device=dev)
-        self.hidden = torch.empty((1, F), device=dev) if gnn else None
-        self.y = torch.empty((1, F), device=dev) if gnn else None
-        self.logp = torch.empty((1, A), device=dev)
-        self.glogp = torch.empty((1, A), device=dev)
+        width = (A + 1) * (int(std) + int(gnn))
+        self.host = ops.HostBuffer(256 * cap + 4 * width * cap)
+        self.h_in = self.host.view(0, torch.int8, (cap, w.board_x, w.board_y))
+        self.h_out = self.host.view(256 * cap, torch.float32, (cap * width,))
+        F = 3136
+        self.feat = torch.empty((cap, F), device=dev)
+        self.hidden = torch.empty((cap, F), device=dev) if gnn else None
+        self.y = torch.empty((cap, F), device=dev) if gnn else None
+        self.logp = torch.empty((cap, A), device=dev)
+        self.glogp = torch.empty((cap, A), device=dev)
         self.ws = torch.empty((16 << 20,), dtype=torch.uint8, device=dev)
         W = w.nnet.params
         G = w.gnn.params if gnn else None
@@ -269,30 +275,47 @@ class _Batch1Direct:
             P(G["output_transform.0.bias"]) if gnn else None,
             P(G["output_transform.2.weight"]) if gnn else None,
             P(G["output_transform.2.bias"]) if gnn else None,
-            1, P(self.feat), P(self.hidden), P(self.y), P(self.logp), P(self.glogp),
+            cap, P(self.feat), P(self.hidden), P(self.y), P(self.logp), P(self.glogp),
             P(self.ws), self.ws.numel())
-        assert int(_lib.lib().az_transform_heads_ws_bytes(1, F, A)) <= self.ws.numel()
-        o = self.h_out.data_ptr()
-        std = kind in ("std", "both")
-        g0 = 0 if kind == "gnn" else A + 1
-        self.args = (ctypes.byref(self.desc), ctypes.c_void_p(self.h_in.data_ptr()), 1,
-                     ctypes.c_void_p(o) if std else None,
-                     ctypes.c_void_p(o + 4 * A) if std else None,
-                     ctypes.c_void_p(o + 4 * g0) if gnn else None,
-                     ctypes.c_void_p(o + 4 * (g0 + A)) if gnn else None)
-        self.fn = _lib.lib().az_c4_eval_fwd
+        L = _lib.lib()
+        assert max(int(L.az_transform_heads_ws_bytes(cap, F, A)),
+                   int(L.az_heads_ws_bytes(cap, F, A))) <= self.ws.numel()
+        o = self.h_out.numpy()
+        # views: pi [cap][A], v [cap], gpi [cap][A], gv [cap] (None where the kind has none)
+        off, views = 0, []
+        for on in (std, gnn):
+            if on:
+                views += [o[off:off + cap * A].reshape(cap, A), o[off + cap * A:off + cap * (A + 1)]]
+                off += cap * (A + 1)
+            else:
+                views += [None, None]
+        self.views = views
+        self.args = (ctypes.byref(self.desc), ctypes.c_void_p(self.h_in.data_ptr()))
+        self.outs = tuple(None if v is None else ctypes.c_void_p(v.ctypes.data) for v in views)
+        self.fn = L.az_c4_eval_fwd
         self.dev = dev
         # keep the parameter tensors alive with the pointers taken above
         self._keep = (W, G)
 
-    def run(self, board):
-        self.h_in.numpy()[0] = board
+    def _call(self, n):
         s = torch.cuda.current_stream(self.dev)
-        rc = self.fn(*self.args, ctypes.c_void_p(s.cuda_stream))
+        rc = self.fn(*self.args, n, *self.outs, ctypes.c_void_p(s.cuda_stream))
         if rc:
             _lib.check(rc, "az_c4_eval_fwd")
         s.synchronize()
-        return self.h_out.numpy()[0].copy()
+
+    def run(self, board):
+        """One board -> the packed row [pi, v(, gpi, gv)] (cap 1)."""
+        self.h_in.numpy()[0] = board
+        self._call(1)
+        return self.h_out.numpy().copy()
+
+    def run_rows(self, boards):
+        """n <= cap boards -> (pi [n][A], v [n], gpi, gv) copies (None where the kind has none)."""
+        n = len(boards)
+        self.h_in.numpy()[:n] = boards
+        self._call(n)
+        return tuple(None if v is None else v[:n].copy() for v in self.views)
 
 
 def _direct_ok(w):
@@ -345,7 +368,10 @@ class NetWrapper:
             self.nnet.eval()
             if self.has_gnn:
                 self.gnn.eval()
-            g[kind] = _Batch1Direct(self, kind) if _direct_ok(self) else _Batch1Graph(self, kind)
+            if _direct_ok(self):
+                g[kind] = _Batch1Direct(self, kind, cap=8 if kind == "both" else 1)
+            else:
+                g[kind] = _Batch1Graph(self, kind)
         return g[kind]
 
     def _eval(self, boards, gnn):
@@ -570,7 +596,10 @@ class GNNWrapperMixin:
         self.nnet.eval()
         self.gnn.eval()
         A = self.action_size
-        if len(boards) == 1 and (g := self._graph1("both")) is not None:
+        g = self._graph1("both") if len(boards) <= 8 else None
+        if isinstance(g, _Batch1Direct) and len(boards) > 0:
+            return g.run_rows(np.asarray(boards))
+        if len(boards) == 1 and g is not None:
             out = g.run(boards[0])[None]
             return out[:, :A], out[:, A], out[:, A + 1:2 * A + 1], out[:, 2 * A + 1]
         b = boards_to_device(boards, self.device)

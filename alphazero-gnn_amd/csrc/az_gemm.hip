@@ -1055,6 +1055,48 @@ __global__ __launch_bounds__(256) void gemv_f32(GemmArgs p) {
   }
 }
 
+// Staging of MG rows of A (zero-padded to S*256 floats each) for the whole-K GEMVs, split into
+// a load phase and an LDS-store phase so that every load of the block is in flight before the
+// first one is waited for: with the loads issued ahead of the weight stream, the store phase
+// waits for A alone (vmcnt is in order), and no load sits next to a branch.
+template <int MG, int S>
+struct RowStage {
+  static constexpr int T = MG * S * 64;          // float4 slots
+  static constexpr int NI = (T + 255) / 256;     // per thread
+  f32x4 v[NI];
+  __device__ __forceinline__ void load(const GemmArgs& p, int m0) {
+    int ar[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      ar[i] = min(m0 + min((int)threadIdx.x + 256 * i, T - 1) / (S * 64), p.M - 1);
+    if (p.a_rows) {                                // gathered rows: all index loads, one wait
+#pragma unroll
+      for (int i = 0; i < NI; ++i) ar[i] = p.a_rows[ar[i]];
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int idx = min((int)threadIdx.x + 256 * i, T - 1);
+      const int k = (idx % (S * 64)) * 4;
+      const int kc = k < p.K ? k : 0;
+      const float* src = (p.A2 && kc >= p.K0) ? p.A2 + (size_t)ar[i] * p.lda2 + (kc - p.K0)
+                                              : p.A + (size_t)ar[i] * p.lda + kc;
+      v[i] = *reinterpret_cast<const f32x4*>(src);
+    }
+  }
+  __device__ __forceinline__ void store(const GemmArgs& p, int m0, float* As) const {
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int idx = (int)threadIdx.x + 256 * i;
+      if (T % 256 == 0 || idx < T) {
+        const int m = idx / (S * 64), k = (idx % (S * 64)) * 4;
+        const bool ok = m0 + m < p.M && k < p.K;
+        *reinterpret_cast<f32x4*>(&As[m * S * 256 + k]) = ok ? v[i] : z;
+      }
+    }
+  }
+};
+
 // Whole-K GEMV for K <= 256*S (the batch-1 predict shapes): A's MR rows are staged in LDS once
 // (zero-padded to 256*S), then each wave issues ALL S float4 loads of its R weight rows before
 // the first FMA -- one HBM round trip per wave instead of one per KC chunk.  Loads past K
@@ -1064,6 +1106,8 @@ template <int MR, int S, int R>
 __device__ __forceinline__ void gemv_full_block(const GemmArgs& p, int bid, float* As) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n_base = (bid * 4 + wave) * R;
+  RowStage<MR, S> st;
+  st.load(p, 0);
   f32x4 w[R][S];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -1074,17 +1118,8 @@ __device__ __forceinline__ void gemv_full_block(const GemmArgs& p, int bid, floa
       w[r][s] = *reinterpret_cast<const f32x4*>(p.B + (size_t)n * p.ldb + (k4 < p.K ? k4 : 0));
     }
   }
-  for (int idx = threadIdx.x; idx < MR * S * 64; idx += 256) {
-    const int m = idx / (S * 64), k = (idx % (S * 64)) * 4;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (m < p.M && k < p.K) {
-      const int ar = p.a_rows ? p.a_rows[m] : m;
-      const float* src = (p.A2 && k >= p.K0) ? p.A2 + (size_t)ar * p.lda2 + (k - p.K0)
-                                             : p.A + (size_t)ar * p.lda + k;
-      v = *reinterpret_cast<const f32x4*>(src);
-    }
-    *reinterpret_cast<f32x4*>(&As[m * S * 256 + k]) = v;
-  }
+  __builtin_amdgcn_sched_barrier(0);        // keep the weight stream issued before A's wait
+  st.store(p, 0, As);
   __syncthreads();
   float acc[MR][R];
 #pragma unroll
@@ -1121,6 +1156,70 @@ template <int MR, int S, int R>
 __global__ __launch_bounds__(256) void gemv_full(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) float As[MR * S * 256];
   gemv_full_block<MR, S, R>(p, blockIdx.x, As);
+}
+
+// gemv_full for 3 <= M <= 8 with S = 13 (K = 3136: output_transform on a speculative arena
+// batch, mcts_native.ArenaPlayer), where MR = 4 / 8 rows of A would not fit gemv_full's LDS
+// budget: the wave's R weight rows are loaded ONCE into registers, then the rows of A go through
+// LDS MG at a time.  Every output is the same lane-strided fmaf chain + wave_sum as gemv_full,
+// so a row's result does not depend on M (bit-identical to the batch-1 launch).
+template <int S, int R, int MG>
+__global__ __launch_bounds__(256) void gemv_rows(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) float As[MG * S * 256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n_base = (blockIdx.x * 4 + wave) * R;
+  RowStage<MG, S> st;
+  st.load(p, 0);
+  f32x4 w[R][S];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = n_base + r < p.N ? n_base + r : 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int k4 = (lane + 64 * s) * 4;
+      w[r][s] = *reinterpret_cast<const f32x4*>(p.B + (size_t)n * p.ldb + (k4 < p.K ? k4 : 0));
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);        // keep the weight stream issued before A's wait
+  st.store(p, 0, As);
+  for (int m0 = 0; m0 < p.M; m0 += MG) {
+    __syncthreads();                        // this group's A is in LDS
+    const bool more = m0 + MG < p.M;
+    if (more) st.load(p, m0 + MG);          // the next group's loads fly under this group's FMAs
+    float acc[MG][R];
+#pragma unroll
+    for (int m = 0; m < MG; ++m)
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[m][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int k4 = (lane + 64 * s) * 4;
+#pragma unroll
+      for (int m = 0; m < MG; ++m) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&As[m * S * 256 + k4]);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          acc[m][r] = fmaf(a[0], w[r][s][0], fmaf(a[1], w[r][s][1],
+                      fmaf(a[2], w[r][s][2], fmaf(a[3], w[r][s][3], acc[m][r]))));
+      }
+    }
+    float mine = 0.f;  // lane m*R + r keeps the reduced sum of output (m0 + m, n_base + r)
+#pragma unroll
+    for (int m = 0; m < MG; ++m)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float t = wave_sum(acc[m][r]);
+        if (lane == m * R + r) mine = t;
+      }
+    if (more) {
+      __syncthreads();                      // every wave is done reading this group
+      st.store(p, m0 + MG, As);
+    }
+    if (lane < MG * R) {
+      const int m = m0 + lane / R, r = lane % R;
+      if (m < p.M && n_base + r < p.N) epilogue_store(p, m, n_base + r, mine);
+    }
+  }
 }
 
 // gemv_full (M = 1) plus B extra blocks that run the policy/value heads of rows of `side.x` --
@@ -1402,6 +1501,10 @@ static bool launch_gemv_full(const GemmArgs& a, hipStream_t s) {
 
 static void launch_gemv(const GemmArgs& a, hipStream_t s) {
   static const bool chunked = tuning_env("AZ_GEMV_CHUNKED") != nullptr;   // A/B experiments
+  if (!chunked && a.M >= 3 && a.K > 256 * 8 && a.K <= 256 * 13) {
+    hipLaunchKernelGGL((gemv_rows<13, 2, 4>), dim3((a.N + 7) / 8), dim3(256), 0, s, a);
+    return;
+  }
   if (!chunked) {
     bool done = false;
     switch (a.M) {

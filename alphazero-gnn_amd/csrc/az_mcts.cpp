@@ -1085,6 +1085,7 @@ int az_game_children(int game, int n, const int8_t* board, int cap, int8_t* out)
   int cnt = 0;
   for (int a = 0; a < R.A && cnt < cap; ++a) {
     if (!v[a] || !R.next(k, a, &nk)) continue;
+    if (R.ended(nk).x != 0.0) continue;         // terminal children are never evaluated
     R.to_board(nk, out + (size_t)cnt * R.cells);
     ++cnt;
   }

@@ -126,9 +126,9 @@ int az_rng_doubles(uint32_t seed, int n, double* out);
 int az_game_ended(int game, int n, const int8_t* board, int* tag, double* value);
 int az_game_valids(int game, int n, const int8_t* board, int8_t* valids);
 int az_game_next_canonical(int game, int n, const int8_t* board, int action, int8_t* out);
-/* The canonical boards one move below a non-terminal `board` (valid actions in ascending order,
- * at most `cap`), written to out [cap][n*n]; returns their count (0 for a terminal board).  The
- * arena's speculative leaf batches use it (mcts_native.ArenaPlayer). */
+/* The non-terminal canonical boards one move below a non-terminal `board` (valid actions in
+ * ascending order, at most `cap`), written to out [cap][n*n]; returns their count (0 for a
+ * terminal board).  The arena's speculative leaf batches use it (mcts_native.ArenaPlayer). */
 int az_game_children(int game, int n, const int8_t* board, int cap, int8_t* out);
 /* np.sum of a float64 vector (NumPy's pairwise summation), for tests. */
 double az_np_pairwise_sum(const double* a, int n);

@@ -45,7 +45,8 @@ def check_dot_error(got, ref, bound, tol=1e-6):
 @pytest.mark.parametrize("M,N,K", [(1, 3136, 3136), (3, 37, 64), (8, 128, 6272), (64, 128, 3136),
                                    (512, 3136, 3136), (130, 70, 48), (4096, 256, 64),
                                    (1, 7, 4096), (2, 1001, 260), (5, 300, 1024), (1, 33, 4100),
-                                   (32768, 1024, 1024)])
+                                   (32768, 1024, 1024), (3, 3136, 3136), (8, 3136, 3136),
+                                   (6, 1000, 2500)])
 @pytest.mark.parametrize("act", [0, 1, 2])
 def test_linear_vs_torch(ops, M, N, K, act):
     g = torch.Generator().manual_seed(M * 7 + N + K + act)
@@ -57,6 +58,22 @@ def test_linear_vs_torch(ops, M, N, K, act):
     y = ops.linear(x.cuda(), w.cuda(), b.cuda(), act=act).cpu()
     bound = x.double().abs() @ w.double().abs().T + b.double().abs()
     check_dot_error(y.numpy(), ref.numpy(), bound.numpy())
+
+
+@pytest.mark.parametrize("K", [3136, 2500, 100])
+def test_small_m_rows_are_batch1_bits(ops, K):
+    """M <= 8 rows (gemv_full / gemv_rows): every row of a batch is bit-identical to the same row
+    computed alone, whatever M -- the premise of the arena's speculative leaf batches."""
+    g = torch.Generator().manual_seed(K)
+    N = 3136
+    x = (torch.rand((8, K), generator=g) * 2 - 1).cuda()
+    w = ((torch.rand((N, K), generator=g) * 2 - 1) / K ** 0.5).cuda()
+    b = (torch.rand((N,), generator=g) - 0.5).cuda()
+    one = [ops.linear(x[i:i + 1].contiguous(), w, b, act=1).cpu() for i in range(8)]
+    for M in range(2, 9):
+        y = ops.linear(x[:M].contiguous(), w, b, act=1).cpu()
+        for i in range(M):
+            assert torch.equal(y[i:i + 1], one[i]), (M, i)
 
 
 def test_linear_split_gather_gated(ops):

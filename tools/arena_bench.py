@@ -24,12 +24,13 @@ game = Connect4Game(7)
 torch.manual_seed(0)
 pnet, nnet = Connect4GNNWrapper(game, args), Connect4GNNWrapper(game, args)
 out = {}
-legs = ["native_speculative", "native_batch1"] + (["python"] if "--python" in sys.argv else [])
+# warm-up leg first (allocations, graph capture), then each leg timed
+legs = ["warmup", "native_speculative", "native_batch1", "native_speculative2", "native_batch1_2"] + (["python"] if "--python" in sys.argv else [])
 for leg in legs:
     np.random.seed(7)
     native = leg != "python"
     if native:
-        pf = leg == "native_speculative"
+        pf = "speculative" in leg or leg == "warmup"
         p1 = ArenaPlayer(game, pnet, args, prefetch=pf)
         p2 = ArenaPlayer(game, nnet, args, prefetch=pf)
     else:
@@ -43,3 +44,16 @@ for leg in legs:
     if native:
         out[leg].update(calls=p1.calls + p2.calls, hits=p1.hits + p2.hits)
     print(json.dumps(out), flush=True)
+
+# per-call latency of the network entry points the arena uses (board in, numpy out)
+z = np.zeros((8, 7, 7), np.int64)
+lat = {}
+for B in (1, 2, 8):
+    for _ in range(50):
+        pnet.predict_both(z[:B])
+    t0 = time.perf_counter()
+    for _ in range(500):
+        pnet.predict_both(z[:B])
+    lat["predict_both_B%d_us" % B] = round((time.perf_counter() - t0) / 500 * 1e6, 2)
+out["latency"] = lat
+print(json.dumps(out), flush=True)
