@@ -1164,10 +1164,9 @@ __global__ __launch_bounds__(256) void gemv_full(GemmArgs p) {
 // LDS MG at a time.  Every output is the same lane-strided fmaf chain + wave_sum as gemv_full,
 // so a row's result does not depend on M (bit-identical to the batch-1 launch).
 template <int S, int R, int MG>
-__global__ __launch_bounds__(256) void gemv_rows(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) float As[MG * S * 256];
+__device__ __forceinline__ void gemv_rows_block(const GemmArgs& p, int bid, float* As) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n_base = (blockIdx.x * 4 + wave) * R;
+  const int n_base = (bid * 4 + wave) * R;
   RowStage<MG, S> st;
   st.load(p, 0);
   f32x4 w[R][S];
@@ -1222,16 +1221,25 @@ __global__ __launch_bounds__(256) void gemv_rows(GemmArgs p) {
   }
 }
 
-// gemv_full (M = 1) plus B extra blocks that run the policy/value heads of rows of `side.x` --
+template <int S, int R, int MG>
+__global__ __launch_bounds__(256) void gemv_rows(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) float As[MG * S * 256];
+  gemv_rows_block<S, R, MG>(p, blockIdx.x, As);
+}
+
+// gemv_full / gemv_rows (M <= 8) plus B extra blocks that run the policy/value heads of rows of
+// `side.x` --
 // the batch-1 leaf's standard heads ride along with output_transform.0 instead of lengthening
 // the launch chain (they only need the trunk's features, which the GEMV reads too).
-template <int S, int R>
+template <int S, int R, int MK>
 __global__ __launch_bounds__(256) void gemv_side_heads(GemmArgs p, SideHeads h, int nblk) {
-  __shared__ __attribute__((aligned(16))) float As[S * 256];
+  // MK: 1 / 2 = gemv_full_block with that many rows, 3 = gemv_rows_block (3..8 rows, 2 per group)
+  __shared__ __attribute__((aligned(16))) float As[(MK == 1 ? 1 : 2) * S * 256];
   __shared__ float part[HEADS_ROWS_MAXC * 9];
   __shared__ float sm[9];
   if ((int)blockIdx.x < nblk) {
-    gemv_full_block<1, S, R>(p, blockIdx.x, As);
+    if constexpr (MK == 3) gemv_rows_block<S, R, 2>(p, blockIdx.x, As);
+    else gemv_full_block<MK, S, R>(p, blockIdx.x, As);
   } else {
     const int row = blockIdx.x - nblk;
     heads_row_block<8, 4>(h.x + (size_t)row * h.ldx, h.x + (size_t)row * h.ldx, h.K, h.wp, h.A,
@@ -1502,7 +1510,21 @@ static bool launch_gemv_full(const GemmArgs& a, hipStream_t s) {
 static void launch_gemv(const GemmArgs& a, hipStream_t s) {
   static const bool chunked = tuning_env("AZ_GEMV_CHUNKED") != nullptr;   // A/B experiments
   if (!chunked && a.M >= 3 && a.K > 256 * 8 && a.K <= 256 * 13) {
-    hipLaunchKernelGGL((gemv_rows<13, 2, 4>), dim3((a.N + 7) / 8), dim3(256), 0, s, a);
+#ifdef AZ_TUNING   // AZ_GEMV_ROWS=<MG><R>: rows per LDS group, weight rows per wave (A/B runs)
+    static const char* env_rows = tuning_env("AZ_GEMV_ROWS");
+    const int v = env_rows ? atoi(env_rows) : 22;
+    switch (v) {
+      case 42: hipLaunchKernelGGL((gemv_rows<13, 2, 4>), dim3((a.N + 7) / 8), dim3(256), 0, s, a); return;
+      case 82: hipLaunchKernelGGL((gemv_rows<13, 2, 8>), dim3((a.N + 7) / 8), dim3(256), 0, s, a); return;
+      case 41: hipLaunchKernelGGL((gemv_rows<13, 1, 4>), dim3((a.N + 3) / 4), dim3(256), 0, s, a); return;
+      case 44: hipLaunchKernelGGL((gemv_rows<13, 4, 4>), dim3((a.N + 15) / 16), dim3(256), 0, s, a); return;
+      case 12: hipLaunchKernelGGL((gemv_rows<13, 2, 1>), dim3((a.N + 7) / 8), dim3(256), 0, s, a); return;
+      default: break;
+    }
+#endif
+    // 2 rows per LDS group: 10.6 us at M = 3..4, 14.6 at M = 8 vs 16.4 / 25.2 with 4-row groups
+    // and 9.9 / 15.7 with 1 (tools/gemv_probe.py on MI355X)
+    hipLaunchKernelGGL((gemv_rows<13, 2, 2>), dim3((a.N + 7) / 8), dim3(256), 0, s, a);
     return;
   }
   if (!chunked) {
@@ -1726,12 +1748,14 @@ int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s) {
   return check_launch("splitk_reduce_kernel");
 }
 
-// gemv_side_heads for the batch-1 leaf: d must be M = 1 with K-major operands, a plain
+// gemv_side_heads for the batch-1 leaf and small speculative batches: d must be M <= 8 (the
+// same per-row arithmetic as gemv for that M) with K-major operands, a plain
 // bias/activation epilogue and 3072 < K <= 3328 (output_transform.0 at F = 3136), and h at most
 // 8 actions; returns 1 when launched, 0 when the shapes do not qualify (nothing launched), or
 // a negative AZ_E* code.
 int gemv1_with_side_heads(const az_gemm_desc* d, const SideHeads* h, hipStream_t s) {
-  if (!(d->M == 1 && d->a_kmajor && d->b_kmajor && !d->A2 && !d->a_rows && !d->C2 && !d->R &&
+  if (!(d->M >= 1 && d->M <= 8 && d->a_kmajor && d->b_kmajor && !d->A2 && !d->a_rows && !d->C2 &&
+        !d->R &&
         !d->G && d->act != AZ_ACT_DRELU && d->K > 3072 && d->K <= 3328 && d->K % 4 == 0 &&
         d->lda % 4 == 0 && d->ldb % 4 == 0 && aligned16(d->A) && aligned16(d->B) &&
         h->A >= 1 && h->A <= 8 && h->K % 4 == 0 && h->ldx % 4 == 0 &&
@@ -1739,13 +1763,16 @@ int gemv1_with_side_heads(const az_gemm_desc* d, const SideHeads* h, hipStream_t
         aligned16(h->wp) && aligned16(h->wv)))
     return 0;
   GemmArgs a = {};
-  a.M = 1; a.N = d->N; a.K = d->K;
+  a.M = d->M; a.N = d->N; a.K = d->K;
   a.A = d->A; a.lda = d->lda; a.K0 = d->K;
   a.B = d->B; a.ldb = d->ldb;
   a.bias = d->bias; a.act = d->act; a.beta = d->beta; a.C = d->C; a.ldc = d->ldc;
   a.splits = 1; a.kc = d->K;
   const int nblk = (a.N + 4 * 2 - 1) / (4 * 2);
-  hipLaunchKernelGGL((gemv_side_heads<13, 2>), dim3(nblk + h->B), dim3(256), 0, s, a, *h, nblk);
+  const dim3 grid(nblk + h->B), blk(256);
+  if (a.M == 1) hipLaunchKernelGGL((gemv_side_heads<13, 2, 1>), grid, blk, 0, s, a, *h, nblk);
+  else if (a.M == 2) hipLaunchKernelGGL((gemv_side_heads<13, 2, 2>), grid, blk, 0, s, a, *h, nblk);
+  else hipLaunchKernelGGL((gemv_side_heads<13, 2, 3>), grid, blk, 0, s, a, *h, nblk);
   const int rc = check_launch("gemv_side_heads");
   return rc == AZ_OK ? 1 : rc;
 }

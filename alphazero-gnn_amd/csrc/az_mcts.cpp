@@ -347,6 +347,7 @@ struct Tree {
   int pending_leaf = -1;                      // node waiting for the network
   std::vector<std::pair<int32_t, int32_t>> path;
   int64_t nsa_total = 0, ps_count = 0;
+  int64_t cache_hits = 0;                     // leaves expanded from az_mcts_cache_put rows
   bool pending_std = false;                   // episode mode: waiting for the root's predict
   Episode ep;
 
@@ -423,6 +424,53 @@ struct Tree {
 
 }  // namespace
 
+// Network rows computed ahead of the search (az_mcts_cache_put): board key -> [pi, v, gpi, gv].
+// Read-only while searches run, so the slots of a parallel collect may share it.
+struct RowCache {
+  std::vector<Key> keys;
+  std::vector<int32_t> table;                   // open addressing, -1 = empty
+  std::vector<float> rows;                      // stride 2A + 2
+  int stride = 0;
+  const float* find(const Key& k) const {
+    if (keys.empty()) return nullptr;
+    const uint64_t mask = table.size() - 1;
+    for (uint64_t h = khash(k) & mask;; h = (h + 1) & mask) {
+      const int32_t i = table[h];
+      if (i < 0) return nullptr;
+      if (keys[i] == k) return &rows[(size_t)i * stride];
+    }
+  }
+  void rehash(size_t cap) {
+    table.assign(cap, -1);
+    for (int32_t i = 0; i < (int32_t)keys.size(); ++i) {
+      uint64_t h = khash(keys[i]) & (cap - 1);
+      while (table[h] >= 0) h = (h + 1) & (cap - 1);
+      table[h] = i;
+    }
+  }
+  float* insert(const Key& k) {               // the row of k (existing rows are overwritten)
+    if (table.empty()) table.assign(1024, -1);
+    const uint64_t mask = table.size() - 1;
+    uint64_t h = khash(k) & mask;
+    for (;; h = (h + 1) & mask) {
+      const int32_t i = table[h];
+      if (i < 0) break;
+      if (keys[i] == k) return &rows[(size_t)i * stride];
+    }
+    const int32_t id = (int32_t)keys.size();
+    keys.push_back(k);
+    rows.resize(rows.size() + stride);
+    table[h] = id;
+    if (keys.size() * 2 > table.size()) rehash(table.size() * 2);
+    return &rows[(size_t)id * stride];
+  }
+  void clear() {
+    keys.clear();
+    table.clear();
+    rows.clear();
+  }
+};
+
 struct az_mcts {
   Rules R;
   double cpuct = 1.0;
@@ -431,6 +479,7 @@ struct az_mcts {
   std::vector<int32_t> last_order;             // slots of the last collect, in output order
   std::vector<int8_t> leafbuf;
   int threads = 1;                             // host threads of the last collect (feed too)
+  RowCache cache;
 };
 
 namespace {
@@ -485,7 +534,11 @@ void backup(az_mcts* m, Tree& t, Val v) {
   t.path.clear();
 }
 
-// Run searches of one slot until it waits on a leaf (returns 1) or has none left (0).
+void expand(az_mcts* m, Tree& t, const float* pi, float v_std, const float* gpi, float gv,
+            bool failed);
+
+// Run searches of one slot until it waits on a leaf (returns 1) or has none left (0).  A new
+// leaf whose board has a cached row (az_mcts_cache_put) is expanded on the spot.
 int advance(az_mcts* m, Tree& t) {
   while (t.remaining > 0 && t.pending_leaf < 0) {
     t.path.clear();
@@ -500,7 +553,14 @@ int advance(az_mcts* m, Tree& t) {
       if (!nd.expanded) {                        // new leaf: Vs, then the network
         t.alloc_edges(id, m->R);
         t.pending_leaf = id;
-        return 1;
+        const float* row = m->cache.find(t.nodes[id].key);
+        if (!row) return 1;
+        // a row computed ahead (bit-identical to this leaf's own evaluation): expand now
+        const int A = m->R.A;
+        expand(m, t, row, row[A], m->use_gnn ? row + A + 1 : nullptr,
+               m->use_gnn ? row[2 * A + 1] : 0.f, false);
+        t.cache_hits += 1;
+        goto next_search;
       }
       int a = select_action(m, t, nd);
       if (a < 0) {                               // MCTS.py:220-221
@@ -520,6 +580,7 @@ int advance(az_mcts* m, Tree& t) {
     }
     backup(m, t, v);
     t.remaining -= 1;
+  next_search:;
   }
   return 0;
 }
@@ -983,6 +1044,45 @@ int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const f
   }
   m->last_order.clear();
   return aborted;
+}
+
+int az_mcts_cache_put(az_mcts* m, int count, const int8_t* boards, const float* pi, const float* v,
+                      const float* gpi, const float* gv) {
+  if (!m || count < 0 || (count > 0 && (!boards || !pi || !v)) ||
+      (count > 0 && m->use_gnn && (!gpi || !gv)))
+    return fail(AZM_EINVAL, "az_mcts_cache_put: bad args");
+  const int A = m->R.A;
+  m->cache.stride = 2 * A + 2;
+  for (int i = 0; i < count; ++i) {
+    Key k;
+    if (!m->R.from_board(boards + (size_t)i * m->R.cells, &k))
+      return fail(AZM_EINVAL, "az_mcts_cache_put: cells must be -1/0/1");
+    float* r = m->cache.insert(k);
+    std::memcpy(r, pi + (size_t)i * A, sizeof(float) * A);
+    r[A] = v[i];
+    if (m->use_gnn) {
+      std::memcpy(r + A + 1, gpi + (size_t)i * A, sizeof(float) * A);
+      r[2 * A + 1] = gv[i];
+    } else {
+      std::fill(r + A + 1, r + 2 * A + 2, 0.f);
+    }
+  }
+  return AZM_OK;
+}
+
+int az_mcts_cache_clear(az_mcts* m) {
+  if (!m) return fail(AZM_EINVAL, "az_mcts_cache_clear: bad args");
+  m->cache.clear();
+  return AZM_OK;
+}
+
+int az_mcts_cache_stats(const az_mcts* m, int64_t* out) {
+  if (!m || !out) return fail(AZM_EINVAL, "az_mcts_cache_stats: bad args");
+  int64_t hits = 0;
+  for (const auto& t : m->trees) hits += t.cache_hits;
+  out[0] = (int64_t)m->cache.keys.size();
+  out[1] = hits;
+  return AZM_OK;
 }
 
 int az_mcts_root_edges(const az_mcts* m, int slot, const int8_t* board, int32_t* nsa, double* q,

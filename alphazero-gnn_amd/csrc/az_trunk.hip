@@ -53,9 +53,9 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   // float4 rows (the MFMA layout puts 16 channels 49 floats apart on consecutive lanes, so
   // direct stores scatter 4-byte writes); NB = 8 lacks the LDS for it
   constexpr bool STAGE = NB <= 4;
-  __shared__ float bd[NB * PP];
+  __shared__ float bd[NB * PP + 1];
   __shared__ float c1[NB * CI * PP];
-  __shared__ float w1s[CI * 9 + CI];   // conv1 weights then bias: one round trip, then LDS only
+  __shared__ float w1s[CI * 9 + CI + 1];   // conv1 weights, bias, pad: one round trip, then LDS
   const int tid = threadIdx.x;
   const int b0 = blockIdx.x * NB;
   const int nb = min(NB, B - b0);
@@ -63,22 +63,37 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   const int nt = wave & 3, mh = wave >> 2;
   const int h = lane >> 4, c16 = lane & 15;
   const int co = nt * 16 + c16;
+  // Every global load of the prologue is issued before the first one is waited for (conv2's
+  // 9 float4 per thread, the boards, conv1's weights, the bias), then the LDS stores: as a
+  // load -> store loop each iteration waited for its own round trip (11 in a row).
   // conv2's weights -> LDS (row co = 288 floats = 72 float4, so no float4 crosses a row)
-  for (int i = tid; i < 64 * 72; i += 512) {
-    const f32x4v w = reinterpret_cast<const f32x4v*>(w2)[i];
-    float* d = un + (i / 72) * W2S_STRIDE + (i % 72) * 4;
-    d[0] = w[0]; d[1] = w[1]; d[2] = w[2]; d[3] = w[3];
-  }
-  const float bias = b2[co];
-
-  for (int i = tid; i < NB * PP; i += 512) {
+  constexpr int NW2 = 64 * 72 / 512;
+  f32x4v wst[NW2];
+#pragma unroll
+  for (int j = 0; j < NW2; ++j) wst[j] = reinterpret_cast<const f32x4v*>(w2)[tid + 512 * j];
+  constexpr int NBD = (NB * PP + 511) / 512;
+  int8_t bdv[NBD];
+  bool bdin[NBD];
+#pragma unroll
+  for (int j = 0; j < NBD; ++j) {
+    const int i = tid + 512 * j;
     const int b = i / PP, pp = i % PP, px = pp / 9, py = pp % 9;
-    float v = 0.f;
-    if (b < nb && px >= 1 && px <= 7 && py >= 1 && py <= 7)
-      v = (float)boards[(size_t)(b0 + b) * P + (px - 1) * 7 + (py - 1)];
-    bd[i] = v;
+    bdin[j] = i < NB * PP && b < nb && px >= 1 && px <= 7 && py >= 1 && py <= 7;
+    bdv[j] = boards[bdin[j] ? (size_t)(b0 + b) * P + (px - 1) * 7 + (py - 1) : (size_t)b0 * P];
   }
-  if (tid < CI * 9 + CI) w1s[tid] = tid < CI * 9 ? w1[tid] : b1[tid - CI * 9];
+  const float w1v = tid < CI * 9 ? w1[tid] : b1[min(tid - CI * 9, CI - 1)];
+  const float bias = b2[co];
+  __builtin_amdgcn_sched_barrier(0);   // no load sinks into the guarded stores below
+#pragma unroll
+  for (int j = 0; j < NW2; ++j) {
+    const int i = tid + 512 * j;
+    float* d = un + (i / 72) * W2S_STRIDE + (i % 72) * 4;
+    d[0] = wst[j][0]; d[1] = wst[j][1]; d[2] = wst[j][2]; d[3] = wst[j][3];
+  }
+#pragma unroll
+  for (int j = 0; j < NBD; ++j)   // unguarded (past-the-end lanes hit bd's pad slot): a guarded
+    bd[min(tid + 512 * j, NB * PP)] = bdin[j] ? (float)bdv[j] : 0.f;   // use sinks the load
+  w1s[min(tid, CI * 9 + CI)] = w1v;     // unguarded: lanes past the 320 weights hit the pad
   __syncthreads();
   float breg[72];
 #pragma unroll
@@ -600,6 +615,88 @@ __global__ __launch_bounds__(1024) void heads_rowsw_kernel(
   });
 }
 
+// Latency form of the trunk for a handful of boards (the arena's leaf + speculative children,
+// B <= 8): block (b, q) computes output channels [16q, 16q + 16) of board b, so one board's
+// trunk is spread over 4 CUs and each block stages a quarter of conv2's weights (18 KB instead
+// of 74 KB).  Every feature value is the same MFMA chain as c4_trunk_tile's (same operands,
+// same k order, same bias + ReLU), so the output is bit-identical to c4_trunk_kernel<1>.
+__global__ __launch_bounds__(256) void c4_trunk_split_kernel(
+    const int8_t* __restrict__ boards, const float* __restrict__ w1, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ feat) {
+  constexpr int P = 49, PP = 81, CI = 32, MT = 4;
+  __shared__ __attribute__((aligned(16))) float w2s[17 * W2S_STRIDE];   // + pad row
+  __shared__ float bd[PP + 1];
+  __shared__ float c1[CI * PP];
+  __shared__ float w1s[CI * 9 + CI + 1];
+  const int tid = threadIdx.x, b = blockIdx.x, q = blockIdx.y;
+  const int lane = tid & 63, mt = tid >> 6;            // wave = m-tile (4 x 16 rows >= 49)
+  const int h = lane >> 4, c16 = lane & 15;
+  const int co = q * 16 + c16;
+  // all prologue loads in flight before the first wait (see c4_trunk_tile), then the stores
+  constexpr int NW2 = (16 * 72 + 255) / 256;
+  f32x4v wst[NW2];
+  const f32x4v* w2q = reinterpret_cast<const f32x4v*>(w2 + (size_t)q * 16 * 288);
+#pragma unroll
+  for (int j = 0; j < NW2; ++j) wst[j] = w2q[min(tid + 256 * j, 16 * 72 - 1)];
+  const int px = tid / 9, py = tid % 9;
+  const bool inside = tid < PP && px >= 1 && px <= 7 && py >= 1 && py <= 7;
+  const int8_t bv = boards[(size_t)b * P + (inside ? (px - 1) * 7 + (py - 1) : 0)];
+  const float w1a = w1[tid];                                   // tid < 256 < CI * 9
+  const int e1 = min(tid + 256, CI * 9 + CI - 1);
+  const float w1b = e1 < CI * 9 ? w1[e1] : b1[e1 - CI * 9];
+  const float bias = b2[co];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < NW2; ++j) {   // unguarded: lanes past the 1152 float4 write the pad row
+    const int i = min(tid + 256 * j, 16 * 72);
+    float* d = w2s + (i / 72) * W2S_STRIDE + (i % 72) * 4;
+    d[0] = wst[j][0]; d[1] = wst[j][1]; d[2] = wst[j][2]; d[3] = wst[j][3];
+  }
+  bd[min(tid, PP)] = inside ? (float)bv : 0.f;   // unguarded (pad slot): keeps the load early
+  w1s[tid] = w1a;
+  w1s[min(tid + 256, CI * 9 + CI)] = w1b;          // unguarded (pad slot)
+  __syncthreads();
+  float breg[72];
+#pragma unroll
+  for (int s = 0; s < 72; ++s) {
+    const int tap = s >> 3, ci = 4 * (s & 7) + h;
+    breg[s] = w2s[c16 * W2S_STRIDE + ci * 9 + (tap / 3) * 3 + (tap % 3)];
+  }
+  for (int i = tid; i < CI * PP; i += 256) {
+    const int ci = i / PP, pp = i % PP, px = pp / 9, py = pp % 9;
+    float v = 0.f;
+    if (px >= 1 && px <= 7 && py >= 1 && py <= 7) {
+      float s = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+          s = fmaf(w1s[ci * 9 + kh * 3 + kw], bd[(px - 1 + kh) * 9 + (py - 1 + kw)], s);
+      s += w1s[CI * 9 + ci];
+      v = s > 0.f ? s : 0.f;
+    }
+    c1[i] = v;
+  }
+  __syncthreads();
+  const int i = mt * 16 + c16;
+  const float* a0 = c1 + (i < P ? h * PP + (i / 7) * 9 + (i % 7) : 0);
+  f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 72; ++s) {
+    const int tap = s >> 3;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[4 * (s & 7) * PP + (tap / 3) * 9 + (tap % 3)],
+                                               breg[s], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int p = mt * 16 + h * 4 + r;
+    if (p < P) {
+      const float v = acc[r] + bias;
+      feat[(size_t)b * 3136 + co * P + p] = v > 0.f ? v : 0.f;
+    }
+  }
+}
+
 // Connect4 trunk + policy/value heads in ONE launch for small batches (the batch-1 MCTS leaf):
 // c4_trunk_kernel's body, then each of the block's boards runs heads_row_block on its feature
 // row straight from the LDS staging tile -- same values and arithmetic as az_c4_trunk_fwd +
@@ -634,7 +731,7 @@ extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w
              "az_c4_trunk_fwd: null pointer");
   hipStream_t s = as_stream(stream);
   static const char* env = tuning_env("AZ_TRUNK_NB");   // tuning experiments only
-  int nbk = B >= 4096 ? 8 : (B >= 2048 ? 4 : (B >= 256 ? 2 : 1));
+  int nbk = B >= 4096 ? 8 : (B >= 2048 ? 4 : (B >= 256 ? 2 : (B <= 8 ? 0 : 1)));
   if (env) nbk = atoi(env);
   switch (nbk) {
     case 8:
@@ -648,6 +745,10 @@ extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w
     case 2:
       hipLaunchKernelGGL(c4_trunk_kernel<2>, dim3((B + 1) / 2), dim3(512), 0, s, boards, B,
                          conv1_w, conv1_b, conv2_w, conv2_b, feat);
+      break;
+    case 0:   // latency form: 4 blocks per board (bit-identical)
+      hipLaunchKernelGGL(c4_trunk_split_kernel, dim3(B, 4), dim3(256), 0, s, boards, conv1_w,
+                         conv1_b, conv2_w, conv2_b, feat);
       break;
     default:
       hipLaunchKernelGGL(c4_trunk_kernel<1>, dim3(B), dim3(512), 0, s, boards, B, conv1_w,
@@ -912,23 +1013,24 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
   AZ_REQUIRE(boards && e->feat, AZ_EINVAL, "az_c4_eval_fwd: null boards / feat");
   int rc;
   static const bool side = tuning_env("AZ_EVAL_NO_SIDE") == nullptr;   // A/B experiments
-  if (B == 1 && v && gv && side && e->ot0_w && e->hidden && e->y && e->glogp) {
-    // batch 1: the standard heads ride along with output_transform.0 (extra blocks of the same
+  if (B <= 8 && v && gv && side && e->ot0_w && e->hidden && e->y && e->glogp) {
+    // batch 1 and small speculative batches: the trunk in its latency form (4 blocks per
+    // board), the standard heads ride along with output_transform.0 (extra blocks of the same
     // launch, off the trunk -> GEMV -> GEMV -> heads chain); same kernels' arithmetic, same bits
-    if ((rc = az_c4_trunk_fwd(boards, 1, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b, e->feat,
+    if ((rc = az_c4_trunk_fwd(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b, e->feat,
                               stream)))
       return rc;
     az_gemm_desc d = {};
-    d.M = 1; d.N = 3136; d.K = 3136;
+    d.M = B; d.N = 3136; d.K = 3136;
     d.A = e->feat; d.lda = 3136; d.a_kmajor = 1;
     d.B = e->ot0_w; d.ldb = 3136; d.b_kmajor = 1; d.bias = e->ot0_b; d.act = AZ_ACT_RELU;
     d.C = e->hidden; d.ldc = 3136;
-    const SideHeads h = {e->feat, 3136, 3136, 1, e->fc_policy_w, e->fc_policy_b, e->A,
+    const SideHeads h = {e->feat, 3136, 3136, B, e->fc_policy_w, e->fc_policy_b, e->A,
                          e->fc_value_w, e->fc_value_b, e->logp, pi, v};
     rc = gemv1_with_side_heads(&d, &h, as_stream(stream));
     if (rc < 0) return rc;
     if (rc == 1)
-      return az_linear_heads_fwd(e->hidden, 1, 3136, e->ot2_w, e->ot2_b, e->fc_policy_w,
+      return az_linear_heads_fwd(e->hidden, B, 3136, e->ot2_w, e->ot2_b, e->fc_policy_w,
                                  e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b, e->y,
                                  e->glogp, gpi, gv, e->ws, e->ws_bytes, stream);
     // shapes not covered: the general sequence below (re-runs the trunk, harmless)

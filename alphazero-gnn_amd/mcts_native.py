@@ -44,6 +44,9 @@ _SIGS = {
     "az_mcts_remaining_all": (ctypes.c_int, [_P, _P]),
     "az_mcts_collect": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, ctypes.c_int]),
     "az_mcts_feed": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int]),
+    "az_mcts_cache_put": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
+    "az_mcts_cache_clear": (ctypes.c_int, [_P]),
+    "az_mcts_cache_stats": (ctypes.c_int, [_P, _P]),
     "az_mcts_root_edges": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P]),
     "az_mcts_get_std": (ctypes.c_int, [_P, ctypes.c_int, _P, _P]),
     "az_mcts_set_std": (ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.c_float]),
@@ -195,6 +198,35 @@ class Engine:
                 for a in (pi, v, gpi, gv)]
         ptrs = [None if a is None else _ptr(a) for a in arrs]
         return _check(lib().az_mcts_feed(self.h, k, *ptrs, int(bool(failed))), "az_mcts_feed")
+
+    def cache_put(self, boards, pi, v, gpi=None, gv=None):
+        """Rows for boards the search has not reached yet (see az_mcts_cache_put): a later new
+        leaf on one of them is expanded inside collect().  Rows must be bit-identical to the
+        board's own evaluation."""
+        boards = np.ascontiguousarray(boards, dtype=np.int8)
+        k = boards.shape[0]
+        if k == 0:
+            return
+        arrs = []
+        for name, a, nd in (("pi", pi, 2), ("v", v, 1), ("gpi", gpi, 2), ("gv", gv, 1)):
+            if a is None:
+                if self.use_gnn or name in ("pi", "v"):
+                    raise ValueError(f"Engine.cache_put: {name} missing")
+                arrs.append(None)
+                continue
+            a = np.ascontiguousarray(a, dtype=np.float32)
+            if a.ndim != nd or a.shape[0] != k or (nd == 2 and a.shape[1] != self.A):
+                raise ValueError(f"Engine.cache_put: {name} has shape {a.shape}")
+            arrs.append(a)
+        _check(lib().az_mcts_cache_put(self.h, k, _ptr(boards),
+                                       *[None if a is None else _ptr(a) for a in arrs]),
+               "az_mcts_cache_put")
+
+    def cache_stats(self):
+        """-> (rows held, leaves expanded from them)."""
+        out = np.zeros(2, np.int64)
+        _check(lib().az_mcts_cache_stats(self.h, _ptr(out)), "az_mcts_cache_stats")
+        return int(out[0]), int(out[1])
 
     def root_edges(self, slot, board):
         """-> (nsa list[int], q list[float64], tags list[int])."""
@@ -436,10 +468,11 @@ class ArenaPlayer:
     one board when use_gnn, else `predict_batch`), as the reference's batch-1 calls.
 
     Speculative leaf batches (nets whose rows are batch-invariant, `batch_invariant_rows`): a
-    leaf the search asks for is evaluated together with the boards one move below it (at most
-    batch_invariant_rows - 1 of them) and every row is cached by board bytes, so the next
-    simulation that reaches one of those children finds it without a network round trip.  The
-    rows of such a batch are bit-identical to batch-1 evaluations of the same boards
+    leaf the search asks for is evaluated together with the non-terminal boards one move below
+    it (at most batch_invariant_rows - 1 of them), and the children's rows go into the engine's
+    row cache (az_mcts_cache_put), so a later simulation that reaches one of them as a new leaf
+    is expanded inside the engine without a network call or a return to Python.  The rows of
+    such a batch are bit-identical to batch-1 evaluations of the same boards
     (tests/test_gpu_selfplay.py), so the search -- and every arena game -- is unchanged; only the
     number of launches drops.  The cache lives as long as the player (one arena: the network
     does not change)."""
@@ -453,31 +486,33 @@ class ArenaPlayer:
         self.mcts = NativeMCTS(self.eng, 0, game, args)
         rows = int(getattr(nnet, "batch_invariant_rows", 0) or 0) if prefetch else 0
         self.spec = rows if rows >= 2 else 0
-        self.cache = {}
-        self.calls = self.hits = 0
+        self.calls = 0
         if self.spec:
             self._kids = np.zeros((self.spec - 1, self.eng.n, self.eng.n), np.int8)
+            self._batch = np.zeros((self.spec, self.eng.n, self.eng.n), np.int8)
+
+    @property
+    def hits(self):
+        """Leaves the search expanded from speculative rows (no network call of their own)."""
+        return self.eng.cache_stats()[1]
 
     def _evaluate(self, boards):
-        """pi, v, gpi, gv for the k leaf boards (k = 1 in the arena)."""
+        """pi, v, gpi, gv for the k leaf boards (k = 1 in the arena); with speculative batches,
+        the leaf's children ride along and their rows go to the engine's cache."""
         from selfplay import _net_call
+        self.calls += 1
         if not self.spec:
-            self.calls += 1
             return _net_call(self.nnet, boards, self.use_gnn)
-        key = boards[0].tobytes()
-        row = self.cache.get(key)
-        if row is None:
-            nk = lib().az_game_children(self.eng.kind, self.eng.n, _ptr(np.ascontiguousarray(
-                boards[0])), self.spec - 1, _ptr(self._kids))
-            batch = np.concatenate([boards[:1], self._kids[:max(0, nk)]])
-            self.calls += 1
-            out = _net_call(self.nnet, batch, self.use_gnn)
-            for i in range(len(batch)):
-                self.cache[batch[i].tobytes()] = tuple(None if a is None else a[i] for a in out)
-            row = self.cache[key]
-        else:
-            self.hits += 1
-        return tuple(None if a is None else np.asarray(a)[None] for a in row)
+        nk = lib().az_game_children(self.eng.kind, self.eng.n, _ptr(np.ascontiguousarray(
+            boards[0])), self.spec - 1, _ptr(self._kids))
+        nk = max(0, nk)
+        batch = self._batch[:1 + nk]
+        batch[0] = boards[0]
+        batch[1:] = self._kids[:nk]
+        out = _net_call(self.nnet, batch, self.use_gnn)
+        if nk:
+            self.eng.cache_put(batch[1:], *[None if a is None else np.asarray(a)[1:] for a in out])
+        return tuple(None if a is None else np.asarray(a)[:1] for a in out)
 
     def _search(self, board, sims):
         self.eng.begin(0, board, sims)

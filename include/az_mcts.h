@@ -81,6 +81,18 @@ int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int thr
 int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const float* gpi,
                  const float* gv, int failed);
 
+/* Speculative rows: network outputs of boards the search has not asked for yet (the arena
+ * evaluates a leaf together with its children, mcts_native.ArenaPlayer), same layout as
+ * az_mcts_feed.  A later search that reaches one of these boards as a new leaf is expanded from
+ * the row inside az_mcts_collect instead of being handed out -- exactly what feeding that row
+ * would do, so callers must only put rows bit-identical to the board's own evaluation.  The
+ * cache is per engine, persists across az_mcts_reset / az_mcts_begin, and is read-only during a
+ * collect.  az_mcts_cache_stats: out[0] = rows held, out[1] = leaves expanded from them. */
+int az_mcts_cache_put(az_mcts* m, int count, const int8_t* boards, const float* pi, const float* v,
+                      const float* gpi, const float* gv);
+int az_mcts_cache_clear(az_mcts* m);
+int az_mcts_cache_stats(const az_mcts* m, int64_t* out);
+
 /* Root statistics: nsa[A] visit counts (0 = no entry), q[A] values, qtag[A] AZM_TAG_*. */
 int az_mcts_root_edges(const az_mcts* m, int slot, const int8_t* board, int32_t* nsa, double* q,
                        int8_t* qtag);

@@ -146,6 +146,20 @@ int run_search(int game, int n, int use_gnn) {
         fake_net(&boards[(size_t)i * cells], cells, A, 3, &pi[(size_t)i * A], &v[i]);
         fake_net(&boards[(size_t)i * cells], cells, A, 4, &gpi[(size_t)i * A], &gv[i]);
       }
+      // speculative rows for the leaves' children (az_mcts_cache_put): later searches that
+      // reach them expand inside collect
+      for (int i = 0; i < k && it % 3 == 0; ++i) {
+        std::vector<int8_t> kids((size_t)8 * cells);
+        const int nk = az_game_children(game, n, &boards[(size_t)i * cells], 8, kids.data());
+        if (nk < 0) return fail("children");
+        std::vector<float> kp((size_t)nk * A + 1), kv(nk + 1), kg((size_t)nk * A + 1), kgv(nk + 1);
+        for (int c = 0; c < nk; ++c) {
+          fake_net(&kids[(size_t)c * cells], cells, A, 3, &kp[(size_t)c * A], &kv[c]);
+          fake_net(&kids[(size_t)c * cells], cells, A, 4, &kg[(size_t)c * A], &kgv[c]);
+        }
+        if (az_mcts_cache_put(m, nk, kids.data(), kp.data(), kv.data(), kg.data(), kgv.data()))
+          return fail("cache_put");
+      }
       if (k && az_mcts_feed(m, k, pi.data(), v.data(), gpi.data(), gv.data(), it % 13 == 5) < 0)
         return fail("feed");
       if (az_mcts_remaining_all(m, rem.data())) return fail("remaining_all");
@@ -169,6 +183,9 @@ int run_search(int game, int n, int use_gnn) {
   }
   int64_t st[4];
   if (az_mcts_tree_stats(m, 0, st)) return fail("tree_stats");
+  int64_t cs[2];
+  if (az_mcts_cache_stats(m, cs) || cs[0] <= 0) return fail("cache_stats");
+  if (az_mcts_cache_clear(m) || az_mcts_cache_stats(m, cs) || cs[0] != 0) return fail("cache_clear");
   // error paths: bad slot, bad board, wrong feed count, feed without a collect
   std::vector<int8_t> bad(cells, 3);
   if (az_mcts_begin(m, 9, root.data(), 1) != AZM_EINVAL) return fail("bad slot accepted");

@@ -166,7 +166,7 @@ def test_c4_trunk_and_heads_vs_oracle(ops):
     np.testing.assert_allclose(v.cpu().numpy()[:256], z["v_b1"], atol=1e-5)
 
 
-@pytest.mark.parametrize("B", [1, 3, 32, 33, 100])
+@pytest.mark.parametrize("B", [1, 3, 8, 32, 33, 100])
 def test_c4_trunk_heads_fused_bit_identical(ops, B):
     """az_c4_trunk_heads_fwd (one launch for B <= 32) == az_c4_trunk_fwd + az_heads_fwd bit for
     bit, and the oracle within 1e-5 (Connect4Net.py:42-60)."""
