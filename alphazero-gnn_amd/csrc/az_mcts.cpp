@@ -480,6 +480,8 @@ struct az_mcts {
   std::vector<int8_t> leafbuf;
   int threads = 1;                             // host threads of the last collect (feed too)
   RowCache cache;
+  int spec_slot = -1;                          // az_mcts_collect_spec: slot of the pending leaf
+  std::vector<Key> spec_keys;                  // ... and the children that ride along
 };
 
 namespace {
@@ -973,6 +975,8 @@ int az_mcts_remaining_all(const az_mcts* m, int32_t* out) {
 
 int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int threads) {
   if (!m || !boards || !slots || cap < 0) return fail(AZM_EINVAL, "az_mcts_collect: bad args");
+  if (m->spec_slot >= 0)
+    return fail(AZM_ESTATE, "az_mcts_collect: a collect_spec request was not fed");
   for (auto& t : m->trees)
     if (t.pending_leaf >= 0 && !m->last_order.empty())
       return fail(AZM_ESTATE, "az_mcts_collect: the previous leaves were not fed");
@@ -1067,6 +1071,69 @@ int az_mcts_cache_put(az_mcts* m, int count, const int8_t* boards, const float* 
       std::fill(r + A + 1, r + 2 * A + 2, 0.f);
     }
   }
+  return AZM_OK;
+}
+
+int az_mcts_collect_spec(az_mcts* m, int slot, int8_t* boards, int cap) {
+  if (!slot_ok(m, slot) || !boards || cap < 1)
+    return fail(AZM_EINVAL, "az_mcts_collect_spec: bad args");
+  if (!m->last_order.empty() || m->spec_slot >= 0)
+    return fail(AZM_ESTATE, "az_mcts_collect_spec: the previous request was not fed");
+  Tree& t = m->trees[slot];
+  if (t.ep.phase != E_IDLE) return fail(AZM_ESTATE, "az_mcts_collect_spec: slot is in episode mode");
+  if (t.pending_leaf < 0) advance(m, t);
+  if (t.pending_leaf < 0) return 0;            // searches done (or none queued)
+  const Rules& R = m->R;
+  const Key leaf = t.nodes[t.pending_leaf].key;
+  R.to_board(leaf, boards);
+  int cnt = 1;
+  m->spec_keys.clear();
+  if (R.ended(leaf).x == 0.0) {
+    uint8_t v[kMaxA];
+    R.valids(leaf, v);
+    Key nk;
+    for (int a = 0; a < R.A && cnt < cap; ++a) {
+      if (!v[a] || !R.next(leaf, a, &nk)) continue;
+      if (R.ended(nk).x != 0.0) continue;       // terminal: never evaluated
+      const int32_t id = t.find(nk);
+      if (id >= 0 && t.nodes[id].expanded) continue;   // already has its row in the tree
+      if (m->cache.find(nk)) continue;                // already speculated
+      R.to_board(nk, boards + (size_t)cnt * R.cells);
+      m->spec_keys.push_back(nk);
+      ++cnt;
+    }
+  }
+  m->spec_slot = slot;
+  return cnt;
+}
+
+int az_mcts_feed_spec(az_mcts* m, int count, const float* pi, const float* v, const float* gpi,
+                      const float* gv, int failed) {
+  if (!m || m->spec_slot < 0) return fail(AZM_ESTATE, "az_mcts_feed_spec: nothing collected");
+  if (count != 1 + (int)m->spec_keys.size())
+    return fail(AZM_EINVAL, "az_mcts_feed_spec: count differs from the last collect_spec");
+  if (!failed && (!pi || !v || (m->use_gnn && (!gpi || !gv))))
+    return fail(AZM_EINVAL, "az_mcts_feed_spec: missing network outputs");
+  Tree& t = m->trees[m->spec_slot];
+  m->spec_slot = -1;
+  const int A = m->R.A;
+  if (failed) {                                 // the leaf degrades (MCTS.py:195-200), no rows kept
+    expand(m, t, nullptr, 0.f, nullptr, 0.f, true);
+    return AZM_OK;
+  }
+  m->cache.stride = 2 * A + 2;
+  for (int i = 1; i < count; ++i) {
+    float* r = m->cache.insert(m->spec_keys[i - 1]);
+    std::memcpy(r, pi + (size_t)i * A, sizeof(float) * A);
+    r[A] = v[i];
+    if (m->use_gnn) {
+      std::memcpy(r + A + 1, gpi + (size_t)i * A, sizeof(float) * A);
+      r[2 * A + 1] = gv[i];
+    } else {
+      std::fill(r + A + 1, r + 2 * A + 2, 0.f);
+    }
+  }
+  expand(m, t, pi, v[0], m->use_gnn ? gpi : nullptr, m->use_gnn ? gv[0] : 0.f, false);
   return AZM_OK;
 }
 

@@ -46,6 +46,8 @@ _SIGS = {
     "az_mcts_feed": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int]),
     "az_mcts_cache_put": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "az_mcts_cache_clear": (ctypes.c_int, [_P]),
+    "az_mcts_collect_spec": (ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.c_int]),
+    "az_mcts_feed_spec": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int]),
     "az_mcts_cache_stats": (ctypes.c_int, [_P, _P]),
     "az_mcts_root_edges": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P]),
     "az_mcts_get_std": (ctypes.c_int, [_P, ctypes.c_int, _P, _P]),
@@ -137,6 +139,15 @@ class Engine:
                                         _ptr(self._rem))
         self._pn, self._pq, self._pt, self._pbb = (_ptr(self._nsa), _ptr(self._q),
                                                    _ptr(self._tag), _ptr(self._b))
+        # small feeds / cache puts (the arena's batch-1 leaves) go through persistent staging
+        # buffers with pointers taken once: a numpy pointer lookup costs ~1.5 us, more than the
+        # copy of a few rows
+        self._scap = 64
+        self._stage = [np.zeros((self._scap, self.A), np.float32), np.zeros(self._scap, np.float32),
+                       np.zeros((self._scap, self.A), np.float32), np.zeros(self._scap, np.float32)]
+        self._sptr = [_ptr(a) for a in self._stage]
+        self._sboards = np.zeros((self._scap, self.n, self.n), np.int8)
+        self._psb = _ptr(self._sboards)
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -182,45 +193,67 @@ class Engine:
         root prediction was among the failed requests: those episodes are aborted (the
         reference's root predict is unguarded, MCTS.py:108-113) and the caller must raise."""
         k = int(k)
-        if not failed:
-            # the C side reads pi + i*A for i < k: check shapes here, before any pointer escapes
-            need = [("pi", pi, 2), ("v", v, 1)]
-            if self.use_gnn:
-                need += [("gpi", gpi, 2), ("gv", gv, 1)]
-            for name, a, nd in need:
-                if a is None:
-                    raise ValueError(f"Engine.feed: {name} missing")
-                a = np.asarray(a)
-                if a.ndim != nd or a.shape[0] < k or (nd == 2 and a.shape[1] != self.A):
-                    raise ValueError(f"Engine.feed: {name} has shape {a.shape}, need "
-                                     f"({'>=%d' % k}{', %d' % self.A if nd == 2 else ''})")
-        arrs = [None if (a is None or failed) else np.ascontiguousarray(a[:k], dtype=np.float32)
-                for a in (pi, v, gpi, gv)]
-        ptrs = [None if a is None else _ptr(a) for a in arrs]
-        return _check(lib().az_mcts_feed(self.h, k, *ptrs, int(bool(failed))), "az_mcts_feed")
+        if failed:
+            return _check(lib().az_mcts_feed(self.h, k, None, None, None, None, 1), "az_mcts_feed")
+        ptrs = self._rows_ptrs("Engine.feed", k, pi, v, gpi, gv, at_least=True)
+        return _check(lib().az_mcts_feed(self.h, k, *ptrs, 0), "az_mcts_feed")
+
+    def _rows_ptrs(self, what, k, pi, v, gpi, gv, at_least):
+        """Checked float32 row pointers for pi / v (/ gpi / gv when use_gnn): the C side reads
+        pi + i*A for i < k, so shapes are verified before any pointer escapes.  Up to 64 rows
+        are copied into the staging buffers (fixed pointers), larger batches are passed as
+        contiguous float32 arrays (kept alive in self._keep until the next call)."""
+        arrs = (pi, v, gpi, gv) if self.use_gnn else (pi, v)
+        out = [None, None, None, None]
+        self._keep = []
+        for j, (name, a) in enumerate(zip(("pi", "v", "gpi", "gv"), arrs)):
+            if a is None:
+                raise ValueError(f"{what}: {name} missing")
+            nd = 2 if j % 2 == 0 else 1
+            sh = np.shape(a)
+            if len(sh) != nd or (sh[0] < k if at_least else sh[0] != k) or \
+                    (nd == 2 and sh[1] != self.A):
+                raise ValueError(f"{what}: {name} has shape {sh}, need "
+                                 f"({'>=' if at_least else ''}{k}{', %d' % self.A if nd == 2 else ''})")
+            if k <= self._scap:
+                self._stage[j][:k] = a[:k]
+                out[j] = self._sptr[j]
+            else:
+                c = np.ascontiguousarray(a[:k], dtype=np.float32)
+                self._keep.append(c)
+                out[j] = _ptr(c)
+        return out
 
     def cache_put(self, boards, pi, v, gpi=None, gv=None):
         """Rows for boards the search has not reached yet (see az_mcts_cache_put): a later new
         leaf on one of them is expanded inside collect().  Rows must be bit-identical to the
         board's own evaluation."""
-        boards = np.ascontiguousarray(boards, dtype=np.int8)
-        k = boards.shape[0]
+        k = len(boards)
         if k == 0:
             return
-        arrs = []
-        for name, a, nd in (("pi", pi, 2), ("v", v, 1), ("gpi", gpi, 2), ("gv", gv, 1)):
-            if a is None:
-                if self.use_gnn or name in ("pi", "v"):
-                    raise ValueError(f"Engine.cache_put: {name} missing")
-                arrs.append(None)
-                continue
-            a = np.ascontiguousarray(a, dtype=np.float32)
-            if a.ndim != nd or a.shape[0] != k or (nd == 2 and a.shape[1] != self.A):
-                raise ValueError(f"Engine.cache_put: {name} has shape {a.shape}")
-            arrs.append(a)
-        _check(lib().az_mcts_cache_put(self.h, k, _ptr(boards),
-                                       *[None if a is None else _ptr(a) for a in arrs]),
-               "az_mcts_cache_put")
+        ptrs = self._rows_ptrs("Engine.cache_put", k, pi, v, gpi, gv, at_least=False)
+        if k <= self._scap:
+            self._sboards[:k] = boards
+            pb = self._psb
+        else:
+            b = np.ascontiguousarray(boards, dtype=np.int8)
+            self._keep.append(b)
+            pb = _ptr(b)
+        _check(lib().az_mcts_cache_put(self.h, k, pb, *ptrs), "az_mcts_cache_put")
+
+    def collect_spec(self, slot, boards_ptr, cap):
+        """Next new leaf of `slot` + up to cap - 1 speculative children into the int8 buffer at
+        boards_ptr (see az_mcts_collect_spec) -> row count, 0 when the searches are done."""
+        return _check(lib().az_mcts_collect_spec(self.h, slot, boards_ptr, int(cap)),
+                      "az_mcts_collect_spec")
+
+    def feed_spec(self, k, pi=None, v=None, gpi=None, gv=None, failed=False):
+        """Rows for the last collect_spec's k boards (row 0 = the leaf)."""
+        if failed:
+            return _check(lib().az_mcts_feed_spec(self.h, k, None, None, None, None, 1),
+                          "az_mcts_feed_spec")
+        ptrs = self._rows_ptrs("Engine.feed_spec", k, pi, v, gpi, gv, at_least=False)
+        return _check(lib().az_mcts_feed_spec(self.h, k, *ptrs, 0), "az_mcts_feed_spec")
 
     def cache_stats(self):
         """-> (rows held, leaves expanded from them)."""
@@ -469,9 +502,10 @@ class ArenaPlayer:
 
     Speculative leaf batches (nets whose rows are batch-invariant, `batch_invariant_rows`): a
     leaf the search asks for is evaluated together with the non-terminal boards one move below
-    it (at most batch_invariant_rows - 1 of them), and the children's rows go into the engine's
-    row cache (az_mcts_cache_put), so a later simulation that reaches one of them as a new leaf
-    is expanded inside the engine without a network call or a return to Python.  The rows of
+    it (at most batch_invariant_rows - 1 of them, skipping boards already expanded or cached),
+    and the children's rows go into the engine's row cache (az_mcts_collect_spec /
+    az_mcts_feed_spec), so a later simulation that reaches one of them as a new leaf is expanded
+    inside the engine without a network call or a return to Python.  The rows of
     such a batch are bit-identical to batch-1 evaluations of the same boards
     (tests/test_gpu_selfplay.py), so the search -- and every arena game -- is unchanged; only the
     number of launches drops.  The cache lives as long as the player (one arena: the network
@@ -488,34 +522,20 @@ class ArenaPlayer:
         self.spec = rows if rows >= 2 else 0
         self.calls = 0
         if self.spec:
-            self._kids = np.zeros((self.spec - 1, self.eng.n, self.eng.n), np.int8)
             self._batch = np.zeros((self.spec, self.eng.n, self.eng.n), np.int8)
+            self._pbatch = _ptr(self._batch)
 
     @property
     def hits(self):
         """Leaves the search expanded from speculative rows (no network call of their own)."""
         return self.eng.cache_stats()[1]
 
-    def _evaluate(self, boards):
-        """pi, v, gpi, gv for the k leaf boards (k = 1 in the arena); with speculative batches,
-        the leaf's children ride along and their rows go to the engine's cache."""
-        from selfplay import _net_call
-        self.calls += 1
-        if not self.spec:
-            return _net_call(self.nnet, boards, self.use_gnn)
-        nk = lib().az_game_children(self.eng.kind, self.eng.n, _ptr(np.ascontiguousarray(
-            boards[0])), self.spec - 1, _ptr(self._kids))
-        nk = max(0, nk)
-        batch = self._batch[:1 + nk]
-        batch[0] = boards[0]
-        batch[1:] = self._kids[:nk]
-        out = _net_call(self.nnet, batch, self.use_gnn)
-        if nk:
-            self.eng.cache_put(batch[1:], *[None if a is None else np.asarray(a)[1:] for a in out])
-        return tuple(None if a is None else np.asarray(a)[:1] for a in out)
-
     def _search(self, board, sims):
         self.eng.begin(0, board, sims)
+        if self.spec:
+            self._search_spec()
+            return
+        from selfplay import _net_call
         idle = 0
         while self.eng.remaining(0) > 0:
             k = self.eng.collect(1)
@@ -525,13 +545,35 @@ class ArenaPlayer:
                     raise RuntimeError("native arena search made no progress")
                 continue
             idle = 0
+            self.calls += 1
             try:
-                pi, v, gpi, gv = self._evaluate(self.eng.leaf_boards[:k])
+                pi, v, gpi, gv = _net_call(self.nnet, self.eng.leaf_boards[:k], self.use_gnn)
             except Exception as ex:  # MCTS.py:195-200: uniform priors, value 0 (counted)
                 nn_fallback.record("ArenaPlayer", ex, k)
                 self.eng.feed(k, failed=True)
                 continue
             self.eng.feed(k, pi, v, gpi, gv)
+
+    def _search_spec(self):
+        """The search loop with speculative leaf batches: the engine hands out the leaf and its
+        children in one buffer and takes all their rows back (az_mcts_collect_spec /
+        az_mcts_feed_spec); leaves found in the row cache never come back to Python."""
+        from selfplay import _net_call
+        eng, batch, pb, cap = self.eng, self._batch, self._pbatch, self.spec
+        while True:
+            k = eng.collect_spec(0, pb, cap)
+            if k == 0:
+                if eng.remaining(0) > 0:
+                    raise RuntimeError("native arena search made no progress")
+                return
+            self.calls += 1
+            try:
+                out = _net_call(self.nnet, batch[:k], self.use_gnn)
+            except Exception as ex:  # MCTS.py:195-200 for the leaf (counted), no rows kept
+                nn_fallback.record("ArenaPlayer", ex, 1)
+                eng.feed_spec(k, failed=True)
+                continue
+            eng.feed_spec(k, *out)
 
     def __call__(self, canonical):
         gen = self.mcts.getActionProb_g(canonical, temp=0)

@@ -90,6 +90,15 @@ int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const f
  * collect.  az_mcts_cache_stats: out[0] = rows held, out[1] = leaves expanded from them. */
 int az_mcts_cache_put(az_mcts* m, int count, const int8_t* boards, const float* pi, const float* v,
                       const float* gpi, const float* gv);
+/* One slot's search step with speculation in one call pair (the arena, mcts_native.ArenaPlayer):
+ * collect_spec advances `slot` to its next new leaf and writes it as boards[0], followed by up to
+ * cap - 1 of its non-terminal children that are neither expanded in the tree nor cached; returns
+ * the row count (0 when the slot's searches are done).  feed_spec takes the rows of those boards
+ * in the same order: row 0 expands the leaf (as az_mcts_feed), rows 1.. go to the row cache.
+ * failed != 0 applies the reference's exception path to the leaf and keeps no rows. */
+int az_mcts_collect_spec(az_mcts* m, int slot, int8_t* boards, int cap);
+int az_mcts_feed_spec(az_mcts* m, int count, const float* pi, const float* v, const float* gpi,
+                      const float* gv, int failed);
 int az_mcts_cache_clear(az_mcts* m);
 int az_mcts_cache_stats(const az_mcts* m, int64_t* out);
 
