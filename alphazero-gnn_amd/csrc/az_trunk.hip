@@ -5,9 +5,10 @@
 //   1. boards (int8) -> zero-padded 9x9 fp32 tiles in LDS
 //   2. conv1 (1->32, 9 MACs/output) on the VALU into a zero-padded [NB][32][9][9] LDS image
 //   3. conv2 as an implicit GEMM on MFMA 16x16x4 f32:  rows = (board, position) flattened
-//      (NB*49), cols = 64 output channels, K = 288 ordered (tap, ci) so that every A-fragment
-//      read is ONE ds_read_b32 at lane-base + compile-time offset.  Each wave owns a 16-channel
-//      column tile and keeps its 72 weight fragments in VGPRs for the whole launch.
+//      (NB*49), cols = 64 output channels, K = 288 ordered (tap, ci = 8h + j) so that the 8
+//      A-fragments of a tap are TWO ds_read_b128 per lane (conv1's output is laid out
+//      [board][position][channel]).  Each wave owns a 16-channel column tile and keeps its 72
+//      weight fragments in VGPRs for the whole launch.
 //   4. bias + ReLU epilogue into an LDS copy of the NB NCHW-flattened feature rows, written to
 //      HBM as contiguous float4 rows.
 #include <stdlib.h>
@@ -26,11 +27,20 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int W2S_STRIDE = 290;
 constexpr int W2S_FLOATS = 64 * W2S_STRIDE;
 
+// conv1's output in LDS: [board][padded 9x9 position][channel], rows of C1S floats.  A lane of
+// conv2's MFMA chain (row = position, lane group h = 16-lane quarter) reads the 8 channels
+// 8h .. 8h+7 of one position as two ds_read_b128, which feed 8 MFMA steps (the k order of a tap
+// is ci = 8h + j, j = 0..7).  C1S = 36 (32 channels + 4 pad): 16 consecutive rows of a
+// quarter then start on 16 distinct 4-bank groups.
+constexpr int C1S = 36;
+constexpr int C1_FLOATS_PER_BOARD = 81 * C1S;
+
 // LDS the kernel hands to c4_trunk_tile: conv2's weights while they are read into registers,
-// then (NB <= 4) the NB*3136-float output staging tile
+// then (NB <= 4) the NB*3136-float output staging tile, or (NB = 8, no staging) conv1's output
 template <int NB>
 constexpr int trunk_union_floats() {
-  return W2S_FLOATS > (NB <= 4 ? NB * 3136 : 0) ? W2S_FLOATS : NB * 3136;
+  constexpr int after = NB <= 4 ? NB * 3136 : NB * C1_FLOATS_PER_BOARD;
+  return W2S_FLOATS > after ? W2S_FLOATS : after;
 }
 
 // The trunk of one 512-thread block (boards blockIdx.x*NB ...).  `un` is LDS of
@@ -54,7 +64,10 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   // direct stores scatter 4-byte writes); NB = 8 lacks the LDS for it
   constexpr bool STAGE = NB <= 4;
   __shared__ float bd[NB * PP + 1];
-  __shared__ float c1[NB * CI * PP];
+  // conv1's output: its own LDS when the output is staged (NB <= 4), else in `un` once conv2's
+  // weights have moved to registers
+  __shared__ __attribute__((aligned(16))) float c1s[STAGE ? NB * C1_FLOATS_PER_BOARD : 4];
+  float* const c1 = STAGE ? c1s : un;
   __shared__ float w1s[CI * 9 + CI + 1];   // conv1 weights, bias, pad: one round trip, then LDS
   const int tid = threadIdx.x;
   const int b0 = blockIdx.x * NB;
@@ -95,14 +108,15 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
     bd[min(tid + 512 * j, NB * PP)] = bdin[j] ? (float)bdv[j] : 0.f;   // use sinks the load
   w1s[min(tid, CI * 9 + CI)] = w1v;     // unguarded: lanes past the 320 weights hit the pad
   __syncthreads();
-  float breg[72];
+  float breg[72];   // step s = tap * 8 + j takes channel ci = 8h + j of tap (lane group h)
 #pragma unroll
   for (int s = 0; s < 72; ++s) {
-    const int tap = s >> 3, ci = 4 * (s & 7) + h;
+    const int tap = s >> 3, ci = 8 * h + (s & 7);
     breg[s] = un[co * W2S_STRIDE + ci * 9 + (tap / 3) * 3 + (tap % 3)];
   }
-  for (int i = tid; i < NB * CI * PP; i += 512) {
-    const int b = i / (CI * PP), rem = i % (CI * PP), ci = rem / PP, pp = rem % PP;
+  if constexpr (!STAGE) __syncthreads();   // conv1's output overwrites the weights in `un`
+  for (int i = tid; i < NB * PP * CI; i += 512) {
+    const int b = i / (PP * CI), rem = i % (PP * CI), pp = rem / CI, ci = rem % CI;
     const int px = pp / 9, py = pp % 9;
     float v = 0.f;
     if (px >= 1 && px <= 7 && py >= 1 && py <= 7) {
@@ -115,7 +129,7 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
       s += w1s[CI * 9 + ci];
       v = s > 0.f ? s : 0.f;
     }
-    c1[i] = v;
+    c1[b * C1_FLOATS_PER_BOARD + pp * C1S + ci] = v;
   }
   __syncthreads();
 
@@ -127,9 +141,9 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
     int base = 0;
     if (mt < MT && i < ROWS) {
       const int b = i / P, p = i % P;
-      base = b * CI * PP + h * PP + (p / 7) * 9 + (p % 7);
+      base = b * C1_FLOATS_PER_BOARD + ((p / 7) * 9 + (p % 7)) * C1S;
     }
-    return c1 + base;
+    return c1 + base + 8 * h;
   };
   auto store_tile = [&](int mt, const f32x4v& acc) {
 #pragma unroll
@@ -148,11 +162,19 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
     const float* a1 = a_base(mt + 2);
     f32x4v acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 72; ++s) {
-      const int tap = s >> 3;
-      const int off = 4 * (s & 7) * PP + (tap / 3) * 9 + (tap % 3);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[off], breg[s], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[off], breg[s], acc1, 0, 0, 0);
+    for (int tap = 0; tap < 9; ++tap) {
+      const int off = ((tap / 3) * 9 + (tap % 3)) * C1S;
+      const f32x4v x0 = *reinterpret_cast<const f32x4v*>(a0 + off);
+      const f32x4v y0 = *reinterpret_cast<const f32x4v*>(a0 + off + 4);
+      const f32x4v x1 = *reinterpret_cast<const f32x4v*>(a1 + off);
+      const f32x4v y1 = *reinterpret_cast<const f32x4v*>(a1 + off + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(j < 4 ? x0[j] : y0[j - 4], breg[tap * 8 + j],
+                                                    acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(j < 4 ? x1[j] : y1[j - 4], breg[tap * 8 + j],
+                                                    acc1, 0, 0, 0);
+      }
     }
     store_tile(mt, acc0);
     if (mt + 2 < MT) store_tile(mt + 2, acc1);
@@ -626,7 +648,7 @@ __global__ __launch_bounds__(256) void c4_trunk_split_kernel(
   constexpr int P = 49, PP = 81, CI = 32, MT = 4;
   __shared__ __attribute__((aligned(16))) float w2s[17 * W2S_STRIDE];   // + pad row
   __shared__ float bd[PP + 1];
-  __shared__ float c1[CI * PP];
+  __shared__ __attribute__((aligned(16))) float c1[C1_FLOATS_PER_BOARD];
   __shared__ float w1s[CI * 9 + CI + 1];
   const int tid = threadIdx.x, b = blockIdx.x, q = blockIdx.y;
   const int lane = tid & 63, mt = tid >> 6;            // wave = m-tile (4 x 16 rows >= 49)
@@ -656,14 +678,14 @@ __global__ __launch_bounds__(256) void c4_trunk_split_kernel(
   w1s[tid] = w1a;
   w1s[min(tid + 256, CI * 9 + CI)] = w1b;          // unguarded (pad slot)
   __syncthreads();
-  float breg[72];
+  float breg[72];   // c4_trunk_tile's k order: step tap * 8 + j takes channel 8h + j
 #pragma unroll
   for (int s = 0; s < 72; ++s) {
-    const int tap = s >> 3, ci = 4 * (s & 7) + h;
+    const int tap = s >> 3, ci = 8 * h + (s & 7);
     breg[s] = w2s[c16 * W2S_STRIDE + ci * 9 + (tap / 3) * 3 + (tap % 3)];
   }
   for (int i = tid; i < CI * PP; i += 256) {
-    const int ci = i / PP, pp = i % PP, px = pp / 9, py = pp % 9;
+    const int pp = i / CI, ci = i % CI, px = pp / 9, py = pp % 9;
     float v = 0.f;
     if (px >= 1 && px <= 7 && py >= 1 && py <= 7) {
       float s = 0.f;
@@ -675,17 +697,21 @@ __global__ __launch_bounds__(256) void c4_trunk_split_kernel(
       s += w1s[CI * 9 + ci];
       v = s > 0.f ? s : 0.f;
     }
-    c1[i] = v;
+    c1[pp * C1S + ci] = v;
   }
   __syncthreads();
   const int i = mt * 16 + c16;
-  const float* a0 = c1 + (i < P ? h * PP + (i / 7) * 9 + (i % 7) : 0);
+  const float* a0 = c1 + (i < P ? ((i / 7) * 9 + (i % 7)) * C1S : 0) + 8 * h;
   f32x4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < 72; ++s) {
-    const int tap = s >> 3;
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[4 * (s & 7) * PP + (tap / 3) * 9 + (tap % 3)],
-                                               breg[s], acc, 0, 0, 0);
+  for (int tap = 0; tap < 9; ++tap) {
+    const int off = ((tap / 3) * 9 + (tap % 3)) * C1S;
+    const f32x4v x = *reinterpret_cast<const f32x4v*>(a0 + off);
+    const f32x4v y = *reinterpret_cast<const f32x4v*>(a0 + off + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(j < 4 ? x[j] : y[j - 4], breg[tap * 8 + j], acc,
+                                                 0, 0, 0);
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {

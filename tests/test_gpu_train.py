@@ -1,8 +1,24 @@
 """Backward / training parity on the MI355X.
 
 Gradients of the HIP backward kernels are compared with torch autograd of the restated
-reference forward (oracle/torch_ref.py) in float64; the criterion is "as accurate as torch's
-own fp32 CPU gradient, within 10x" (plus a 1e-7-of-scale floor), measured per tensor.
+reference forward (oracle/torch_ref.py) in float64.  Criterion, per element i of a tensor:
+
+    |ours_i - ref64_i| <= 10 * max|torch32 - ref64|  +  C_ROUND * u32 * S_i
+
+The first term: as accurate as torch's own fp32 CPU gradient of the same restatement, within
+10x.  The second term is the rounding floor of ANY fp32 evaluation of that gradient element:
+S_i is the sum of the absolute values of the terms that make up the element -- for every
+F.linear / F.conv2d y = x W^T + b of the float64 forward, |dy|^T |x| into W and sum_rows |dy|
+into b, dy being the loss gradient at y (abs_contributions below).  An fp32 sum of n terms is
+within a small multiple of u32 sum|t| of exact for the blocked / pairwise orders used here
+((n-1) u32 sum|t| only for one long recursive chain, Higham 4.2), and a different but equally
+valid summation order (the HIP kernels') moves a result by the same amount.  This matters for gradients that are a near-total cancellation -- e.g. the attention
+MLP's final bias on the star, sum over edges of dL/dlogit ~ 1e-8 from terms ~ 1e-4 -- where
+torch32's single sample of the error can be far below what another order gives.  For tensors
+that are not such a cancellation, S_i u32 is far below 10 x torch32's error and the bound
+stays what it was.  C_ROUND = 4; the largest need measured on MI355X is 0.09 (the star's
+attention.2.bias, profiles/r02i_grad_round_margins.json), every other tensor needs 0.
+Tensors with no traced contributions (dx, the mlp2 test) keep the old 1e-7-of-scale floor.
 Full NeuralNet.train() calls are compared with the goldens captured from the reference."""
 import numpy as np
 import pytest
@@ -24,14 +40,74 @@ def cu(a, dtype=None):
     return (t.to(dtype) if dtype is not None else t).cuda()
 
 
-def check_grad(name, got, ref64, ref32):
+U32 = 2.0 ** -24
+C_ROUND = 4
+MARGINS = {}     # name -> the C_ROUND this tensor needed (reported by test_report_margins)
+
+
+def check_grad(name, got, ref64, ref32, S=None):
     got = np.asarray(got, np.float64).reshape(-1)
     r = np.asarray(ref64, np.float64).reshape(-1)
     r32 = np.asarray(ref32, np.float64).reshape(-1)
     scale = max(np.abs(r).max(), 1e-30)
-    e_ours = np.abs(got - r).max()
+    err = np.abs(got - r)
     e_t32 = np.abs(r32 - r).max()
-    assert e_ours <= 10 * e_t32 + 1e-7 * scale, (name, e_ours, e_t32, scale)
+    if S is None:
+        assert err.max() <= 10 * e_t32 + 1e-7 * scale, (name, err.max(), e_t32, scale)
+        return
+    S = np.asarray(S, np.float64).reshape(-1)
+    over = err - 10 * e_t32
+    need = float(np.max(np.where(over > 0, over / np.maximum(U32 * S, 1e-300), 0.0)))
+    MARGINS[name] = need
+    assert need <= C_ROUND, (name, err.max(), e_t32, need)
+
+
+def abs_contributions(run, P):
+    """S per parameter of the float64 restatement: |dy|^T |x| (weights) and sum |dy| (biases)
+    over every F.linear / F.conv2d that uses it, dy = d loss / d (that call's output).  `run`
+    builds the loss from P; the hooks fire during its backward."""
+    import torch.nn.functional as F
+    S = {k: torch.zeros_like(v.detach()) for k, v in P.items()}
+    name = {id(v): k for k, v in P.items()}
+    lin, conv = F.linear, F.conv2d
+
+    def track(y, x, w, b, kind, kw):
+        kw_, kb_ = name.get(id(w)), (name.get(id(b)) if b is not None else None)
+        if not y.requires_grad or (kw_ is None and kb_ is None):
+            return
+        xa = x.detach().abs()
+
+        def hook(dy):
+            d = dy.detach().abs()
+            if kind == "linear":
+                d2, x2 = d.reshape(-1, d.shape[-1]), xa.reshape(-1, xa.shape[-1])
+                if kw_:
+                    S[kw_] += d2.T @ x2
+                if kb_:
+                    S[kb_] += d2.sum(0)
+            else:
+                if kw_:
+                    S[kw_] += torch.nn.grad.conv2d_weight(xa, w.shape, d, **kw)
+                if kb_:
+                    S[kb_] += d.sum((0, 2, 3))
+        y.register_hook(hook)
+
+    def lin_t(x, w, b=None):
+        y = lin(x, w, b)
+        track(y, x, w, b, "linear", {})
+        return y
+
+    def conv_t(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
+        y = conv(x, w, b, stride, padding, dilation, groups)
+        track(y, x, w, b, "conv", dict(stride=stride, padding=padding, dilation=dilation,
+                                       groups=groups))
+        return y
+    F.linear, F.conv2d = lin_t, conv_t
+    try:
+        run(P).backward()
+    finally:
+        F.linear, F.conv2d = lin, conv
+    return {k: v.numpy() for k, v in S.items()}
 
 
 def ref_grads(fn, W, dtype):
@@ -40,6 +116,11 @@ def ref_grads(fn, W, dtype):
     loss = fn(P)
     loss.backward()
     return {k: v.grad.numpy() for k, v in P.items() if v.grad is not None}, loss.item()
+
+
+def ref_contrib(fn, W):
+    from oracle import torch_ref as R
+    return abs_contributions(fn, R.params(W, torch.float64))
 
 
 def make_net(kind, W, G=None, dropout=0.0):
@@ -83,8 +164,9 @@ def test_c4_cnn_grads_with_dropout(lib):
         return R.losses(*R.c4_heads(R.c4_features(boards, P, m, 0.3), P), tpi, tv)
     g64, _ = ref_grads(fn, W, torch.float64)
     g32, _ = ref_grads(fn, W, torch.float32)
+    S = ref_contrib(fn, W)
     for k in g64:
-        check_grad(k, got[k], g64[k], g32[k])
+        check_grad("c4_cnn/" + k, got[k], g64[k], g32[k], S[k])
 
 
 def test_ttt_cnn_grads(lib):
@@ -103,22 +185,27 @@ def test_ttt_cnn_grads(lib):
         return R.losses(*R.ttt_heads(R.ttt_features(boards, P), P), tpi, tv)
     g64, _ = ref_grads(fn, W, torch.float64)
     g32, _ = ref_grads(fn, W, torch.float32)
+    S = ref_contrib(fn, W)
     for k in g64:
-        check_grad(k, got[k], g64[k], g32[k])
+        check_grad("ttt_cnn/" + k, got[k], g64[k], g32[k], S[k])
 
 
-def _gnn_ref(kind, boards, Wn, G, tpi, tv, dtype, drop=None, p=0.0):
+def _gnn_ref(kind, boards, Wn, G, tpi, tv, dtype, drop=None, p=0.0, contrib=False):
     from oracle import torch_ref as R
     Pn = R.params(Wn, dtype, requires_grad=False)
     PG = R.params(G, dtype)
-    if kind == "c4":
-        f = R.c4_features(boards, Pn, drop, p)
-        logp, v = R.c4_heads(R.policy_value_gnn(f, PG), Pn)
-    else:
-        f = R.ttt_features(boards, Pn)
-        logp, v = R.ttt_heads(R.policy_value_gnn(f, PG), Pn)
-    loss = R.losses(logp, v, tpi, tv)
-    loss.backward()
+
+    def run(PG):
+        if kind == "c4":
+            f = R.c4_features(boards, Pn, drop, p)
+            logp, v = R.c4_heads(R.policy_value_gnn(f, PG), Pn)
+        else:
+            f = R.ttt_features(boards, Pn)
+            logp, v = R.ttt_heads(R.policy_value_gnn(f, PG), Pn)
+        return R.losses(logp, v, tpi, tv)
+    if contrib:
+        return abs_contributions(run, PG)
+    run(PG).backward()
     return {k: t.grad.numpy() for k, t in PG.items()}
 
 
@@ -134,8 +221,9 @@ def test_ttt_gnn_grads_star64(lib):
     got = {k: v.cpu().numpy() for k, v in gnn.params.grads.items()}
     g64 = _gnn_ref("ttt", boards, W, G, tpi, tv, torch.float64)
     g32 = _gnn_ref("ttt", boards, W, G, tpi, tv, torch.float32)
+    S = _gnn_ref("ttt", boards, W, G, tpi, tv, torch.float64, contrib=True)
     for k in g64:
-        check_grad(k, got[k], g64[k], g32[k])
+        check_grad("ttt_gnn/" + k, got[k], g64[k], g32[k], S[k])
 
 
 @pytest.mark.slow
@@ -153,8 +241,9 @@ def test_c4_gnn_grads_star(lib, c4_gnn_weights):
     m = mask.cpu().numpy().reshape(B, 3136)
     g64 = _gnn_ref("c4", boards, W, c4_gnn_weights, tpi, tv, torch.float64, m, 0.3)
     g32 = _gnn_ref("c4", boards, W, c4_gnn_weights, tpi, tv, torch.float32, m, 0.3)
+    S = _gnn_ref("c4", boards, W, c4_gnn_weights, tpi, tv, torch.float64, m, 0.3, contrib=True)
     for k in g64:
-        check_grad(k, got[k], g64[k], g32[k])
+        check_grad("c4_gnn/" + k, got[k], g64[k], g32[k], S[k])
 
 
 def test_grid_layer_grads(lib):
@@ -187,10 +276,14 @@ def test_grid_layer_grads(lib):
         return gr, xt.grad.numpy(), out.detach().numpy()
     r64, dx64, y64 = ref(torch.float64)
     r32, dx32, _ = ref(torch.float32)
+    S = abs_contributions(lambda P: (R.gnn_layer_csr(torch.from_numpy(x0).double(), z["rowptr"],
+                                                      z["col"], P, 0) *
+                                     torch.from_numpy(dout).double()).sum(),
+                          R.params(G, torch.float64))
     np.testing.assert_allclose(y.cpu().numpy(), y64, atol=1e-5)
     check_grad("dx", dx.cpu().numpy(), dx64, dx32)
     for k in r64:
-        check_grad(k, Gl[k].cpu().numpy(), r64[k], r32[k])
+        check_grad("grid/" + k, Gl[k].cpu().numpy(), r64[k], r32[k], S["layers.0." + k])
 
 
 def test_mlp2_bwd(lib):
@@ -272,3 +365,14 @@ def test_c4_train_matches_reference_golden(lib, c4_gnn_weights):
         np.testing.assert_allclose(a[zz["gidx/" + k]], zz["gval/" + k], atol=2e-5, err_msg=k)
         assert abs(a.astype(np.float64).sum() - zz["gsum/" + k]) <= 1e-4 * max(
             1.0, zz["gabs/" + k]), k
+
+
+def test_report_margins():
+    """Writes the C_ROUND each tensor needed (AZ_REPORT_DIR): runs after the gradient tests."""
+    import json
+    import os
+    d = os.environ.get("AZ_REPORT_DIR")
+    if d and MARGINS:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "grad_round_margins.json"), "w") as f:
+            json.dump(dict(sorted(MARGINS.items(), key=lambda kv: -kv[1])), f, indent=1)
