@@ -1247,6 +1247,148 @@ __global__ __launch_bounds__(256) void gemv_side_heads(GemmArgs p, SideHeads h, 
   }
 }
 
+// --------------------------------------------------------------------- K-sliced row panels
+// C = epi(A . W^T) for mid-size M (the B = 512 output_transform: 512 x 3136 x 3136).  A tile
+// grid cannot fill 256 CUs there without split-K, whose slabs cost a 32 MB write + re-read and
+// a reduce launch per call.  Here block (mb, nb) owns 32 rows x one column panel over the WHOLE
+// K (16 x 16 blocks for that shape: one per CU, no slabs):
+//   - column panels are 16*CT wide except the first n_narrow, which are 16 narrower (3136 =
+//     12 x 192 + 4 x 208); every block computes CT sub-tiles, so a narrow panel's last one
+//     overlaps its neighbour (computed, not stored) and no row of W is ever out of range -- the
+//     lanes need no clamps, hence one base pointer each instead of 15;
+//   - its KW waves split K into KW contiguous slices; each wave streams its A and W fragments
+//     straight from L2 into registers (double-buffered: the next step's loads fly under this
+//     step's MFMAs), so the loop has no LDS traffic and no barriers;
+//   - MFMA (h, t) of a step takes k = 16h + 4g + t in lane group g for both operands (a
+//     bijection of the step's k values);
+//   - the partial tiles meet in LDS and are summed in wave order (deterministic), then bias /
+//     activation and float4 stores.
+// One wave's share of a gemm_kslice block: NC column sub-tiles starting at sub-tile cs0, the
+// 32 rows, k steps [it0, it1) of 32; the partial tile goes to LDS slot `slot` (row stride SP).
+template <int NC, int SP>
+__device__ __forceinline__ void kslice_wave(const GemmArgs& p, int m0, int n0, int cs0, int it0,
+                                            int it1, float* slot) {
+  constexpr int RT = 2;
+  const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  // buffer loads: one 32-bit per-lane byte offset per operand plus a wave-uniform SGPR offset
+  // per 16-row sub-tile (no hoisted 64-bit addresses)
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.A), 0, p.M * p.lda * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.B), 0, p.N * p.ldb * 4, 0x00020000);
+  const int va = ((m0 + c16) * p.lda + 4 * g) * 4;               // host: M % 32 == 0
+  const int vb = ((n0 + cs0 * 16 + c16) * p.ldb + 4 * g) * 4;    // rows < N by the panel layout
+  const int sa = 16 * p.lda * 4, sb = 16 * p.ldb * 4;
+  f32x4 acc[RT][NC];
+#pragma unroll
+  for (int rs = 0; rs < RT; ++rs)
+#pragma unroll
+    for (int cs = 0; cs < NC; ++cs) acc[rs][cs] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // step `it` covers k in [32 it, 32 it + 32); lane group g holds k = 16h + 4g .. +3 of half h
+  auto load = [&](f32x4 (&a)[RT][2], f32x4 (&b)[NC][2], int it) {
+    const int k = it * 32;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int rs = 0; rs < RT; ++rs)
+        a[rs][h] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, va + (k + 16 * h) * 4, rs * sa, 0));
+#pragma unroll
+      for (int cs = 0; cs < NC; ++cs)
+        b[cs][h] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vb + (k + 16 * h) * 4, cs * sb, 0));
+    }
+  };
+  // MFMA (h, t) of a step takes k = 16h + 4g + t in lane group g for both operands
+  auto mma = [&](const f32x4 (&a)[RT][2], const f32x4 (&b)[NC][2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int rs = 0; rs < RT; ++rs)
+#pragma unroll
+          for (int cs = 0; cs < NC; ++cs)
+            acc[rs][cs] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rs][h][t], b[cs][h][t],
+                                                               acc[rs][cs], 0, 0, 0);
+  };
+  f32x4 a0[RT][2], b0[NC][2], a1[RT][2], b1[NC][2];
+  int it = it0;
+  if (it < it1) load(a0, b0, it);
+  // sched_barrier: the next step's loads stay issued BEFORE this step's MFMAs (left alone, the
+  // scheduler sinks them behind the MFMAs and the prefetch distance collapses)
+  for (; it + 1 < it1; it += 2) {
+    load(a1, b1, it + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (it + 2 < it1) load(a0, b0, it + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (it < it1) mma(a0, b0);
+#pragma unroll
+  for (int rs = 0; rs < RT; ++rs)
+#pragma unroll
+    for (int cs = 0; cs < NC; ++cs)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        slot[(rs * 16 + 4 * g + r) * SP + (cs0 + cs) * 16 + c16] = acc[rs][cs][r];
+}
+
+// 512 threads: wave w takes K slice w & 3 (of 4) and column half w >> 2 (sub-tiles 0..CT0-1 or
+// CT0..CT0+CT1-1); the two waves of a SIMD (w, w + 4) hold CT0 + CT1 sub-tiles between them, so
+// every SIMD does the same MFMA work and has two waves to issue it.
+template <int CT0, int CT1>
+__global__ __launch_bounds__(512) void gemm_kslice(GemmArgs p, int n_narrow) {
+  constexpr int CT = CT0 + CT1;
+  constexpr int SP = 16 * CT + 4;           // partial-tile row stride: conflict-free writes
+  __shared__ __attribute__((aligned(16))) float part[4 * 32 * SP];
+  const int wave = threadIdx.x >> 6;
+  // XCD-aware placement (1-D grid, block id b runs on XCD b % 8): each XCD owns nb / 8 whole
+  // column panels and all row blocks of them, so a W panel is fetched into ONE L2 and shared by
+  // the row blocks there (host: nb % 8 == 0)
+  const int mb = p.M / 32, nb = gridDim.x / mb;
+  const int per = nb / 8, j = blockIdx.x >> 3;
+  const int by = (blockIdx.x & 7) * per + j % per, bx = j / per;
+  const int m0 = bx * 32;
+  const int n0 = by < n_narrow ? by * (16 * CT - 16)
+                               : n_narrow * (16 * CT - 16) + (by - n_narrow) * 16 * CT;
+  const int cw = by < n_narrow ? 16 * CT - 16 : 16 * CT;      // columns this block stores
+  const int nit = p.K / 32;                 // host: K % 32 == 0
+  const int ks = wave & 3;
+  const int it0 = nit * ks / 4, it1 = nit * (ks + 1) / 4;
+  float* slot = part + ks * 32 * SP;
+  if (wave < 4) kslice_wave<CT0, SP>(p, m0, n0, 0, it0, it1, slot);
+  else kslice_wave<CT1, SP>(p, m0, n0, CT0, it0, it1, slot);
+  __syncthreads();
+  const int c4n = cw / 4;
+  for (int i = threadIdx.x; i < 32 * c4n; i += 512) {
+    const int row = i / c4n, c4 = (i % c4n) * 4;
+    const float* q = part + row * SP + c4;
+    f32x4 v = *reinterpret_cast<const f32x4*>(q);
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const f32x4 u = *reinterpret_cast<const f32x4*>(q + w * 32 * SP);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] += u[c];
+    }
+    epilogue_store4(p, m0 + row, n0 + c4, v);
+  }
+}
+
+// gemm_kslice<7, 6> covers the shape when 16 column panels of 192 / 208 columns tile N exactly
+// and 32-row blocks x 16 panels make one round of 256 blocks (M = 512, N = 3072 .. 3328: the
+// B = 512 output_transform).  Returns the number of narrow (192) panels, or -1.
+static int kslice_narrow(const GemmArgs& a) {
+  if (a.M != 512 || a.K % 32 != 0 || a.K < 1024 || a.lda % 4 != 0 || a.ldb % 4 != 0 || !a.vec_epi)
+    return -1;
+  const int nb = 16;
+  if (a.N % 16 != 0 || a.N < 192 * nb || a.N > 208 * nb) return -1;
+  return nb - (a.N - 192 * nb) / 16;        // 208 x (nb - n) + 192 x n = N
+}
+
 // ------------------------------------------------------------------------ tall-skinny GEMM
 // C[M][N] = epi(A[M][K] . W[N][K]^T) for the grid-graph layers: M ~ 10^5..10^6 rows, K in
 // {64, 128}, N in {64, 128, 256}.  A tile kernel with K <= 128 spends most of each block on its
@@ -1664,6 +1806,18 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
     return check_launch("gemv_f32");
   }
   if (akm && bkm && launch_tall(a, s)) return check_launch("gemm_tall");
+  // gemm_kslice: measured slower than the split-K tile so far (111 vs 103 us at M = 512), so
+  // only the tuning build runs it, on request (AZ_GEMM_KSLICE=1, tools/gemm_sweep.py kslice)
+  static const bool use_kslice = tuning_env("AZ_GEMM_KSLICE") != nullptr;
+  if (akm && bkm && use_kslice && !d->A2 && !d->a_rows && !d->b_rows && !d->C2 && !d->R &&
+      !d->G && d->beta == 0.f && d->act != AZ_ACT_DRELU && aligned16(d->A) && aligned16(d->B)) {
+    const int nn = kslice_narrow(a);
+    if (nn >= 0) {
+      const dim3 grid(a.M / 32 * 16);
+      hipLaunchKernelGGL((gemm_kslice<7, 6>), grid, dim3(512), 0, s, a, nn);
+      return check_launch("gemm_kslice");
+    }
+  }
   // tile choice (tuning override for experiments: AZ_GEMM_CFG=<index into kCfgs>)
   static const char* env_cfg = tuning_env("AZ_GEMM_CFG");
   const bool glds_ok = akm && bkm && !d->A2 && !d->a_rows;

@@ -108,6 +108,10 @@ if __name__ == "__main__":
                 res = run(env, M, N, K)
                 print(json.dumps({"M": M, "N": N, "K": K, "env": env, **res}), flush=True)
         sys.exit(0)
+    if mode == "kslice":       # gemm_kslice (M = 512) vs the split-K tile (default dispatch)
+        for env in ({"AZ_GEMM_KSLICE": "1"}, {}):
+            print(json.dumps({"env": env, **run(env)}), flush=True)
+        sys.exit(0)
     if mode == "mgrid":        # default dispatch vs cfg x split at given M (self-play batch sizes)
         Ms = [int(x) for x in sys.argv[2].split(",")]
         cfgs = sys.argv[3].split(",")
