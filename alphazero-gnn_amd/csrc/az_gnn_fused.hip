@@ -17,6 +17,8 @@
 //
 // Block: 256 threads = 4 waves, two blocks per CU (72 KB LDS each), persistent over a
 // contiguous run of tiles so consecutive tiles' neighbour rows are warm in the XCD's L2.
+#include <stdlib.h>
+
 #include "az_common.h"
 
 namespace az {
@@ -150,7 +152,7 @@ __device__ __forceinline__ f32x4 edge_pass(const Gather& g, int deg, const float
 __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
     int D, int identity, const int* __restrict__ dst_rows, const int* __restrict__ rowptr,
     const int* __restrict__ col, const float* __restrict__ x, const float* __restrict__ Ps,
-    FusedW W, float* __restrict__ x_out, int ntiles, int tiles_per_block) {
+    FusedW W, float* __restrict__ x_out, int ntiles, int tiles_per_block, int stagger) {
   __shared__ float C[LDS_C];
   __shared__ float R[LDS_R];
   __shared__ int IDX[2][TT][8];           // per destination: node, in-degree (-1: none), sources
@@ -180,6 +182,11 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
   const int t0 = blockIdx.x * tiles_per_block;
   const int t1 = min(ntiles, t0 + tiles_per_block);
   if (t0 >= t1) return;                   // uniform per block
+#ifdef AZ_TUNING   // experiment: the second half of the grid (the CUs' second block) starts
+                   // `stagger` x 8128 cycles late, so the two blocks of a CU run opposite phases
+  for (int i = 0; i < stagger && (int)blockIdx.x >= (int)gridDim.x / 2; ++i)
+    __builtin_amdgcn_s_sleep(127);
+#endif
 
   // prologue: the first tile's indices and x rows
   {
@@ -355,9 +362,14 @@ int gnn_layer_fused_kernel_launch(const az_graph* g, const float* x, const float
   const int blocks = (ntiles + per - 1) / per;
   const FusedW fw = {w->att_w1, w->att_b1, w->att_w2, w->att_b2, w->gate_w, w->gate_b,
                      w->upd_w1, w->upd_b1, w->upd_w2, w->upd_b2};
+  int stagger = 0;
+#ifdef AZ_TUNING
+  static const char* env_st = tuning_env("AZ_FUSED_STAGGER");
+  stagger = env_st ? atoi(env_st) : 0;
+#endif
   hipLaunchKernelGGL(gnn_layer_fused_kernel, dim3(blocks), dim3(NT), 0, s, g->D,
                      g->D == g->V ? 1 : 0, g->dst_rows, g->rowptr, g->col, x, Ps, fw, x_out,
-                     ntiles, per);
+                     ntiles, per, stagger);
   return check_launch("gnn_layer_fused_kernel");
 }
 

@@ -1,5 +1,6 @@
 """Time gnn_layer_fused_kernel alone on the config-5 shard (512 grids; GRIDS=n), 20 warm
-back-to-back launches:  python tools/fused_probe.py one"""
+back-to-back launches:  python tools/fused_probe.py one
+    python tools/fused_probe.py sweep 0 1 2 4   # AZ_FUSED_STAGGER values, tuning build"""
 import os
 import sys
 import subprocess
@@ -32,7 +33,7 @@ def one():
     ev[1].record()
     torch.cuda.synchronize()
     us = ev[0].elapsed_time(ev[1]) / 20 * 1e3
-    print(f"var={os.environ.get('AZ_FUSED_VAR', '0')} grids={os.environ.get('GRIDS', '512')} "
+    print(f"stagger={os.environ.get('AZ_FUSED_STAGGER', '0')} grids={os.environ.get('GRIDS', '512')} "
           f"fused_us={us:.1f}", flush=True)
 
 
@@ -40,6 +41,6 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "one":
         one()
     else:
-        for m in sys.argv[2:] or ["0", "1"]:
-            env = dict(os.environ, AZ_FUSED_VAR=m)
+        for m in sys.argv[2:] or ["0", "1"]:     # AZ_FUSED_STAGGER values (tuning build)
+            env = dict(os.environ, AZ_FUSED_STAGGER=m, AZ_TUNING_LIB="1")
             subprocess.run([sys.executable, __file__, "one"], env=env, check=True, timeout=120)

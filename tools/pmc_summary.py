@@ -88,6 +88,28 @@ def main(d, tag):
                             "hbm_bytes_per_launch": int((2 * sum(agg) / len(agg)
                                                          + sum(aggw) / len(aggw)) * 1024),
                             "algorithmic_bytes": V * 64 * 4 * 2 + E * 8 + (V + 1) * 4}
+    # round 2: the fused eval-mode GNN layer and its source projection (tools/fused_probe.py one:
+    # 512 grids, x warm from the previous launch as in the bench's "warm" figure)
+    ff, fw = (os.path.join(d, "ffetch", "run_counter_collection.csv"),
+              os.path.join(d, "fwrite", "run_counter_collection.csv"))
+    if os.path.exists(ff) and os.path.exists(fw):
+        fe2, wr2 = load(ff, "FETCH_SIZE"), load(fw, "WRITE_SIZE")
+        V, E = 512 * 1024, 512 * 3968
+        for key, pred, alg in (
+                ("gnn_layer_fused", lambda n: "gnn_layer_fused_kernel" in n,
+                 V * 1024 + 4 * E + 4 * (V + 1)),
+                ("gnn_source_proj", lambda n: "gemm_tall" in n or "gemm_f32" in n,
+                 V * 64 * 4 + 128 * 64 * 4 + V * 128 * 4)):
+            a = [kb for _, n, kb, _ in fe2 if pred(n)]
+            b = [kb for _, n, kb, _ in wr2 if pred(n)]
+            if a and b:
+                res[key] = {"kernel": key, "dispatches": len(a),
+                            "hbm_bytes_per_launch": int((2 * sum(a) / len(a) + sum(b) / len(b))
+                                                        * 1024),
+                            "algorithmic_bytes": alg,
+                            "note": "512 32x32 grids, back-to-back launches (x and Ps partly "
+                                    "Infinity-Cache resident between them)"}
+    res["round"] = 2 if tag.startswith("r02") else res["round"]
     json.dump(res, open(os.path.join(ROOT, "profiles", "pmc.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
