@@ -15,6 +15,7 @@
 //   P    =  float32 pi * int64 valids -> float64, divided by np.sum (pairwise summation).
 #include "../../include/az_mcts.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -343,6 +344,7 @@ struct Tree {
   int32_t epoch = 1;
   // search state
   Key root{0, 0};
+  int32_t root_id = -1;         // node of `root` once looked up (set_root invalidates it)
   int remaining = 0;
   int pending_leaf = -1;                      // node waiting for the network
   std::vector<std::pair<int32_t, int32_t>> path;
@@ -361,8 +363,14 @@ struct Tree {
     remaining = 0;
     pending_leaf = -1;
     pending_std = false;
+    root_id = -1;
     path.clear();
     nsa_total = ps_count = 0;
+  }
+
+  void set_root(const Key& k) {
+    root = k;
+    root_id = -1;
   }
 
   int32_t find(const Key& k) const {
@@ -539,52 +547,114 @@ void backup(az_mcts* m, Tree& t, Val v) {
 void expand(az_mcts* m, Tree& t, const float* pi, float v_std, const float* gpi, float gv,
             bool failed);
 
-// Run searches of one slot until it waits on a leaf (returns 1) or has none left (0).  A new
-// leaf whose board has a cached row (az_mcts_cache_put) is expanded on the spot.
-int advance(az_mcts* m, Tree& t) {
-  while (t.remaining > 0 && t.pending_leaf < 0) {
-    t.path.clear();
-    int32_t id = t.find_or_add(t.root, m->R);
-    Val v;
-    for (;;) {
-      Node& nd = t.nodes[id];
-      if (nd.es.x != 0.0) {                      // terminal (MCTS.py:152-157)
-        v = nd.es;
-        break;
-      }
-      if (!nd.expanded) {                        // new leaf: Vs, then the network
-        t.alloc_edges(id, m->R);
-        t.pending_leaf = id;
-        const float* row = m->cache.find(t.nodes[id].key);
-        if (!row) return 1;
-        // a row computed ahead (bit-identical to this leaf's own evaluation): expand now
-        const int A = m->R.A;
-        expand(m, t, row, row[A], m->use_gnn ? row + A + 1 : nullptr,
-               m->use_gnn ? row[2 * A + 1] : 0.f, false);
-        t.cache_hits += 1;
-        goto next_search;
-      }
-      int a = select_action(m, t, nd);
-      if (a < 0) {                               // MCTS.py:220-221
-        v = vint(0);
-        break;
-      }
-      t.path.emplace_back(id, a);
-      const size_t e = (size_t)nd.edge * m->R.A + a;
-      int32_t child = t.EP[e].C;
-      if (child < 0) {
-        Key nk;
-        m->R.next(nd.key, a, &nk);
-        child = t.find_or_add(nk, m->R);       // may grow t.nodes: nd is not used after this
-        t.EP[e].C = child;
-      }
-      id = child;
-    }
+// Searches of several slots, interleaved one tree level at a time (the slots' trees are
+// independent, so each tree sees exactly the sequence of searches advance() would run).  A
+// descent is a chain of dependent cache misses -- a node, then its edge block, then the child --
+// so one slot at a time leaves the core waiting on DRAM; here the node and edge lines of every
+// slot's next step are prefetched and the other slots' steps run while they arrive.  Each slot
+// runs until it waits on a new leaf or has no searches left; a new leaf with a cached row
+// (az_mcts_cache_put / az_mcts_feed_spec) is expanded on the spot.
+constexpr int kGroup = 8;
+
+inline bool searching(const Tree& t) { return t.remaining > 0 && t.pending_leaf < 0; }
+
+inline void prefetch_node(const Tree& t, int32_t id) { __builtin_prefetch(&t.nodes[id]); }
+
+inline void prefetch_edges(const Tree& t, int32_t edge, int A) {
+  const char* p = reinterpret_cast<const char*>(&t.EP[(size_t)edge * A]);
+  const size_t bytes = sizeof(Edge) * (size_t)A;
+  for (size_t o = 0; o < bytes; o += 64) __builtin_prefetch(p + o);
+}
+
+void advance_group(az_mcts* m, Tree* const* ts, int n) {
+  enum : uint8_t { START, NODE, SELECT, DONE };
+  const int A = m->R.A;
+  int32_t id[kGroup];
+  uint8_t ph[kGroup];
+  int live = 0;
+  for (int i = 0; i < n; ++i) {
+    ph[i] = searching(*ts[i]) ? START : DONE;
+    live += ph[i] != DONE;
+  }
+  auto finish = [&](int i, Tree& t, Val v) {   // a search ended at a terminal / stuck node
     backup(m, t, v);
     t.remaining -= 1;
-  next_search:;
+    ph[i] = searching(t) ? START : DONE;
+  };
+  while (live > 0) {
+    for (int i = 0; i < n; ++i) {
+      if (ph[i] == DONE) continue;
+      Tree& t = *ts[i];
+      switch (ph[i]) {
+        case START:
+          t.path.clear();
+          if (t.root_id < 0) t.root_id = t.find_or_add(t.root, m->R);
+          id[i] = t.root_id;
+          prefetch_node(t, id[i]);
+          ph[i] = NODE;
+          break;
+        case NODE: {
+          const Node& nd = t.nodes[id[i]];
+          if (nd.es.x != 0.0) {                  // terminal (MCTS.py:152-157)
+            finish(i, t, nd.es);
+          } else if (!nd.expanded) {             // new leaf: Vs, then the network
+            t.alloc_edges(id[i], m->R);
+            t.pending_leaf = id[i];
+            const float* row = m->cache.find(t.nodes[id[i]].key);
+            if (row) {
+              // a row computed ahead (bit-identical to this leaf's own evaluation): expand now
+              expand(m, t, row, row[A], m->use_gnn ? row + A + 1 : nullptr,
+                     m->use_gnn ? row[2 * A + 1] : 0.f, false);
+              t.cache_hits += 1;
+              ph[i] = searching(t) ? START : DONE;
+            } else {
+              ph[i] = DONE;
+            }
+          } else {
+            prefetch_edges(t, nd.edge, A);
+            ph[i] = SELECT;
+          }
+          break;
+        }
+        default: {                               // SELECT
+          const Node& nd = t.nodes[id[i]];
+          const int a = select_action(m, t, nd);
+          if (a < 0) {                           // MCTS.py:220-221
+            finish(i, t, vint(0));
+            break;
+          }
+          t.path.emplace_back(id[i], a);
+          const size_t e = (size_t)nd.edge * A + a;
+          int32_t child = t.EP[e].C;
+          if (child < 0) {
+            Key nk;
+            m->R.next(nd.key, a, &nk);
+            child = t.find_or_add(nk, m->R);     // may grow t.nodes: nd is not used after this
+            t.EP[e].C = child;
+          }
+          id[i] = child;
+          prefetch_node(t, child);
+          ph[i] = NODE;
+          break;
+        }
+      }
+      live -= ph[i] == DONE;
+    }
   }
-  return 0;
+}
+
+// Run searches of one slot until it waits on a leaf (returns 1) or has none left (0).
+int advance(az_mcts* m, Tree& t) {
+  Tree* one = &t;
+  advance_group(m, &one, 1);
+  return t.pending_leaf >= 0 ? 1 : 0;
+}
+
+// drive_episode's view of a slot's queued searches: 1 = waiting on a leaf, 2 = descents to run
+// (advance_group), 0 = none left
+inline int search_state(const Tree& t) {
+  if (t.pending_leaf >= 0) return 1;
+  return t.remaining > 0 ? 2 : 0;
 }
 
 // Expand the pending leaf with one network row and back its value up (MCTS.py:162-200).
@@ -695,13 +765,13 @@ int drive_episode(az_mcts* m, Tree& t) {
         E.exp_q.resize(E.exp_q.size() + A, 0.0);
         E.exp_tag.resize(E.exp_tag.size() + A, (int8_t)AZM_TAG_NONE);
         E.std_v.push_back(0.f);
-        t.root = E.board;
+        t.set_root(E.board);
         t.remaining = E.sims;
         E.phase = E_AP;
         break;
       }
       case E_AP:
-        if (advance(m, t)) return 1;
+        if (const int r = search_state(t)) return r;
         finish_action_prob(m, t);
         E.phase = m->use_gnn ? E_EXP_CHECK : E_MOVE;
         break;
@@ -713,14 +783,14 @@ int drive_episode(az_mcts* m, Tree& t) {
         if (any) {
           E.phase = E_EXP_STD;
         } else {
-          t.root = E.board;
+          t.set_root(E.board);
           t.remaining = E.sims;
           E.phase = E_EXP_PRE;
         }
         break;
       }
       case E_EXP_PRE: {
-        if (advance(m, t)) return 1;
+        if (const int r = search_state(t)) return r;
         const size_t mv = E.curs.size() - 1;
         root_snapshot(m, t, E.board, &E.init_nsa[mv * A], nullptr, &E.init_has[mv * A]);
         E.phase = E_EXP_STD;
@@ -730,7 +800,7 @@ int drive_episode(az_mcts* m, Tree& t) {
         const int32_t id = t.find(E.board);
         if (id >= 0 && t.nodes[id].std_epoch == t.epoch) {
           E.std_v.back() = t.nodes[id].std_v;
-          t.root = E.board;
+          t.set_root(E.board);
           t.remaining = E.expand_by;
           E.phase = E_EXP;
         } else {
@@ -740,7 +810,7 @@ int drive_episode(az_mcts* m, Tree& t) {
         break;
       }
       case E_EXP: {
-        if (advance(m, t)) return 1;
+        if (const int r = search_state(t)) return r;
         const size_t mv = E.curs.size() - 1;
         root_snapshot(m, t, E.board, &E.exp_nsa[mv * A], &E.exp_q[mv * A], &E.exp_tag[mv * A]);
         E.phase = E_MOVE;
@@ -957,7 +1027,7 @@ int az_mcts_begin(az_mcts* m, int slot, const int8_t* board, int sims) {
     return fail(AZM_ESTATE, "az_mcts_begin: slot still has searches queued");
   Key k;
   if (!m->R.from_board(board, &k)) return fail(AZM_EINVAL, "az_mcts_begin: cells must be -1/0/1");
-  t.root = k;
+  t.set_root(k);
   t.remaining = sims;
   return AZM_OK;
 }
@@ -984,19 +1054,33 @@ int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int thr
   std::vector<uint8_t> has(S, 0);
   if (threads < 1) threads = 1;
   m->threads = threads;
-#pragma omp parallel for schedule(dynamic, 8) num_threads(threads)
-  for (int s = 0; s < S; ++s) {
-    Tree& t = m->trees[s];
-    if (t.pending_leaf < 0 && !t.pending_std) {
-      if (t.ep.phase != E_IDLE) drive_episode(m, t);
-      else advance(m, t);
+  // groups of kGroup consecutive slots: the episode state machines of a group run until every
+  // slot waits on the network or is idle, their descents interleaved by advance_group
+  const int ngroups = (S + kGroup - 1) / kGroup;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+  for (int gi = 0; gi < ngroups; ++gi) {
+    const int s0 = gi * kGroup, s1 = std::min(S, s0 + kGroup);
+    for (;;) {
+      Tree* need[kGroup];
+      int nn = 0;
+      for (int s = s0; s < s1; ++s) {
+        Tree& t = m->trees[s];
+        if (t.pending_leaf >= 0 || t.pending_std) continue;
+        const int r = t.ep.phase != E_IDLE ? drive_episode(m, t) : (searching(t) ? 2 : 0);
+        if (r == 2) need[nn++] = &t;
+      }
+      if (nn == 0) break;
+      advance_group(m, need, nn);
     }
-    if (t.pending_leaf >= 0) {
-      has[s] = 1;
-      m->R.to_board(t.nodes[t.pending_leaf].key, &m->leafbuf[(size_t)s * m->R.cells]);
-    } else if (t.pending_std) {
-      has[s] = 1;
-      m->R.to_board(t.ep.board, &m->leafbuf[(size_t)s * m->R.cells]);
+    for (int s = s0; s < s1; ++s) {
+      const Tree& t = m->trees[s];
+      if (t.pending_leaf >= 0) {
+        has[s] = 1;
+        m->R.to_board(t.nodes[t.pending_leaf].key, &m->leafbuf[(size_t)s * m->R.cells]);
+      } else if (t.pending_std) {
+        has[s] = 1;
+        m->R.to_board(t.ep.board, &m->leafbuf[(size_t)s * m->R.cells]);
+      }
     }
   }
   m->last_order.clear();
