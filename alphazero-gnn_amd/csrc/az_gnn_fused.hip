@@ -184,7 +184,7 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
   if (t0 >= t1) return;                   // uniform per block
 #ifdef AZ_TUNING   // experiment: the second half of the grid (the CUs' second block) starts
                    // `stagger` x 8128 cycles late, so the two blocks of a CU run opposite phases
-  for (int i = 0; i < stagger && (int)blockIdx.x >= (int)gridDim.x / 2; ++i)
+  for (int i = 0; i < stagger && (int)blockIdx.x >= (int)gridDim.x / 2; ++i)   // (< 0: none)
     __builtin_amdgcn_s_sleep(127);
 #endif
 
@@ -326,9 +326,16 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = 16 * mt + 4 * lg + r;
-          if (IDX[cur][row][1] >= 0)
-            x_out[(size_t)IDX[cur][row][0] * FF + f] =
-                C[row * CS + f] + G[row * GS + f] * (acc[mt][0][r] + ubias);
+          if (IDX[cur][row][1] >= 0) {
+            const float o = C[row * CS + f] + G[row * GS + f] * (acc[mt][0][r] + ubias);
+            float* dst = x_out + (size_t)IDX[cur][row][0] * FF + f;
+#ifdef AZ_TUNING   // experiment (AZ_FUSED_NT=1): non-temporal x_out stores, so the output
+                   // stream does not evict the gathered x / Ps rows from L2
+            if (stagger < 0) __builtin_nontemporal_store(o, dst);
+            else
+#endif
+              *dst = o;
+          }
         }
     }
     __syncthreads();                      // C / R / IDX[cur] are rewritten by the next tile
@@ -365,7 +372,8 @@ int gnn_layer_fused_kernel_launch(const az_graph* g, const float* x, const float
   int stagger = 0;
 #ifdef AZ_TUNING
   static const char* env_st = tuning_env("AZ_FUSED_STAGGER");
-  stagger = env_st ? atoi(env_st) : 0;
+  static const char* env_nt = tuning_env("AZ_FUSED_NT");
+  stagger = env_nt ? -1 : (env_st ? atoi(env_st) : 0);   // -1: non-temporal output stores
 #endif
   hipLaunchKernelGGL(gnn_layer_fused_kernel, dim3(blocks), dim3(NT), 0, s, g->D,
                      g->D == g->V ? 1 : 0, g->dst_rows, g->rowptr, g->col, x, Ps, fw, x_out,

@@ -33,7 +33,8 @@ def one():
     ev[1].record()
     torch.cuda.synchronize()
     us = ev[0].elapsed_time(ev[1]) / 20 * 1e3
-    print(f"stagger={os.environ.get('AZ_FUSED_STAGGER', '0')} grids={os.environ.get('GRIDS', '512')} "
+    print(f"stagger={os.environ.get('AZ_FUSED_STAGGER', '0')} nt={os.environ.get('AZ_FUSED_NT', '0')} "
+          f"grids={os.environ.get('GRIDS', '512')} "
           f"fused_us={us:.1f}", flush=True)
 
 
