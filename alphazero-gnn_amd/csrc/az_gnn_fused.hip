@@ -28,14 +28,16 @@ namespace {
 
 constexpr int FF = 64;        // node features
 constexpr int HH = 128;       // attention hidden units
-constexpr int TT = 64;        // destinations per tile
+constexpr int TT = 64;        // destinations per tile (gnn_layer_fused_kernel<TT>; 32 = tuning)
 constexpr int NT = 256;       // threads per block (4 waves); two blocks per CU
 constexpr int CS = 132;       // LDS row stride of [x_d | agg] and Pt: = 4 (mod 64), so a wave's
                               // ds_read_b128 of 16 rows x 16 B is bank-conflict free
 constexpr int GS = 68;        // LDS row stride of the gate / u1 images (= 4 mod 64 as well)
 constexpr int MAXD = 4;       // in-degree bound of the fused path
-constexpr int LDS_C = TT * CS;                       // [x_d | agg]
-constexpr int LDS_R = (TT * CS > 2 * TT * GS) ? TT * CS : 2 * TT * GS;   // Pt, then gate + u1
+template <int T_>
+constexpr int lds_c() { return T_ * CS; }                                   // [x_d | agg]
+template <int T_>
+constexpr int lds_r() { return (T_ * CS > 2 * T_ * GS) ? T_ * CS : 2 * T_ * GS; }   // Pt, gate+u1
 
 struct FusedW {
   const float *w1, *b1, *w2, *b2, *gw, *gb, *uw1, *ub1, *uw2, *ub2;
@@ -149,12 +151,14 @@ __device__ __forceinline__ f32x4 edge_pass(const Gather& g, int deg, const float
 // group ahead of the MFMAs; the next tile's CSR indices are fetched one tile ahead into LDS and
 // its x rows into registers; half of a tile's neighbour gathers are in flight during step 1's
 // MFMAs, the other half during the first half's edge arithmetic.
-__global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
+template <int TT>
+__global__ __launch_bounds__(NT, TT == 64 ? 2 : 3) void gnn_layer_fused_kernel(
     int D, int identity, const int* __restrict__ dst_rows, const int* __restrict__ rowptr,
     const int* __restrict__ col, const float* __restrict__ x, const float* __restrict__ Ps,
     FusedW W, float* __restrict__ x_out, int ntiles, int tiles_per_block, int stagger) {
-  __shared__ float C[LDS_C];
-  __shared__ float R[LDS_R];
+  constexpr int MT = TT / 16;             // 16-row MFMA tiles of a tile
+  __shared__ float C[lds_c<TT>()];
+  __shared__ float R[lds_r<TT>()];
   __shared__ int IDX[2][TT][8];           // per destination: node, in-degree (-1: none), sources
   __shared__ float AB[2 * HH];            // attention.0 bias, attention.2 weight
   const int tid = threadIdx.x;
@@ -189,7 +193,7 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
 #endif
 
   // prologue: the first tile's indices and x rows
-  {
+  if (im < TT) {
     const int i = t0 * TT + im;
     int d = 0, e0 = 0, deg = -1;
     if (i < D) {
@@ -203,9 +207,9 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
       IDX[0][im][1] = deg;
     }
   }
-  f32x4 xnext[4];
+  f32x4 xnext[MT];
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
+  for (int p = 0; p < MT; ++p) {
     const int i = t0 * TT + p * 16 + (tid >> 4);
     xnext[p] = i < D ? *reinterpret_cast<const f32x4*>(
                            x + (size_t)(identity ? i : dst_rows[i]) * FF + (tid & 15) * 4)
@@ -219,27 +223,27 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
     const bool has_next = tile + 1 < t1;
     // ---- step 0: x rows -> C[:, 0:64]; passes 0 and 1 of the neighbour gathers in flight
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int p = 0; p < MT; ++p)
       *reinterpret_cast<f32x4*>(&C[(p * 16 + (tid >> 4)) * CS + (tid & 15) * 4]) = xnext[p];
     Gather g0, g1;
     issue_gather(g0, IDX[cur][grp], Ps, x, j);
     issue_gather(g1, IDX[cur][16 + grp], Ps, x, j);
     // the next tile's index chain, link 1: its destination node
     const int ni = (tile + 1) * TT + im;
-    const bool nvalid = has_next && ni < D;
+    const bool nvalid = has_next && im < TT && ni < D;
     int nd = 0, ne0 = 0, ndeg = -1;
     if (nvalid) nd = identity ? ni : dst_rows[ni];
     __syncthreads();
 
     // ---- step 1: Pt = X_d W1[:, :F]^T -> R[m][n]   (wave: n in [32 wave, 32 wave + 32))
     {
-      f32x4 acc[4][2];
+      f32x4 acc[MT][2];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_tile<4, 2, FF / 16>(acc, C, CS, w1r, lr, lg);
+      for (int mt = 0; mt < MT; ++mt) acc[mt][0] = acc[mt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_tile<MT, 2, FF / 16>(acc, C, CS, w1r, lr, lg);
       float* dst = R + 4 * lg * CS + 32 * wave + lr;
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           dst[(16 * mt + r) * CS] = acc[mt][0][r];
@@ -255,17 +259,20 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
 
     // ---- step 2: attention + normalised aggregation, four passes of 16 destinations
     {
-      const int m0 = grp, m1 = 16 + grp, m2 = 32 + grp, m3 = 48 + grp;
+      const int m0 = grp, m1 = 16 + grp;
       *reinterpret_cast<f32x4*>(&C[m0 * CS + FF + 4 * j]) =
           edge_pass(g0, IDX[cur][m0][1], &R[m0 * CS], AB, b2, j);
-      issue_gather(g0, IDX[cur][m2], Ps, x, j);
+      if constexpr (TT == 64) issue_gather(g0, IDX[cur][32 + grp], Ps, x, j);
       *reinterpret_cast<f32x4*>(&C[m1 * CS + FF + 4 * j]) =
           edge_pass(g1, IDX[cur][m1][1], &R[m1 * CS], AB, b2, j);
-      issue_gather(g1, IDX[cur][m3], Ps, x, j);
-      *reinterpret_cast<f32x4*>(&C[m2 * CS + FF + 4 * j]) =
-          edge_pass(g0, IDX[cur][m2][1], &R[m2 * CS], AB, b2, j);
-      *reinterpret_cast<f32x4*>(&C[m3 * CS + FF + 4 * j]) =
-          edge_pass(g1, IDX[cur][m3][1], &R[m3 * CS], AB, b2, j);
+      if constexpr (TT == 64) {
+        const int m2 = 32 + grp, m3 = 48 + grp;
+        issue_gather(g1, IDX[cur][m3], Ps, x, j);
+        *reinterpret_cast<f32x4*>(&C[m2 * CS + FF + 4 * j]) =
+            edge_pass(g0, IDX[cur][m2][1], &R[m2 * CS], AB, b2, j);
+        *reinterpret_cast<f32x4*>(&C[m3 * CS + FF + 4 * j]) =
+            edge_pass(g1, IDX[cur][m3][1], &R[m3 * CS], AB, b2, j);
+      }
     }
     // link 3: its sources
     const int nsq = iq < ndeg ? col[ne0 + iq] : nd;
@@ -273,12 +280,12 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
 
     // ---- step 3: [gate | u1] = [x_d; agg] [Wg; Wu1]^T + b  (wave: n in [32 wave, 32 wave + 32))
     {
-      f32x4 acc[4][2];
+      f32x4 acc[MT][2];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_tile<4, 2, 2 * FF / 16>(acc, C, CS, wcr, lr, lg);
+      for (int mt = 0; mt < MT; ++mt) acc[mt][0] = acc[mt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_tile<MT, 2, 2 * FF / 16>(acc, C, CS, wcr, lr, lg);
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {       // the next tile's x rows, in flight during the epilogue
+      for (int p = 0; p < MT; ++p) {      // the next tile's x rows, in flight during the epilogue
         const int i = (tile + 1) * TT + p * 16 + (tid >> 4);
         if (has_next && i < D)
           xnext[p] = *reinterpret_cast<const f32x4*>(
@@ -288,7 +295,7 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
       if (wave < 2) {
         float* dst = R + 4 * lg * GS + 32 * wave + lr;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             dst[(16 * mt + r) * GS] = sigmoidf_ref(acc[mt][0][r] + cbias0);
@@ -297,7 +304,7 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
       } else {
         float* dst = R + TT * GS + 4 * lg * GS + 32 * (wave - 2) + lr;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             dst[(16 * mt + r) * GS] = relu(acc[mt][0][r] + cbias0);
@@ -305,10 +312,12 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
           }
       }
     }
-    IDX[nxt][im][2 + iq] = nsq;
-    if (iq == 0) {
-      IDX[nxt][im][0] = nd;
-      IDX[nxt][im][1] = nvalid ? ndeg : -1;
+    if (im < TT) {
+      IDX[nxt][im][2 + iq] = nsq;
+      if (iq == 0) {
+        IDX[nxt][im][0] = nd;
+        IDX[nxt][im][1] = nvalid ? ndeg : -1;
+      }
     }
     __syncthreads();
 
@@ -316,13 +325,13 @@ __global__ __launch_bounds__(NT, 2) void gnn_layer_fused_kernel(
     {
       const float* G = R;
       const float* U = R + TT * GS;
-      f32x4 acc[4][1];
+      f32x4 acc[MT][1];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_tile<4, 1, FF / 16>(acc, U, GS, w4r, lr, lg);
+      for (int mt = 0; mt < MT; ++mt) acc[mt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_tile<MT, 1, FF / 16>(acc, U, GS, w4r, lr, lg);
       const int f = 16 * wave + lr;
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = 16 * mt + 4 * lg + r;
@@ -353,8 +362,14 @@ size_t gnn_layer_fused_ws_bytes(int V) {
 
 int gnn_layer_fused_kernel_launch(const az_graph* g, const float* x, const float* Ps,
                                   const az_gnn_layer_w* w, float* x_out, hipStream_t s) {
-  // persistent blocks (two per CU) over contiguous runs of 64-destination tiles
-  const int ntiles = (g->D + TT - 1) / TT;
+  // persistent blocks (two per CU) over contiguous runs of 64-destination tiles (tuning build:
+  // AZ_FUSED_TT=32 selects 32-destination tiles, four blocks per CU)
+  int tt = TT;
+#ifdef AZ_TUNING
+  static const char* env_tt = tuning_env("AZ_FUSED_TT");
+  if (env_tt && atoi(env_tt) == 32) tt = 32;
+#endif
+  const int ntiles = (g->D + tt - 1) / tt;
   static int cus = 0;                     // queried once per process
   if (cus <= 0) {
     int dev = 0, n = 0;
@@ -364,7 +379,7 @@ int gnn_layer_fused_kernel_launch(const az_graph* g, const float* x, const float
     else
       cus = 256;
   }
-  const int want = 2 * cus;
+  const int want = (tt == 64 ? 2 : 3) * cus;
   const int per = (ntiles + want - 1) / want;
   const int blocks = (ntiles + per - 1) / per;
   const FusedW fw = {w->att_w1, w->att_b1, w->att_w2, w->att_b2, w->gate_w, w->gate_b,
@@ -375,9 +390,17 @@ int gnn_layer_fused_kernel_launch(const az_graph* g, const float* x, const float
   static const char* env_nt = tuning_env("AZ_FUSED_NT");
   stagger = env_nt ? -1 : (env_st ? atoi(env_st) : 0);   // -1: non-temporal output stores
 #endif
-  hipLaunchKernelGGL(gnn_layer_fused_kernel, dim3(blocks), dim3(NT), 0, s, g->D,
-                     g->D == g->V ? 1 : 0, g->dst_rows, g->rowptr, g->col, x, Ps, fw, x_out,
-                     ntiles, per, stagger);
+#ifdef AZ_TUNING   // measured slower: 642 vs 515 us (168 VGPRs + 124 B/lane of spills at 3
+                   // blocks per CU, and the weights re-streamed per 32 destinations)
+  if (tt == 32)
+    hipLaunchKernelGGL(gnn_layer_fused_kernel<32>, dim3(blocks), dim3(NT), 0, s, g->D,
+                       g->D == g->V ? 1 : 0, g->dst_rows, g->rowptr, g->col, x, Ps, fw, x_out,
+                       ntiles, per, stagger);
+  else
+#endif
+    hipLaunchKernelGGL(gnn_layer_fused_kernel<64>, dim3(blocks), dim3(NT), 0, s, g->D,
+                       g->D == g->V ? 1 : 0, g->dst_rows, g->rowptr, g->col, x, Ps, fw, x_out,
+                       ntiles, per, stagger);
   return check_launch("gnn_layer_fused_kernel");
 }
 
