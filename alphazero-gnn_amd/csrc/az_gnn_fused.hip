@@ -86,8 +86,10 @@ __device__ __forceinline__ void mfma_tile(f32x4 (&acc)[MT][NTL], const float* A,
   }
 }
 
-// The gathered neighbour rows of one destination (16 lanes: lane j holds hidden units 8j..8j+7
-// of Ps and features 4j..4j+3 of x for each in-edge).
+// The gathered neighbour rows of one destination (16 lanes: lane j holds hidden units 4j..4j+3
+// and 64+4j..64+4j+3 of Ps and features 4j..4j+3 of x for each in-edge).  With that split the
+// 16 lanes' float4 reads of Pt / b1 / w2 in LDS are 256 contiguous bytes (8j..8j+7 made lanes j
+// and j + 8 share banks: 2-way conflicts on every edge-phase LDS read).
 struct Gather {
   f32x4 ps[MAXD][2];
   f32x4 xs[MAXD];
@@ -98,9 +100,9 @@ __device__ __forceinline__ void issue_gather(Gather& g, const int* idx, const fl
 #pragma unroll
   for (int q = 0; q < MAXD; ++q) {
     const int sq = idx[2 + q];
-    const float* pr = Ps + (size_t)sq * HH + 8 * j;
+    const float* pr = Ps + (size_t)sq * HH + 4 * j;
     g.ps[q][0] = *reinterpret_cast<const f32x4*>(pr);
-    g.ps[q][1] = *reinterpret_cast<const f32x4*>(pr + 4);
+    g.ps[q][1] = *reinterpret_cast<const f32x4*>(pr + HH / 2);
     g.xs[q] = *reinterpret_cast<const f32x4*>(x + (size_t)sq * FF + 4 * j);
   }
 }
@@ -111,12 +113,12 @@ __device__ __forceinline__ f32x4 edge_pass(const Gather& g, int deg, const float
                                            const float* AB, float b2, int j) {
   f32x4 agg = {0.f, 0.f, 0.f, 0.f};
   if (deg <= 0) return agg;
-  const f32x4 pt0 = *reinterpret_cast<const f32x4*>(pt + 8 * j);
-  const f32x4 pt1 = *reinterpret_cast<const f32x4*>(pt + 8 * j + 4);
-  const f32x4 bb0 = *reinterpret_cast<const f32x4*>(AB + 8 * j);
-  const f32x4 bb1 = *reinterpret_cast<const f32x4*>(AB + 8 * j + 4);
-  const f32x4 ww0 = *reinterpret_cast<const f32x4*>(AB + HH + 8 * j);
-  const f32x4 ww1 = *reinterpret_cast<const f32x4*>(AB + HH + 8 * j + 4);
+  const f32x4 pt0 = *reinterpret_cast<const f32x4*>(pt + 4 * j);
+  const f32x4 pt1 = *reinterpret_cast<const f32x4*>(pt + HH / 2 + 4 * j);
+  const f32x4 bb0 = *reinterpret_cast<const f32x4*>(AB + 4 * j);
+  const f32x4 bb1 = *reinterpret_cast<const f32x4*>(AB + HH / 2 + 4 * j);
+  const f32x4 ww0 = *reinterpret_cast<const f32x4*>(AB + HH + 4 * j);
+  const f32x4 ww1 = *reinterpret_cast<const f32x4*>(AB + HH + HH / 2 + 4 * j);
   float a[MAXD];
 #pragma unroll
   for (int q = 0; q < MAXD; ++q) {
