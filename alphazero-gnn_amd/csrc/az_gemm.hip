@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 #include "az_common.h"
 #include "az_heads.h"
@@ -951,6 +952,215 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
                                                                        : nullptr);
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 GEMM on the bf16 matrix cores ("x3").  Every fp32 operand element x is split into three
+// bf16 terms x = h + m + l, each rounded to nearest even (h = rne(x), m = rne(x - h),
+// l = rne(x - h - m); |m| <= 2^-8 |x|, |l| <= 2^-16 |x|, and the three hold all 24 significand
+// bits of x), and every product a*b is the sum of the six leading cross terms
+//   ah*bl + al*bh + am*bm + ah*bm + am*bh + ah*bh
+// on v_mfma_f32_32x32x16_bf16 (a bf16 x bf16 product is exact in fp32; sums are fp32).  The
+// three dropped terms am*bl + al*bm + al*bl are below 2^-23 |a||b|, the size of one fp32
+// rounding of the product, so the result keeps fp32 accuracy (tests/test_gpu_kernels.py holds
+// it to the same 1e-6 * sum|a*b| bound as the fp32 MFMA path and compares both errors).  Cost:
+// 6 x 32 cycles per 16 k against 8 x 64 for v_mfma_f32_32x32x2_f32, i.e. 2.67x the fp32 MFMA
+// rate (MI355X_MICROARCH.md constants: 32x32x16 bf16 issues every 32 cycles per SIMD).
+//
+// Register-staged tile: each thread loads 8-k segments (two float4) of A and W rows, splits them
+// after the current tile's MFMAs and writes the three planes to the other LDS buffer (one
+// ds_write_b128 per plane); one barrier per 32-k tile.  LDS image per plane: [row][32 bf16]
+// (64 B rows), 16-B chunk c stored at c ^ ((row >> 2) & 3), which makes the MFMA operand reads
+// (lane: row lane & 31, chunk 2s + (lane >> 5)) conflict-free for every ds_read_b128 lane group.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// two floats -> one dword of two bf16 (round to nearest even; v_cvt_pk_bf16_f32, low = a)
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const bf16x2 h = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, h);
+}
+
+// 8 consecutive floats -> three planes of 8 bf16 (element j in bits 16j.. of the 128-bit word):
+// per pair one v_cvt_pk_bf16_f32 per plane, the residual from the packed halves (shift / mask).
+// The two residuals of a pair are formed by different (exact) instructions, a - h and
+// fma(h, -1, b), so the compiler does not pack them into v_pk_add_f32, which costs extra
+// cycles beside MFMAs (MI355X_MICROARCH.md, filler prices).
+__device__ __forceinline__ void split3(const f32x4& x0, const f32x4& x1, u32x4 (&o)[3]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float a = q < 2 ? x0[2 * q] : x1[2 * q - 4];
+    const float b = q < 2 ? x0[2 * q + 1] : x1[2 * q - 3];
+    const unsigned h = pk_bf16(a, b);
+    const float ra = a - __uint_as_float(h << 16);
+    const float rb = __builtin_fmaf(__uint_as_float(h & 0xFFFF0000u), -1.f, b);
+    const unsigned m = pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(m << 16);
+    const float sb = __builtin_fmaf(__uint_as_float(m & 0xFFFF0000u), -1.f, rb);
+    o[0][q] = h;
+    o[1][q] = m;
+    o[2][q] = pk_bf16(sa, sb);
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
+  constexpr int BK = 32;
+  constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TI = WM / 32, TJ = WN / 32;
+  constexpr int ASEG = BM * 4 / NT, BSEG = BN * 4 / NT, NSEG = ASEG + BSEG;
+  static_assert(TI >= 1 && TJ >= 1 && ASEG >= 1 && BSEG >= 1 && (BM * 4) % NT == 0 &&
+                (BN * 4) % NT == 0, "bad x3 tile");
+  constexpr int PLANE = (BM + BN) * 64;          // bytes of one bf16 plane (A rows, then W rows)
+  constexpr int BUF = 3 * PLANE;
+  constexpr int STAGE = NW * WM * 36 * 4;
+  constexpr int SMEM = 2 * BUF > STAGE ? 2 * BUF : STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
+  const int nwg = mt_n * nt_n * p.splits;
+  const int bid = xcd_swizzle(blockIdx.x, nwg);
+  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+
+  // loader: segment q covers row idx >> 2 (A rows first, then W rows), k = 8 * (idx & 3) ..+7
+  const float* src[NSEG];
+  int soff[NSEG], sk[NSEG];
+#pragma unroll
+  for (int q = 0; q < NSEG; ++q) {
+    const bool isa = q < ASEG;
+    const int idx = threadIdx.x + (isa ? q : q - ASEG) * NT;
+    const int r = idx >> 2, c = idx & 3;
+    if (isa) {
+      const int gr = m0 + r < p.M ? m0 + r : 0;     // clamped rows feed outputs never stored
+      src[q] = p.A + (size_t)gr * p.lda;
+    } else {
+      const int gr = n0 + r < p.N ? n0 + r : 0;
+      src[q] = p.B + (size_t)gr * p.ldb;
+    }
+    const int row = isa ? r : BM + r;
+    soff[q] = row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
+    sk[q] = c * 8;
+  }
+  using Regs = f32x4[NSEG][2];
+  // every load is unconditional (k clamped in bounds); k >= kend is zeroed at the split
+  auto gload = [&](Regs& ld, int k0) {
+#pragma unroll
+    for (int q = 0; q < NSEG; ++q) {
+      const int k = k0 + sk[q];
+      ld[q][0] = *reinterpret_cast<const f32x4*>(src[q] + (k < p.K ? k : 0));
+      ld[q][1] = *reinterpret_cast<const f32x4*>(src[q] + (k + 4 < p.K ? k + 4 : 0));
+    }
+  };
+  auto split_store = [&](const Regs& ld, int buf, int k0, int q, auto mask) {
+    char* base = smem + buf * BUF;
+    u32x4 o[3];
+    if constexpr (decltype(mask)::value) {
+      const int k = k0 + sk[q];
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      split3(k < kend ? ld[q][0] : z, k + 4 < kend ? ld[q][1] : z, o);
+    } else {
+      split3(ld[q][0], ld[q][1], o);
+    }
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(base + pl * PLANE + soff[q]) = o[pl];
+  };
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  int aoff[TI], akey[TI], boff[TJ], bkey[TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int row = wm * WM + i * 32 + (lane & 31);
+    aoff[i] = row * 64;
+    akey[i] = (row >> 2) & 3;
+  }
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int row = BM + wn * WN + j * 32 + (lane & 31);
+    boff[j] = row * 64;
+    bkey[j] = (row >> 2) & 3;
+  }
+  const int hk = lane >> 5;
+  struct Frags { bf16x8 a[3][TI], b[3][TJ]; };
+  auto read = [&](Frags& f, const char* S, int s) {
+    const int c = 2 * s + hk;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+        f.a[pl][i] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + aoff[i] + ((c ^ akey[i]) << 4));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        f.b[pl][j] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + boff[j] + ((c ^ bkey[j]) << 4));
+    }
+  };
+  auto mfma6 = [&](const Frags& f, int i, int j) {
+    f32x16 t = acc[i][j];
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[2][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[2][i], f.b[0][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[1][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[1][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[0][j], t, 0, 0, 0);
+    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[0][j], t, 0, 0, 0);
+  };
+
+  // One 32-k tile: tile kt + 2's global loads first, step 0's fragments and its first MFMA
+  // group, step 1's fragment reads, then the remaining groups of both steps with tile kt + 1's
+  // split + LDS stores (its registers were loaded one tile earlier) pinned between them, so the
+  // conversion VALU issues while earlier MFMAs run.  `nxt` holds tile kt + 1, `fut` receives
+  // tile kt + 2; MASK zeroes k >= kend (only the last tile can be partial).
+  constexpr int NG = TI * TJ;
+  auto body = [&](auto mask, int kt, const Regs& nxt, Regs& fut) {
+    const char* S = smem + (kt & 1) * BUF;
+    gload(fut, kbeg + (kt + 2) * BK);
+    Frags f0, f1;
+    read(f0, S, 0);
+#pragma unroll
+    for (int g = 0; g < 2 * NG; ++g) {
+      if (g < NG) mfma6(f0, g / TJ, g % TJ);
+      else mfma6(f1, (g - NG) / TJ, (g - NG) % TJ);
+      if (g == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        read(f1, S, 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int q = 0; q < NSEG; ++q)
+        if (q * 2 * NG / NSEG == g) {
+          __builtin_amdgcn_sched_barrier(0);
+          split_store(nxt, (kt + 1) & 1, kbeg + (kt + 1) * BK, q, mask);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    __syncthreads();
+  };
+  auto step = [&](int kt, const Regs& nxt, Regs& fut) { body(std::true_type{}, kt, nxt, fut); };
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  Regs r0, r1;
+  gload(r0, kbeg);
+  gload(r1, kbeg + BK);
+#pragma unroll
+  for (int q = 0; q < NSEG; ++q) split_store(r0, 0, kbeg, q, std::true_type{});
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, r1, r0);                 // tile kt + 1 in r1, tile kt + 2 -> r0
+    if (kt + 1 < nk) step(kt + 1, r0, r1);
+  }
+  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
+                            reinterpret_cast<float*>(smem) + wave * (WM * 36));
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
   const long total = (long)p.M * p.N;
   const size_t plane = (size_t)p.M * p.N;
@@ -1746,6 +1956,43 @@ static int splits_256x128(int M, int N, int K, size_t ws_bytes) {
   return S;
 }
 
+// gemm_x3 launch for a K-major A and W (no A2 / gathered rows), M >= 64: 256x128 (8 waves) above
+// M = 256, else 128x128 (4 waves); split-K so the grid nears one block per CU (measured on
+// MI355X, tools/gemm_sweep.py x3: M = 512 75 us vs 103 us for the fp32 MFMA tile, M = 800 147 vs
+// 185, M = 4096 516 vs 767).  Tuning build: AZ_GEMM_X3=0 keeps the fp32 MFMA tiles, 1..4 forces
+// a tile, AZ_GEMM_SPLITS the split.  Sets a.splits / a.kc; false = not launched.
+static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
+  static const char* env = tuning_env("AZ_GEMM_X3");
+  static const char* env_split = tuning_env("AZ_GEMM_SPLITS");
+  int tile = env ? atoi(env) : 0;
+  if (env && tile == 0) return false;
+  if (!env && a.M < 64) return false;   // tools/gemm_sweep.py x3: the fp32 tiles win below
+  const int bms[5] = {0, 256, 128, 128, 256}, bns[5] = {0, 128, 128, 64, 128};
+  if (tile < 1 || tile > 4) {
+    tile = a.M > 256 ? 1 : 2;
+  }
+  const int bm = bms[tile], bn = bns[tile];
+  const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+  int S = 1;
+  if (env_split) {
+    S = std::max(1, atoi(env_split));
+  } else if (tiles < 256) {
+    S = (int)std::min<long>(256 / tiles, 8);
+  }
+  while (S > 1 && (!a.slab || (size_t)S * a.M * a.N * 4 > ws_bytes || a.K / S < 8 * 32)) --S;
+  a.splits = S;
+  a.kc = S > 1 ? ((a.K + S - 1) / S + 31) / 32 * 32 : a.K;
+  if (S > 1) a.splits = (a.K + a.kc - 1) / a.kc;
+  const dim3 grid((unsigned)(tiles * a.splits));
+  switch (tile) {
+    case 1: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2>), grid, dim3(512), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_x3<128, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((gemm_x3<256, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL((gemm_x3<128, 64, 2, 1>), grid, dim3(128), 0, s, a); break;
+  }
+  return true;
+}
+
 // True when the 256x128 grid is >= 4 rounds of one block per CU and its last round is >= 95 %
 // full (wave quantisation otherwise costs the 8-wave tile its edge: M = 8,192 / 16,384).
 static bool full_waves_256x128(int M, int N) {
@@ -1818,9 +2065,13 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
       return check_launch("gemm_kslice");
     }
   }
+  const bool glds_ok = akm && bkm && !d->A2 && !d->a_rows;
+  if (glds_ok && d->M > 8 && d->K >= 1024 && d->N >= 256 && launch_x3(a, d->ws_bytes, s)) {
+    *splits_out = a.splits;
+    return check_launch("gemm_x3");
+  }
   // tile choice (tuning override for experiments: AZ_GEMM_CFG=<index into kCfgs>)
   static const char* env_cfg = tuning_env("AZ_GEMM_CFG");
-  const bool glds_ok = akm && bkm && !d->A2 && !d->a_rows;
   int cfg = 0;
   int s256 = 0;   // split factor when the 256x128 8-wave tile packs the chip (one block per CU)
   if (env_cfg) {

@@ -7,8 +7,9 @@ its own on the same inputs, and the product library's default run is compared to
   - the GNN tail's split-K heads: rowsw (default) vs one row per block
     (AZ_SPLITK_HEADS_MODE=rows) vs chunk partials + finalize (=chunks) -- gnn_utils.py:115;
   - the split-K reduce: float4 (default) vs scalar (AZ_GEMM_NOVEC=1);
-  - the 256x128 GEMM tile: 2-buffer (default) vs 3-buffer ring and its stagger
-    (AZ_GEMM_RING=3 / 4): the same k order, so the same sums."""
+  - the fp32 MFMA 256x128 GEMM tile (AZ_GEMM_X3=0, the path before gemm_x3 took these shapes):
+    2-buffer vs 3-buffer ring and its stagger (AZ_GEMM_RING=3 / 4): the same k order, so the same
+    sums (compared with the fp32 tile's own default, since gemm_x3 sums differently)."""
 import os
 import subprocess
 import sys
@@ -53,8 +54,12 @@ VARIANTS = {
     "twopass_chunks": {"AZ_HEADS_TWOPASS": "1", "AZ_SPLITK_HEADS_MODE": "chunks"},
     "rows": {"AZ_SPLITK_HEADS_MODE": "rows"},
     "novec": {"AZ_GEMM_NOVEC": "1"},
-    "ring3": {"AZ_GEMM_RING": "3"},
-    "ring_stagger": {"AZ_GEMM_RING": "4"},
+}
+FP32_VARIANTS = {
+    "fp32": {"AZ_GEMM_X3": "0"},
+    "ring3": {"AZ_GEMM_X3": "0", "AZ_GEMM_RING": "3"},
+    "ring_stagger": {"AZ_GEMM_X3": "0", "AZ_GEMM_RING": "4"},
+    "fp32_novec": {"AZ_GEMM_X3": "0", "AZ_GEMM_NOVEC": "1"},
 }
 
 
@@ -63,7 +68,8 @@ def _run(tmp_path, name, env_extra, tuning=True):
     env.pop("AZ_TUNING_LIB", None)
     if tuning:
         env["AZ_TUNING_LIB"] = "1"
-    for k in ("AZ_HEADS_TWOPASS", "AZ_SPLITK_HEADS_MODE", "AZ_GEMM_NOVEC", "AZ_GEMM_RING"):
+    for k in ("AZ_HEADS_TWOPASS", "AZ_SPLITK_HEADS_MODE", "AZ_GEMM_NOVEC", "AZ_GEMM_RING",
+              "AZ_GEMM_X3"):
         env.pop(k, None)
     env.update(env_extra)
     path = str(tmp_path / f"{name}.npz")
@@ -84,4 +90,11 @@ def test_kernel_variants_bit_identical(tmp_path):
             continue
         got = _run(tmp_path, name, env)
         for k, a in ref.items():
+            assert np.array_equal(a, got[k]), f"{name}: {k} differs"
+    ref32 = _run(tmp_path, "fp32", FP32_VARIANTS["fp32"])
+    for name, env in FP32_VARIANTS.items():
+        if name == "fp32":
+            continue
+        got = _run(tmp_path, name, env)
+        for k, a in ref32.items():
             assert np.array_equal(a, got[k]), f"{name}: {k} differs"

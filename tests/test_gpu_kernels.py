@@ -60,6 +60,30 @@ def test_linear_vs_torch(ops, M, N, K, act):
     check_dot_error(y.numpy(), ref.numpy(), bound.numpy())
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 3136, 3136), (800, 3136, 3136), (64, 3136, 3136),
+                                   (37, 1001, 1028), (4096, 1024, 2048)])
+def test_x3_gemm_has_fp32_accuracy(ops, M, N, K):
+    """The K-major GEMMs with K >= 1024, N >= 256, M > 8 (output_transform) run gemm_x3: fp32
+    operands split into three bf16 terms, six cross products on the bf16 matrix cores.  Its
+    error against float64 must be of the size of an ordinary fp32 GEMM's: within 1e-6 *
+    sum|a*b| per element (the fp32 MFMA bound above) and at most 2x the error of torch's fp32
+    CPU GEMM on the same operands (max and mean over the outputs), with the same scaling
+    (rand * 2 - 1 activations, 1/sqrt(K) weights) as output_transform."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.rand((M, K), generator=g) * 2 - 1
+    w = (torch.rand((N, K), generator=g) * 2 - 1) / K ** 0.5
+    b = torch.rand((N,), generator=g) - 0.5
+    ref = x.double() @ w.double().T + b.double()
+    bound = (x.double().abs() @ w.double().abs().T + b.double().abs()).numpy()
+    y = ops.linear(x.cuda(), w.cuda(), b.cuda(), act=0).cpu()
+    check_dot_error(y.numpy(), ref.numpy(), bound)
+    cpu = (x @ w.T + b).double()
+    e_x3 = ((y.double() - ref).abs().numpy() / bound)
+    e_cpu = ((cpu - ref).abs().numpy() / bound)
+    assert e_x3.max() <= 2 * e_cpu.max(), (e_x3.max(), e_cpu.max())
+    assert e_x3.mean() <= 2 * e_cpu.mean(), (e_x3.mean(), e_cpu.mean())
+
+
 @pytest.mark.parametrize("K", [3136, 2500, 100])
 def test_small_m_rows_are_batch1_bits(ops, K):
     """M <= 8 rows (gemv_full / gemv_rows): every row of a batch is bit-identical to the same row

@@ -129,6 +129,23 @@ if __name__ == "__main__":
             r = run({"AZ_GEMM_CFG": cfg, "AZ_GEMM_SPLITS": "1"}, M=M)
             print(json.dumps({"M": M, "cfg": cfg, **r}), flush=True)
         sys.exit(0)
+    if mode == "x3":           # fp32 on the bf16 matrix cores (gemm_x3) vs the fp32 MFMA tiles
+        # argv: Ms  tiles  splits ("auto" = the dispatch's own choice)
+        shapes = [tuple(int(v) for v in (x + ":3136:3136").split(":")[:3])
+                  for x in sys.argv[2].split(",")]     # "M" or "M:N:K"
+        tiles = sys.argv[3].split(",")
+        splits = sys.argv[4].split(",")
+        for (M, N, K) in shapes:
+            print(json.dumps({"M": M, "N": N, "K": K, "x3": "off",
+                              **run({"AZ_GEMM_X3": "0"}, M, N, K)}), flush=True)
+            for t in tiles:
+                for sp in splits:
+                    env = {"AZ_GEMM_X3": t}
+                    if sp != "auto":
+                        env["AZ_GEMM_SPLITS"] = sp
+                    print(json.dumps({"M": M, "N": N, "K": K, "x3": t, "splits": sp,
+                                      **run(env, M, N, K)}), flush=True)
+        sys.exit(0)
     if mode == "ablate":       # glds2 timing ablations (results wrong by design)
         cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else ("15", "16")
         abls = sys.argv[3].split(",") if len(sys.argv) > 3 else ("0", "1", "2", "3")
