@@ -1002,7 +1002,7 @@ __device__ __forceinline__ void split3(const f32x4& x0, const f32x4& x1, u32x4 (
   }
 }
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, bool MASK>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
   constexpr int BK = 32;
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
@@ -1144,14 +1144,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
     }
     __syncthreads();
   };
-  auto step = [&](int kt, const Regs& nxt, Regs& fut) { body(std::true_type{}, kt, nxt, fut); };
+  // MASK = false when every split's k range is whole 32-k tiles (K % 32 == 0, e.g. 3136): no
+  // k >= kend selects in the split
+  auto step = [&](int kt, const Regs& nxt, Regs& fut) {
+    body(std::integral_constant<bool, MASK>{}, kt, nxt, fut);
+  };
 
   const int nk = (kend - kbeg + BK - 1) / BK;
   Regs r0, r1;
   gload(r0, kbeg);
   gload(r1, kbeg + BK);
 #pragma unroll
-  for (int q = 0; q < NSEG; ++q) split_store(r0, 0, kbeg, q, std::true_type{});
+  for (int q = 0; q < NSEG; ++q) split_store(r0, 0, kbeg, q, std::integral_constant<bool, MASK>{});
   __syncthreads();
   for (int kt = 0; kt < nk; kt += 2) {
     step(kt, r1, r0);                 // tile kt + 1 in r1, tile kt + 2 -> r0
@@ -1956,7 +1960,7 @@ static int splits_256x128(int M, int N, int K, size_t ws_bytes) {
   return S;
 }
 
-// gemm_x3 launch for a K-major A and W (no A2 / gathered rows), M >= 64: 256x128 (8 waves) above
+// gemm_x3 launch for a K-major A and W (no A2 / gathered rows), M > 64: 256x128 (8 waves) above
 // M = 256, else 128x128 (4 waves); split-K so the grid nears one block per CU (measured on
 // MI355X, tools/gemm_sweep.py x3: M = 512 75 us vs 103 us for the fp32 MFMA tile, M = 800 147 vs
 // 185, M = 4096 516 vs 767).  Tuning build: AZ_GEMM_X3=0 keeps the fp32 MFMA tiles, 1..4 forces
@@ -1966,7 +1970,7 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   static const char* env_split = tuning_env("AZ_GEMM_SPLITS");
   int tile = env ? atoi(env) : 0;
   if (env && tile == 0) return false;
-  if (!env && a.M < 64) return false;   // tools/gemm_sweep.py x3: the fp32 tiles win below
+  if (!env && a.M <= 64) return false;  // tools/gemm_sweep.py x3: fp32 tiles win to M = 64 (27 vs 31 us)
   const int bms[5] = {0, 256, 128, 128, 256}, bns[5] = {0, 128, 128, 64, 128};
   if (tile < 1 || tile > 4) {
     tile = a.M > 256 ? 1 : 2;
@@ -1984,12 +1988,20 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   a.kc = S > 1 ? ((a.K + S - 1) / S + 31) / 32 * 32 : a.K;
   if (S > 1) a.splits = (a.K + a.kc - 1) / a.kc;
   const dim3 grid((unsigned)(tiles * a.splits));
+  const bool whole = a.K % 32 == 0;   // kc is a multiple of 32 too: no partial k tile anywhere
+#define AZ_X3(BM_, BN_, WM_, WN_)                                                              \
+  if (whole) hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, false>), grid, dim3(64 * WM_ * WN_), \
+                                0, s, a);                                                      \
+  else hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, true>), grid, dim3(64 * WM_ * WN_), 0, s, a);
   switch (tile) {
-    case 1: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2>), grid, dim3(512), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((gemm_x3<128, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((gemm_x3<256, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL((gemm_x3<128, 64, 2, 1>), grid, dim3(128), 0, s, a); break;
+    case 1: AZ_X3(256, 128, 4, 2) break;
+#ifdef AZ_TUNING
+    case 3: AZ_X3(128, 64, 2, 1) break;
+    case 4: AZ_X3(256, 128, 2, 2) break;
+#endif
+    default: AZ_X3(128, 128, 2, 2) break;
   }
+#undef AZ_X3
   return true;
 }
 

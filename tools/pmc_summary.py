@@ -58,7 +58,8 @@ def main(d, tag):
         n = max(1, len(tile))
         return sum(tile) / n, sum(red) / n, len(tile)
 
-    is_fwd_gemm = lambda n: "gemm_f32_glds" in n  # the forward Linear path (bench GEMMs)
+    # the forward Linear path of the bench GEMMs (gemm_x3 from r02m on)
+    is_fwd_gemm = lambda n: "gemm_f32_glds" in n or "gemm_x3" in n
     ft, fr, nf = call_bytes(fetch, is_fwd_gemm)
     wt, wr, _ = call_bytes(write, is_fwd_gemm)
     gemm_tile = int((2 * ft + wt) * 1024)
@@ -75,8 +76,9 @@ def main(d, tag):
                   f"(tools/gpu_profile.sh {tag}); per-kernel averages over all dispatches; "
                   f"bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE reports "
                   f"half of wide reads, MI355X_MICROARCH.md HBM section)",
-        "gemm": {"kernel": "az_gemm_f32 output_transform.0 call (gemm_f32_glds2 tile kernel + "
-                           "splitk_reduce4_kernel)",
+        "gemm": {"kernel": "az_gemm_f32 output_transform.0 call (%s tile kernel + "
+                           "splitk_reduce4_kernel)" % ("gemm_x3" if any(
+                               "gemm_x3" in r[1] for r in fetch) else "gemm_f32_glds2"),
                  "dispatches": nf,
                  "hbm_bytes_per_launch": gemm_tile + gemm_red,
                  "gemm_kernel_bytes": gemm_tile, "reduce_kernel_bytes": gemm_red,
@@ -110,7 +112,17 @@ def main(d, tag):
                             "note": "512 32x32 grids, back-to-back launches (x and Ps partly "
                                     "Infinity-Cache resident between them)"}
     res["round"] = 2 if tag.startswith("r02") else res["round"]
-    json.dump(res, open(os.path.join(ROOT, "profiles", "pmc.json"), "w"), indent=1)
+    # keep the entries of earlier passes this one did not measure (e.g. the fused-layer probe)
+    path = os.path.join(ROOT, "profiles", "pmc.json")
+    try:
+        old = json.load(open(path))
+    except (OSError, ValueError):
+        old = {}
+    for k, v in old.items():
+        if isinstance(v, dict) and k not in res:
+            v.setdefault("tag", old.get("tag"))
+            res[k] = v
+    json.dump(res, open(path, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
