@@ -205,9 +205,15 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
 // around a ticket counter -- was measured 1.8x slower here: a tile's 5 slabs are 320 KB, far
 // above the few tens of KB where one block's serial combine beats a separate launch;
 // cdna_hip_programming.md §5 "In-launch split-K reduction".)
-template <int MF, int TI, int TJ, class Acc>
+// WAVE_LOCAL: only some of the block's waves run the epilogue (gemm_x3ws: the producer waves
+// have left), each in its own stage region, so the block barriers become wave-local LDS waits.
+template <int MF, int TI, int TJ, bool WAVE_LOCAL = false, class Acc>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][TJ], int r0,
                                               int c0, int sp, float* stage = nullptr) {
+  auto sync = [] {
+    if constexpr (WAVE_LOCAL) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else __syncthreads();
+  };
   constexpr int NACC = MF == 32 ? 16 : 4;
   constexpr int WM = TI * MF, WN = TJ * MF;
   const int lane = threadIdx.x & 63;
@@ -223,7 +229,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][
     // stores over 2-4 rows per instruction): each 32-column chunk of the wave tile is written
     // to LDS [WM][36] and read back as float4 rows, 8 lanes per 128-B row segment.
     constexpr int LD = 36, CH = 32 / MF;   // MFMA column tiles per 32-column chunk
-    __syncthreads();                        // the k loop's last LDS reads are done everywhere
+    sync();                                 // the k loop's last LDS reads are done everywhere
 #pragma unroll
     for (int cc = 0; cc < WN / 32; ++cc) {
 #pragma unroll
@@ -233,7 +239,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][
 #pragma unroll
           for (int r = 0; r < NACC; ++r)
             stage[row_in(i, r) * LD + jj * MF + cl] = acc[i][cc * CH + jj][r];
-      __syncthreads();
+      sync();
 #pragma unroll
       for (int it = 0; it < WM / 8; ++it) {
         const int idx = it * 64 + lane, rl = idx >> 3, c4 = (idx & 7) * 4;
@@ -246,7 +252,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][
           epilogue_store4(p, row, col, v);
         }
       }
-      __syncthreads();
+      sync();
     }
     return;
   }
@@ -1165,6 +1171,178 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
 }
 
+// gemm_x3 with specialised waves ("x3ws"): WGM x WGN consumer waves (the product tile: 4 x 2
+// waves of 64 x 64) only read the bf16 planes from LDS and issue MFMAs; 4 producer waves (one per
+// SIMD) only load the fp32 tiles, split them and write the planes.  The split's VALU and the
+// global-load waits then run in the producer wave beside the consumers' MFMA stream instead of
+// between its MFMA groups (gemm_x3 at 2 waves per SIMD: MFMA busy 0.40, half of the wave-cycles
+// waiting; MI355X PMC, profiles/r02m_*).  12 waves = 3 per SIMD: 168 VGPRs each, which both
+// roles fit (a 4 + 4 wave form with 128 x 64 consumer tiles spills at 256).  Same LDS image,
+// split and product order as gemm_x3; one block barrier per 32-k tile: consumers read buffer
+// kt & 1 while producers fill buffer (kt + 1) & 1 from registers loaded one tile earlier.
+template <int BM, int BN, int WGM, int WGN, bool MASK>
+__global__ __launch_bounds__(64 * (WGM * WGN + 4)) void gemm_x3ws(GemmArgs p) {
+  constexpr int BK = 32, NC = WGM * WGN;       // consumer waves; 4 producer waves after them
+  constexpr int WM = BM / WGM, WN = BN / WGN, TI = WM / 32, TJ = WN / 32;
+  constexpr int NPT = 256;                        // producer threads
+  constexpr int NSEG = (BM + BN) * 4 / NPT;       // 8-k segments per producer thread and tile
+  static_assert((BM + BN) * 4 % NPT == 0 && TI >= 1 && TJ >= 1, "bad x3ws tile");
+  constexpr int PLANE = (BM + BN) * 64, BUF = 3 * PLANE;
+  constexpr int STAGE = NC * WM * 36 * 4;
+  constexpr int SMEM = 2 * BUF > STAGE ? 2 * BUF : STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
+  const int nwg = mt_n * nt_n * p.splits;
+  const int bid = xcd_swizzle(blockIdx.x, nwg);
+  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool producer = __builtin_amdgcn_readfirstlane(wave) >= NC;
+
+  if (producer) {
+    const int pt = threadIdx.x - 64 * NC;
+    const float* src[NSEG];
+    int soff[NSEG], sk[NSEG];
+#pragma unroll
+    for (int q = 0; q < NSEG; ++q) {
+      const int idx = pt + q * NPT;
+      const int row = idx >> 2, c = idx & 3;
+      if (row < BM) {
+        const int gr = m0 + row < p.M ? m0 + row : 0;   // clamped rows feed unstored outputs
+        src[q] = p.A + (size_t)gr * p.lda;
+      } else {
+        const int gr = n0 + row - BM < p.N ? n0 + row - BM : 0;
+        src[q] = p.B + (size_t)gr * p.ldb;
+      }
+      soff[q] = row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
+      sk[q] = c * 8;
+    }
+    using Regs = f32x4[NSEG][2];
+    auto gload = [&](Regs& ld, int k0) {
+#pragma unroll
+      for (int q = 0; q < NSEG; ++q) {
+        const int k = k0 + sk[q];
+        ld[q][0] = *reinterpret_cast<const f32x4*>(src[q] + (k < p.K ? k : 0));
+        ld[q][1] = *reinterpret_cast<const f32x4*>(src[q] + (k + 4 < p.K ? k + 4 : 0));
+      }
+    };
+    auto split_store = [&](const Regs& ld, int buf, int k0) {
+      char* base = smem + buf * BUF;
+#pragma unroll
+      for (int q = 0; q < NSEG; ++q) {
+        u32x4 o[3];
+        if constexpr (MASK) {
+          const int k = k0 + sk[q];
+          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+          split3(k < kend ? ld[q][0] : z, k + 4 < kend ? ld[q][1] : z, o);
+        } else {
+          split3(ld[q][0], ld[q][1], o);
+        }
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          *reinterpret_cast<u32x4*>(base + pl * PLANE + soff[q]) = o[pl];
+      }
+    };
+    Regs r0, r1;
+    gload(r0, kbeg);
+    gload(r1, kbeg + BK);
+    split_store(r0, 0, kbeg);
+    __syncthreads();
+    // tile kt: tile kt + 2's loads issued, tile kt + 1 (loaded one tile ago) split into the
+    // other buffer, then the barrier that hands it to the consumers
+    for (int kt = 0; kt < nk; kt += 2) {
+      gload(r0, kbeg + (kt + 2) * BK);
+      split_store(r1, (kt + 1) & 1, kbeg + (kt + 1) * BK);
+      __syncthreads();
+      if (kt + 1 < nk) {
+        gload(r1, kbeg + (kt + 3) * BK);
+        split_store(r0, kt & 1, kbeg + (kt + 2) * BK);
+        __syncthreads();
+      }
+    }
+    return;
+  }
+
+  const int wm = wave / WGN, wn = wave % WGN;
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  int aoff[TI], akey[TI], boff[TJ], bkey[TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int row = wm * WM + i * 32 + (lane & 31);
+    aoff[i] = row * 64;
+    akey[i] = (row >> 2) & 3;
+  }
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int row = BM + wn * WN + j * 32 + (lane & 31);
+    boff[j] = row * 64;
+    bkey[j] = (row >> 2) & 3;
+  }
+  const int hk = lane >> 5;
+  // fragments per unit u = (k step s, row block i): A's three planes of row block i, and W's
+  // three planes of all TJ column blocks (held for the whole step); the next unit's fragments
+  // are read while this unit's MFMAs run (double buffers indexed by the unrolled unit parity:
+  // 72 VGPRs of fragments beside the 128 of accumulators, within the 256 of two waves per SIMD)
+  bf16x8 fa[2][3], fb[2][3][TJ];
+  auto rd_a = [&](bf16x8 (&d)[3], const char* S, int s, int i) {
+    const int c = 2 * s + hk;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      d[pl] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + aoff[i] + ((c ^ akey[i]) << 4));
+  };
+  auto rd_b = [&](bf16x8 (&d)[3][TJ], const char* S, int s, int j) {
+    const int c = 2 * s + hk;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      d[pl][j] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + boff[j] + ((c ^ bkey[j]) << 4));
+  };
+  auto mfma6 = [&](const bf16x8 (&A)[3], const bf16x8 (&B)[3][TJ], int i, int j) {
+    f32x16 t = acc[i][j];
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0][j], t, 0, 0, 0);
+    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0][j], t, 0, 0, 0);
+  };
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* S = smem + (kt & 1) * BUF;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) rd_b(fb[0], S, 0, j);
+    rd_a(fa[0], S, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 2 * TI; ++u) {
+      const int s = u / TI, i = u % TI;
+      const int s1 = (u + 1) / TI, i1 = (u + 1) % TI;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        mfma6(fa[u & 1], fb[s], i, j);
+        // after column block j's MFMAs: the next unit's A fragments (once), and at the step
+        // change step 1's W fragments of column block j, whose step-0 copy just died
+        if (u + 1 < 2 * TI) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (j == 0) rd_a(fa[(u + 1) & 1], S, s1, i1);
+          if (s1 != s) rd_b(fb[s1], S, s1, j);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  tile_epilogue<32, TI, TJ, true>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
+                                  reinterpret_cast<float*>(smem) + wave * (WM * 36));
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
   const long total = (long)p.M * p.N;
   const size_t plane = (size_t)p.M * p.N;
@@ -1971,8 +2149,8 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   int tile = env ? atoi(env) : 0;
   if (env && tile == 0) return false;
   if (!env && a.M <= 64) return false;  // tools/gemm_sweep.py x3: fp32 tiles win to M = 64 (27 vs 31 us)
-  const int bms[5] = {0, 256, 128, 128, 256}, bns[5] = {0, 128, 128, 64, 128};
-  if (tile < 1 || tile > 4) {
+  const int bms[7] = {0, 256, 128, 128, 256, 256, 256}, bns[7] = {0, 128, 128, 64, 128, 128, 128};
+  if (tile < 1 || tile > 6) {
     tile = a.M > 256 ? 1 : 2;
   }
   const int bm = bms[tile], bn = bns[tile];
@@ -1998,6 +2176,16 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
 #ifdef AZ_TUNING
     case 3: AZ_X3(128, 64, 2, 1) break;
     case 4: AZ_X3(256, 128, 2, 2) break;
+#endif
+    case 5:
+      if (whole) hipLaunchKernelGGL((gemm_x3ws<256, 128, 4, 2, false>), grid, dim3(768), 0, s, a);
+      else hipLaunchKernelGGL((gemm_x3ws<256, 128, 4, 2, true>), grid, dim3(768), 0, s, a);
+      break;
+#ifdef AZ_TUNING
+    case 6:   // 4 consumer waves with 128 x 64 wave tiles (two waves per SIMD)
+      if (whole) hipLaunchKernelGGL((gemm_x3ws<256, 128, 2, 2, false>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((gemm_x3ws<256, 128, 2, 2, true>), grid, dim3(512), 0, s, a);
+      break;
 #endif
     default: AZ_X3(128, 128, 2, 2) break;
   }
