@@ -1008,7 +1008,9 @@ __device__ __forceinline__ void split3(const f32x4& x0, const f32x4& x1, u32x4 (
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, bool MASK>
+// ABL (tuning build only, timing ablations whose results are wrong by design): 1 = every tile's
+// loads from the split's first four tiles (L2-resident), 2 = no MFMA, 4 = no split (raw bits)
+template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
   constexpr int BK = 32;
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
@@ -1054,6 +1056,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
   using Regs = f32x4[NSEG][2];
   // every load is unconditional (k clamped in bounds); k >= kend is zeroed at the split
   auto gload = [&](Regs& ld, int k0) {
+    if constexpr ((ABL & 1) != 0) k0 = kbeg + (k0 - kbeg) % (4 * BK);
 #pragma unroll
     for (int q = 0; q < NSEG; ++q) {
       const int k = k0 + sk[q];
@@ -1068,6 +1071,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
       const int k = k0 + sk[q];
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       split3(k < kend ? ld[q][0] : z, k + 4 < kend ? ld[q][1] : z, o);
+    } else if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[0][e] = __float_as_uint(ld[q][0][e]);
+        o[1][e] = __float_as_uint(ld[q][1][e]);
+        o[2][e] = o[0][e];
+      }
     } else {
       split3(ld[q][0], ld[q][1], o);
     }
@@ -1111,6 +1121,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
     }
   };
   auto mfma6 = [&](const Frags& f, int i, int j) {
+    if constexpr ((ABL & 2) != 0) {
+      acc[i][j][0] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, f.a[0][i])[0] ^
+                                                    __builtin_bit_cast(u32x4, f.b[0][j])[0]);
+      return;
+    }
     f32x16 t = acc[i][j];
     t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[2][j], t, 0, 0, 0);
     t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[2][i], f.b[0][j], t, 0, 0, 0);
@@ -1125,11 +1140,24 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
   // split + LDS stores (its registers were loaded one tile earlier) pinned between them, so the
   // conversion VALU issues while earlier MFMAs run.  `nxt` holds tile kt + 1, `fut` receives
   // tile kt + 2; MASK zeroes k >= kend (only the last tile can be partial).
+  Frags fz;
+  if constexpr ((ABL & 8) != 0) read(fz, smem, 0);
   constexpr int NG = TI * TJ;
   auto body = [&](auto mask, int kt, const Regs& nxt, Regs& fut) {
     const char* S = smem + (kt & 1) * BUF;
-    gload(fut, kbeg + (kt + 2) * BK);
+    if constexpr ((ABL & 8) == 0) gload(fut, kbeg + (kt + 2) * BK);
     Frags f0, f1;
+    if constexpr ((ABL & 8) != 0) {          // MFMA-only ablation: no loads, split or LDS reads
+      f0 = fz;
+      f1 = fz;
+#pragma unroll
+      for (int g = 0; g < 2 * NG; ++g) {
+        if (g < NG) mfma6(f0, g / TJ, g % TJ);
+        else mfma6(f1, (g - NG) / TJ, (g - NG) % TJ);
+      }
+      __syncthreads();
+      return;
+    }
     read(f0, S, 0);
 #pragma unroll
     for (int g = 0; g < 2 * NG; ++g) {
@@ -1166,6 +1194,198 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
   for (int kt = 0; kt < nk; kt += 2) {
     step(kt, r1, r0);                 // tile kt + 1 in r1, tile kt + 2 -> r0
     if (kt + 1 < nk) step(kt + 1, r0, r1);
+  }
+  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
+                            reinterpret_cast<float*>(smem) + wave * (WM * 36));
+}
+
+// gemm_x3 as a two-group ping-pong ("x3pp").  The timing ablations of gemm_x3 (tools/gemm_sweep.py
+// x3, tuning tiles 7-11) showed its MFMAs and its other work do not overlap: M = 4096 takes
+// 518 us, 219 us of it without any MFMA and ~200 us of MFMA alone; the loads are not the
+// bound (L2-resident loads: 503 us).  Both waves of a SIMD reach the same phase together after
+// every barrier.  Here the 8 waves (4 x 2, 64 x 64 each) form two groups of one wave per SIMD,
+// G0 = waves 0-3 and G1 = waves 4-7, and each 32-k tile t is two phases split by block
+// barriers:
+//   P1(t): G0 runs tile t's 48 MFMAs from fragments already in registers; G1 reads tile t's
+//          fragments, splits its share of tile t + 1 into LDS and issues its loads for t + 2;
+//   P2(t): G1 runs tile t's MFMAs; G0 reads tile t + 1's fragments, splits its share of tile
+//          t + 2 and issues its loads for t + 3.
+// So each SIMD's MFMA pipe alternates between its two waves while the other one does the LDS /
+// VALU / load work.  LDS: the planes of tiles t and t + 1 (the same double-buffered image as
+// gemm_x3); tile t + 2's shares overwrite tile t's buffer only after both groups have read it.
+// Same split and product order as gemm_x3.
+template <int BM, int BN, bool MASK>
+__global__ __launch_bounds__(512) void gemm_x3pp(GemmArgs p) {
+  constexpr int BK = 32, WGM = 4, WGN = 2, NT = 512;
+  constexpr int WM = BM / WGM, WN = BN / WGN, TI = WM / 32, TJ = WN / 32;
+  constexpr int ASEG = BM * 4 / NT, BSEG = BN * 4 / NT, NSEG = ASEG + BSEG;
+  static_assert(TI >= 1 && TJ >= 1 && ASEG >= 1 && BSEG >= 1 && (BM * 4) % NT == 0 &&
+                (BN * 4) % NT == 0, "bad x3pp tile");
+  constexpr int PLANE = (BM + BN) * 64, BUF = 3 * PLANE;
+  constexpr int STAGE = 8 * WM * 36 * 4;
+  constexpr int SMEM = 2 * BUF > STAGE ? 2 * BUF : STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
+  const int nwg = mt_n * nt_n * p.splits;
+  const int bid = xcd_swizzle(blockIdx.x, nwg);
+  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const bool g1 = __builtin_amdgcn_readfirstlane(wave) >= 4;
+
+  const float* src[NSEG];
+  int soff[NSEG], sk[NSEG];
+#pragma unroll
+  for (int q = 0; q < NSEG; ++q) {
+    const bool isa = q < ASEG;
+    const int idx = threadIdx.x + (isa ? q : q - ASEG) * NT;
+    const int r = idx >> 2, c = idx & 3;
+    if (isa) {
+      const int gr = m0 + r < p.M ? m0 + r : 0;     // clamped rows feed outputs never stored
+      src[q] = p.A + (size_t)gr * p.lda;
+    } else {
+      const int gr = n0 + r < p.N ? n0 + r : 0;
+      src[q] = p.B + (size_t)gr * p.ldb;
+    }
+    const int row = isa ? r : BM + r;
+    soff[q] = row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
+    sk[q] = c * 8;
+  }
+  f32x4 ld[NSEG][2];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < NSEG; ++q) {
+      const int k = k0 + sk[q];
+      ld[q][0] = *reinterpret_cast<const f32x4*>(src[q] + (k < p.K ? k : 0));
+      ld[q][1] = *reinterpret_cast<const f32x4*>(src[q] + (k + 4 < p.K ? k + 4 : 0));
+    }
+  };
+  // buffer indices are compile-time (B = 0 / 1) so the LDS addresses are a few per-lane bases
+  // plus immediate offsets, not a hoisted copy per buffer
+  auto split_store = [&](auto B, int k0) {
+    char* base = smem + decltype(B)::value * BUF;
+#pragma unroll
+    for (int q = 0; q < NSEG; ++q) {
+      u32x4 o[3];
+      if constexpr (MASK) {
+        const int k = k0 + sk[q];
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        split3(k < kend ? ld[q][0] : z, k + 4 < kend ? ld[q][1] : z, o);
+      } else {
+        split3(ld[q][0], ld[q][1], o);
+      }
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        *reinterpret_cast<u32x4*>(base + pl * PLANE + soff[q]) = o[pl];
+    }
+  };
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  int aoff[TI], akey[TI], boff[TJ], bkey[TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int row = wm * WM + i * 32 + (lane & 31);
+    aoff[i] = row * 64;
+    akey[i] = (row >> 2) & 3;
+  }
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int row = BM + wn * WN + j * 32 + (lane & 31);
+    boff[j] = row * 64;
+    bkey[j] = (row >> 2) & 3;
+  }
+  const int hk = lane >> 5;
+  bf16x8 fa[2][3][TI], fb[2][3][TJ];        // both k steps of one tile
+  auto read = [&](auto B) {
+    const char* S = smem + decltype(B)::value * BUF;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 2 * s + hk;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+          fa[s][pl][i] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + aoff[i] + ((c ^ akey[i]) << 4));
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          fb[s][pl][j] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + boff[j] + ((c ^ bkey[j]) << 4));
+      }
+    }
+  };
+  auto mfma_tile = [&]() {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          f32x16 t = acc[i][j];
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][0][i], fb[s][2][j], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][2][i], fb[s][0][j], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][1][i], fb[s][1][j], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][0][i], fb[s][1][j], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][1][i], fb[s][0][j], t, 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][0][i], fb[s][0][j], t, 0, 0, 0);
+        }
+  };
+  // memory phase of a wave: its fragments of the tile in buffer RB, its share of tile wr
+  // (registers loaded one tile earlier) into buffer 1 - RB, then its loads for tile wr + 1
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  auto mem_phase = [&](auto RB, int wr) {
+    using WB = std::integral_constant<int, 1 - decltype(RB)::value>;
+    read(RB);
+    split_store(WB{}, kbeg + wr * BK);
+    gload(kbeg + (wr + 1) * BK);
+  };
+  // one tile t held in buffer E = t & 1: G0's MFMAs while G1 reads it and writes tile t + 1,
+  // then G1's MFMAs while G0 reads tile t + 1 and writes tile t + 2.  Each group runs its own
+  // copy of the loop (the same two barriers per tile), so the accumulators never merge across a
+  // role branch and stay in place.
+  auto tile_g0 = [&](auto E, int t) {
+    using NE = std::integral_constant<int, 1 - decltype(E)::value>;
+    mfma_tile();
+    __syncthreads();
+    mem_phase(NE{}, t + 2);
+    __syncthreads();
+  };
+  auto tile_g1 = [&](auto E, int t) {
+    mem_phase(E, t + 1);
+    __syncthreads();
+    mfma_tile();
+    __syncthreads();
+  };
+
+  // prologue: tile 0 complete (all shares); G0's share of tile 1 written and its loads for tile 2
+  // issued; G1's loads for tile 1 in registers; G0 holds tile 0's fragments
+  gload(kbeg);
+  split_store(B0{}, kbeg);
+  gload(kbeg + BK);
+  if (!g1) {
+    split_store(B1{}, kbeg + BK);
+    gload(kbeg + 2 * BK);
+    __syncthreads();
+    read(B0{});
+    for (int t = 0; t < nk; t += 2) {
+      tile_g0(B0{}, t);
+      if (t + 1 < nk) tile_g0(B1{}, t + 1);
+    }
+  } else {
+    __syncthreads();
+    for (int t = 0; t < nk; t += 2) {
+      tile_g1(B0{}, t);
+      if (t + 1 < nk) tile_g1(B1{}, t + 1);
+    }
   }
   tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
@@ -2149,8 +2369,10 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   int tile = env ? atoi(env) : 0;
   if (env && tile == 0) return false;
   if (!env && a.M <= 64) return false;  // tools/gemm_sweep.py x3: fp32 tiles win to M = 64 (27 vs 31 us)
-  const int bms[7] = {0, 256, 128, 128, 256, 256, 256}, bns[7] = {0, 128, 128, 64, 128, 128, 128};
-  if (tile < 1 || tile > 6) {
+  // 7..11: gemm_x3<256,128> timing ablations (ABL 1, 2, 4, 5, 3), K % 32 == 0 only
+  const int bms[14] = {0, 256, 128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
+  const int bns[14] = {0, 128, 128, 64, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
+  if (tile < 1 || tile > 13 || ((tile >= 7 && tile <= 11) || tile == 13) && a.K % 32 != 0) {
     tile = a.M > 256 ? 1 : 2;
   }
   const int bm = bms[tile], bn = bns[tile];
@@ -2181,6 +2403,16 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
       if (whole) hipLaunchKernelGGL((gemm_x3ws<256, 128, 4, 2, false>), grid, dim3(768), 0, s, a);
       else hipLaunchKernelGGL((gemm_x3ws<256, 128, 4, 2, true>), grid, dim3(768), 0, s, a);
       break;
+    case 12:
+      if (whole) hipLaunchKernelGGL((gemm_x3pp<256, 128, false>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((gemm_x3pp<256, 128, true>), grid, dim3(512), 0, s, a);
+      break;
+    case 7: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 1>), grid, dim3(512), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 2>), grid, dim3(512), 0, s, a); break;
+    case 9: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 4>), grid, dim3(512), 0, s, a); break;
+    case 10: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 5>), grid, dim3(512), 0, s, a); break;
+    case 11: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 3>), grid, dim3(512), 0, s, a); break;
+    case 13: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 8>), grid, dim3(512), 0, s, a); break;
     case 6:   // 4 consumer waves with 128 x 64 wave tiles (two waves per SIMD)
       if (whole) hipLaunchKernelGGL((gemm_x3ws<256, 128, 2, 2, false>), grid, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((gemm_x3ws<256, 128, 2, 2, true>), grid, dim3(512), 0, s, a);
