@@ -43,6 +43,9 @@ struct GemmArgs {
                 // so whole float4 rows can leave through epilogue_store4
   int ablate;   // timing experiments only (AZ_GEMM_ABLATE, glds2): 1 = no DMA after the first
                 // tile, 2 = no barrier in the k loop; results are then wrong
+  // gemm_x3 with A already split (x3_split_kernel): three bf16 planes [3][M][K] at apl
+  const unsigned short* apl;
+  size_t apl_plane;   // elements per plane (M * K)
 };
 
 __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int col, float acc) {
@@ -1010,8 +1013,11 @@ __device__ __forceinline__ void split3(const f32x4& x0, const f32x4& x1, u32x4 (
 
 // ABL (tuning build only, timing ablations whose results are wrong by design): 1 = every tile's
 // loads from the split's first four tiles (L2-resident), 2 = no MFMA, 4 = no split (raw bits)
-template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0>
+// APL: A comes as three bf16 planes split once by x3_split_kernel (p.apl, row stride K, K % 32
+// == 0): the tile copies them into the LDS image without any VALU, only W is split here.
+template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
+  static_assert(!APL || !MASK, "pre-split A needs whole 32-k tiles");
   constexpr int BK = 32;
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -1053,33 +1059,54 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
     soff[q] = row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
     sk[q] = c * 8;
   }
-  using Regs = f32x4[NSEG][2];
+  struct Regs {
+    f32x4 f[NSEG][2];                 // fp32 segments (A's only when !APL)
+    u32x4 pa[APL ? ASEG : 1][3];      // A's three bf16 planes when APL
+  };
   // every load is unconditional (k clamped in bounds); k >= kend is zeroed at the split
   auto gload = [&](Regs& ld, int k0) {
     if constexpr ((ABL & 1) != 0) k0 = kbeg + (k0 - kbeg) % (4 * BK);
 #pragma unroll
     for (int q = 0; q < NSEG; ++q) {
       const int k = k0 + sk[q];
-      ld[q][0] = *reinterpret_cast<const f32x4*>(src[q] + (k < p.K ? k : 0));
-      ld[q][1] = *reinterpret_cast<const f32x4*>(src[q] + (k + 4 < p.K ? k + 4 : 0));
+      if constexpr (APL) {
+        if (q < ASEG) {
+          const int r = (threadIdx.x + q * NT) >> 2;
+          const size_t off = (size_t)min(m0 + r, p.M - 1) * p.K + (k < p.K ? k : 0);
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            ld.pa[q][pl] = *reinterpret_cast<const u32x4*>(p.apl + pl * p.apl_plane + off);
+          continue;
+        }
+      }
+      ld.f[q][0] = *reinterpret_cast<const f32x4*>(src[q] + (k < p.K ? k : 0));
+      ld.f[q][1] = *reinterpret_cast<const f32x4*>(src[q] + (k + 4 < p.K ? k + 4 : 0));
     }
   };
   auto split_store = [&](const Regs& ld, int buf, int k0, int q, auto mask) {
     char* base = smem + buf * BUF;
     u32x4 o[3];
+    if constexpr (APL) {
+      if (q < ASEG) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          *reinterpret_cast<u32x4*>(base + pl * PLANE + soff[q]) = ld.pa[q][pl];
+        return;
+      }
+    }
     if constexpr (decltype(mask)::value) {
       const int k = k0 + sk[q];
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      split3(k < kend ? ld[q][0] : z, k + 4 < kend ? ld[q][1] : z, o);
+      split3(k < kend ? ld.f[q][0] : z, k + 4 < kend ? ld.f[q][1] : z, o);
     } else if constexpr ((ABL & 4) != 0) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        o[0][e] = __float_as_uint(ld[q][0][e]);
-        o[1][e] = __float_as_uint(ld[q][1][e]);
+        o[0][e] = __float_as_uint(ld.f[q][0][e]);
+        o[1][e] = __float_as_uint(ld.f[q][1][e]);
         o[2][e] = o[0][e];
       }
     } else {
-      split3(ld[q][0], ld[q][1], o);
+      split3(ld.f[q][0], ld.f[q][1], o);
     }
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(base + pl * PLANE + soff[q]) = o[pl];
@@ -1561,6 +1588,24 @@ __global__ __launch_bounds__(64 * (WGM * WGN + 4)) void gemm_x3ws(GemmArgs p) {
   }
   tile_epilogue<32, TI, TJ, true>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                                   reinterpret_cast<float*>(smem) + wave * (WM * 36));
+}
+
+// A [M][K] (row stride lda) -> three bf16 planes [3][M][K] (plane stride `plane` elements), the
+// same split3 as gemm_x3's in-tile split, so a GEMM on the planes gives the same bits; one 8-k
+// segment per thread (K % 8 == 0)
+__global__ __launch_bounds__(256) void x3_split_kernel(const float* __restrict__ A, int lda, int M,
+                                                       int K, unsigned short* __restrict__ out,
+                                                       size_t plane) {
+  const long idx = blockIdx.x * 256L + threadIdx.x;
+  const int segs = K >> 3;
+  if (idx >= (long)M * segs) return;
+  const int r = (int)(idx / segs), c = (int)(idx % segs);
+  const float* s = A + (size_t)r * lda + c * 8;
+  u32x4 o[3];
+  split3(*reinterpret_cast<const f32x4*>(s), *reinterpret_cast<const f32x4*>(s + 4), o);
+  unsigned short* d = out + (size_t)r * K + c * 8;
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(d + pl * plane) = o[pl];
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
@@ -2363,6 +2408,7 @@ static int splits_256x128(int M, int N, int K, size_t ws_bytes) {
 // MI355X, tools/gemm_sweep.py x3: M = 512 75 us vs 103 us for the fp32 MFMA tile, M = 800 147 vs
 // 185, M = 4096 516 vs 767).  Tuning build: AZ_GEMM_X3=0 keeps the fp32 MFMA tiles, 1..4 forces
 // a tile, AZ_GEMM_SPLITS the split.  Sets a.splits / a.kc; false = not launched.
+constexpr bool kX3PresplitA = false;   // product default: decided by tools/gemm_sweep.py x3
 static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   static const char* env = tuning_env("AZ_GEMM_X3");
   static const char* env_split = tuning_env("AZ_GEMM_SPLITS");
@@ -2389,6 +2435,23 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   if (S > 1) a.splits = (a.K + a.kc - 1) / a.kc;
   const dim3 grid((unsigned)(tiles * a.splits));
   const bool whole = a.K % 32 == 0;   // kc is a multiple of 32 too: no partial k tile anywhere
+  // A split once into bf16 planes (x3_split_kernel) in the workspace after the slabs, when it
+  // fits, for the 256 x 128 tile (tuning: AZ_GEMM_X3APL=0/1)
+  static const char* env_apl = tuning_env("AZ_GEMM_X3APL");
+  const bool want_apl = env_apl ? atoi(env_apl) != 0 : kX3PresplitA;
+  const size_t slab_bytes = a.splits > 1 ? ((size_t)a.splits * a.M * a.N * 4 + 255) / 256 * 256 : 0;
+  const size_t apl_bytes = (size_t)3 * a.M * a.K * 2;
+  if (want_apl && tile == 1 && whole && a.lda % 4 == 0 && a.slab &&
+      slab_bytes + apl_bytes <= ws_bytes) {
+    unsigned short* pl = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(a.slab) + slab_bytes);
+    const long segs = (long)a.M * (a.K / 8);
+    hipLaunchKernelGGL(x3_split_kernel, dim3((unsigned)((segs + 255) / 256)), dim3(256), 0, s,
+                       a.A, a.lda, a.M, a.K, pl, (size_t)a.M * a.K);
+    a.apl = pl;
+    a.apl_plane = (size_t)a.M * a.K;
+    hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 0, true>), grid, dim3(512), 0, s, a);
+    return true;
+  }
 #define AZ_X3(BM_, BN_, WM_, WN_)                                                              \
   if (whole) hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, false>), grid, dim3(64 * WM_ * WN_), \
                                 0, s, a);                                                      \
