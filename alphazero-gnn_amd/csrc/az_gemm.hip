@@ -1590,6 +1590,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + 4)) void gemm_x3ws(GemmArgs p) {
                                   reinterpret_cast<float*>(smem) + wave * (WM * 36));
 }
 
+#ifdef AZ_TUNING   // gemm_x3 APL experiment only
 // A [M][K] (row stride lda) -> three bf16 planes [3][M][K] (plane stride `plane` elements), the
 // same split3 as gemm_x3's in-tile split, so a GEMM on the planes gives the same bits; one 8-k
 // segment per thread (K % 8 == 0)
@@ -1607,6 +1608,7 @@ __global__ __launch_bounds__(256) void x3_split_kernel(const float* __restrict__
 #pragma unroll
   for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(d + pl * plane) = o[pl];
 }
+#endif
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
   const long total = (long)p.M * p.N;
@@ -2408,7 +2410,6 @@ static int splits_256x128(int M, int N, int K, size_t ws_bytes) {
 // MI355X, tools/gemm_sweep.py x3: M = 512 75 us vs 103 us for the fp32 MFMA tile, M = 800 147 vs
 // 185, M = 4096 516 vs 767).  Tuning build: AZ_GEMM_X3=0 keeps the fp32 MFMA tiles, 1..4 forces
 // a tile, AZ_GEMM_SPLITS the split.  Sets a.splits / a.kc; false = not launched.
-constexpr bool kX3PresplitA = false;   // product default: decided by tools/gemm_sweep.py x3
 static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   static const char* env = tuning_env("AZ_GEMM_X3");
   static const char* env_split = tuning_env("AZ_GEMM_SPLITS");
@@ -2435,10 +2436,12 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   if (S > 1) a.splits = (a.K + a.kc - 1) / a.kc;
   const dim3 grid((unsigned)(tiles * a.splits));
   const bool whole = a.K % 32 == 0;   // kc is a multiple of 32 too: no partial k tile anywhere
-  // A split once into bf16 planes (x3_split_kernel) in the workspace after the slabs, when it
-  // fits, for the 256 x 128 tile (tuning: AZ_GEMM_X3APL=0/1)
+#ifdef AZ_TUNING
+  // A split once into bf16 planes (x3_split_kernel) in the workspace after the slabs, only W
+  // split in the tile (AZ_GEMM_X3APL=1): measured slower -- M = 512 82.8 vs 75.0 us incl. the
+  // split launch, M = 4096 557 vs 514 (1.5x the A bytes through L2, no clock gain)
   static const char* env_apl = tuning_env("AZ_GEMM_X3APL");
-  const bool want_apl = env_apl ? atoi(env_apl) != 0 : kX3PresplitA;
+  const bool want_apl = env_apl && atoi(env_apl) != 0;
   const size_t slab_bytes = a.splits > 1 ? ((size_t)a.splits * a.M * a.N * 4 + 255) / 256 * 256 : 0;
   const size_t apl_bytes = (size_t)3 * a.M * a.K * 2;
   if (want_apl && tile == 1 && whole && a.lda % 4 == 0 && a.slab &&
@@ -2452,6 +2455,7 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
     hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 0, true>), grid, dim3(512), 0, s, a);
     return true;
   }
+#endif
 #define AZ_X3(BM_, BN_, WM_, WN_)                                                              \
   if (whole) hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, false>), grid, dim3(64 * WM_ * WN_), \
                                 0, s, a);                                                      \
