@@ -1015,13 +1015,18 @@ __device__ __forceinline__ void split3(const f32x4& x0, const f32x4& x1, u32x4 (
 // loads from the split's first four tiles (L2-resident), 2 = no MFMA, 4 = no split (raw bits)
 // APL: A comes as three bf16 planes split once by x3_split_kernel (p.apl, row stride K, K % 32
 // == 0): the tile copies them into the LDS image without any VALU, only W is split here.
-template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false>
+// MF = 16 (tuning build): v_mfma_f32_16x16x32_bf16 blocks, one k step per 32-k tile (lane l
+// holds row l & 15, k chunk l >> 4), against two 32x32x16 steps for MF = 32.
+template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false, int MF = 32>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
   static_assert(!APL || !MASK, "pre-split A needs whole 32-k tiles");
   constexpr int BK = 32;
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
   constexpr int WM = BM / WGM, WN = BN / WGN;
-  constexpr int TI = WM / 32, TJ = WN / 32;
+  constexpr int TI = WM / MF, TJ = WN / MF;
+  constexpr int NSTEP = MF == 32 ? 2 : 1;
+  using acc_t = typename std::conditional<MF == 32, f32x16, f32x4>::type;
+  constexpr int NACC = MF == 32 ? 16 : 4;
   constexpr int ASEG = BM * 4 / NT, BSEG = BN * 4 / NT, NSEG = ASEG + BSEG;
   static_assert(TI >= 1 && TJ >= 1 && ASEG >= 1 && BSEG >= 1 && (BM * 4) % NT == 0 &&
                 (BN * 4) % NT == 0, "bad x3 tile");
@@ -1112,31 +1117,31 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
     for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(base + pl * PLANE + soff[q]) = o[pl];
   };
 
-  f32x16 acc[TI][TJ];
+  acc_t acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < NACC; ++r) acc[i][j][r] = 0.f;
 
   int aoff[TI], akey[TI], boff[TJ], bkey[TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
-    const int row = wm * WM + i * 32 + (lane & 31);
+    const int row = wm * WM + i * MF + (lane & (MF - 1));
     aoff[i] = row * 64;
     akey[i] = (row >> 2) & 3;
   }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    const int row = BM + wn * WN + j * 32 + (lane & 31);
+    const int row = BM + wn * WN + j * MF + (lane & (MF - 1));
     boff[j] = row * 64;
     bkey[j] = (row >> 2) & 3;
   }
-  const int hk = lane >> 5;
+  const int hk = MF == 32 ? lane >> 5 : lane >> 4;
   struct Frags { bf16x8 a[3][TI], b[3][TJ]; };
   auto read = [&](Frags& f, const char* S, int s) {
-    const int c = 2 * s + hk;
+    const int c = MF == 32 ? 2 * s + hk : hk;
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
@@ -1153,13 +1158,22 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
                                                     __builtin_bit_cast(u32x4, f.b[0][j])[0]);
       return;
     }
-    f32x16 t = acc[i][j];
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[2][j], t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[2][i], f.b[0][j], t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[1][j], t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[1][j], t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[0][j], t, 0, 0, 0);
-    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[0][j], t, 0, 0, 0);
+    acc_t t = acc[i][j];
+    if constexpr (MF == 32) {
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[2][j], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[2][i], f.b[0][j], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[1][j], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[1][j], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[0][j], t, 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[0][j], t, 0, 0, 0);
+    } else {
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[0][i], f.b[2][j], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[2][i], f.b[0][j], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[1][i], f.b[1][j], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[0][i], f.b[1][j], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[1][i], f.b[0][j], t, 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[0][i], f.b[0][j], t, 0, 0, 0);
+    }
   };
 
   // One 32-k tile: tile kt + 2's global loads first, step 0's fragments and its first MFMA
@@ -1178,7 +1192,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
       f0 = fz;
       f1 = fz;
 #pragma unroll
-      for (int g = 0; g < 2 * NG; ++g) {
+      for (int g = 0; g < NSTEP * NG; ++g) {
         if (g < NG) mfma6(f0, g / TJ, g % TJ);
         else mfma6(f1, (g - NG) / TJ, (g - NG) % TJ);
       }
@@ -1187,17 +1201,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
     }
     read(f0, S, 0);
 #pragma unroll
-    for (int g = 0; g < 2 * NG; ++g) {
+    for (int g = 0; g < NSTEP * NG; ++g) {
       if (g < NG) mfma6(f0, g / TJ, g % TJ);
       else mfma6(f1, (g - NG) / TJ, (g - NG) % TJ);
-      if (g == 0) {
+      if (g == 0 && NSTEP == 2) {
         __builtin_amdgcn_sched_barrier(0);
         read(f1, S, 1);
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int q = 0; q < NSEG; ++q)
-        if (q * 2 * NG / NSEG == g) {
+        if (q * NSTEP * NG / NSEG == g) {
           __builtin_amdgcn_sched_barrier(0);
           split_store(nxt, (kt + 1) & 1, kbeg + (kt + 1) * BK, q, mask);
           __builtin_amdgcn_sched_barrier(0);
@@ -1222,7 +1236,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
     step(kt, r1, r0);                 // tile kt + 1 in r1, tile kt + 2 -> r0
     if (kt + 1 < nk) step(kt + 1, r0, r1);
   }
-  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
+  tile_epilogue<MF, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
 }
 
@@ -2417,9 +2431,9 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   if (env && tile == 0) return false;
   if (!env && a.M <= 64) return false;  // tools/gemm_sweep.py x3: fp32 tiles win to M = 64 (27 vs 31 us)
   // 7..11: gemm_x3<256,128> timing ablations (ABL 1, 2, 4, 5, 3), K % 32 == 0 only
-  const int bms[14] = {0, 256, 128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
-  const int bns[14] = {0, 128, 128, 64, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
-  if (tile < 1 || tile > 13 || ((tile >= 7 && tile <= 11) || tile == 13) && a.K % 32 != 0) {
+  const int bms[15] = {0, 256, 128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
+  const int bns[15] = {0, 128, 128, 64, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
+  if (tile < 1 || tile > 14 || ((tile >= 7 && tile <= 11) || tile == 13) && a.K % 32 != 0) {
     tile = a.M > 256 ? 1 : 2;
   }
   const int bm = bms[tile], bn = bns[tile];
@@ -2480,6 +2494,10 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
     case 10: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 5>), grid, dim3(512), 0, s, a); break;
     case 11: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 3>), grid, dim3(512), 0, s, a); break;
     case 13: hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 8>), grid, dim3(512), 0, s, a); break;
+    case 14:   // 16x16x32 MFMA blocks
+      if (whole) hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 0, false, 16>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, true, 0, false, 16>), grid, dim3(512), 0, s, a);
+      break;
     case 6:   // 4 consumer waves with 128 x 64 wave tiles (two waves per SIMD)
       if (whole) hipLaunchKernelGGL((gemm_x3ws<256, 128, 2, 2, false>), grid, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((gemm_x3ws<256, 128, 2, 2, true>), grid, dim3(512), 0, s, a);
