@@ -51,8 +51,8 @@ def parse():
     ap.add_argument("--no-b1", action="store_true", help="skip the as-called batch-1 leg")
     ap.add_argument("--large-batch", type=int, default=65536,
                     help="extra leg at this batch (SURVEY §8d config 2); 0 = skip")
-    ap.add_argument("--sp-games", type=int, default=2048,
-                    help="self-play leg: games per GPU, all played in lock step")
+    ap.add_argument("--sp-games", type=int, default=4096,
+                    help="self-play leg: games per GPU, all played in lock step (4096: 'tools/sp_sweep.py' r02s, 779 vs 702 games/s for 2048 with the x3 GEMMs)")
     ap.add_argument("--sp-sims", type=int, default=100, help="numMCTSSims (SURVEY §8d config 3)")
     ap.add_argument("--sp-threads", type=int, default=16, help="host threads for the engine")
     ap.add_argument("--sp-lanes", type=int, default=2,
