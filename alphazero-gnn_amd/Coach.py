@@ -20,6 +20,31 @@ from azhip import dist as D
 log = logging.getLogger(__name__)
 
 
+class ExamplesUnpickler(Unpickler):
+    """Loads a `.examples` history (Coach.py:187-201: a list of deques of example tuples of numpy
+    arrays, floats and ints) and nothing else.  Only the globals such a file needs resolve --
+    numpy array / dtype / scalar reconstruction and collections.deque -- so a file that names
+    any other callable raises pickle.UnpicklingError instead of running it."""
+
+    _ALLOWED = {
+        ("collections", "deque"),
+        ("numpy", "ndarray"), ("numpy", "dtype"),
+        ("numpy.core.multiarray", "_reconstruct"), ("numpy.core.multiarray", "scalar"),
+        ("numpy._core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "scalar"),
+        ("builtins", "list"), ("builtins", "tuple"), ("builtins", "dict"), ("builtins", "set"),
+        ("builtins", "frozenset"), ("builtins", "int"), ("builtins", "float"),
+        ("builtins", "bool"), ("builtins", "str"), ("builtins", "bytes"),
+    }
+
+    def find_class(self, module, name):
+        if (module, name) in self._ALLOWED or \
+                (module == "numpy.dtypes" and name.endswith("DType")):
+            return super().find_class(module, name)
+        import pickle
+        raise pickle.UnpicklingError(f".examples file names {module}.{name}: not an example "
+                                     "history (only numpy arrays, scalars and deques load)")
+
+
 def _flag(args, name, default=False):
     try:
         return args[name] if isinstance(args, dict) else getattr(args, name)
@@ -234,6 +259,6 @@ class Coach:
         else:
             log.info("File with trainExamples found. Loading it...")
             with open(examplesFile, "rb") as f:
-                self.trainExamplesHistory = Unpickler(f).load()
+                self.trainExamplesHistory = ExamplesUnpickler(f).load()
             log.info("Loading done!")
             self.skipFirstSelfPlay = True

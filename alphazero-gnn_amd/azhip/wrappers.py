@@ -40,25 +40,42 @@ class PendingPrediction:
 
 class _PendingDirect:
     """A batched Connect4 prediction queued by _DirectBatch: the kernels write pi / v straight
-    into mapped host memory; result() waits for the event and copies them out."""
+    into mapped host memory; result() waits for the event and copies them out.
+
+    The ring entry is owned through a token: only the prediction that took the entry may hand
+    it back.  (A stale prediction object -- read long ago, dropped only when its variable is
+    rebound -- must not free an entry a LATER prediction now holds: the next launch would then
+    take the same host buffers and overwrite that prediction's outputs, which is what two
+    self-play lanes did before the token.)  result() may be called more than once."""
+
+    _tokens = iter(range(1, 1 << 62))
 
     def __init__(self, entry, views, event, n):
         # entry: the ring entry (its HostBuffer stays alive and reserved until result())
         self.entry, self.views, self.event, self.n = entry, views, event, n
+        self.token = next(self._tokens)
+        self.out = None
         entry["busy"] = True
+        entry["owner"] = self.token
+
+    def _release(self):
+        if self.entry.get("owner") == self.token:
+            self.entry["owner"] = None
+            self.entry["busy"] = False
 
     def result(self):
-        self.event.synchronize()
-        n = self.n
-        pi, v, gpi, gv = (None if a is None else a.numpy()[:n].copy() for a in self.views)
-        self.entry["busy"] = False
-        return pi, v, gpi, gv
+        if self.out is None:
+            self.event.synchronize()
+            n = self.n
+            self.out = tuple(None if a is None else a.numpy()[:n].copy() for a in self.views)
+            self._release()
+        return self.out
 
     def __del__(self):
         # dropped unread: the entry is free again once the device is done with it
-        if self.entry.get("busy"):
+        if self.entry.get("owner") == self.token:
             self.event.synchronize()
-            self.entry["busy"] = False
+            self._release()
 
 
 class _DirectBatch:

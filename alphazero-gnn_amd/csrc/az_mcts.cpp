@@ -1037,6 +1037,14 @@ int az_mcts_remaining(const az_mcts* m, int slot) {
   return m->trees[slot].remaining;
 }
 
+int az_mcts_abandon(az_mcts* m, int slot) {
+  if (!slot_ok(m, slot)) return fail(AZM_EINVAL, "az_mcts_abandon: bad slot");
+  Tree& t = m->trees[slot];
+  if (t.pending_leaf >= 0) return fail(AZM_ESTATE, "az_mcts_abandon: a leaf waits for its feed");
+  t.remaining = 0;
+  return AZM_OK;
+}
+
 int az_mcts_remaining_all(const az_mcts* m, int32_t* out) {
   if (!m || !out) return fail(AZM_EINVAL, "az_mcts_remaining_all: bad args");
   for (size_t s = 0; s < m->trees.size(); ++s) out[s] = m->trees[s].remaining;

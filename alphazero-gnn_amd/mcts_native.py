@@ -41,6 +41,7 @@ _SIGS = {
     "az_mcts_clear_predictions": (ctypes.c_int, [_P, ctypes.c_int]),
     "az_mcts_begin": (ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.c_int]),
     "az_mcts_remaining": (ctypes.c_int, [_P, ctypes.c_int]),
+    "az_mcts_abandon": (ctypes.c_int, [_P, ctypes.c_int]),
     "az_mcts_remaining_all": (ctypes.c_int, [_P, _P]),
     "az_mcts_collect": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, ctypes.c_int]),
     "az_mcts_feed": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int]),
@@ -176,6 +177,9 @@ class Engine:
 
     def remaining(self, slot):
         return _check(lib().az_mcts_remaining(self.h, slot), "az_mcts_remaining")
+
+    def abandon(self, slot):
+        _check(lib().az_mcts_abandon(self.h, slot), "az_mcts_abandon")
 
     def remaining_all(self):
         """int32 [slots] view (overwritten by the next call)."""
@@ -532,6 +536,13 @@ class ArenaPlayer:
 
     def _search(self, board, sims):
         self.eng.begin(0, board, sims)
+        try:
+            self._search_loop()
+        except BaseException:
+            self.eng.abandon(0)     # a raise mid-search (AZ_STRICT_NN) leaves the slot reusable
+            raise
+
+    def _search_loop(self):
         if self.spec:
             self._search_spec()
             return
@@ -549,8 +560,8 @@ class ArenaPlayer:
             try:
                 pi, v, gpi, gv = _net_call(self.nnet, self.eng.leaf_boards[:k], self.use_gnn)
             except Exception as ex:  # MCTS.py:195-200: uniform priors, value 0 (counted)
-                nn_fallback.record("ArenaPlayer", ex, k)
-                self.eng.feed(k, failed=True)
+                self.eng.feed(k, failed=True)      # engine first: left consistent if
+                nn_fallback.record("ArenaPlayer", ex, k)   # AZ_STRICT_NN raises here
                 continue
             self.eng.feed(k, pi, v, gpi, gv)
 
@@ -570,8 +581,8 @@ class ArenaPlayer:
             try:
                 out = _net_call(self.nnet, batch[:k], self.use_gnn)
             except Exception as ex:  # MCTS.py:195-200 for the leaf (counted), no rows kept
-                nn_fallback.record("ArenaPlayer", ex, 1)
                 eng.feed_spec(k, failed=True)
+                nn_fallback.record("ArenaPlayer", ex, 1)
                 continue
             eng.feed_spec(k, *out)
 

@@ -247,9 +247,9 @@ class _Lane:
             if k:
                 if err is None:
                     self.eng.feed(k, pi, v, gpi, gv)
-                else:
-                    nn_fallback.record("selfplay.native", err, k)
+                else:    # the engine first (so it is left consistent), then the count
                     self.eng.feed(k, failed=True)
+                    nn_fallback.record("selfplay.native", err, k)
             for i, (slot, _) in enumerate(self.pred):
                 if err is None:
                     self._resume(slot, (pi[k + i], v[k + i]))
@@ -374,7 +374,13 @@ class _EpisodeLane:
                 aborted = self.eng.feed(self.k, failed=True)
                 if aborted:
                     # an expand_tree root predict was in the batch: unguarded in the reference
-                    # (MCTS.py:108-113), so the failure propagates out of the episode
+                    # (MCTS.py:108-113), so the failure propagates out of the episode -- after
+                    # counting the batch's other leaves, which the same feed degraded
+                    if self.k > 1:
+                        try:
+                            nn_fallback.record("selfplay.engine", err, self.k - 1)
+                        except Exception:     # AZ_STRICT_NN: the original error wins
+                            pass
                     raise err
                 nn_fallback.record("selfplay.engine", err, self.k)
             else:                     # engine errors (shapes, state) propagate as themselves

@@ -55,6 +55,9 @@ def parse():
                     help="self-play leg: games per GPU, all played in lock step (4096: 'tools/sp_sweep.py' r02s, 779 vs 702 games/s for 2048 with the x3 GEMMs)")
     ap.add_argument("--sp-sims", type=int, default=100, help="numMCTSSims (SURVEY §8d config 3)")
     ap.add_argument("--sp-threads", type=int, default=16, help="host threads for the engine")
+    ap.add_argument("--sp-check", type=int, default=4,
+                    help="self-play leg: episodes of the timed run compared afterwards with the "
+                         "sequential reference loop (rank 0; 'agreement')")
     ap.add_argument("--sp-lanes", type=int, default=2,
                     help="engines taking turns so host search overlaps the GPU batch")
     return ap.parse_args()
@@ -288,7 +291,8 @@ def layer_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True)
            "bound": "mfma", "achieved": round(c["fused_tflops"], 2),
            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
            "frac": round(c["fused_tflops"] / FP32_MFMA_PEAK_TFLOPS, 4),
-           "traffic": pmc_traffic("gnn_layer_fused"), "avg_launch_us": round(c["fused_us"], 2),
+           "traffic": pmc_traffic("gnn_layer_fused"), "traffic_run": pmc_run("gnn_layer_fused"),
+           "avg_launch_us": round(c["fused_us"], 2),
            "flop_per_launch": c["fused_flop"], "algorithmic_bytes": c["fused_bytes"],
            "hbm_gbs_algorithmic": round(c["fused_gbs"], 1),
            "workload": f"{graphs} 32x32 grids, V={c['V']}, E={c['E']}, F=64, H=128 (config-5 "
@@ -303,7 +307,8 @@ def layer_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True)
                                  "frac": round(2 * c["V"] * 128 * 64 / c["proj_us"] / 1e6
                                                / FP32_MFMA_PEAK_TFLOPS, 4),
                                  "hbm_gbs_algorithmic": round(c["proj_gbs"], 1),
-                                 "traffic": pmc_traffic("gnn_source_proj")},
+                                 "traffic": pmc_traffic("gnn_source_proj"),
+                                 "traffic_run": pmc_run("gnn_source_proj")},
            "layer_us": round(c["fused_us"] + c["proj_us"], 2)}
     del flush
     if extra:
@@ -407,14 +412,54 @@ def large_batch_leg(torch, ops, ev, device, B=65536, reps=5):
     torch.cuda.synchronize()
     ms = e[0].elapsed_time(e[1]) / reps
     gemm_ms = e[1].elapsed_time(e[2]) / reps
-    tflops = 2.0 * B * F * F / (gemm_ms * 1e-3) / 1e12
     del x, hid, boards
     torch.cuda.empty_cache()
     return {"batch": B, "ms_per_batch": round(ms, 3), "boards_per_s": round(B / (ms * 1e-3), 1),
-            "gemm": {"kernel": "az_gemm_f32 output_transform.0 at M = %d" % B,
-                     "ms": round(gemm_ms, 3), "achieved": round(tflops, 2),
-                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(tflops / FP32_MFMA_PEAK_TFLOPS, 4)}}
+            "gemm": x3_roofline("az_gemm_f32 output_transform.0 at M = %d" % B,
+                                2.0 * B * F * F, gemm_ms * 1e-3)}
+
+
+def x3_roofline(kernel, flop, seconds, traffic=None, traffic_run=None):
+    """Roofline of a gemm_x3 call: it runs every fp32 product as 6 bf16 MFMA products, so the
+    pipe it is bound by is the bf16 one -- achieved = 6 x 2MNK / time against the dense bf16
+    MFMA peak (frac <= 1 by construction).  The fp32-equivalent rate (2MNK / time, whose
+    ceiling on this pipe is x3_peak = bf16 peak / 6) is kept beside it."""
+    fp32_eq = flop / seconds / 1e12
+    return {"kernel": kernel, "bound": "mfma", "pipe": "bf16 (v_mfma_f32_32x32x16_bf16)",
+            "achieved": round(6 * fp32_eq, 2), "peak": BF16_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(6 * fp32_eq / BF16_MFMA_PEAK_TFLOPS, 4),
+            "traffic": traffic, "traffic_run": traffic_run,
+            "avg_launch_us": round(seconds * 1e6, 2), "flop_per_launch_fp32": flop, "bf16_flop_per_launch": 6 * flop,
+            "fp32_equiv_tflops": round(fp32_eq, 2), "x3_peak_fp32_equiv": X3_PEAK_TFLOPS,
+            "frac_of_fp32_mfma_peak": round(fp32_eq / FP32_MFMA_PEAK_TFLOPS, 4)}
+
+
+def gemm_shapes_leg(torch, ops, ev, device, Ms=(800, 1576), reps=20):
+    """output_transform.0 (one az_gemm_f32 call, Linear 3136x3136 + ReLU) at the self-play
+    leg's batch sizes: 4096 lock-step games on 2 lanes put ~1,576 rows into each predict_both,
+    the tail of a run ~800 (HIP events around each call, on the launch stream)."""
+    Gn = ev.gnn.params
+    out = []
+    for M in Ms:
+        x = torch.empty((M, F), device=device).uniform_(0, 1)
+        y = torch.empty((M, F), device=device)
+        for _ in range(3):
+            ops.linear(x, Gn["output_transform.0.weight"], Gn["output_transform.0.bias"],
+                       act=ops.ACT_RELU, out=y)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+        for i in range(reps):
+            e[2 * i].record()
+            ops.linear(x, Gn["output_transform.0.weight"], Gn["output_transform.0.bias"],
+                       act=ops.ACT_RELU, out=y)
+            e[2 * i + 1].record()
+        torch.cuda.synchronize()
+        us = float(np.mean([e[2 * i].elapsed_time(e[2 * i + 1]) for i in range(reps)])) * 1e3
+        r = x3_roofline("az_gemm_f32 output_transform.0 at M = %d" % M, 2.0 * M * F * F,
+                        us * 1e-6)
+        out.append({"M": M, "avg_call_us": r["avg_launch_us"], "frac": r["frac"],
+                    "fp32_equiv_tflops": r["fp32_equiv_tflops"]})
+        del x, y
+    return out
 
 
 def selfplay_args(sims):
@@ -451,10 +496,42 @@ def selfplay_leg(W, G, args, device, rank):
     if failures:     # degraded play (uniform priors, v = 0) is not a throughput to report
         raise RuntimeError(f"self-play leg: {failures} network fallbacks {nn_fallback.counts()}")
     moves = sum(len(std) // 2 for std, _ in out.values())
+    agreement = selfplay_agreement(net, sa, out, eps[:args.sp_check] if rank == 0 else [], seeds)
     return dt, {"games": len(out), "moves": moves, "evals": st["rows"], "rounds": st["rounds"],
-                "nn_failures": failures,
+                "nn_failures": failures, "agreement": agreement,
                 "net_wait_s": round(st["net_s"], 3), "host_s": round(st["host_s"], 3),
                 "assemble_s": round(st.get("assemble_s", 0.0), 3)}
+
+
+def selfplay_agreement(net, sa, out, sample, seeds):
+    """Move agreement of a sample of the timed run's own lock-step episodes with the reference's
+    sequential loop (Coach.executeEpisode after np.random.seed(seed), batch-1 predict /
+    predict_with_gnn through the same HIP network), untimed: per episode, the moves whose
+    (board, visit-count pi) match before the first divergence.  A lock-step row rides in a batch
+    of ~1,500 and is within 1e-5 of the batch-1 row, not bit-equal, so an episode can leave the
+    sequential one at a UCB near tie (tests/test_gpu_selfplay.py proves every such divergence is
+    one, at this batch size)."""
+    import Coach as C
+    import MCTS as M
+    from connect4.Connect4Game import Connect4Game
+    game = Connect4Game(7)
+    per = []
+    for e in sample:
+        coach = C.Coach.__new__(C.Coach)
+        coach.game, coach.args, coach.nnet = game, sa, net
+        np.random.seed(seeds[e])
+        coach.mcts = M.MCTS(game, net, sa)
+        std, _ = coach.executeEpisode()
+        a = [(np.asarray(b).tolist(), [float(x) for x in p]) for b, p, _ in std]
+        b = [(np.asarray(b).tolist(), [float(x) for x in p]) for b, p, _ in out[e][0]]
+        n = min(len(a), len(b))
+        k = next((i for i in range(n) if a[i] != b[i]), n)
+        per.append({"episode": e, "moves": len(a) // 2, "agreeing_moves": k // 2,
+                    "identical": a == b})
+    moves = sum(p["moves"] for p in per)
+    return {"episodes": len(per), "move_agreement": round(sum(p["agreeing_moves"] for p in per)
+                                                          / max(1, moves), 4),
+            "episodes_identical": sum(p["identical"] for p in per), "per_episode": per}
 
 
 def train_leg(W, G, device):
@@ -580,6 +657,15 @@ def pmc_traffic(key):
         return None
 
 
+def pmc_run(key):
+    """The run tag (profiles/<tag>_*) whose PMC pass measured pmc_traffic(key)."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc.json")))
+        return d[key].get("tag", d.get("tag"))
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     args = parse()
     import torch
@@ -658,7 +744,6 @@ def main():
     gemm_ms = [e[0].elapsed_time(e[1]) for e in evs]       # output_transform.0: one az_gemm_f32
     avg_gemm_s = float(np.mean(gemm_ms)) * 1e-3
     flop = 2.0 * B * F * F
-    achieved = flop / avg_gemm_s / 1e12
 
     agg = layer = None
     if not args.no_aggregate:
@@ -690,9 +775,11 @@ def main():
     if args.large_batch > 0:
         large = large_batch_leg(torch, ops, ev, device, B=args.large_batch)
 
+    shapes = gemm_shapes_leg(torch, ops, ev, device)
     traffic = pmc_traffic("gemm")
     if agg is not None:
         agg["traffic"] = pmc_traffic("aggregate")
+        agg["traffic_run"] = pmc_run("aggregate")
 
     sp = None
     if not args.no_selfplay:
@@ -749,19 +836,11 @@ def main():
                                    "-> heads, batch of random boards per GPU",
                        "global_batch": B * world, "batch_per_gpu": B, "feature_dim": F,
                        "parallelism": f"dp{world} (independent shards, no collective)"},
-            "roofline": {"kernel": "az_gemm_f32 output_transform.0 (gemm_x3<256,128,4,2> split-K 5 "
-                                   "+ splitk_reduce4_kernel<5>), Linear 3136x3136: fp32 operands "
-                                   "split into 3 bf16 terms, 6 cross products on the bf16 MFMA",
-                         "bound": "mfma", "achieved": round(achieved, 2),
-                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                         "avg_launch_us": round(avg_gemm_s * 1e6, 2),
-                         "flop_per_launch": flop,
-                         "peak_note": "peak = the dense fp32 MFMA peak (the dtype's); the kernel "
-                                      "runs on the bf16 pipe at 6 products per fp32 product, "
-                                      "whose fp32-equivalent ceiling is x3_peak",
-                         "x3_peak": X3_PEAK_TFLOPS,
-                         "frac_of_x3_peak": round(achieved / X3_PEAK_TFLOPS, 4)},
+            "roofline": x3_roofline(
+                "az_gemm_f32 output_transform.0 call (gemm_x3 tile kernel + its split-K reduce), "
+                "Linear 3136x3136 at M = %d: fp32 operands split into 3 bf16 terms, 6 cross "
+                "products on the bf16 MFMA" % B, flop, avg_gemm_s, traffic, pmc_run("gemm")),
+            "gemm_shapes": shapes,
             "layer_roofline": layer,
             "cnn_b512": cnn,
             "as_called_b1": b1,

@@ -64,6 +64,10 @@ int az_mcts_begin(az_mcts* m, int slot, const int8_t* board, int sims);
 int az_mcts_remaining(const az_mcts* m, int slot);
 /* The same for every slot at once: out[slots]. */
 int az_mcts_remaining_all(const az_mcts* m, int32_t* out);
+/* Drop a slot's queued searches (the tree keeps every finished simulation), so the caller
+ * can recover after an exception it raised mid-search (AZ_STRICT_NN).  AZM_ESTATE while a
+ * collected leaf is still waiting for its feed. */
+int az_mcts_abandon(az_mcts* m, int slot);
 
 /* Advance every slot with queued searches until it waits on a new leaf or has none left.
  * Writes up to `cap` leaf boards [n*n] and their slot ids, in ascending slot order; returns

@@ -128,3 +128,45 @@ def test_speculative_leaf_batches_play_the_same_games(name, use_gnn):
     (c0, h0, b0), (c1, h1, b1) = calls
     assert h0 == 0 and b0 == 1 and h1 > 0 and b1 <= 8
     assert c1 + h1 == c0 and c1 < c0
+
+
+class FlakyNet(SpecHashNet):
+    """Fails the first `fail` batched calls, then serves like SpecHashNet."""
+
+    def __init__(self, A, salt, fail):
+        super().__init__(A, salt)
+        self.fail = fail
+
+    def predict_both(self, boards):
+        if self.fail > 0:
+            self.fail -= 1
+            raise RuntimeError("device lost")
+        return super().predict_both(boards)
+
+    def predict_batch(self, boards):
+        if self.fail > 0:
+            self.fail -= 1
+            raise RuntimeError("device lost")
+        return super().predict_batch(boards)
+
+
+@pytest.mark.nn_failures_expected
+@pytest.mark.parametrize("prefetch", [False, True])
+def test_strict_failure_leaves_engine_usable(monkeypatch, prefetch):
+    """Under AZ_STRICT_NN=1 a failed leaf batch raises NNFailure -- after the engine took the
+    failed feed, so the same player searches on cleanly once the network recovers."""
+    import nn_fallback
+    from connect4.Connect4Game import Connect4Game
+    from mcts_native import ArenaPlayer
+    game = Connect4Game(7)
+    args = Args(numMCTSSims=6, cpuct=1.0, use_gnn=True)
+    net = FlakyNet(game.getActionSize(), 3, fail=1)
+    p = ArenaPlayer(game, net, args, prefetch=prefetch)
+    monkeypatch.setenv("AZ_STRICT_NN", "1")
+    board = game.getInitBoard()
+    with pytest.raises(nn_fallback.NNFailure):
+        p(board)
+    monkeypatch.delenv("AZ_STRICT_NN")
+    b2 = game.getNextState(board, 1, 3)[0]
+    a = p(game.getCanonicalForm(b2, -1))
+    assert 0 <= a < game.getActionSize()

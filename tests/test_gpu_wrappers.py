@@ -342,3 +342,28 @@ def test_direct_batch_async_equals_predict_both(c4_wrapper):
     ref = c4_wrapper.predict_both(boards[:300])
     assert np.array_equal(pi, ref[0]) and np.array_equal(v, ref[1])
     np.testing.assert_allclose(pend[2][1].result()[2][256:], z2["pi_gnn_b1"][:44], atol=TOL)
+
+
+@pytest.mark.parametrize("n", [3, 8, 40])
+def test_async_predictions_own_their_host_buffers(c4_wrapper, n):
+    """Two lock-step lanes keep two predictions in flight and read them in either order, and a
+    prediction object that was read long ago is only dropped when its variable is rebound.
+    Every prediction must still return ITS rows: the stale object must not free the host
+    buffers a later prediction holds (regression: the next launch then overwrote them)."""
+    import gc
+    z = golden("c4_gnn.npz")
+    boards = np.concatenate([z["boards"]] * 4)[:3 * n].astype(np.int8)
+    X = [boards[i * n:(i + 1) * n] for i in range(3)]
+    ref = [c4_wrapper.predict_both(x.astype(np.int64)) for x in X]
+    p0 = c4_wrapper.predict_both_async(X[0])
+    r0 = p0.result()
+    p1 = c4_wrapper.predict_both_async(X[1])    # reuses p0's (released) host buffers
+    del p0                                      # the stale object goes while p1 holds them
+    gc.collect()
+    p2 = c4_wrapper.predict_both_async(X[2])    # must not take p1's buffers
+    r2 = p2.result()                            # read in reverse launch order
+    r1 = p1.result()
+    assert p1.result() is r1                    # idempotent
+    for got, want in ((r0, ref[0]), (r1, ref[1]), (r2, ref[2])):
+        for a, b in zip(got, want):
+            np.testing.assert_allclose(a, b, atol=TOL)

@@ -54,6 +54,35 @@ def test_reference_examples_history_loads(tmp_path):
     assert len(gnn[0]) == 7
 
 
+class _Boom:
+    def __reduce__(self):
+        return (os.system, ("echo should-not-run",))
+
+
+def test_examples_unpickler_refuses_foreign_globals(tmp_path):
+    """loadTrainExamples resolves only numpy / deque globals: a history that names any other
+    callable raises instead of running it; a history this Coach saved round-trips."""
+    import pickle
+    from collections import deque
+    from Coach import Coach, ExamplesUnpickler
+    from test_mcts_golden import Args
+    bad = tmp_path / "bad.pth.tar.examples"
+    bad.write_bytes(pickle.dumps([deque([_Boom()])]))
+    with open(bad, "rb") as f, pytest.raises(pickle.UnpicklingError, match="os|posix|system"):
+        ExamplesUnpickler(f).load()
+    coach = Coach.__new__(Coach)
+    coach.args = Args(checkpoint=str(tmp_path), load_folder_file=(str(tmp_path), "x.pth.tar"))
+    hist = [([(np.zeros((3, 3), np.int64), [0.5, 0.5], 1)],
+             [(np.ones((3, 3)), 1, np.full(2, 0.5), np.float32(0.25), np.full(2, 0.5), 0.1, -1)])]
+    coach.trainExamplesHistory = hist
+    coach.getCheckpointFile = lambda i: "x.pth.tar"
+    coach.saveTrainExamples(0)
+    coach.trainExamplesHistory, coach.skipFirstSelfPlay = [], False
+    coach.loadTrainExamples()
+    (std, gnn), = coach.trainExamplesHistory
+    assert np.array_equal(std[0][0], hist[0][0][0][0]) and gnn[0][3] == np.float32(0.25)
+
+
 @pytest.mark.gpu
 def test_load_model_resume_matches_reference(tmp_path):
     import torch

@@ -6,7 +6,7 @@ T=${1:-final}
 O=gpurun_out/$T
 mkdir -p $O
 export AZ_REPORT_DIR=$O/reports
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --durations=30 --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
 timeout -k 10 420 python -u bench.py > $O/bench.json 2> $O/bench.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-selfplay --no-train --no-agg-extra --large-batch 0 > $O/kt.log 2>&1 || exit $?
