@@ -45,7 +45,7 @@ class Graph(ctypes.Structure):
     _fields_ = [("V", c_int), ("E", c_int), ("rowptr", c_void_p), ("col", c_void_p),
                 ("edge_dst", c_void_p), ("D", c_int), ("dst_rows", c_void_p),
                 ("src_rowptr", c_void_p), ("src_edges", c_void_p), ("dst_index", c_void_p),
-                ("max_deg", c_int)]
+                ("max_deg", c_int), ("band", c_int)]
 
 
 LAYER_FIELDS = ("att_w1", "att_b1", "att_w2", "att_b2", "upd_w1", "upd_b1", "upd_w2", "upd_b2",

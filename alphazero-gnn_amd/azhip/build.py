@@ -30,7 +30,7 @@ HOST_FLAGS = ["-O3", "-fPIC", "-shared", "-std=c++17", "-fopenmp", "-ffp-contrac
               "-Wall", "-Wl,-z,defs"]
 OBJ = os.path.join(CSRC, "build")
 SOURCES = ["az_runtime.hip", "az_gemm.hip", "az_trunk.hip", "az_gnn.hip", "az_gnn_fused.hip",
-           "az_optim.hip", "az_backward.hip"]
+           "az_gnn_band.hip", "az_optim.hip", "az_backward.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wall",
          "-Wno-unused-function", "-fno-gpu-rdc"]
 

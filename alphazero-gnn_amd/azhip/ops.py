@@ -269,6 +269,8 @@ class DeviceGraph:
         rows = np.flatnonzero(deg > 0)
         self.D = len(rows)
         self.max_deg = int(deg.max()) if V else 0
+        # max |src - dst| (the band kernel's condition: the row-major 32x32 grid gives 32)
+        self.band = int(np.abs(col - np.repeat(np.arange(V), deg)).max()) if self.E else 0
         order = np.argsort(col, kind="stable")           # edges grouped by source
         src_rowptr = np.zeros(V + 1, np.int64)
         np.cumsum(np.bincount(col, minlength=V), out=src_rowptr[1:])
@@ -280,7 +282,7 @@ class DeviceGraph:
         self.c = Graph(V, self.E, self.rowptr.data_ptr(), self.col.data_ptr(),
                        self.edge_dst.data_ptr(), self.D, self.dst_rows.data_ptr(),
                        self.src_rowptr.data_ptr(), self.src_edges.data_ptr(),
-                       self.dst_index.data_ptr(), self.max_deg)
+                       self.dst_index.data_ptr(), self.max_deg, self.band)
 
     @staticmethod
     def star(n, device="cuda"):

@@ -16,6 +16,7 @@
 #include <utility>
 
 #include "az_common.h"
+#include "az_x3.h"
 #include "az_heads.h"
 
 namespace az {
@@ -979,38 +980,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
 // ds_write_b128 per plane); one barrier per 32-k tile.  LDS image per plane: [row][32 bf16]
 // (64 B rows), 16-B chunk c stored at c ^ ((row >> 2) & 3), which makes the MFMA operand reads
 // (lane: row lane & 31, chunk 2s + (lane >> 5)) conflict-free for every ds_read_b128 lane group.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// two floats -> one dword of two bf16 (round to nearest even; v_cvt_pk_bf16_f32, low = a)
-__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
-  const bf16x2 h = {(__bf16)a, (__bf16)b};
-  return __builtin_bit_cast(unsigned, h);
-}
-
-// 8 consecutive floats -> three planes of 8 bf16 (element j in bits 16j.. of the 128-bit word):
-// per pair one v_cvt_pk_bf16_f32 per plane, the residual from the packed halves (shift / mask).
-// The two residuals of a pair are formed by different (exact) instructions, a - h and
-// fma(h, -1, b), so the compiler does not pack them into v_pk_add_f32, which costs extra
-// cycles beside MFMAs (MI355X_MICROARCH.md, filler prices).
-__device__ __forceinline__ void split3(const f32x4& x0, const f32x4& x1, u32x4 (&o)[3]) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float a = q < 2 ? x0[2 * q] : x1[2 * q - 4];
-    const float b = q < 2 ? x0[2 * q + 1] : x1[2 * q - 3];
-    const unsigned h = pk_bf16(a, b);
-    const float ra = a - __uint_as_float(h << 16);
-    const float rb = __builtin_fmaf(__uint_as_float(h & 0xFFFF0000u), -1.f, b);
-    const unsigned m = pk_bf16(ra, rb);
-    const float sa = ra - __uint_as_float(m << 16);
-    const float sb = __builtin_fmaf(__uint_as_float(m & 0xFFFF0000u), -1.f, rb);
-    o[0][q] = h;
-    o[1][q] = m;
-    o[2][q] = pk_bf16(sa, sb);
-  }
-}
-
 // ABL (tuning build only, timing ablations whose results are wrong by design): 1 = every tile's
 // loads from the split's first four tiles (L2-resident), 2 = no MFMA, 4 = no split (raw bits)
 // APL: A comes as three bf16 planes split once by x3_split_kernel (p.apl, row stride K, K % 32

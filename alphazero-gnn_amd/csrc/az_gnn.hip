@@ -14,6 +14,10 @@
 namespace az {
 int gemm_f32(const az_gemm_desc* d, hipStream_t s);
 bool gnn_layer_fusable(const az_graph* g, int F, int H);
+bool gnn_layer_band_ok(const az_graph* g, int F, int H);
+size_t gnn_layer_band_ws_bytes();
+int gnn_layer_band(const az_graph* g, const float* x, const az_gnn_layer_w* w, float* x_out,
+                   void* ws, hipStream_t s);
 size_t gnn_layer_fused_ws_bytes(int V);
 int gnn_layer_fused(const az_graph* g, const float* x, const az_gnn_layer_w* w, float* x_out,
                     void* ws, size_t ws_bytes, hipStream_t s);
@@ -258,6 +262,7 @@ __global__ __launch_bounds__(256) void aggregate_small_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (j < deg[t]) S += a[t][j];
+    for (int j = 4; j < deg[t]; ++j) S += alpha[e0[t] + j];   // in-degree above 4 (never dropped)
     const bool norm = S > 0.f;
     float w[4];
 #pragma unroll
@@ -271,6 +276,15 @@ __global__ __launch_bounds__(256) void aggregate_small_kernel(
         if (j < deg[t])
 #pragma unroll
           for (int c = 0; c < 4; ++c) acc[c] = fmaf(w[j], v[t][j][q][c], acc[c]);
+      for (int j = 4; j < deg[t]; ++j) {     // a caller whose max_deg understates the graph
+        const float aj = alpha[e0[t] + j];
+        const float wj = norm ? aj / S : aj;
+        if (f < F) {
+          const f32x4 xj = *reinterpret_cast<const f32x4*>(x + (size_t)col[e0[t] + j] * ldx + f);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[c] = fmaf(wj, xj[c], acc[c]);
+        }
+      }
       if (f < F) {
         f32x4* dst = reinterpret_cast<f32x4*>(agg + (size_t)d[t] * ldagg + f);
         if constexpr (NT) __builtin_nontemporal_store(acc, dst);
@@ -343,14 +357,38 @@ __global__ __launch_bounds__(256) void attn_aggregate_small_kernel(
     for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
     a[j] = sigmoidf_ref(acc + bias2);
   }
-  if (l < deg) {   // lane j writes edge j's score (deg <= 4 < 16)
+  if (l < deg && l < 4) {   // lane j writes edge j's score
     const float aj = l == 0 ? a[0] : (l == 1 ? a[1] : (l == 2 ? a[2] : a[3]));
     alpha[e0 + l] = aj;
   }
+  // in-degree above 4 (a caller's az_graph.max_deg understating the graph): the remaining
+  // edges' scores from global memory, in CSR order -- slower, never dropped
+  auto alpha_far = [&](int q) {
+    const float* ps = P + (size_t)col[e0 + q] * ldp;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const f32x4 uq = *reinterpret_cast<const f32x4*>(ps + 4 * (l + 16 * k));
+      float h0 = t[k][0] + uq[1] + bb[2 * k];
+      float h1 = t[k][2] + uq[3] + bb[2 * k + 1];
+      h0 = h0 > 0.f ? h0 : 0.f;
+      h1 = h1 > 0.f ? h1 : 0.f;
+      acc = fmaf(h0, ww[2 * k], acc);
+      acc = fmaf(h1, ww[2 * k + 1], acc);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
+    return sigmoidf_ref(acc + bias2);
+  };
   float S = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (j < deg) S += a[j];
+  for (int q = 4; q < deg; ++q) {
+    const float aq = alpha_far(q);
+    if (l == 0) alpha[e0 + q] = aq;
+    S += aq;
+  }
   const bool norm = S > 0.f;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -360,6 +398,13 @@ __global__ __launch_bounds__(256) void attn_aggregate_small_kernel(
 #pragma unroll
       for (int c = 0; c < 4; ++c) acc[c] = fmaf(w, xv[j][c], acc[c]);
     }
+  for (int q = 4; q < deg; ++q) {
+    const float aq = alpha_far(q);
+    const float w = norm ? aq / S : aq;
+    const f32x4 xq = *reinterpret_cast<const f32x4*>(x + (size_t)col[e0 + q] * ldx + 4 * l);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = fmaf(w, xq[c], acc[c]);
+  }
   (void)H;
   (void)F;
   __builtin_nontemporal_store(acc, reinterpret_cast<f32x4*>(agg + (size_t)d * ldagg + 4 * l));
@@ -553,6 +598,7 @@ extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
 
 extern "C" size_t az_gnn_layer_infer_ws_bytes(const az_graph* g, int F, int H) {
   if (!g) return 0;
+  if (gnn_layer_band_ok(g, F, H)) return gnn_layer_band_ws_bytes();
   return gnn_layer_fusable(g, F, H) ? gnn_layer_fused_ws_bytes(g->V)
                                     : az_gnn_layer_ws_bytes(g->V, g->E, g->D, F, H);
 }
@@ -562,6 +608,13 @@ extern "C" int az_gnn_layer_infer(const az_graph* g, const float* x, int F, int 
                                   size_t ws_bytes, void* stream) {
   int rc = check_graph(g);
   if (rc) return rc;
+  if (gnn_layer_band_ok(g, F, H)) {
+    AZ_REQUIRE(x && w && x_out && x_out != x && ws, AZ_EINVAL,
+               "az_gnn_layer_infer: null pointer or x_out aliasing x");
+    AZ_REQUIRE(ws_bytes >= gnn_layer_band_ws_bytes(), AZ_EINVAL,
+               "az_gnn_layer_infer: workspace too small");
+    return gnn_layer_band(g, x, w, x_out, ws, as_stream(stream));
+  }
   if (!gnn_layer_fusable(g, F, H))
     return az_gnn_layer_fwd(g, x, F, H, w, x_out, ws, ws_bytes, stream);
   AZ_REQUIRE(x && x_out && w && ws && x != x_out, AZ_EINVAL, "az_gnn_layer_infer: bad pointers");

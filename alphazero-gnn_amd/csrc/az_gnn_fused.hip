@@ -107,11 +107,36 @@ __device__ __forceinline__ void issue_gather(Gather& g, const int* idx, const fl
   }
 }
 
+// alpha of one in-edge from source sq (16 lanes of the destination's group; lane j holds hidden
+// units 4j.. and 64+4j..): sigmoid(w2 . relu(Pt[d] + Ps[sq] + b1) + b2), Ps / x from global
+__device__ __forceinline__ float edge_alpha_global(int sq, const float* __restrict__ Ps,
+                                                  const f32x4& pt0, const f32x4& pt1,
+                                                  const f32x4& bb0, const f32x4& bb1,
+                                                  const f32x4& ww0, const f32x4& ww1, float b2,
+                                                  int j) {
+  const float* pr = Ps + (size_t)sq * HH + 4 * j;
+  const f32x4 p0 = *reinterpret_cast<const f32x4*>(pr);
+  const f32x4 p1 = *reinterpret_cast<const f32x4*>(pr + HH / 2);
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc = fmaf(relu(pt0[c] + p0[c] + bb0[c]), ww0[c], acc);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc = fmaf(relu(pt1[c] + p1[c] + bb1[c]), ww1[c], acc);
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
+  return sigmoidf_ref(acc + b2);
+}
+
 // attention scores of one destination's in-edges and its normalised aggregation (gnn_utils.py:
-// 48-65): agg = sum_e alpha_e / S x_s, S = sum alpha (> 0; else un-normalised)
-__device__ __forceinline__ f32x4 edge_pass(const Gather& g, int deg, const float* pt,
-                                           const float* AB, float b2, int j) {
+// 48-65): agg = sum_e alpha_e / S x_s, S = sum alpha (> 0; else un-normalised).  The first
+// MAXD edges come from the gathered registers; a destination with more in-edges (a caller whose
+// az_graph.max_deg understates the graph) takes the rest from global memory in CSR order --
+// slower, never dropped.
+__device__ __forceinline__ f32x4 edge_pass(const Gather& g, const int* idx, const int* __restrict__ col,
+                                           const float* __restrict__ Ps, const float* __restrict__ x,
+                                           const float* pt, const float* AB, float b2, int j) {
   f32x4 agg = {0.f, 0.f, 0.f, 0.f};
+  const int deg = idx[1];
   if (deg <= 0) return agg;
   const f32x4 pt0 = *reinterpret_cast<const f32x4*>(pt + 4 * j);
   const f32x4 pt1 = *reinterpret_cast<const f32x4*>(pt + HH / 2 + 4 * j);
@@ -135,6 +160,9 @@ __device__ __forceinline__ f32x4 edge_pass(const Gather& g, int deg, const float
 #pragma unroll
   for (int q = 0; q < MAXD; ++q)
     if (q < deg) S += a[q];
+  const int e0 = idx[6];
+  for (int q = MAXD; q < deg; ++q)        // in-degree above MAXD: the remaining edges
+    S += edge_alpha_global(col[e0 + q], Ps, pt0, pt1, bb0, bb1, ww0, ww1, b2, j);
   const bool norm = S > 0.f;
 #pragma unroll
   for (int q = 0; q < MAXD; ++q)
@@ -143,6 +171,14 @@ __device__ __forceinline__ f32x4 edge_pass(const Gather& g, int deg, const float
 #pragma unroll
       for (int c = 0; c < 4; ++c) agg[c] = fmaf(wq, g.xs[q][c], agg[c]);
     }
+  for (int q = MAXD; q < deg; ++q) {
+    const int sq = col[e0 + q];
+    const float aq = edge_alpha_global(sq, Ps, pt0, pt1, bb0, bb1, ww0, ww1, b2, j);
+    const float wq = norm ? aq / S : aq;
+    const f32x4 xs = *reinterpret_cast<const f32x4*>(x + (size_t)sq * FF + 4 * j);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) agg[c] = fmaf(wq, xs[c], agg[c]);
+  }
   return agg;
 }
 
@@ -207,6 +243,7 @@ __global__ __launch_bounds__(NT, TT == 64 ? 2 : 3) void gnn_layer_fused_kernel(
     if (iq == 0) {
       IDX[0][im][0] = d;
       IDX[0][im][1] = deg;
+      IDX[0][im][6] = e0;
     }
   }
   f32x4 xnext[MT];
@@ -263,17 +300,17 @@ __global__ __launch_bounds__(NT, TT == 64 ? 2 : 3) void gnn_layer_fused_kernel(
     {
       const int m0 = grp, m1 = 16 + grp;
       *reinterpret_cast<f32x4*>(&C[m0 * CS + FF + 4 * j]) =
-          edge_pass(g0, IDX[cur][m0][1], &R[m0 * CS], AB, b2, j);
+          edge_pass(g0, IDX[cur][m0], col, Ps, x, &R[m0 * CS], AB, b2, j);
       if constexpr (TT == 64) issue_gather(g0, IDX[cur][32 + grp], Ps, x, j);
       *reinterpret_cast<f32x4*>(&C[m1 * CS + FF + 4 * j]) =
-          edge_pass(g1, IDX[cur][m1][1], &R[m1 * CS], AB, b2, j);
+          edge_pass(g1, IDX[cur][m1], col, Ps, x, &R[m1 * CS], AB, b2, j);
       if constexpr (TT == 64) {
         const int m2 = 32 + grp, m3 = 48 + grp;
         issue_gather(g1, IDX[cur][m3], Ps, x, j);
         *reinterpret_cast<f32x4*>(&C[m2 * CS + FF + 4 * j]) =
-            edge_pass(g0, IDX[cur][m2][1], &R[m2 * CS], AB, b2, j);
+            edge_pass(g0, IDX[cur][m2], col, Ps, x, &R[m2 * CS], AB, b2, j);
         *reinterpret_cast<f32x4*>(&C[m3 * CS + FF + 4 * j]) =
-            edge_pass(g1, IDX[cur][m3][1], &R[m3 * CS], AB, b2, j);
+            edge_pass(g1, IDX[cur][m3], col, Ps, x, &R[m3 * CS], AB, b2, j);
       }
     }
     // link 3: its sources
@@ -319,6 +356,7 @@ __global__ __launch_bounds__(NT, TT == 64 ? 2 : 3) void gnn_layer_fused_kernel(
       if (iq == 0) {
         IDX[nxt][im][0] = nd;
         IDX[nxt][im][1] = nvalid ? ndeg : -1;
+        IDX[nxt][im][6] = ne0;
       }
     }
     __syncthreads();
@@ -354,8 +392,11 @@ __global__ __launch_bounds__(NT, TT == 64 ? 2 : 3) void gnn_layer_fused_kernel(
 }
 
 // Host side -----------------------------------------------------------------------------------
+// The fused kernel is exact for any in-degree (edges past MAXD take its slow path), so max_deg
+// only picks the faster path; a zero max_deg with edges (an unset field) is not taken as
+// "in-degree <= 4".
 bool gnn_layer_fusable(const az_graph* g, int F, int H) {
-  return F == FF && H == HH && g->max_deg >= 0 && g->max_deg <= MAXD && g->D > 0;
+  return F == FF && H == HH && g->D > 0 && g->max_deg <= MAXD && (g->max_deg > 0 || g->E == 0);
 }
 
 size_t gnn_layer_fused_ws_bytes(int V) {

@@ -1,0 +1,60 @@
+// fp32 on the bf16 matrix cores ("x3"): the exact three-term bf16 split of fp32 operands and the
+// six-product MFMA step, shared by gemm_x3 (az_gemm.hip) and the band-mode GNN layer
+// (az_gnn_band.hip).  Every fp32 x = h + m + l with h = rne(x), m = rne(x - h), l = rne(x - h - m)
+// (|m| <= 2^-8 |x|, |l| <= 2^-16 |x|; all 24 significand bits kept), and a*b is the sum of the
+// six leading cross products ah*bl + al*bh + am*bm + ah*bm + am*bh + ah*bh, each exact in fp32.
+// Operands must be finite and below the bf16 maximum (~3.39e38): an infinite x (or one that
+// rounds to an infinite h) leaves a NaN residual, so the product is NaN where an fp32 GEMM gives
+// +-inf.  Network weights and activations on this path are finite; a non-finite operand is an
+// upstream fault in either case.
+#pragma once
+#include "az_common.h"
+
+namespace az {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// two floats -> one dword of two bf16 (round to nearest even; v_cvt_pk_bf16_f32, low = a)
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const bf16x2 h = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, h);
+}
+
+// 8 consecutive floats -> three planes of 8 bf16 (element j in bits 16j.. of the 128-bit word):
+// per pair one v_cvt_pk_bf16_f32 per plane, the residual from the packed halves (shift / mask).
+// The two residuals of a pair are formed by different (exact) instructions, a - h and
+// fma(h, -1, b), so the compiler does not pack them into v_pk_add_f32, which costs extra
+// cycles beside MFMAs (MI355X_MICROARCH.md, filler prices).
+__device__ __forceinline__ void split3(const f32x4& x0, const f32x4& x1, u32x4 (&o)[3]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float a = q < 2 ? x0[2 * q] : x1[2 * q - 4];
+    const float b = q < 2 ? x0[2 * q + 1] : x1[2 * q - 3];
+    const unsigned h = pk_bf16(a, b);
+    const float ra = a - __uint_as_float(h << 16);
+    const float rb = __builtin_fmaf(__uint_as_float(h & 0xFFFF0000u), -1.f, b);
+    const unsigned m = pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(m << 16);
+    const float sb = __builtin_fmaf(__uint_as_float(m & 0xFFFF0000u), -1.f, rb);
+    o[0][q] = h;
+    o[1][q] = m;
+    o[2][q] = pk_bf16(sa, sb);
+  }
+}
+
+
+// acc += A . B over one 16-k step of v_mfma_f32_32x32x16_bf16 with both operands as three bf16
+// planes (a[0..2] = h, m, l of A's fragment, b[0..2] of B's), the dropped terms smallest first
+__device__ __forceinline__ f32x16 mfma6_32x32x16(const bf16x8 (&a)[3], const bf16x8 (&b)[3],
+                                                  f32x16 t) {
+  t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], t, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], t, 0, 0, 0);
+}
+
+}  // namespace az

@@ -234,15 +234,15 @@ def aggregate_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=T
 
 def layer_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True):
     """The eval-mode GNN layer exactly as az_gnn_layer_infer runs it on the config-5 grid (what
-    PolicyValueGNN.forward_graph launches): (1) the source-projection GEMM Ps = x W1[:, F:]^T,
-    (2) gnn_layer_fused_kernel (target projection, attention, normalised aggregation, gate /
-    update MLPs, gated residual; nothing else reaches HBM).  Each launch timed alone with HIP
-    events on the launch stream, Infinity Cache flushed before each (the headline) and
-    back-to-back.  Algorithmic work (per layer):
-      fused kernel: 57,344 FLOP per destination (73,728 minus the 16,384 of the source
-                    projection) + 640 FLOP per edge; bytes = x (V*256) + Ps (V*512) + col (4E)
-                    + rowptr (4(V+1)) + x_out (V*256)
-      projection:   16,384 FLOP per node; bytes = x (V*256) + Ps written (V*512)."""
+    PolicyValueGNN.forward_graph launches): band_split_weights (221 KB of bf16 weight planes)
+    + gnn_layer_band_kernel (projections, attention, normalised aggregation, gate / update MLPs,
+    gated residual; x and each node's source projection once, in a rolling LDS window; nothing
+    but x_out reaches HBM).  Timed per layer call with HIP events on the launch stream, Infinity
+    Cache flushed before each (the headline) and back-to-back.  Algorithmic work (SURVEY.md §8d
+    config 5, per layer): 73,728 FLOP per node on the matrix cores (target + source projections
+    2 x 16,384, gate / update_net.0 32,768, update_net.2 8,192) + 640 FLOP per edge; bytes = x
+    read (V * 256) + x_out written (V * 256) + col (4E) + rowptr (4(V+1)).  The MFMAs run fp32
+    as 6 bf16 products (x3), so the pipe is the bf16 one."""
     from azhip.weights import gnn_spec, synthetic_state_dict
     Gw = synthetic_state_dict(gnn_spec(64, 2), 3)
     Wl = {k[len("layers.0."):]: torch.from_numpy(v).to(device) for k, v in Gw.items()
@@ -253,75 +253,51 @@ def layer_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True)
         V, E = g.V, g.E
         x = torch.rand((V, 64), device=device,
                        generator=torch.Generator(device=device).manual_seed(0)) * 2 - 1
-        Ps = torch.empty((V, 128), device=device)
         out = torch.empty_like(x)
-        for _ in range(2):
-            ops.gnn_source_proj(g, x, Wl, Ps)
-            ops.gnn_layer_fused(g, x, Ps, Wl, out)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4 * reps)]
+        _, ws = ops.gnn_layer(g, x, Wl, save=False, out=out)
+        ops.gnn_layer(g, x, Wl, save=False, out=out, ws=ws)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
         for i in range(reps):
             if flush is not None:
                 flush.sum()
-            ev[4 * i].record()
-            ops.gnn_source_proj(g, x, Wl, Ps)
-            ev[4 * i + 1].record()
-            if flush is not None:
-                flush.sum()
-            ev[4 * i + 2].record()
-            ops.gnn_layer_fused(g, x, Ps, Wl, out)
-            ev[4 * i + 3].record()
+            ev[2 * i].record()
+            ops.gnn_layer(g, x, Wl, save=False, out=out, ws=ws)
+            ev[2 * i + 1].record()
         torch.cuda.synchronize()
-        proj_ms = float(np.mean([ev[4 * i].elapsed_time(ev[4 * i + 1]) for i in range(reps)]))
-        fused_ms = float(np.mean([ev[4 * i + 2].elapsed_time(ev[4 * i + 3]) for i in range(reps)]))
-        D = g.D
-        f_flop = 57344 * D + 640 * E
-        f_bytes = V * 256 + V * 512 + 4 * E + 4 * (V + 1) + D * 256
-        p_flop, p_bytes = 16384 * V, V * 256 + V * 512
-        del x, Ps, out
-        return {"V": V, "E": E, "fused_us": fused_ms * 1e3, "proj_us": proj_ms * 1e3,
-                "fused_tflops": f_flop / (fused_ms * 1e-3) / 1e12,
-                "fused_gbs": f_bytes / (fused_ms * 1e-3) / 1e9,
-                "proj_gbs": p_bytes / (proj_ms * 1e-3) / 1e9,
-                "proj_tflops": p_flop / (proj_ms * 1e-3) / 1e12,
-                "fused_flop": f_flop, "fused_bytes": f_bytes, "proj_bytes": p_bytes}
+        us = float(np.mean([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps)])) * 1e3
+        mflop = 73728 * V
+        flop = mflop + 640 * E
+        nbytes = V * 512 + 4 * E + 4 * (V + 1)
+        del x, out
+        return {"V": V, "E": E, "us": us, "flop": flop, "bytes": nbytes,
+                "bf16_tflops": 6 * mflop / (us * 1e-6) / 1e12,
+                "fp32_equiv_tflops": flop / (us * 1e-6) / 1e12,
+                "gbs": nbytes / (us * 1e-6) / 1e9, "band": g.band}
 
     flush = torch.zeros((128 << 20,), dtype=torch.float32, device=device)
     c = run(graphs, flush)
-    out = {"kernel": "gnn_layer_fused_kernel (az_gnn_layer_infer, eval-mode GNNLayer)",
-           "bound": "mfma", "achieved": round(c["fused_tflops"], 2),
-           "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-           "frac": round(c["fused_tflops"] / FP32_MFMA_PEAK_TFLOPS, 4),
-           "traffic": pmc_traffic("gnn_layer_fused"), "traffic_run": pmc_run("gnn_layer_fused"),
-           "avg_launch_us": round(c["fused_us"], 2),
-           "flop_per_launch": c["fused_flop"], "algorithmic_bytes": c["fused_bytes"],
-           "hbm_gbs_algorithmic": round(c["fused_gbs"], 1),
+    del flush
+    out = {"kernel": "gnn_layer_band_kernel + band_split_weights (az_gnn_layer_infer, eval-mode "
+                     "GNNLayer, band %d graph)" % c["band"],
+           "bound": "mfma", "pipe": "bf16 (x3: 6 bf16 products per fp32 product)",
+           "achieved": round(c["bf16_tflops"], 2), "peak": BF16_MFMA_PEAK_TFLOPS,
+           "unit": "TFLOP/s", "frac": round(c["bf16_tflops"] / BF16_MFMA_PEAK_TFLOPS, 4),
+           "fp32_equiv_tflops": round(c["fp32_equiv_tflops"], 2),
+           "traffic": pmc_traffic("gnn_layer_band"), "traffic_run": pmc_run("gnn_layer_band"),
+           "avg_launch_us": round(c["us"], 2), "flop_per_launch": c["flop"],
+           "algorithmic_bytes": c["bytes"], "hbm_gbs_algorithmic": round(c["gbs"], 1),
+           "hbm_frac_algorithmic": round(c["gbs"] / HBM_PEAK_GBS, 4),
            "workload": f"{graphs} 32x32 grids, V={c['V']}, E={c['E']}, F=64, H=128 (config-5 "
                        f"shard per GPU), Infinity Cache flushed before each launch",
-           # 2*V*128*64 FLOP over V*64*4 + V*128*4 B: 21.3 FLOP/B, just above the 19.7 ridge,
-           # so its floor is the MFMA one (55 us at 512 grids vs 50 us of HBM time)
-           "source_projection": {"kernel": "az_gemm_f32 Ps = x W1[:, F:]^T (M=V, N=128, K=64, "
-                                           "gemm_tall<128,64,8,2>)",
-                                 "bound": "mfma", "avg_launch_us": round(c["proj_us"], 2),
-                                 "achieved": round(2 * c["V"] * 128 * 64 / c["proj_us"] / 1e6, 2),
-                                 "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                 "frac": round(2 * c["V"] * 128 * 64 / c["proj_us"] / 1e6
-                                               / FP32_MFMA_PEAK_TFLOPS, 4),
-                                 "hbm_gbs_algorithmic": round(c["proj_gbs"], 1),
-                                 "traffic": pmc_traffic("gnn_source_proj"),
-                                 "traffic_run": pmc_run("gnn_source_proj")},
-           "layer_us": round(c["fused_us"] + c["proj_us"], 2)}
-    del flush
+           "layer_us": round(c["us"], 2)}
     if extra:
         w = run(graphs)
-        out["warm"] = {"fused_us": round(w["fused_us"], 2), "proj_us": round(w["proj_us"], 2),
-                       "fused_tflops": round(w["fused_tflops"], 2),
+        out["warm"] = {"us": round(w["us"], 2), "bf16_tflops": round(w["bf16_tflops"], 2),
                        "note": "back-to-back launches, x cache-warm"}
         if full_graphs:
             f = run(full_graphs, reps=5)
-            out["full_config"] = {"fused_us": round(f["fused_us"], 2),
-                                  "proj_us": round(f["proj_us"], 2),
-                                  "fused_tflops": round(f["fused_tflops"], 2),
-                                  "fused_frac": round(f["fused_tflops"] / FP32_MFMA_PEAK_TFLOPS, 4),
+            out["full_config"] = {"us": round(f["us"], 2), "bf16_tflops": round(f["bf16_tflops"], 2),
+                                  "frac": round(f["bf16_tflops"] / BF16_MFMA_PEAK_TFLOPS, 4),
                                   "workload": f"{full_graphs} grids, V={f['V']} (all of config 5 "
                                               f"on one GPU)"}
     return out

@@ -196,7 +196,12 @@ typedef struct az_graph {
   const int* src_rowptr;  /* [V+1] reverse CSR by source */
   const int* src_edges;   /* [E] edge ids grouped by source (ascending within a source) */
   const int* dst_index;   /* [V] compact destination index, -1 when no in-edge */
-  int max_deg;            /* max in-degree (backward supports <= 256) */
+  int max_deg;            /* max in-degree (backward supports <= 256); only picks kernels: an
+                             understated value is slower, never wrong (edges are not dropped) */
+  int band;               /* max |src - dst| over the edges when the caller knows it, else 0.
+                             Eval-mode layers on F = 64, H = 128 graphs with 0 < band <= 32 (the
+                             row-major grid: 32) run the band kernel (az_gnn_layer_infer); a
+                             source outside the claimed band takes a slow path, never wrong */
 } az_graph;
 
 typedef struct az_gnn_layer_w {     /* GNNLayer parameters, state_dict order */
@@ -241,11 +246,15 @@ int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H, const az_g
                      float* x_out, void* ws, size_t ws_bytes, void* stream);
 
 /* Inference form of az_gnn_layer_fwd (eval mode: same function, nothing kept for a backward
- * pass).  When F == 64, H == 128 and g->max_deg <= 4 (the synthetic grid, config 5; the graph's
- * max_deg must be its true maximum in-degree) the layer runs as ONE source-projection GEMM
- * (Ps = x W1[:, F:]^T, [V][H] in ws) plus ONE fused kernel per 64-destination tile: the target
- * projection, attention scores, normalised aggregation, gate / update MLPs and the gated residual
- * stay in LDS / registers (gnn_utils.py:30-74).  Other shapes run az_gnn_layer_fwd.
+ * pass).  F == 64, H == 128:
+ *  - 0 < g->band <= 32 (node-ordered band graphs: the synthetic grid, config 5): ONE band
+ *    kernel launch (after a 221 KB weight split into ws): per 64-destination tile, projections,
+ *    attention scores, normalised aggregation, gate / update MLPs and the gated residual in LDS /
+ *    registers on fp32-accurate bf16x3 MFMAs; x and the source projection of each node are read /
+ *    computed once, in a rolling window (gnn_utils.py:30-74);
+ *  - else 0 < g->max_deg <= 4: ONE source-projection GEMM (Ps = x W1[:, F:]^T, [V][H] in ws) plus
+ *    ONE fused kernel per 64-destination tile;
+ *  - other shapes run az_gnn_layer_fwd.
  * ws >= az_gnn_layer_infer_ws_bytes(g, F, H). */
 size_t az_gnn_layer_infer_ws_bytes(const az_graph* g, int F, int H);
 int az_gnn_layer_infer(const az_graph* g, const float* x, int F, int H, const az_gnn_layer_w* w,

@@ -506,6 +506,98 @@ def test_fused_layer_equals_training_path(ops, V, maxdeg, local):
         np.testing.assert_allclose(b, ref, atol=1e-5)
 
 
+def _band_graph(V, maxdeg, R, seed, p_empty=0.1):
+    """Random node-ordered graph with every source within R of its destination (|s - d| <= R),
+    ragged in-degrees 0..maxdeg, sorted distinct sources per destination."""
+    rng = np.random.default_rng(seed)
+    rowptr, col = [0], []
+    for d in range(V):
+        k = 0 if rng.random() < p_empty else int(rng.integers(1, maxdeg + 1))
+        lo, hi = max(0, d - R), min(V - 1, d + R)
+        cand = np.arange(lo, hi + 1)
+        src = np.sort(rng.choice(cand, size=min(k, len(cand)), replace=False))
+        col += src.tolist()
+        rowptr.append(len(col))
+    return np.array(rowptr), np.array(col)
+
+
+@pytest.mark.parametrize("V,maxdeg,R", [(1000, 4, 32), (4099, 6, 32), (130, 3, 5), (64, 4, 32),
+                                        (20011, 4, 20)])
+def test_band_layer_equals_training_path(ops, V, maxdeg, R):
+    """The band kernel (az_gnn_layer_infer on graphs with 0 < band <= 32: one launch, x / Ps in a
+    rolling LDS window, bf16x3 MFMAs) == az_gnn_layer_fwd within 2e-6 and the oracle within
+    1e-5 (gnn_utils.py:34-74) on random banded graphs: ragged in-degrees incl. 0 and above 4,
+    V not a multiple of the 64-node tile, many tiles per block (V = 20,011)."""
+    from oracle import nets as O
+    _, G, _ = _synth()
+    rowptr, col = _band_graph(V, maxdeg, R, seed=V + R)
+    g = ops.DeviceGraph(rowptr, col)
+    assert 0 < g.band <= 32 and g.D < V
+    Gd = {k: cu(v) for k, v in G.items()}
+    x0 = (np.random.default_rng(V + 2).random((V, 64), dtype=np.float32) * 2 - 1)
+    x = cu(x0)
+    Wl = {k[len("layers.1."):]: v for k, v in Gd.items() if k.startswith("layers.1.")}
+    a, _ = ops.gnn_layer(g, x, Wl, save=True)
+    b, _ = ops.gnn_layer(g, x, Wl, save=False)
+    a, b = a.cpu().numpy(), b.cpu().numpy()
+    np.testing.assert_allclose(b, a, atol=2e-6, rtol=1e-6)
+    empty = np.diff(rowptr) == 0
+    np.testing.assert_array_equal(b[empty], x0[empty])
+    if V <= 4099:
+        ref = O.gnn_layer_csr(x0.astype(np.float64), rowptr, col, G, 1)
+        np.testing.assert_allclose(b, ref, atol=1e-5)
+
+
+def test_band_layer_with_understated_band(ops):
+    """A caller claiming band 32 for a graph whose sources reach 40 nodes away and 5 % anywhere:
+    out-of-window sources take the band kernel's slow path -- same result as the training path."""
+    _, G, _ = _synth()
+    V = 3000
+    rowptr, col = _random_graph(V, 4, seed=91)
+    g = ops.DeviceGraph(rowptr, col)
+    assert g.band > 32
+    Gd = {k: cu(v) for k, v in G.items()}
+    x0 = (np.random.default_rng(92).random((V, 64), dtype=np.float32) * 2 - 1)
+    x = cu(x0)
+    Wl = {k[len("layers.0."):]: v for k, v in Gd.items() if k.startswith("layers.0.")}
+    a, _ = ops.gnn_layer(g, x, Wl, save=True)
+    g.c.band = 32
+    b, _ = ops.gnn_layer(g, x, Wl, save=False)
+    np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), atol=2e-6, rtol=1e-6)
+
+
+@pytest.mark.parametrize("claimed", [4, 0, 2])
+def test_fused_layer_with_understated_max_deg(ops, claimed):
+    """az_graph.max_deg is the caller's claim; the eval-mode layer must not trust it: a graph with
+    in-degrees up to 7 whose max_deg says 4 or 2 takes the fused kernel (edges past 4 on its
+    slow path, none dropped), one whose max_deg is 0 (an unset field) the unfused kernels --
+    every result equals the training path and the oracle (gnn_utils.py:34-74)."""
+    from oracle import nets as O
+    _, G, _ = _synth()
+    V = 2000
+    rowptr, col = _random_graph(V, 7, seed=77)
+    g = ops.DeviceGraph(rowptr, col)
+    assert g.max_deg == 7
+    Gd = {k: cu(v) for k, v in G.items()}
+    x0 = (np.random.default_rng(78).random((V, 64), dtype=np.float32) * 2 - 1)
+    x = cu(x0)
+    Wl = {k[len("layers.0."):]: v for k, v in Gd.items() if k.startswith("layers.0.")}
+    a, _ = ops.gnn_layer(g, x, Wl, save=True)
+    g.c.max_deg = claimed
+    g.c.band = 0                      # keep this test on the degree-dispatched kernels
+    b, _ = ops.gnn_layer(g, x, Wl, save=False)
+    c, _ = ops.gnn_layer(g, x, Wl, save=True)     # the training path under the same claim
+    a, b, c = a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy()
+    if claimed == 0:
+        np.testing.assert_array_equal(a, b)
+    else:
+        np.testing.assert_allclose(b, a, atol=2e-6, rtol=1e-6)
+    np.testing.assert_allclose(c, a, atol=2e-6, rtol=1e-6)
+    ref = O.gnn_layer_csr(x0.astype(np.float64), rowptr, col, G, 0)
+    np.testing.assert_allclose(b, ref, atol=1e-5)
+    np.testing.assert_allclose(c, ref, atol=1e-5)
+
+
 def test_star_literal_n4096(ops):
     z, G, _ = _synth()
     Gd = {k: cu(v) for k, v in G.items()}
