@@ -16,8 +16,14 @@
 //   tile's window [d0 - 32, d0 + 96): each tile adds 64 new rows (their x and Ps) and drops 64,
 //   so every node's x is read from HBM once and its Ps computed once per block run -- the
 //   separate Ps projection GEMM (and its 268 MB write + gather at 512 grids) is gone.  Nothing
-//   but x_out leaves the CU.  The weights (three bf16 planes, split once per launch) stream
-//   from L2.
+//   but x_out leaves the CU.  The weights (three bf16 planes in MFMA fragment order, split once
+//   per launch) stream from L2.
+//
+//   MFMA operands that come from LDS are stored ALREADY split: x rows enter the ring as their
+//   three bf16 planes (split once, when the row arrives), and each destination's agg is written
+//   as planes over its own (consumed) Pt row -- the split is exact (x = h + m + l), so the
+//   aggregation and the residual rebuild x from the planes bit for bit.  Only update_net.0's
+//   output (u1, the last GEMM's A) is split in the waves.
 //
 // Edges are never dropped: a destination with any in-degree is aggregated completely, and a
 // source outside the window (a graph that is not banded as the caller claimed) takes a slow
@@ -36,9 +42,10 @@ constexpr int BT = 64;        // destinations per tile
 constexpr int BR = 32;        // band radius the window covers
 constexpr int RING = 128;     // window rows = BT + 2 BR (node n lives in slot n & 127)
 constexpr int BNT = 512;      // threads: 8 waves, one block per CU
-constexpr int XS = 68;        // row strides (floats) = 4 (mod 64): the 32-row MFMA fragment reads
-constexpr int PSS = 132;      //   (lane: row lane & 31, 16 B at k 8 (lane >> 5)) are conflict free
-constexpr int AS = 68;
+constexpr int PSS = 132;      // Pt / agg-plane / [gate | u1] row stride (floats), = 4 (mod 64)
+constexpr int PSRS = 128;     // Ps ring row stride: every row starts on bank 0, and the two
+                              // destinations of a 16-lane read group take opposite halves
+constexpr int XRS = 3 * BF;   // ring row: three planes of 64 bf16 (384 B), 16-B chunks swizzled
 
 // weight planes [3][WTOT] bf16 in MFMA-fragment order: a matrix W [N][K] (nn.Linear [out][in])
 // is stored as (N / 32) x (K / 16) blocks of 512 bf16, block (nb, ks) holding the B operand of
@@ -62,6 +69,13 @@ struct BandW {
 };
 
 __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+
+// 1 / (1 + e^-v) with the hardware exp2 and reciprocal (~1 ulp each) instead of expf and an IEEE
+// division: a few instructions instead of ~20, within 3e-7 relative of torch.sigmoid -- far
+// inside the 2e-6 the layer is held to against the training path (tests/test_gpu_kernels.py)
+__device__ __forceinline__ float sigmoid_fast(float v) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(-v));
+}
 
 // 8 consecutive weights -> their three bf16 planes
 __global__ __launch_bounds__(256) void band_split_weights(const float* __restrict__ w1,
@@ -94,39 +108,46 @@ __global__ __launch_bounds__(256) void band_split_weights(const float* __restric
     *reinterpret_cast<u32x4*>(planes + (size_t)pl * WTOT + dst) = o[pl];
 }
 
-// acc[mb] += A[32 rows of m-block mb][K = 16 KS] . W[32 rows][K]^T on x3 MFMAs.  arow[mb]: this
-// lane's A row in LDS (fp32) at k = 8 (lane >> 5); w: plane 0 of the first fragment block
-// (frag_off(n0, k0, K) + 8 lane; the KS blocks of one row block are consecutive).  Every B
-// fragment is requested before the first MFMA (L2 latency); A is split per step.
-template <int MB, int KS>
-__device__ __forceinline__ void x3_rows(f32x16 (&acc)[MB], const float* const (&arow)[MB],
-                                        const unsigned short* __restrict__ w, int abl = 0) {
+// acc[mb] += A[32 rows of m-block mb][K = 16 KS] . W[32 rows][K]^T on x3 MFMAs, both operands
+// as bf16 planes.  a(mb, ks, pl) -> this lane's A fragment (plane pl of step ks); w: plane 0 of
+// the first weight fragment block (frag_off(n0, k0, K) + 8 lane; the KS blocks of a row block
+// are consecutive).  Every B fragment is requested first; `after_loads` runs between those loads
+// and the first wait for them: global loads it issues stay in flight through this GEMM (the
+// vector-memory counter retires loads in issue order, so a long-latency load issued BEFORE the
+// B loads would hold up the first MFMA).
+struct NoHook {
+  __device__ void operator()() const {}
+};
+
+template <int MB, int KS, int ABL, typename AFrag, typename Hook = NoHook>
+__device__ __forceinline__ void x3_planes(f32x16 (&acc)[MB], const AFrag& afrag,
+                                          const unsigned short* __restrict__ w,
+                                          const Hook& after_loads = Hook()) {
   bf16x8 b[KS][3];
-  if (abl & 16) {                         // tuning ablation: no weight loads
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) b[ks][pl] = bf16x8{};
-  } else {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        b[ks][pl] = *reinterpret_cast<const bf16x8*>(w + (size_t)pl * WTOT + FRAG * ks);
-  }
-  if (abl & 32) return;                   // tuning ablation: no A reads / split / MFMAs
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(arow[mb] + 16 * ks);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(arow[mb] + 16 * ks + 4);
-      u32x4 o[3];
-      split3(x0, x1, o);
-      const bf16x8 a[3] = {__builtin_bit_cast(bf16x8, o[0]), __builtin_bit_cast(bf16x8, o[1]),
-                           __builtin_bit_cast(bf16x8, o[2])};
-      acc[mb] = mfma6_32x32x16(a, b[ks], acc[mb]);
+    for (int pl = 0; pl < 3; ++pl) {
+      if constexpr ((ABL & 16) != 0) b[ks][pl] = bf16x8{};   // tuning ablation: no weight loads
+      else b[ks][pl] = *reinterpret_cast<const bf16x8*>(w + (size_t)pl * WTOT + FRAG * ks);
     }
+  __builtin_amdgcn_sched_barrier(0);
+  after_loads();
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr ((ABL & 32) != 0) return;  // tuning ablation: no A reads / MFMAs
+  // A fragments one k step ahead of their MFMAs (LDS latency behind the previous step's)
+  bf16x8 a[2][MB][3];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) afrag(mb, 0, a[0][mb]);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (ks + 1 < KS) {
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) afrag(mb, ks + 1, a[(ks + 1) & 1][mb]);
+    }
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[mb] = mfma6_32x32x16(a[ks & 1][mb], b[ks], acc[mb]);
+  }
 }
 
 // row of register r of a 32x32 MFMA accumulator (column = lane & 31)
@@ -134,22 +155,35 @@ __device__ __forceinline__ int acc_row(int r, int lane) {
   return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
 }
 
+// ring row `slot`, plane pl, 16-B chunk c (8 features) -> bf16 offset; the chunk index is
+// XOR-swizzled by (slot >> 1) & 7 so the 32 rows of an MFMA fragment read hit distinct banks
+__device__ __forceinline__ int xr_off(int slot, int pl, int c) {
+  return slot * XRS + pl * BF + ((c ^ ((slot >> 1) & 7)) << 3);
+}
+
+__device__ __forceinline__ void zero(f32x16& a) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) a[r] = 0.f;
+}
+
 }  // namespace
 
+// ABL != 0 only in the tuning build: timing ablations, results wrong by design (bits 1 / 2 / 4 /
+// 8 = no phase A / B / C / D math, 16 = no weight loads, 64 = no x_out stores, 128 = no x loads)
+template <int ABL>
 __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
-    int V, const int* __restrict__ rowptr, const int* __restrict__ col,
-    const float* __restrict__ x, BandW W, float* __restrict__ x_out, int ntiles, int per,
-    int abl) {
-  __shared__ __attribute__((aligned(16))) float XR[RING * XS];   // x rows of the window
-  __shared__ __attribute__((aligned(16))) float PSR[RING * PSS]; // Ps rows of the window
-  __shared__ __attribute__((aligned(16))) float PT[BT * PSS];    // Pt; then C partials; then u1
-  __shared__ __attribute__((aligned(16))) float AG[BT * AS];     // agg; then gate
+    int V, int E, const int* __restrict__ rowptr, const int* __restrict__ col,
+    const float* __restrict__ x, BandW W, float* __restrict__ x_out, int ntiles, int per) {
+  __shared__ __attribute__((aligned(16))) unsigned short XR[RING * XRS];  // x planes (ring)
+  __shared__ __attribute__((aligned(16))) float PSR[RING * PSRS]; // Ps rows of the window
+  __shared__ __attribute__((aligned(16))) float PT[BT * PSS];     // Pt -> agg planes ->
+                                                                   // C partials -> [gate | u1]
   __shared__ __attribute__((aligned(16))) float B1W2[2 * BH];
   __shared__ int DEG[BT];
   __shared__ int RPS[2][BT + 1];          // rowptr of the tile's destinations (+1), prefetched
   __shared__ int CLS[2][BNT];             // the tile's sources (col), when it has <= 512 edges
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int lr = lane & 31, hk = 8 * (lane >> 5);
+  const int lr = lane & 31, hc = lane >> 5;          // fragment row, k half (8-element chunk)
   const int t0 = blockIdx.x * per, t1 = min(ntiles, t0 + per);
   if (t0 >= t1) return;                   // uniform per block
   if (tid < BH) {
@@ -158,39 +192,61 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   }
   const float b2 = W.b2[0];
 
-  // 64 x rows [r0, r0 + 64) <-> the ring: thread = (row tid >> 3, 8 floats at 8 (tid & 7))
+  // 64 x rows [r0, r0 + 64) -> the ring as planes: thread = (row tid >> 3, features 8 (tid & 7))
+  // (every load is unconditional -- clamped address, result masked -- so the compiler can count
+  // the loads in flight instead of draining all of them at the next wait)
   auto load_rows = [&](int r0, f32x4 (&v)[2]) {
     const int n = r0 + (tid >> 3), c = (tid & 7) * 8;
-    if (n >= 0 && n < V) {
-      v[0] = *reinterpret_cast<const f32x4*>(x + (size_t)n * BF + c);
-      v[1] = *reinterpret_cast<const f32x4*>(x + (size_t)n * BF + c + 4);
-    } else {
-      v[0] = v[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    const size_t nc = (size_t)min(max(n, 0), V - 1) * BF + c;
+    v[0] = *reinterpret_cast<const f32x4*>(x + nc);
+    v[1] = *reinterpret_cast<const f32x4*>(x + nc + 4);
+    if (n < 0 || n >= V) v[0] = v[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
   auto store_rows = [&](int r0, const f32x4 (&v)[2]) {
-    const int n = r0 + (tid >> 3), c = (tid & 7) * 8;
-    float* d = XR + (n & (RING - 1)) * XS + c;
-    *reinterpret_cast<f32x4*>(d) = v[0];
-    *reinterpret_cast<f32x4*>(d + 4) = v[1];
+    const int slot = (r0 + (tid >> 3)) & (RING - 1);
+    u32x4 o[3];
+    split3(v[0], v[1], o);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      *reinterpret_cast<u32x4*>(XR + xr_off(slot, pl, tid & 7)) = o[pl];
+  };
+  // x of ring row `slot`, features 8c .. 8c + 7, rebuilt exactly from its planes
+  auto x_ring = [&](int slot, int c, f32x4 (&v)[2]) {
+    const u32x4 h = *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 0, c));
+    const u32x4 m = *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 1, c));
+    const u32x4 l = *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 2, c));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float lo = (__uint_as_float(h[q] << 16) + __uint_as_float(m[q] << 16)) +
+                       __uint_as_float(l[q] << 16);
+      const float hi = (__uint_as_float(h[q] & 0xFFFF0000u) + __uint_as_float(m[q] & 0xFFFF0000u)) +
+                       __uint_as_float(l[q] & 0xFFFF0000u);
+      v[q >> 1][2 * (q & 1)] = lo;
+      v[q >> 1][2 * (q & 1) + 1] = hi;
+    }
+  };
+  // A fragments straight from the ring planes: rows r0 + 32 mb + (lane & 31)
+  auto ring_frag = [&](int r0) {
+    return [=](int mb, int ks, bf16x8 (&a)[3]) {
+      const int slot = (r0 + 32 * mb + lr) & (RING - 1);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[pl] = *reinterpret_cast<const bf16x8*>(XR + xr_off(slot, pl, 2 * ks + hc));
+    };
   };
   // Ps rows [r0, r0 + 64) into the ring (waves 4-7: wave = n-block, both m-blocks)
-  auto ps_rows = [&](int r0) {
+  auto ps_rows = [&](int r0, auto hook) {
     const int nb = wave - 4;
     f32x16 acc[2];
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mb][r] = 0.f;
-    const float* const arow[2] = {XR + ((r0 + lr) & (RING - 1)) * XS + hk,
-                                  XR + ((r0 + 32 + lr) & (RING - 1)) * XS + hk};
-    x3_rows<2, 4>(acc, arow, W.planes + W1_OFF + frag_off(32 * nb, BF, 2 * BF) + 8 * lane,
-                  (abl & 1) ? (abl | 32) : abl);
+    zero(acc[0]);
+    zero(acc[1]);
+    x3_planes<2, 4, (ABL & 1) ? (ABL | 32) : ABL>(
+        acc, ring_frag(r0), W.planes + W1_OFF + frag_off(32 * nb, BF, 2 * BF) + 8 * lane, hook);
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        PSR[((r0 + 32 * mb + acc_row(r, lane)) & (RING - 1)) * PSS + 32 * nb + lr] = acc[mb][r];
+        PSR[((r0 + 32 * mb + acc_row(r, lane)) & (RING - 1)) * PSRS + 32 * nb + lr] = acc[mb][r];
   };
 
   // prologue: the first tile's window [d0 - 32, d0 + 96) and the Ps of its first 64 rows
@@ -201,11 +257,14 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     store_rows(d0 - BR, v);
     load_rows(d0 + BR, v);
     store_rows(d0 + BR, v);
-    if (tid <= BT) RPS[t0 & 1][tid] = rowptr[min(d0 + tid, V)];
+    if (tid <= BT) {
+      RPS[t0 & 1][tid] = rowptr[min(d0 + tid, V)];
+      if (t0 + 1 < t1) RPS[(t0 + 1) & 1][tid] = rowptr[min(d0 + BT + tid, V)];
+    }
     __syncthreads();
     const int eb = RPS[t0 & 1][0], ne = RPS[t0 & 1][BT] - eb;
     if (tid < ne && ne <= BNT) CLS[t0 & 1][tid] = col[eb + tid];
-    if (wave >= 4) ps_rows(d0 - BR);
+    if (wave >= 4) ps_rows(d0 - BR, NoHook());
   }
 
   // edge-phase lane roles: destination i (8 lanes), hidden units 4j + 32c (+0..3), features 8j..
@@ -217,201 +276,213 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     const int lo = d0 - BR;               // the window: nodes [lo, lo + RING)
     const bool has_next = tile + 1 < t1;
     const int cur = tile & 1, nxt = cur ^ 1;
-    f32x4 nextx[2];                       // the next tile's new rows [d0 + 96, d0 + 160)
-    if (has_next) load_rows(d0 + BT + BR, nextx);
-    int rpn = 0, cln = 0;                 // the next tile's rowptr (tid <= 64), then its col
-    if (has_next && tid <= BT) rpn = rowptr[min(d0 + BT + tid, V)];
+    // prefetch, issued at the start of the edge phase and stored at the end of the tile: the
+    // next tile's new x rows [d0 + 96, d0 + 160), its sources (col, from its rowptr staged a
+    // tile earlier) and the rowptr of the tile after it
+    f32x4 nextx[2];
+    int cln = 0, rp2 = 0;
+    auto prefetch = [&]() {               // unconditional (clamped) loads, see load_rows
+      if constexpr ((ABL & 128) != 0) nextx[0] = nextx[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      else load_rows(d0 + BT + BR, nextx);
+      cln = col[min(RPS[nxt][0] + tid, E - 1)];
+      rp2 = rowptr[min(d0 + 2 * BT + min(tid, BT), V)];
+    };
 
     // ---- A: Pt (waves 0-3: wave = n-block) | Ps of rows [d0 + 32, d0 + 96) (waves 4-7)
     if (wave < 4) {
       f32x16 acc[2];
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[mb][r] = 0.f;
-      const float* const arow[2] = {XR + ((d0 + lr) & (RING - 1)) * XS + hk,
-                                    XR + ((d0 + 32 + lr) & (RING - 1)) * XS + hk};
-      x3_rows<2, 4>(acc, arow, W.planes + W1_OFF + frag_off(32 * wave, 0, 2 * BF) + 8 * lane,
-                    (abl & 1) ? (abl | 32) : abl);
+      zero(acc[0]);
+      zero(acc[1]);
+      x3_planes<2, 4, (ABL & 1) ? (ABL | 32) : ABL>(
+          acc, ring_frag(d0), W.planes + W1_OFF + frag_off(32 * wave, 0, 2 * BF) + 8 * lane);
+      const float b1n = B1W2[32 * wave + lr];     // attention.0's bias, folded into Pt
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          PT[(32 * mb + acc_row(r, lane)) * PSS + 32 * wave + lr] = acc[mb][r];
+          PT[(32 * mb + acc_row(r, lane)) * PSS + 32 * wave + lr] = acc[mb][r] + b1n;
     } else {
-      ps_rows(d0 + BR);
+      ps_rows(d0 + BR, NoHook());
     }
     __syncthreads();
 
-    // ---- B: attention scores and normalised aggregation (gnn_utils.py:48-65)
-    if (abl & 2) {                        // tuning ablation: no edge phase
+    // ---- B: attention scores and normalised aggregation (gnn_utils.py:48-65); each
+    //      destination's agg replaces its Pt row, as three planes.  The prefetch goes out first:
+    //      this phase issues no other global load, so its HBM latency hides behind the edge
+    //      math (the vector-memory counter retires in order: issued before a GEMM's weight
+    //      loads, it would hold up that GEMM's first MFMA)
+    prefetch();
+    if constexpr ((ABL & 2) != 0) {       // tuning ablation: no edge phase
       if (tid < BT) DEG[tid] = 0;
     } else {
       const int d = d0 + ei;
       const int eb = RPS[cur][0], ne = RPS[cur][BT] - eb;
       const int e0 = RPS[cur][ei], deg = RPS[cur][ei + 1] - e0;   // 0 past V
-      const bool staged = ne <= BNT;
-      auto col_of = [&](int q) { return staged ? CLS[cur][e0 - eb + q] : col[e0 + q]; };
-      f32x4 pt[4], bb[4], ww[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        pt[c] = *reinterpret_cast<const f32x4*>(PT + ei * PSS + 4 * ej + 32 * c);
-        bb[c] = *reinterpret_cast<const f32x4*>(B1W2 + 4 * ej + 32 * c);
-        ww[c] = *reinterpret_cast<const f32x4*>(B1W2 + BH + 4 * ej + 32 * c);
-      }
-      auto alpha_of = [&](int s) {
-        float acc = 0.f;
-        if ((unsigned)(s - lo) < (unsigned)RING) {
-          const float* ps = PSR + (s & (RING - 1)) * PSS + 4 * ej;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const f32x4 p = *reinterpret_cast<const f32x4*>(ps + 32 * c);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc = fmaf(relu(pt[c][u] + p[u] + bb[c][u]), ww[c][u], acc);
-          }
-        } else {    // source outside the window: its Ps from global memory, on the VALU
-          const float* xs = x + (size_t)s * BF;
-#pragma unroll 1
-          for (int q = 0; q < 16; ++q) {
-            const int c = q >> 2, u = q & 3;
-            const float* wr = W.w1 + (size_t)(4 * ej + 32 * c + u) * (2 * BF) + BF;
-            float p = 0.f;
-#pragma unroll 4
-            for (int k = 0; k < BF; ++k) p = fmaf(wr[k], xs[k], p);
-            const float hb = B1W2[4 * ej + 32 * c + u], hw = B1W2[BH + 4 * ej + 32 * c + u];
-            const float ht = PT[ei * PSS + 4 * ej + 32 * c + u];
-            acc = fmaf(relu(ht + p + hb), hw, acc);
-          }
-        }
-#pragma unroll
-        for (int o = 4; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 8);
-        return sigmoidf_ref(acc + b2);
-      };
-      auto x_of = [&](int s, f32x4 (&v)[2]) {
-        const float* src = (unsigned)(s - lo) < (unsigned)RING ? XR + (s & (RING - 1)) * XS
-                                                               : x + (size_t)s * BF;
-        v[0] = *reinterpret_cast<const f32x4*>(src + 8 * ej);
-        v[1] = *reinterpret_cast<const f32x4*>(src + 8 * ej + 4);
-      };
-      int src[4];
-      float a[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) src[q] = q < deg ? col_of(q) : d;
-      float S = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        a[q] = 0.f;
-        if (q < deg) {
-          a[q] = alpha_of(src[q]);
-          S += a[q];
-        }
-      }
-#pragma unroll 1
-      for (int q = 4; q < deg; ++q) S += alpha_of(col_of(q));
-      const bool norm = S > 0.f;
-      f32x4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (q < deg) {
-          const float wq = norm ? a[q] / S : a[q];
-          f32x4 v[2];
-          x_of(src[q], v);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            g0[c] = fmaf(wq, v[0][c], g0[c]);
-            g1[c] = fmaf(wq, v[1][c], g1[c]);
-          }
-        }
-#pragma unroll 1
-      for (int q = 4; q < deg; ++q) {
-        const int s = col_of(q);
-        const float aq = alpha_of(s);
-        const float wq = norm ? aq / S : aq;
-        f32x4 v[2];
-        x_of(s, v);
+      // the edge math, once for staged sources (LDS) and once for a tile with > 512 edges
+      // (global col): two instantiations, so neither load is a generic (flat) one that would
+      // make the compiler drain the prefetch before it
+      auto edges = [&](auto col_of) {
+        // lane: hidden units 4 ej + 32 cc (+0..3), cc = c ^ (ei & 1) -- the two destinations
+        // of a 16-lane LDS read group read opposite 128-B halves of their rows
+        const int par = ei & 1;
+        f32x4 pt[4], ww[4];                 // Pt + b1, w2
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          g0[c] = fmaf(wq, v[0][c], g0[c]);
-          g1[c] = fmaf(wq, v[1][c], g1[c]);
+          pt[c] = *reinterpret_cast<const f32x4*>(PT + ei * PSS + 4 * ej + 32 * (c ^ par));
+          ww[c] = *reinterpret_cast<const f32x4*>(B1W2 + BH + 4 * ej + 32 * (c ^ par));
         }
-      }
-      *reinterpret_cast<f32x4*>(AG + ei * AS + 8 * ej) = g0;
-      *reinterpret_cast<f32x4*>(AG + ei * AS + 8 * ej + 4) = g1;
+        auto alpha_of = [&](int s) {
+          float acc = 0.f;
+          if ((unsigned)(s - lo) < (unsigned)RING) {
+            const float* ps = PSR + (s & (RING - 1)) * PSRS + 4 * ej;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const f32x4 p = *reinterpret_cast<const f32x4*>(ps + 32 * (c ^ par));
+#pragma unroll
+              for (int u = 0; u < 4; ++u) acc = fmaf(relu(pt[c][u] + p[u]), ww[c][u], acc);
+            }
+          } else {    // source outside the window: its Ps from global memory, on the VALU
+            const float* xs = x + (size_t)s * BF;
+#pragma unroll 1
+            for (int q = 0; q < 16; ++q) {
+              const int c = q >> 2, u = q & 3, h = 4 * ej + 32 * (c ^ par) + u;
+              const float* wr = W.w1 + (size_t)h * (2 * BF) + BF;
+              float p = 0.f;
+#pragma unroll 4
+              for (int k = 0; k < BF; ++k) p = fmaf(wr[k], xs[k], p);
+              acc = fmaf(relu(PT[ei * PSS + h] + p), B1W2[BH + h], acc);
+            }
+          }
+#pragma unroll
+          for (int o = 4; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 8);
+          return sigmoid_fast(acc + b2);
+        };
+        auto x_of = [&](int s, f32x4 (&v)[2]) {
+          if ((unsigned)(s - lo) < (unsigned)RING) {
+            x_ring(s & (RING - 1), ej, v);
+          } else {
+            v[0] = *reinterpret_cast<const f32x4*>(x + (size_t)s * BF + 8 * ej);
+            v[1] = *reinterpret_cast<const f32x4*>(x + (size_t)s * BF + 8 * ej + 4);
+          }
+        };
+        int src[4];
+        float a[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) src[q] = q < deg ? col_of(q) : d;
+        float S = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a[q] = 0.f;
+          if (q < deg) {
+            a[q] = alpha_of(src[q]);
+            S += a[q];
+          }
+        }
+#pragma unroll 1
+        for (int q = 4; q < deg; ++q) S += alpha_of(col_of(q));
+        const bool norm = S > 0.f;
+        f32x4 g[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (q < deg) {
+            const float wq = norm ? a[q] / S : a[q];
+            f32x4 v[2];
+            x_of(src[q], v);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              g[0][c] = fmaf(wq, v[0][c], g[0][c]);
+              g[1][c] = fmaf(wq, v[1][c], g[1][c]);
+            }
+          }
+#pragma unroll 1
+        for (int q = 4; q < deg; ++q) {
+          const int s = col_of(q);
+          const float aq = alpha_of(s);
+          const float wq = norm ? aq / S : aq;
+          f32x4 v[2];
+          x_of(s, v);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            g[0][c] = fmaf(wq, v[0][c], g[0][c]);
+            g[1][c] = fmaf(wq, v[1][c], g[1][c]);
+          }
+        }
+        // the group's 8 lanes read their Pt row above (same wave, in order): the row now takes
+        // agg's planes, plane pl at byte 128 pl, 16-B chunk ej
+        u32x4 o[3];
+        split3(g[0], g[1], o);
+        unsigned short* arow = reinterpret_cast<unsigned short*>(PT + ei * PSS);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(arow + pl * BF + 8 * ej) = o[pl];
+      };
+      if (ne <= BNT) edges([&](int q) { return CLS[cur][e0 - eb + q]; });
+      else edges([&](int q) { return col[e0 + q]; });
       if (ej == 0) DEG[ei] = deg;
     }
     __syncthreads();
 
-    // ---- C: [gate | u1] over [x_d ; agg]: waves 0-3 the x_d half of K, 4-7 the agg half;
-    //      wave & 3 = 32-column quarter of the 128 outputs (0-1 gate, 2-3 u1)
+    // ---- C: [gate | u1] over [x_d ; agg]: waves 0-3 the x_d half of K (ring planes), 4-7 the
+    //      agg half (planes in the Pt rows); wave & 3 = 32-column quarter (0-1 gate, 2-3 u1)
     {
       const int nq = wave & 3, kh = wave >> 2;
       f32x16 acc[2];
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[mb][r] = 0.f;
-      const float* arow[2];
+      zero(acc[0]);
+      zero(acc[1]);
+      const unsigned short* wc = W.planes + WC_OFF + frag_off(32 * nq, BF * kh, 2 * BF) + 8 * lane;
+      constexpr int CAB = (ABL & 4) ? (ABL | 32) : ABL;
       if (kh == 0) {
-        arow[0] = XR + ((d0 + lr) & (RING - 1)) * XS + hk;
-        arow[1] = XR + ((d0 + 32 + lr) & (RING - 1)) * XS + hk;
+        x3_planes<2, 4, CAB>(acc, ring_frag(d0), wc);
       } else {
-        arow[0] = AG + lr * AS + hk;
-        arow[1] = AG + (32 + lr) * AS + hk;
+        x3_planes<2, 4, CAB>(acc, [&](int mb, int ks, bf16x8 (&a)[3]) {
+          const unsigned short* row = reinterpret_cast<const unsigned short*>(PT + (32 * mb + lr) * PSS);
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            a[pl] = *reinterpret_cast<const bf16x8*>(row + pl * BF + 8 * (2 * ks + hc));
+        }, wc);
       }
-      const float* const ar[2] = {arow[0], arow[1]};
-      x3_rows<2, 4>(acc, ar, W.planes + WC_OFF + frag_off(32 * nq, BF * kh, 2 * BF) + 8 * lane,
-                    (abl & 4) ? (abl | 32) : abl);
-      // the agg half's partials -> PT (accumulator layout), summed by the partner wave in order
+      __syncthreads();                    // agg planes read: PT takes the partials
+      // the two K halves' partials meet in PT (accumulator layout): each wave of a pair keeps
+      // m-block kh, hands the other to its partner, and finishes its own (sum = x_d half + agg
+      // half either way round: fp32 addition commutes)
       float* part = PT + nq * 2048 + lane;
-      if (kh == 1) {
+      f32x16 mine;
+      if (kh == 0) {
 #pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
+        for (int r = 0; r < 16; ++r) part[(16 + r) * 64] = acc[1][r];
+        mine = acc[0];
+      } else {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) part[(mb * 16 + r) * 64] = acc[mb][r];
+        for (int r = 0; r < 16; ++r) part[r * 64] = acc[0][r];
+        mine = acc[1];
       }
-      if (has_next && tid <= BT) RPS[nxt][tid] = rpn;
       __syncthreads();
-      if (has_next) {                     // the next tile's sources, in flight during D
-        const int nb0 = RPS[nxt][0], nn = RPS[nxt][BT] - nb0;
-        if (tid < nn && nn <= BNT) cln = col[nb0 + tid];
-      }
-      if (kh == 0) {
 #pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
+      for (int r = 0; r < 16; ++r) mine[r] += part[(kh * 16 + r) * 64];
+      __syncthreads();                    // partials read: PT takes [gate | u1]
+      const int n = 32 * nq + lr;         // output column: gate (n < 64) or u1 (n - 64)
+      const float bias = nq < 2 ? W.gb[n] : W.ub1[n - BF];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[mb][r] += part[(mb * 16 + r) * 64];
-      }
-      __syncthreads();                    // partials read: PT and AG are free
-      if (kh == 0) {
-        const int n = 32 * nq + lr;       // output column: gate (n < 64) or u1 (n - 64)
-        if (nq < 2) {
-          const float bias = W.gb[n];
-#pragma unroll
-          for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              AG[(32 * mb + acc_row(r, lane)) * AS + n] = sigmoidf_ref(acc[mb][r] + bias);
-        } else {
-          const float bias = W.ub1[n - BF];
-#pragma unroll
-          for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              PT[(32 * mb + acc_row(r, lane)) * PSS + (n - BF)] = relu(acc[mb][r] + bias);
-        }
+      for (int r = 0; r < 16; ++r) {
+        const float v = mine[r] + bias;
+        PT[(32 * kh + acc_row(r, lane)) * PSS + n] = nq < 2 ? sigmoid_fast(v) : relu(v);
       }
     }
     __syncthreads();
 
-    // ---- D: x_out = x_d + gate * (u1 Wu2^T + bu2)  (waves 0-3: 32 x 32 each)
+    // ---- D: x_out = x_d + gate * (u1 Wu2^T + bu2)  (waves 0-3: 32 x 32 each; u1 split here)
     if (wave < 4) {
       const int mb = wave >> 1, nb = wave & 1;
       f32x16 acc[1];
+      zero(acc[0]);
+      x3_planes<1, 4, (ABL & 8) ? (ABL | 32) : ABL>(acc, [&](int, int ks, bf16x8 (&a)[3]) {
+        const float* u = PT + (32 * mb + lr) * PSS + BF + 16 * ks + 8 * hc;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(u);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(u + 4);
+        u32x4 o[3];
+        split3(x0, x1, o);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[0][r] = 0.f;
-      const float* const arow[1] = {PT + (32 * mb + lr) * PSS + hk};
-      x3_rows<1, 4>(acc, arow, W.planes + WU2_OFF + frag_off(32 * nb, 0, BF) + 8 * lane,
-                    (abl & 8) ? (abl | 32) : abl);
+        for (int pl = 0; pl < 3; ++pl) a[pl] = __builtin_bit_cast(bf16x8, o[pl]);
+      }, W.planes + WU2_OFF + frag_off(32 * nb, 0, BF) + 8 * lane);
       const int n = 32 * nb + lr;
       const float ub = W.ub2[n];
 #pragma unroll
@@ -419,17 +490,23 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         const int row = 32 * mb + acc_row(r, lane);
         const int d = d0 + row;
         if (d < V) {
-          const float xd = XR[(d & (RING - 1)) * XS + n];
-          x_out[(size_t)d * BF + n] =
-              DEG[row] > 0 ? xd + AG[row * AS + n] * (acc[0][r] + ub) : xd;
+          const int slot = d & (RING - 1);
+          const int k = xr_off(slot, 0, n >> 3) + (n & 7);
+          const float xd = (__uint_as_float((unsigned)XR[k] << 16) +
+                            __uint_as_float((unsigned)XR[k + BF] << 16)) +
+                           __uint_as_float((unsigned)XR[k + 2 * BF] << 16);
+          const float o = DEG[row] > 0 ? xd + PT[row * PSS + n] * (acc[0][r] + ub) : xd;
+          if constexpr ((ABL & 64) == 0) x_out[(size_t)d * BF + n] = o;
+          else if (o == 12345.f) x_out[0] = o;
         }
       }
     }
     __syncthreads();                      // x_d rows read: their slots take the next rows
     if (has_next) {
       store_rows(d0 + BT + BR, nextx);
-      CLS[nxt][tid] = cln;
+      CLS[nxt][tid] = cln;                // used only when the next tile has <= 512 edges
     }
+    if (tile + 2 < t1 && tid <= BT) RPS[cur][tid] = rp2;   // tile + 2 has this tile's parity
     __syncthreads();
   }
 }
@@ -462,14 +539,26 @@ int gnn_layer_band(const az_graph* g, const float* x, const az_gnn_layer_w* w, f
   const int blocks = (ntiles + per - 1) / per;
   const BandW bw = {planes, w->att_w1, w->att_b1, w->att_w2, w->att_b2, w->gate_b, w->upd_b1,
                     w->upd_b2};
-  int abl = 0;
-#ifdef AZ_TUNING   // timing ablations (results wrong by design): AZ_BAND_ABL bits 1 / 2 / 4 / 8 =
-                   // no phase A / B / C / D math, 16 = no weight loads
+#define AZ_BAND(A_)                                                                          \
+  hipLaunchKernelGGL(gnn_layer_band_kernel<A_>, dim3(blocks), dim3(BNT), 0, s, g->V, g->E,    \
+                     g->rowptr, g->col, x, bw, x_out, ntiles, per)
+#ifdef AZ_TUNING   // timing ablations (tools/gpu_band_abl.sh): AZ_BAND_ABL=<bits>
   static const char* env_abl = tuning_env("AZ_BAND_ABL");
-  abl = env_abl ? atoi(env_abl) : 0;
+  switch (env_abl ? atoi(env_abl) : 0) {
+    case 1: AZ_BAND(1); break;
+    case 2: AZ_BAND(2); break;
+    case 4: AZ_BAND(4); break;
+    case 8: AZ_BAND(8); break;
+    case 16: AZ_BAND(16); break;
+    case 15: AZ_BAND(15); break;
+    case 31: AZ_BAND(31); break;
+    case 223: AZ_BAND(223); break;
+    default: AZ_BAND(0); break;
+  }
+#else
+  AZ_BAND(0);
 #endif
-  hipLaunchKernelGGL(gnn_layer_band_kernel, dim3(blocks), dim3(BNT), 0, s, g->V, g->rowptr, g->col,
-                     x, bw, x_out, ntiles, per, abl);
+#undef AZ_BAND
   return check_launch("gnn_layer_band_kernel");
 }
 

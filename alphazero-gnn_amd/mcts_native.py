@@ -363,31 +363,39 @@ def _assemble_connect4(game, use_gnn, rec):
     """assemble_episode for Connect4Game with whole-episode array operations.  The objects are
     the generic path's: getSymmetries' identity comes first, so the GNN example's board is the
     canonical board itself; the mirror is np.fliplr (a view) and mirror_pi np.copy of the pi
-    list (int64 for a temp-0 one-hot, float64 otherwise) with its first n entries reversed."""
+    list (int64 for a temp-0 one-hot, float64 otherwise) with its first n entries reversed.
+    Per-move objects are rows (views) of whole-episode arrays the record owns, converted to
+    lists / scalars once per episode, not per move."""
     n = game.board_size
     boards = rec["boards"].astype(np.int64)
     flips = boards[:, :, ::-1]
     pis = rec["pi"]
-    one_hot = rec["temp"] == 0
+    one_hot = (rec["temp"] == 0).tolist()
     mirror_f = pis.copy()
     mirror_f[:, :n] = pis[:, n - 1::-1]
     mirror_i = mirror_f.astype(np.int64)
+    pl_f, pl_i = pis.tolist(), pis.astype(np.int64).tolist()
     curs = rec["cur"].tolist()
     r = rec["result"]
     last = -int(curs[-1])
-    std, gnn = [], []
-    for i, cur in enumerate(curs):
-        sg = r * ((-1) ** (cur != last))
+    signs = [r * ((-1) ** (c != last)) for c in curs]
+    std = []
+    for i, sg in enumerate(signs):
         if one_hot[i]:
-            pl, mp = pis[i].astype(np.int64).tolist(), mirror_i[i]
+            std.append((boards[i], pl_i[i], sg))
+            std.append((flips[i], mirror_i[i], sg))
         else:
-            pl, mp = pis[i].tolist(), mirror_f[i]
-        std.append((boards[i], pl, sg))
-        std.append((flips[i], mp, sg))
-        if use_gnn:
-            gnn.append((boards[i], cur, rec["init_policy"][i].copy(), np.float32(rec["std_v"][i]),
-                        rec["exp_policy"][i].copy(),
-                        typed_q(int(rec["exp_value_tag"][i]), rec["exp_value"][i]), sg))
+            std.append((boards[i], pl_f[i], sg))
+            std.append((flips[i], mirror_f[i], sg))
+    if not use_gnn:
+        return std, []
+    ip, ep = rec["init_policy"], rec["exp_policy"]      # arrays of this record alone
+    sv = rec["std_v"]                                   # float32: sv[i] is an np.float32
+    tags, vals = rec["exp_value_tag"], rec["exp_value"]
+    v32 = vals.astype(np.float32)
+    ev = [typed_q(t, v) if t != TAG_F32 else v32[i]
+          for i, (t, v) in enumerate(zip(tags.tolist(), vals.tolist()))]
+    gnn = [(boards[i], c, ip[i], sv[i], ep[i], ev[i], signs[i]) for i, c in enumerate(curs)]
     return std, gnn
 
 

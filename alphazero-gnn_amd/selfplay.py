@@ -31,6 +31,7 @@ import os
 
 import numpy as np
 
+import hostcpu
 import nn_fallback
 from Coach import episode_g
 from MCTS import MCTS
@@ -276,7 +277,7 @@ def play_episodes_native(game, nnet, args, episodes, seeds, parallel_games=256, 
     batched network launch -> feed -> resume.  Same per-episode results as play_episodes for
     any lane count or slot count (each game owns its RandomState and tree)."""
     import time
-    threads = int(threads or min(16, os.cpu_count() or 1))
+    threads = int(threads or hostcpu.threads_per_rank())
     use_gnn = bool(getattr(args, "use_gnn", False) if not isinstance(args, dict)
                    else args.get("use_gnn", False))
     cpuct = args["cpuct"] if isinstance(args, dict) else args.cpuct
@@ -338,6 +339,7 @@ class _EpisodeLane:
         self.k = 0
         self.rounds = self.rows = 0
         self.assemble_s = 0.0
+        self.assembler, self.pending = None, []
 
     def start(self):
         while self.queue and self.free:
@@ -348,15 +350,28 @@ class _EpisodeLane:
             self.running[slot] = e
 
     def harvest(self):
+        """Finished slots: their records are copied out now (the slot is reused right away);
+        the examples are assembled on the assembler thread when there is one (the engine's
+        calls release the GIL, so assembly overlaps the search and the GPU wait)."""
         import time
         from mcts_native import assemble_episode
         t = time.perf_counter()
         for slot in self.eng.episodes_finished():
             e = self.running.pop(slot)
-            self.results[e] = assemble_episode(self.game, self.args, self.eng.episode_record(slot))
+            rec = self.eng.episode_record(slot)
+            if self.assembler is None:
+                self.results[e] = assemble_episode(self.game, self.args, rec)
+            else:
+                self.pending.append((e, self.assembler.submit(assemble_episode, self.game,
+                                                              self.args, rec)))
             self.free.append(slot)
         self.assemble_s += time.perf_counter() - t
         self.start()
+
+    def finish(self):
+        for e, f in self.pending:
+            self.results[e] = f.result()
+        self.pending = []
 
     def gather(self):
         self.k = self.eng.collect(self.threads)
@@ -392,7 +407,7 @@ class _EpisodeLane:
 
 
 def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024, threads=None,
-                         stats=None, lanes=2):
+                         stats=None, lanes=2, assembler_thread=True):
     """Whole self-play episodes in the native engine (episode mode, include/az_mcts.h): search,
     pi, move draws with each game's RandomState emulated draw for draw, expand_tree, rules --
     Python only batches the leaves for the network and assembles each finished game's
@@ -400,7 +415,7 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
     (tests/test_native_mcts.py)."""
     import time
     _ = _args_val(args, "numMCTSSims")
-    threads = int(threads or min(16, os.cpu_count() or 1))
+    threads = int(threads or hostcpu.threads_per_rank())
     use_gnn = bool(_args_val(args, "use_gnn", False))
     episodes = list(episodes)
     G = max(1, min(int(parallel_games), len(episodes) or 1))
@@ -411,6 +426,12 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
     L = [_EpisodeLane(game, args, n, _args_val(args, "cpuct"), use_gnn, threads, queue, seeds,
                       results, _args_val(args, "numMCTSSims"), _args_val(args, "expand_by", 5),
                       _args_val(args, "tempThreshold")) for n in per]
+    pool = None
+    if assembler_thread:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="az-assemble")
+        for lane in L:
+            lane.assembler = pool
     for lane in L:
         lane.start()
     inflight = [None] * lanes
@@ -418,29 +439,38 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
     t_wait = 0.0
     idle = 0
     i = 0
-    while any(lane.live() for lane in L) or any(x is not None for x in inflight):
-        lane = L[i]
-        if inflight[i] is not None:
-            tw = time.perf_counter()
-            p, inflight[i] = inflight[i], None
-            if hasattr(p, "event"):
-                p.event.synchronize()
-            t_wait += time.perf_counter() - tw
-            lane.deliver(p)
-            idle = 0
-        if lane.live():
-            boards = lane.gather()
-            if boards is not None:
-                inflight[i] = _launch(nnet, boards, use_gnn)
+    try:
+        while any(lane.live() for lane in L) or any(x is not None for x in inflight):
+            lane = L[i]
+            if inflight[i] is not None:
+                tw = time.perf_counter()
+                p, inflight[i] = inflight[i], None
+                if hasattr(p, "event"):
+                    p.event.synchronize()
+                t_wait += time.perf_counter() - tw
+                lane.deliver(p)
                 idle = 0
-            else:
-                lane.deliver(None)
-                idle += 1
-                if idle > 4 * lanes + 4 and not any(x is not None for x in inflight) and \
-                        any(ln.live() for ln in L):
-                    raise RuntimeError("native self-play made no progress (engine/driver bug)")
-        i = (i + 1) % lanes
+            if lane.live():
+                boards = lane.gather()
+                if boards is not None:
+                    inflight[i] = _launch(nnet, boards, use_gnn)
+                    idle = 0
+                else:
+                    lane.deliver(None)
+                    idle += 1
+                    if idle > 4 * lanes + 4 and not any(x is not None for x in inflight) and \
+                            any(ln.live() for ln in L):
+                        raise RuntimeError("native self-play made no progress (engine/driver bug)")
+            i = (i + 1) % lanes
+        tf = time.perf_counter()
+        for lane in L:
+            lane.finish()
+        drain_s = time.perf_counter() - tf
+    finally:
+        if pool is not None:
+            pool.shutdown(wait=True)
     if stats is not None:
+        stats["assemble_drain_s"] = drain_s
         stats.update(rounds=sum(ln.rounds for ln in L), rows=sum(ln.rows for ln in L),
                      net_s=t_wait, host_s=time.perf_counter() - t0 - t_wait, lanes=lanes,
                      assemble_s=sum(ln.assemble_s for ln in L))

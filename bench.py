@@ -54,7 +54,9 @@ def parse():
     ap.add_argument("--sp-games", type=int, default=4096,
                     help="self-play leg: games per GPU, all played in lock step (4096: 'tools/sp_sweep.py' r02s, 779 vs 702 games/s for 2048 with the x3 GEMMs)")
     ap.add_argument("--sp-sims", type=int, default=100, help="numMCTSSims (SURVEY §8d config 3)")
-    ap.add_argument("--sp-threads", type=int, default=16, help="host threads for the engine")
+    ap.add_argument("--sp-threads", type=int, default=0,
+                    help="host threads for the engine (0: this rank's share of the visible "
+                         "cores, hostcpu.threads_per_rank)")
     ap.add_argument("--sp-check", type=int, default=4,
                     help="self-play leg: episodes of the timed run compared afterwards with the "
                          "sequential reference loop (rank 0; 'agreement')")
@@ -479,6 +481,40 @@ def selfplay_leg(W, G, args, device, rank):
                 "assemble_s": round(st.get("assemble_s", 0.0), 3)}
 
 
+class _HostOnlyNet:
+    """A network that costs (almost) nothing: priors / values from a fixed function of the
+    board, so the engine's host work is what gets timed (the search shape differs from the
+    real network's, the per-move work does not)."""
+
+    def predict_both(self, boards):
+        n = len(boards)
+        h = boards.reshape(n, -1).astype(np.float32) @ np.linspace(0.01, 0.49, 49, dtype=np.float32)
+        p = np.abs(np.sin(h[:, None] + np.arange(8, dtype=np.float32))) + 0.05
+        p = (p / p.sum(1, keepdims=True)).astype(np.float32)
+        v = np.tanh(h * 0.3).astype(np.float32)
+        return p, v, p, (0.5 * v).astype(np.float32)
+
+
+def selfplay_host_only(threads, sims, games=512):
+    """Host-only self-play rate (no GPU in the loop): `games` Connect4 GNN-setting episodes
+    through the native engine on `threads` threads with a near-free network.  games/s per core
+    is the budget figure: a node with C cores and P ranks sustains about P x min(GPU-bound
+    rate, (C / P) x per-core rate)."""
+    from connect4.Connect4Game import Connect4Game
+    from selfplay import play_episodes_engine
+    eps = list(range(games))
+    st = {}
+    t0 = time.perf_counter()
+    out = play_episodes_engine(Connect4Game(7), _HostOnlyNet(), selfplay_args(sims), eps,
+                               {e: 777 + e for e in eps}, games, threads=threads, stats=st)
+    dt = time.perf_counter() - t0
+    rate = len(out) / dt
+    return {"games": len(out), "threads": threads, "seconds": round(dt, 2),
+            "games_per_s": round(rate, 1), "games_per_s_per_core": round(rate / threads, 2),
+            "assemble_s": round(st.get("assemble_s", 0.0), 3),
+            "note": "native engine + example assembly only (a near-free network)"}
+
+
 def selfplay_agreement(net, sa, out, sample, seeds):
     """Move agreement of a sample of the timed run's own lock-step episodes with the reference's
     sequential loop (Coach.executeEpisode after np.random.seed(seed), batch-1 predict /
@@ -644,6 +680,11 @@ def pmc_run(key):
 
 def main():
     args = parse()
+    # before any GPU call: this rank on its GPU's NUMA node (best effort; hostcpu.py)
+    import hostcpu
+    pin = hostcpu.pin_rank_to_gpu_numa(int(os.environ.get("LOCAL_RANK", "0")))
+    if not args.sp_threads:
+        args.sp_threads = hostcpu.threads_per_rank()
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -766,6 +807,11 @@ def main():
             t = torch.tensor([dt], device=red_dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
+        sp.update({"threads_per_rank": args.sp_threads,
+                   "host_cores_visible": hostcpu.host_cpus(),
+                   "local_world_size": hostcpu.local_world_size(), "numa_pin": pin})
+        if rank == 0 and not args.no_cpu:
+            sp["host_only"] = selfplay_host_only(args.sp_threads, args.sp_sims)
         sp.update({"games_per_s": round(world * sp["games"] / dt, 3),
                    "evals_per_s": round(world * sp["evals"] / dt, 1),
                    "seconds": round(dt, 2), "games_per_gpu": args.sp_games,

@@ -116,3 +116,41 @@ def test_gnn_root_predict_failure_propagates():
     args = Args(numMCTSSims=3, cpuct=1.0, tempThreshold=15, use_gnn=True, expand_by=2)
     with pytest.raises(RuntimeError, match="root predict failed"):
         play_episodes(Connect4Game(7), FailsOnRoot(), args, [0], {0: 0}, parallel_games=1)
+
+
+def test_host_thread_budget(monkeypatch):
+    """hostcpu: engine threads are this rank's share of the visible cores (LOCAL_WORLD_SIZE
+    ranks per node), at most 16; the NUMA pin is best effort and never fails."""
+    import hostcpu
+    n = hostcpu.host_cpus()
+    assert 1 <= n <= (__import__("os").cpu_count() or 1)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert hostcpu.threads_per_rank() == max(1, min(16, n))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert hostcpu.threads_per_rank() == max(1, min(16, n // 8))
+    assert hostcpu._cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    before = hostcpu.affinity()
+    info = hostcpu.pin_rank_to_gpu_numa(0, 1)
+    assert set(info) == {"numa_node", "cpus", "pinned"}
+    if not info["pinned"]:
+        assert hostcpu.affinity() == before
+
+
+def test_engine_assembler_thread_equals_inline():
+    """Examples assembled on the assembler thread equal the inline assembly, episode by
+    episode (recorded reference outputs, so both equal the reference's examples too)."""
+    from connect4.Connect4Game import Connect4Game
+    from selfplay import play_episodes_engine
+    from test_mcts_golden import RecordedNet
+    meta = json.load(open(os.path.join(GOLDEN, "mcts_c4.json")))
+    net = BatchedRecordedNet(golden("mcts_c4.npz"), 7)
+    args = Args(meta["args"])
+    eps = [ep["episode"] for ep in meta["episodes"]]
+    a = play_episodes_engine(Connect4Game(7), net, args, eps, {e: e for e in eps}, 2,
+                             threads=2, assembler_thread=True)
+    b = play_episodes_engine(Connect4Game(7), net, args, eps, {e: e for e in eps}, 2,
+                             threads=2, assembler_thread=False)
+    for e in eps:
+        assert _norm_std(a[e][0]) == _norm_std(b[e][0])
+        assert _norm_std(a[e][0]) == [tuple(x) for x in
+                                      meta["episodes"][eps.index(e)]["std_examples"]]
