@@ -102,6 +102,10 @@ SIGNATURES = {
     "az_gnn_layer_infer": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int,
                                    ctypes.POINTER(LayerW), c_void_p, c_void_p, c_size_t,
                                    c_void_p]),
+    "az_gnn_layer_ot_infer_ws_bytes": (c_size_t, [ctypes.POINTER(Graph), c_int, c_int]),
+    "az_gnn_layer_ot_infer": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int,
+                                      ctypes.POINTER(LayerW), c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "az_gnn_source_proj_fwd": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int,
                                        ctypes.POINTER(LayerW), c_void_p, c_void_p, c_size_t,
                                        c_void_p]),

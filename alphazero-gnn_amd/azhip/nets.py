@@ -203,8 +203,20 @@ class PolicyValueGNN(_Net):
         return self.output_transform(features)
 
     def forward_graph(self, x, graph):
-        """Per-destination generalisation over a CSR graph (synthetic grid workload)."""
-        return self.output_transform(self.run_layers(x, graph))
+        """Per-destination generalisation over a CSR graph (synthetic grid workload).  In eval
+        mode the last layer and output_transform are one call (az_gnn_layer_ot_infer: on band
+        graphs one launch, the layer's output never reaches HBM)."""
+        if self.training or not self.layers:
+            return self.output_transform(self.run_layers(x, graph))
+        for layer in self.layers[:-1]:
+            x, self._ws = ops.gnn_layer(graph, x, layer.weights(), ws=self._ws, save=False)
+        W = self.params
+        y, self._ws = ops.gnn_layer_ot(graph, x, self.layers[-1].weights(),
+                                       W["output_transform.0.weight"],
+                                       W["output_transform.0.bias"],
+                                       W["output_transform.2.weight"],
+                                       W["output_transform.2.bias"], ws=self._ws)
+        return y
 
 
 def gnn_per_row_heads(nnet, gnn, feat, want_pi=True, pi=None, v=None):

@@ -347,6 +347,23 @@ def gnn_layer(g, x, Wl, out=None, ws=None, H=128, save=True):
     return out, ws
 
 
+def gnn_layer_ot(g, x, Wl, w0, b0, w2, b2, out=None, ws=None, H=128):
+    """The network's last GNNLayer followed by output_transform, eval mode
+    (az_gnn_layer_ot_infer: one band-kernel launch on band graphs).  Returns (y, ws)."""
+    F = x.shape[1]
+    out = torch.empty_like(x) if out is None else out
+    L = _lib.lib()
+    nbytes = int(L.az_gnn_layer_ot_infer_ws_bytes(ctypes.byref(g.c), F, H))
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty((nbytes,), dtype=torch.uint8, device=x.device)
+    lw = layer_weights(Wl)
+    _lib.check(L.az_gnn_layer_ot_infer(ctypes.byref(g.c), _p(x), F, H, ctypes.byref(lw),
+                                       _p(w0), _p(b0), _p(w2), _p(b2), _p(out), _p(ws),
+                                       ctypes.c_size_t(ws.numel()), _stream()),
+               "az_gnn_layer_ot_infer")
+    return out, ws
+
+
 def gnn_source_proj(g, x, Wl, Ps=None, H=128):
     """Ps [V][H] = x W1[:, F:]^T (the fused layer path's first launch)."""
     Ps = torch.empty((g.V, H), device=x.device) if Ps is None else Ps

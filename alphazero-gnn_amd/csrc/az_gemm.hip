@@ -986,8 +986,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
 // == 0): the tile copies them into the LDS image without any VALU, only W is split here.
 // MF = 16 (tuning build): v_mfma_f32_16x16x32_bf16 blocks, one k step per 32-k tile (lane l
 // holds row l & 15, k chunk l >> 4), against two 32x32x16 steps for MF = 32.
+template <int BM, int BN, int WGM, int WGN, int MF = 32>
+constexpr int x3_smem_bytes() {
+  constexpr int NW = WGM * WGN, WM = BM / WGM;
+  constexpr int BUF = 3 * (BM + BN) * 64, STAGE = NW * WM * 36 * 4;
+  return 2 * BUF > STAGE ? 2 * BUF : STAGE;
+}
+
+// One (tile, k range) of gemm_x3: C tile (mt, nt) over k in [kbeg, kend); sp = the split-K
+// slab it writes when p.splits > 1 (raw partial sums), else the fused epilogue.
 template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false, int MF = 32>
-__global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
+__device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int mt, int nt,
+                                             int sp, int kbeg, int kend) {
   static_assert(!APL || !MASK, "pre-split A needs whole 32-k tiles");
   constexpr int BK = 32;
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
@@ -1001,16 +1011,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
                 (BN * 4) % NT == 0, "bad x3 tile");
   constexpr int PLANE = (BM + BN) * 64;          // bytes of one bf16 plane (A rows, then W rows)
   constexpr int BUF = 3 * PLANE;
-  constexpr int STAGE = NW * WM * 36 * 4;
-  constexpr int SMEM = 2 * BUF > STAGE ? 2 * BUF : STAGE;
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-
-  const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
-  const int nwg = mt_n * nt_n * p.splits;
-  const int bid = xcd_swizzle(blockIdx.x, nwg);
-  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
   const int m0 = mt * BM, n0 = nt * BN;
-  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
 
@@ -1207,6 +1208,79 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
   }
   tile_epilogue<MF, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
+}
+
+template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false, int MF = 32>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<BM, BN, WGM, WGN, MF>()];
+  const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
+  const int nwg = mt_n * nt_n * p.splits;
+  const int bid = xcd_swizzle(blockIdx.x, nwg);
+  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
+  gemm_x3_body<BM, BN, WGM, WGN, MASK, ABL, APL, MF>(p, smem, mt, nt, sp, kbeg, kend);
+}
+
+// Stream-K form of gemm_x3 for grids whose tile count does not fill the chip in whole rounds
+// (M ~ 600 .. 2,000 at N = 3,136: 100 .. 200 tiles of 256 x 128 on 256 CUs).  The I = tiles x KT
+// k-iterations (KT 32-k steps per tile, tiles in (mt fastest, nt) order) are cut into B equal
+// contiguous ranges, one per block: a block finishes the tail of one tile and starts the next.
+// A range that covers a whole tile writes C through the fused epilogue; a piece of a tile writes
+// its raw partial sums to slab[piece] (piece = its index among the tile's blocks), and
+// streamk_fixup4_kernel sums a split tile's pieces in piece order (deterministic) and runs the
+// epilogue.  Block b's range: [b I / B, (b + 1) I / B); the block holding iteration i is
+// ceil((i + 1) B / I) - 1.
+__device__ __forceinline__ int sk_block_of(long i, long I, int B) {
+  return (int)(((i + 1) * B + I - 1) / I - 1);
+}
+
+template <int BM, int BN, int WGM, int WGN, bool MASK>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3_sk(GemmArgs p, int KT, long I) {
+  __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<BM, BN, WGM, WGN>()];
+  const int B = gridDim.x;
+  const int b = xcd_swizzle(blockIdx.x, B);
+  const int mt_n = (p.M + BM - 1) / BM;
+  long i0 = (long)b * I / B;
+  const long i1 = (long)(b + 1) * I / B;
+  while (i0 < i1) {
+    const int t = (int)(i0 / KT);
+    const int k0 = (int)(i0 - (long)t * KT);
+    const int k1 = (int)min((long)KT, k0 + (i1 - i0));
+    GemmArgs q = p;
+    int sp = 0;
+    if (k0 == 0 && k1 == KT) {
+      q.splits = 1;                       // the whole tile: fused epilogue into C
+    } else {
+      q.splits = 2;                       // a piece: raw partials into slab[piece]
+      sp = b - sk_block_of((long)t * KT, I, B);
+    }
+    gemm_x3_body<BM, BN, WGM, WGN, MASK>(q, smem, t % mt_n, t / mt_n, sp, 32 * k0,
+                                         min(p.K, 32 * k1));
+    i0 += k1 - k0;
+    if (i0 < i1) __syncthreads();         // the next segment's prologue reuses the LDS
+  }
+}
+
+// Sums the pieces of every tile gemm_x3_sk split (slab[0 .. np), np = the tile's block count)
+// and runs the epilogue on them; whole tiles were written by their block.  float4 per lane.
+__global__ __launch_bounds__(256) void streamk_fixup4_kernel(GemmArgs p, int BM, int BN, int KT,
+                                                             long I, int B) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const int n4 = p.N >> 2;
+  if (idx >= (long)p.M * n4) return;
+  const int row = (int)(idx / n4), col = (int)(idx % n4) * 4;
+  const int mt_n = (p.M + BM - 1) / BM;
+  const long t = (long)(col / BN) * mt_n + row / BM;
+  const int bf = sk_block_of(t * KT, I, B), bl = sk_block_of(t * KT + KT - 1, I, B);
+  if (bf == bl) return;
+  const size_t plane = (size_t)p.M * p.N, off = (size_t)row * p.N + col;
+  f32x4 v = *reinterpret_cast<const f32x4*>(p.slab + off);
+  for (int s = 1; s <= bl - bf; ++s) {
+    const f32x4 u = *reinterpret_cast<const f32x4*>(p.slab + s * plane + off);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] += u[c];
+  }
+  epilogue_store4(p, row, col, v);
 }
 
 // gemm_x3 as a two-group ping-pong ("x3pp").  The timing ablations of gemm_x3 (tools/gemm_sweep.py
@@ -2419,6 +2493,36 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   if (S > 1) a.splits = (a.K + a.kc - 1) / a.kc;
   const dim3 grid((unsigned)(tiles * a.splits));
   const bool whole = a.K % 32 == 0;   // kc is a multiple of 32 too: no partial k tile anywhere
+  // Stream-K (gemm_x3_sk) for the 256 x 128 tile when the split-K grid leaves CUs idle (below
+  // 90 % of its last round: M = 800 -> 200 blocks, M = 1,576 -> 175): one block per CU, equal
+  // k-iteration ranges, split tiles summed by streamk_fixup4_kernel.  C is complete on return
+  // (a.splits = 1).  Product dispatch only (the tuning overrides keep the split-K forms).
+  if (!env && !env_split && tile == 1 && a.vec_epi && a.slab && tiles >= 64) {
+    static int cus = 0;
+    if (cus <= 0) {
+      int dev = 0, n = 0;
+      cus = (hipGetDevice(&dev) == hipSuccess &&
+             hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+             n > 0) ? n : 256;
+    }
+    const long blocks = tiles * a.splits;
+    const long rounds = (blocks + cus - 1) / cus;
+    const int KT = (a.K + 31) / 32;
+    const long I = tiles * (long)KT;
+    const int B = (int)std::min<long>(cus, I);
+    const long per = I / B;
+    const long smax = per > 0 ? (KT + per - 1) / per + 1 : 0;
+    if ((double)blocks / (double)(rounds * cus) < 0.9 && per >= 8 &&
+        (size_t)smax * a.M * a.N * 4 <= ws_bytes) {
+      if (whole) hipLaunchKernelGGL((gemm_x3_sk<256, 128, 4, 2, false>), dim3(B), dim3(512), 0, s, a, KT, I);
+      else hipLaunchKernelGGL((gemm_x3_sk<256, 128, 4, 2, true>), dim3(B), dim3(512), 0, s, a, KT, I);
+      const long n4 = (long)a.M * (a.N / 4);
+      hipLaunchKernelGGL(streamk_fixup4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                         a, 256, 128, KT, I, B);
+      a.splits = 1;
+      return true;
+    }
+  }
 #ifdef AZ_TUNING
   // A split once into bf16 planes (x3_split_kernel) in the workspace after the slabs, only W
   // split in the tile (AZ_GEMM_X3APL=1): measured slower -- M = 512 82.8 vs 75.0 us incl. the

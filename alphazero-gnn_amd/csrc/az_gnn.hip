@@ -17,7 +17,7 @@ bool gnn_layer_fusable(const az_graph* g, int F, int H);
 bool gnn_layer_band_ok(const az_graph* g, int F, int H);
 size_t gnn_layer_band_ws_bytes();
 int gnn_layer_band(const az_graph* g, const float* x, const az_gnn_layer_w* w, float* x_out,
-                   void* ws, hipStream_t s);
+                   void* ws, hipStream_t s, const float* const* ot = nullptr);
 size_t gnn_layer_fused_ws_bytes(int V);
 int gnn_layer_fused(const az_graph* g, const float* x, const az_gnn_layer_w* w, float* x_out,
                     void* ws, size_t ws_bytes, hipStream_t s);
@@ -631,6 +631,38 @@ extern "C" int az_gnn_layer_infer(const az_graph* g, const float* x, int F, int 
       return check_launch("hipMemcpyAsync");
   }
   return gnn_layer_fused(g, x, w, x_out, ws, ws_bytes, s);
+}
+
+extern "C" size_t az_gnn_layer_ot_infer_ws_bytes(const az_graph* g, int F, int H) {
+  if (!g) return 0;
+  if (gnn_layer_band_ok(g, F, H)) return gnn_layer_band_ws_bytes();
+  // the layer's output and output_transform's hidden activations, then the layer's workspace
+  const size_t act = ((size_t)g->V * F * 4 + 255) / 256 * 256;
+  return 2 * act + az_gnn_layer_infer_ws_bytes(g, F, H) + kSplitWsBytes;
+}
+
+extern "C" int az_gnn_layer_ot_infer(const az_graph* g, const float* x, int F, int H,
+                                     const az_gnn_layer_w* w, const float* ot_w0,
+                                     const float* ot_b0, const float* ot_w2, const float* ot_b2,
+                                     float* y, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_graph(g);
+  if (rc) return rc;
+  AZ_REQUIRE(x && w && y && y != x && ws && ot_w0 && ot_b0 && ot_w2 && ot_b2, AZ_EINVAL,
+             "az_gnn_layer_ot_infer: null pointer or y aliasing x");
+  AZ_REQUIRE(ws_bytes >= az_gnn_layer_ot_infer_ws_bytes(g, F, H), AZ_EINVAL,
+             "az_gnn_layer_ot_infer: workspace too small");
+  if (gnn_layer_band_ok(g, F, H)) {
+    const float* const ot[4] = {ot_w0, ot_b0, ot_w2, ot_b2};
+    return gnn_layer_band(g, x, w, y, ws, as_stream(stream), ot);
+  }
+  const size_t act = ((size_t)g->V * F * 4 + 255) / 256 * 256;
+  float* layer_out = static_cast<float*>(ws);
+  float* hidden = reinterpret_cast<float*>(static_cast<char*>(ws) + act);
+  char* rest = static_cast<char*>(ws) + 2 * act;
+  const size_t rest_bytes = ws_bytes - 2 * act;
+  if ((rc = az_gnn_layer_infer(g, x, F, H, w, layer_out, rest, rest_bytes, stream))) return rc;
+  return az_mlp2_fwd(layer_out, g->V, F, ot_w0, ot_b0, ot_w2, ot_b2, hidden, y, rest,
+                     rest_bytes, stream);
 }
 
 extern "C" int az_gnn_source_proj_fwd(const az_graph* g, const float* x, int F, int H,

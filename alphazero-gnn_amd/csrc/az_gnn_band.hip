@@ -55,7 +55,10 @@ constexpr int XRS = 3 * BF;   // ring row: three planes of 64 bf16 (384 B), 16-B
 constexpr int W1_OFF = 0;                    // attention.0    [128][128]
 constexpr int WC_OFF = BH * 2 * BF;          // [gate.0 ; update_net.0]  [128][128]
 constexpr int WU2_OFF = WC_OFF + 2 * BF * 2 * BF;   // update_net.2 [64][64]
-constexpr int WTOT = WU2_OFF + BF * BF;
+constexpr int OT0_OFF = WU2_OFF + BF * BF;  // output_transform.0 [64][64] (fused tail, OT)
+constexpr int OT2_OFF = OT0_OFF + BF * BF;   // output_transform.2 [64][64]
+constexpr int WLAYER = OT0_OFF;              // the layer's own weights
+constexpr int WTOT = OT2_OFF + BF * BF;      // plane stride
 constexpr int FRAG = 512;                    // bf16 per fragment block
 
 // offset of W[n][k .. k + 7] (k % 8 == 0) in a fragment-ordered matrix of K columns
@@ -66,6 +69,7 @@ __host__ __device__ constexpr int frag_off(int n, int k, int K) {
 struct BandW {
   const unsigned short* planes;              // [3][WTOT]
   const float *w1, *b1, *w2, *b2, *gb, *ub1, *ub2;
+  const float *ob0, *ob2;                    // output_transform biases (OT only)
 };
 
 __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
@@ -82,9 +86,12 @@ __global__ __launch_bounds__(256) void band_split_weights(const float* __restric
                                                           const float* __restrict__ gw,
                                                           const float* __restrict__ uw1,
                                                           const float* __restrict__ uw2,
-                                                          unsigned short* __restrict__ planes) {
-  const int i = (blockIdx.x * 256 + threadIdx.x) * 8;   // element of [W1 | Wg ; Wu1 | Wu2]
-  if (i >= WTOT) return;
+                                                          const float* __restrict__ ow0,
+                                                          const float* __restrict__ ow2,
+                                                          unsigned short* __restrict__ planes,
+                                                          int n) {
+  const int i = (blockIdx.x * 256 + threadIdx.x) * 8;   // element of [W1 | Wg ; Wu1 | Wu2 | ..]
+  if (i >= n) return;
   const float* src;
   int dst;
   if (i < WC_OFF) {                       // W1 [128][128]
@@ -94,10 +101,10 @@ __global__ __launch_bounds__(256) void band_split_weights(const float* __restric
     const int j = i - WC_OFF;
     src = j < BF * 2 * BF ? gw + j : uw1 + (j - BF * 2 * BF);
     dst = WC_OFF + frag_off(j >> 7, j & 127, 2 * BF);
-  } else {                                // Wu2 [64][64]
-    const int j = i - WU2_OFF;
-    src = uw2 + j;
-    dst = WU2_OFF + frag_off(j >> 6, j & 63, BF);
+  } else {                                // Wu2, then output_transform.0 / .2: [64][64] each
+    const int m = (i - WU2_OFF) / (BF * BF), j = (i - WU2_OFF) % (BF * BF);
+    src = (m == 0 ? uw2 : m == 1 ? ow0 : ow2) + j;
+    dst = WU2_OFF + m * BF * BF + frag_off(j >> 6, j & 63, BF);
   }
   const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
   const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
@@ -170,7 +177,9 @@ __device__ __forceinline__ void zero(f32x16& a) {
 
 // ABL != 0 only in the tuning build: timing ablations, results wrong by design (bits 1 / 2 / 4 /
 // 8 = no phase A / B / C / D math, 16 = no weight loads, 64 = no x_out stores, 128 = no x loads)
-template <int ABL>
+// OT: the layer is the network's last -- output_transform (gnn_utils.py:101-105,115: Linear +
+// ReLU + Linear, every row) runs on the tile in LDS and only its output y is stored.
+template <int ABL, bool OT>
 __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     int V, int E, const int* __restrict__ rowptr, const int* __restrict__ col,
     const float* __restrict__ x, BandW W, float* __restrict__ x_out, int ntiles, int per) {
@@ -488,16 +497,58 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = 32 * mb + acc_row(r, lane);
-        const int d = d0 + row;
-        if (d < V) {
-          const int slot = d & (RING - 1);
-          const int k = xr_off(slot, 0, n >> 3) + (n & 7);
-          const float xd = (__uint_as_float((unsigned)XR[k] << 16) +
-                            __uint_as_float((unsigned)XR[k + BF] << 16)) +
-                           __uint_as_float((unsigned)XR[k + 2 * BF] << 16);
-          const float o = DEG[row] > 0 ? xd + PT[row * PSS + n] * (acc[0][r] + ub) : xd;
-          if constexpr ((ABL & 64) == 0) x_out[(size_t)d * BF + n] = o;
-          else if (o == 12345.f) x_out[0] = o;
+        const int slot = (d0 + row) & (RING - 1);
+        const int k = xr_off(slot, 0, n >> 3) + (n & 7);
+        const float xd = (__uint_as_float((unsigned)XR[k] << 16) +
+                          __uint_as_float((unsigned)XR[k + BF] << 16)) +
+                         __uint_as_float((unsigned)XR[k + 2 * BF] << 16);
+        const float o = DEG[row] > 0 ? xd + PT[row * PSS + n] * (acc[0][r] + ub) : xd;
+        if constexpr (OT) {
+          PT[row * PSS + n] = o;          // in place of the gate element it consumed
+        } else {
+          const int d = d0 + row;
+          if (d < V) {
+            if constexpr ((ABL & 64) == 0) x_out[(size_t)d * BF + n] = o;
+            else if (o == 12345.f) x_out[0] = o;
+          }
+        }
+      }
+    }
+    if constexpr (OT) {
+      // ---- E: h = relu(x_out W0^T + b0) -> PT[:, 64:128] (u1's, free once every wave's D
+      //      MFMAs are done);  F: y = h W2^T + b2 -> HBM  (waves 0-3, 32 x 32 each; x_out / h
+      //      are split in the waves)
+      __syncthreads();
+      const int mb = (wave >> 1) & 1, nb = wave & 1, n = 32 * nb + lr;
+      auto split_rows = [&](int col0) {
+        return [=](int, int ks, bf16x8 (&a)[3]) {
+          const float* u = PT + (32 * mb + lr) * PSS + col0 + 16 * ks + 8 * hc;
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(u);
+          const f32x4 x1 = *reinterpret_cast<const f32x4*>(u + 4);
+          u32x4 t[3];
+          split3(x0, x1, t);
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) a[pl] = __builtin_bit_cast(bf16x8, t[pl]);
+        };
+      };
+      f32x16 acc[1];
+      if (wave < 4) {
+        zero(acc[0]);
+        x3_planes<1, 4, ABL>(acc, split_rows(0), W.planes + OT0_OFF + frag_off(32 * nb, 0, BF) + 8 * lane);
+        const float bias = W.ob0[n];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          PT[(32 * mb + acc_row(r, lane)) * PSS + BF + n] = relu(acc[0][r] + bias);
+      }
+      __syncthreads();
+      if (wave < 4) {
+        zero(acc[0]);
+        x3_planes<1, 4, ABL>(acc, split_rows(BF), W.planes + OT2_OFF + frag_off(32 * nb, 0, BF) + 8 * lane);
+        const float bias = W.ob2[n];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = d0 + 32 * mb + acc_row(r, lane);
+          if (d < V) x_out[(size_t)d * BF + n] = acc[0][r] + bias;
         }
       }
     }
@@ -518,19 +569,24 @@ bool gnn_layer_band_ok(const az_graph* g, int F, int H) {
 
 size_t gnn_layer_band_ws_bytes() { return ((size_t)3 * WTOT * 2 + 255) / 256 * 256; }
 
+// One eval-mode GNNLayer on a band graph; with `ot` (output_transform.{0,2}.{weight,bias}: w0,
+// b0, w2, b2) the layer is the network's last and x_out receives output_transform's output.
 int gnn_layer_band(const az_graph* g, const float* x, const az_gnn_layer_w* w, float* x_out,
-                   void* ws, hipStream_t s) {
+                   void* ws, hipStream_t s, const float* const* ot) {
   unsigned short* planes = static_cast<unsigned short*>(ws);
-  hipLaunchKernelGGL(band_split_weights, dim3((WTOT / 8 + 255) / 256), dim3(256), 0, s,
-                     w->att_w1, w->gate_w, w->upd_w1, w->upd_w2, planes);
+  const int n = ot ? WTOT : WLAYER;
+  hipLaunchKernelGGL(band_split_weights, dim3((n / 8 + 255) / 256), dim3(256), 0, s,
+                     w->att_w1, w->gate_w, w->upd_w1, w->upd_w2, ot ? ot[0] : nullptr,
+                     ot ? ot[2] : nullptr, planes, n);
   int rc = check_launch("band_split_weights");
   if (rc) return rc;
   static int cus = 0;                     // queried once per process
   if (cus <= 0) {
-    int dev = 0, n = 0;
+    int dev = 0, nc = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-      cus = n;
+        hipDeviceGetAttribute(&nc, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        nc > 0)
+      cus = nc;
     else
       cus = 256;
   }
@@ -538,10 +594,16 @@ int gnn_layer_band(const az_graph* g, const float* x, const az_gnn_layer_w* w, f
   const int per = (ntiles + cus - 1) / cus;
   const int blocks = (ntiles + per - 1) / per;
   const BandW bw = {planes, w->att_w1, w->att_b1, w->att_w2, w->att_b2, w->gate_b, w->upd_b1,
-                    w->upd_b2};
+                    w->upd_b2, ot ? ot[1] : nullptr, ot ? ot[3] : nullptr};
 #define AZ_BAND(A_)                                                                          \
-  hipLaunchKernelGGL(gnn_layer_band_kernel<A_>, dim3(blocks), dim3(BNT), 0, s, g->V, g->E,    \
-                     g->rowptr, g->col, x, bw, x_out, ntiles, per)
+  do {                                                                                       \
+    if (ot)                                                                                  \
+      hipLaunchKernelGGL((gnn_layer_band_kernel<A_, true>), dim3(blocks), dim3(BNT), 0, s,   \
+                         g->V, g->E, g->rowptr, g->col, x, bw, x_out, ntiles, per);          \
+    else                                                                                     \
+      hipLaunchKernelGGL((gnn_layer_band_kernel<A_, false>), dim3(blocks), dim3(BNT), 0, s,  \
+                         g->V, g->E, g->rowptr, g->col, x, bw, x_out, ntiles, per);          \
+  } while (0)
 #ifdef AZ_TUNING   // timing ablations (tools/gpu_band_abl.sh): AZ_BAND_ABL=<bits>
   static const char* env_abl = tuning_env("AZ_BAND_ABL");
   switch (env_abl ? atoi(env_abl) : 0) {

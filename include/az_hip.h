@@ -259,6 +259,17 @@ int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H, const az_g
 size_t az_gnn_layer_infer_ws_bytes(const az_graph* g, int F, int H);
 int az_gnn_layer_infer(const az_graph* g, const float* x, int F, int H, const az_gnn_layer_w* w,
                        float* x_out, void* ws, size_t ws_bytes, void* stream);
+/* The network's LAST layer followed by output_transform (gnn_utils.py:87-117 in eval mode:
+ * y = output_transform(GNNLayer(x)), output_transform = Linear + ReLU + Linear on every row).
+ * On band graphs (see az_gnn_layer_infer) ONE launch: the tile's layer output never leaves LDS
+ * and only y is written.  Otherwise az_gnn_layer_infer into ws, then az_mlp2_fwd.
+ * ot_w0 / ot_w2: [F][F] nn.Linear weights; y may not alias x.
+ * ws >= az_gnn_layer_ot_infer_ws_bytes(g, F, H). */
+size_t az_gnn_layer_ot_infer_ws_bytes(const az_graph* g, int F, int H);
+int az_gnn_layer_ot_infer(const az_graph* g, const float* x, int F, int H,
+                          const az_gnn_layer_w* w, const float* ot_w0, const float* ot_b0,
+                          const float* ot_w2, const float* ot_b2, float* y, void* ws,
+                          size_t ws_bytes, void* stream);
 /* The two launches of the fused path, separately (profiling / callers that keep Ps):
  * Ps [V][H] = x W1[:, F:]^T, then the fused layer kernel given Ps (copies non-destination rows
  * of x to x_out first when D < V).  Fused shapes only (AZ_EINVAL otherwise). */

@@ -122,6 +122,27 @@ def test_x3_gemm_has_fp32_accuracy(ops, M, N, K):
     assert rep["x3_max"] <= x3_bound(K) and rep_cpu <= x3_bound(K)   # torch fp32 meets it too
 
 
+@pytest.mark.parametrize("M", [700, 800, 1576, 2048])
+def test_streamk_gemm_deterministic_and_accurate(ops, M):
+    """Self-play batch sizes (M ~ 700 .. 2,048 at 3136 x 3136) run gemm_x3 in stream-K form
+    (equal k-iteration ranges per CU, split tiles summed by streamk_fixup4_kernel in piece
+    order): every call returns the same bits, within x3_bound of float64."""
+    N = K = 3136
+    g = torch.Generator().manual_seed(M)
+    x = torch.rand((M, K), generator=g) * 2 - 1
+    w = (torch.rand((N, K), generator=g) * 2 - 1) / K ** 0.5
+    b = torch.rand((N,), generator=g) - 0.5
+    xd, wd, bd = x.cuda(), w.cuda(), b.cuda()
+    y1 = ops.linear(xd, wd, bd, act=1)
+    y2 = ops.linear(xd, wd, bd, act=1)
+    assert torch.equal(y1, y2)
+    rows = torch.randperm(M, generator=g)[:256]
+    ref = torch.relu(x[rows].double() @ w.double().T + b.double())
+    bound = (x[rows].double().abs() @ w.double().abs().T + b.double().abs()).numpy()
+    e = ((y1.cpu()[rows].double() - ref).abs().numpy() / bound).max()
+    assert e <= x3_bound(K), e
+
+
 def test_x3_gemm_accuracy_at_65536_rows(ops):
     """The large-batch leg's shape (M = 65,536: the 128x128 x3 tile, no split): 512 sampled
     rows against float64 (rows are independent)."""
@@ -546,6 +567,43 @@ def test_band_layer_equals_training_path(ops, V, maxdeg, R):
     if V <= 4099:
         ref = O.gnn_layer_csr(x0.astype(np.float64), rowptr, col, G, 1)
         np.testing.assert_allclose(b, ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("kind", ["grid", "band", "random"])
+def test_layer_ot_equals_layer_then_mlp2(ops, kind):
+    """az_gnn_layer_ot_infer (the last layer + output_transform; ONE launch on band graphs,
+    the layer's output never reaching HBM) == az_gnn_layer_fwd followed by az_mlp2_fwd
+    (gnn_utils.py:87-117), on the reference's grid, a random band graph and a non-band graph."""
+    z, G, x0 = _synth()
+    if kind == "grid":
+        rowptr, col = z["rowptr"], z["col"]
+    elif kind == "band":
+        rowptr, col = _band_graph(3001, 5, 32, seed=5)
+    else:
+        rowptr, col = _random_graph(2500, 4, seed=6)
+    g = ops.DeviceGraph(rowptr, col)
+    V = g.V
+    x0 = (np.random.default_rng(V).random((V, 64), dtype=np.float32) * 2 - 1)
+    Gd = {k: cu(v) for k, v in G.items()}
+    x = cu(x0)
+    Wl = {k[len("layers.1."):]: v for k, v in Gd.items() if k.startswith("layers.1.")}
+    ot = [Gd["output_transform.0.weight"], Gd["output_transform.0.bias"],
+          Gd["output_transform.2.weight"], Gd["output_transform.2.bias"]]
+    a, _ = ops.gnn_layer(g, x, Wl, save=True)
+    ref, _ = ops.mlp2(a, *ot)
+    y, _ = ops.gnn_layer_ot(g, x, Wl, *ot)
+    np.testing.assert_allclose(y.cpu().numpy(), ref.cpu().numpy(), atol=4e-6, rtol=1e-6)
+
+
+def test_grid_forward_eval_vs_golden(ops):
+    """PolicyValueGNN.forward_graph in eval mode (layer 0, then layer 1 + output_transform as
+    one call) on the reference's 32x32 grid (G3): within 1e-5 of the reference's output."""
+    from azhip.nets import PolicyValueGNN
+    z, G, x0 = _synth()
+    g = ops.DeviceGraph(z["rowptr"], z["col"])
+    net = PolicyValueGNN(64, 2, init=G).eval()
+    y = net.forward_graph(cu(x0), g)
+    np.testing.assert_allclose(y.cpu().numpy(), z["grid_out"], atol=1e-5)
 
 
 def test_band_layer_with_understated_band(ops):

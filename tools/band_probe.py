@@ -38,6 +38,23 @@ def main():
     us = e[0].elapsed_time(e[1]) / reps * 1e3
     print(f"graphs={graphs} V={g.V} band={g.band} layer_us={us:.1f} "
           f"bf16_tflops={6 * 73728 * g.V / us / 1e6:.1f} max_diff_vs_training={err:.3g}", flush=True)
+    # the whole eval forward (PolicyValueGNN.forward_graph: layer, then layer + output_transform
+    # fused) vs the training-mode forward (unfused kernels)
+    from azhip.nets import PolicyValueGNN
+    net = PolicyValueGNN(64, 2, device=dev, init=Gw)
+    ref = net.train().forward_graph(x, g)
+    net.eval()
+    y = net.forward_graph(x, g)
+    torch.cuda.synchronize()
+    ferr = float((y - ref).abs().max())
+    e[0].record()
+    for _ in range(reps):
+        net.forward_graph(x, g)
+    e[1].record()
+    torch.cuda.synchronize()
+    fms = e[0].elapsed_time(e[1]) / reps
+    print(f"forward_ms={fms:.3f} node_updates_per_s={2 * g.V / fms / 1e3:.4g} "
+          f"max_diff_vs_training_forward={ferr:.3g}", flush=True)
 
 
 if __name__ == "__main__":
