@@ -266,9 +266,9 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     store_rows(d0 - BR, v);
     load_rows(d0 + BR, v);
     store_rows(d0 + BR, v);
-    if (tid <= BT) {
-      RPS[t0 & 1][tid] = rowptr[min(d0 + tid, V)];
-      if (t0 + 1 < t1) RPS[(t0 + 1) & 1][tid] = rowptr[min(d0 + BT + tid, V)];
+    if (tid <= BT) {                      // both parities: the unconditional prefetch reads
+      RPS[t0 & 1][tid] = rowptr[min(d0 + tid, V)];         // RPS[nxt] even with no next tile
+      RPS[(t0 + 1) & 1][tid] = rowptr[min(d0 + BT + tid, V)];
     }
     __syncthreads();
     const int eb = RPS[t0 & 1][0], ne = RPS[t0 & 1][BT] - eb;
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     auto prefetch = [&]() {               // unconditional (clamped) loads, see load_rows
       if constexpr ((ABL & 128) != 0) nextx[0] = nextx[1] = f32x4{0.f, 0.f, 0.f, 0.f};
       else load_rows(d0 + BT + BR, nextx);
-      cln = col[min(RPS[nxt][0] + tid, E - 1)];
+      cln = col[max(0, min(RPS[nxt][0] + tid, E - 1))];
       rp2 = rowptr[min(d0 + 2 * BT + min(tid, BT), V)];
     };
 
