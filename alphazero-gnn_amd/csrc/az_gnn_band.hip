@@ -118,29 +118,33 @@ __global__ __launch_bounds__(256) void band_split_weights(const float* __restric
 // acc[mb] += A[32 rows of m-block mb][K = 16 KS] . W[32 rows][K]^T on x3 MFMAs, both operands
 // as bf16 planes.  a(mb, ks, pl) -> this lane's A fragment (plane pl of step ks); w: plane 0 of
 // the first weight fragment block (frag_off(n0, k0, K) + 8 lane; the KS blocks of a row block
-// are consecutive).  Every B fragment is requested first; `after_loads` runs between those loads
-// and the first wait for them: global loads it issues stay in flight through this GEMM (the
-// vector-memory counter retires loads in issue order, so a long-latency load issued BEFORE the
-// B loads would hold up the first MFMA).
-struct NoHook {
-  __device__ void operator()() const {}
-};
-
-template <int MB, int KS, int ABL, typename AFrag, typename Hook = NoHook>
-__device__ __forceinline__ void x3_planes(f32x16 (&acc)[MB], const AFrag& afrag,
-                                          const unsigned short* __restrict__ w,
-                                          const Hook& after_loads = Hook()) {
-  bf16x8 b[KS][3];
+// are consecutive).
+// this lane's weight fragments of KS k steps (3 planes each), requested from L2: issued a phase
+// ahead of their MFMAs, so no GEMM of the tile starts by waiting for its weights.  Buffer loads
+// off one descriptor: the lane part (16 B x lane) is the only VGPR, the fragment block's offset
+// `w` (bf16 elements, wave-uniform) rides in an SGPR -- flat pointers per fragment would hold
+// 24 VGPRs of addresses per weight set across the whole tile loop.
+template <int KS, int ABL = 0>
+__device__ __forceinline__ void load_w(bf16x8 (&b)[KS][3], __amdgpu_buffer_rsrc_t planes,
+                                       int lane_off, int w) {
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) {
-      if constexpr ((ABL & 16) != 0) b[ks][pl] = bf16x8{};   // tuning ablation: no weight loads
-      else b[ks][pl] = *reinterpret_cast<const bf16x8*>(w + (size_t)pl * WTOT + FRAG * ks);
+      if constexpr ((ABL & 16) != 0) {
+        b[ks][pl] = bf16x8{};             // tuning ablation: no weight loads
+      } else {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+            planes, lane_off, 2 * (w + pl * WTOT + FRAG * ks), 0);
+        b[ks][pl] = __builtin_bit_cast(bf16x8, v);
+      }
     }
-  __builtin_amdgcn_sched_barrier(0);
-  after_loads();
-  __builtin_amdgcn_sched_barrier(0);
+}
+
+// acc[mb] += A . W^T with the weight fragments already in registers (load_w)
+template <int MB, int KS, int ABL, typename AFrag>
+__device__ __forceinline__ void x3_mfma(f32x16 (&acc)[MB], const AFrag& afrag,
+                                        const bf16x8 (&b)[KS][3]) {
   if constexpr ((ABL & 32) != 0) return;  // tuning ablation: no A reads / MFMAs
   // A fragments one k step ahead of their MFMAs (LDS latency behind the previous step's)
   bf16x8 a[2][MB][3];
@@ -188,6 +192,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   __shared__ __attribute__((aligned(16))) float PT[BT * PSS];     // Pt -> agg planes ->
                                                                    // C partials -> [gate | u1]
   __shared__ __attribute__((aligned(16))) float B1W2[2 * BH];
+  __shared__ float BS[5 * BF];            // biases: gate.0 | update_net.0 | update_net.2 | OT .0 | .2
   __shared__ int DEG[BT];
   __shared__ int RPS[2][BT + 1];          // rowptr of the tile's destinations (+1), prefetched
   __shared__ int CLS[2][BNT];             // the tile's sources (col), when it has <= 512 edges
@@ -198,6 +203,11 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   if (tid < BH) {
     B1W2[tid] = W.b1[tid];
     B1W2[BH + tid] = W.w2[tid];
+  }
+  if (tid < 5 * BF) {
+    const int m = tid / BF, j = tid % BF;
+    const float* b = m == 0 ? W.gb : m == 1 ? W.ub1 : m == 2 ? W.ub2 : m == 3 ? W.ob0 : W.ob2;
+    BS[tid] = (OT || m < 3) ? b[j] : 0.f;
   }
   const float b2 = W.b2[0];
 
@@ -243,14 +253,30 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         a[pl] = *reinterpret_cast<const bf16x8*>(XR + xr_off(slot, pl, 2 * ks + hc));
     };
   };
-  // Ps rows [r0, r0 + 64) into the ring (waves 4-7: wave = n-block, both m-blocks)
-  auto ps_rows = [&](int r0, auto hook) {
+  // Each wave's weight fragments for the GEMM of the NEXT phase are requested as soon as the
+  // current phase's MFMAs are issued (bw is one register set, reloaded after its last use): they
+  // arrive behind the barriers and the edge phase instead of at the head of each GEMM.
+  //   A  attention.0: waves 0-3 the target half (n-block = wave), 4-7 the source half
+  //   C  [gate ; update_net.0]: n quarter wave & 3, K half wave >> 2
+  //   D  update_net.2 (waves 0-3: n-block wave & 1); OT: output_transform.0 / .2 likewise
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(W.planes), 0, 3 * WTOT * 2, 0x00020000);
+  const int wl = 16 * lane;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int wA = W1_OFF + frag_off(32 * (wv & 3), wv < 4 ? 0 : BF, 2 * BF);
+  const int wC = WC_OFF + frag_off(32 * (wv & 3), BF * (wv >> 2), 2 * BF);
+  const int wD = WU2_OFF + frag_off(32 * (wv & 1), 0, BF);
+  bf16x8 bw[4][3];
+  constexpr int AAB = (ABL & 1) ? (ABL | 32) : ABL;
+  load_w<4, ABL>(bw, wr, wl, wA);
+
+  // Ps rows [r0, r0 + 64) into the ring (waves 4-7: wave = n-block, both m-blocks; bw = wA)
+  auto ps_rows = [&](int r0) {
     const int nb = wave - 4;
     f32x16 acc[2];
     zero(acc[0]);
     zero(acc[1]);
-    x3_planes<2, 4, (ABL & 1) ? (ABL | 32) : ABL>(
-        acc, ring_frag(r0), W.planes + W1_OFF + frag_off(32 * nb, BF, 2 * BF) + 8 * lane, hook);
+    x3_mfma<2, 4, AAB>(acc, ring_frag(r0), bw);
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
@@ -273,7 +299,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     __syncthreads();
     const int eb = RPS[t0 & 1][0], ne = RPS[t0 & 1][BT] - eb;
     if (tid < ne && ne <= BNT) CLS[t0 & 1][tid] = col[eb + tid];
-    if (wave >= 4) ps_rows(d0 - BR, NoHook());
+    if (wave >= 4) ps_rows(d0 - BR);
   }
 
   // edge-phase lane roles: destination i (8 lanes), hidden units 4j + 32c (+0..3), features 8j..
@@ -302,8 +328,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       f32x16 acc[2];
       zero(acc[0]);
       zero(acc[1]);
-      x3_planes<2, 4, (ABL & 1) ? (ABL | 32) : ABL>(
-          acc, ring_frag(d0), W.planes + W1_OFF + frag_off(32 * wave, 0, 2 * BF) + 8 * lane);
+      x3_mfma<2, 4, AAB>(acc, ring_frag(d0), bw);
       const float b1n = B1W2[32 * wave + lr];     // attention.0's bias, folded into Pt
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
@@ -311,7 +336,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         for (int r = 0; r < 16; ++r)
           PT[(32 * mb + acc_row(r, lane)) * PSS + 32 * wave + lr] = acc[mb][r] + b1n;
     } else {
-      ps_rows(d0 + BR, NoHook());
+      ps_rows(d0 + BR);
     }
     __syncthreads();
 
@@ -330,7 +355,12 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       // the edge math, once for staged sources (LDS) and once for a tile with > 512 edges
       // (global col): two instantiations, so neither load is a generic (flat) one that would
       // make the compiler drain the prefetch before it
-      auto edges = [&](auto col_of) {
+      // fast: every destination of this wave has deg <= 4 and all its sources inside the window
+      // (any banded graph, the grid) -- no global loads and no loops in that instantiation, so
+      // nothing in it has to wait for the prefetch (a global load on a rarely taken path shares
+      // its destination registers with the LDS path and makes the compiler wait vmcnt there too)
+      auto edges = [&](auto col_of, auto fast) {
+        constexpr bool FAST = decltype(fast)::value;
         // lane: hidden units 4 ej + 32 cc (+0..3), cc = c ^ (ei & 1) -- the two destinations
         // of a 16-lane LDS read group read opposite 128-B halves of their rows
         const int par = ei & 1;
@@ -342,7 +372,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         }
         auto alpha_of = [&](int s) {
           float acc = 0.f;
-          if ((unsigned)(s - lo) < (unsigned)RING) {
+          if (FAST || (unsigned)(s - lo) < (unsigned)RING) {
             const float* ps = PSR + (s & (RING - 1)) * PSRS + 4 * ej;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -367,7 +397,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
           return sigmoid_fast(acc + b2);
         };
         auto x_of = [&](int s, f32x4 (&v)[2]) {
-          if ((unsigned)(s - lo) < (unsigned)RING) {
+          if (FAST || (unsigned)(s - lo) < (unsigned)RING) {
             x_ring(s & (RING - 1), ej, v);
           } else {
             v[0] = *reinterpret_cast<const f32x4*>(x + (size_t)s * BF + 8 * ej);
@@ -387,8 +417,10 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
             S += a[q];
           }
         }
+        if constexpr (!FAST) {
 #pragma unroll 1
-        for (int q = 4; q < deg; ++q) S += alpha_of(col_of(q));
+          for (int q = 4; q < deg; ++q) S += alpha_of(col_of(q));
+        }
         const bool norm = S > 0.f;
         f32x4 g[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -404,7 +436,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
             }
           }
 #pragma unroll 1
-        for (int q = 4; q < deg; ++q) {
+        for (int q = FAST ? deg : 4; q < deg; ++q) {
           const int s = col_of(q);
           const float aq = alpha_of(s);
           const float wq = norm ? aq / S : aq;
@@ -424,10 +456,20 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(arow + pl * BF + 8 * ej) = o[pl];
       };
-      if (ne <= BNT) edges([&](int q) { return CLS[cur][e0 - eb + q]; });
-      else edges([&](int q) { return col[e0 + q]; });
+      bool ok = deg <= 4 && ne <= BNT;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < deg && ne <= BNT)
+          ok = ok && (unsigned)(CLS[cur][e0 - eb + q] - lo) < (unsigned)RING;
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0)      // wave-uniform
+        edges([&](int q) { return CLS[cur][e0 - eb + q]; }, std::true_type{});
+      else if (ne <= BNT)
+        edges([&](int q) { return CLS[cur][e0 - eb + q]; }, std::false_type{});
+      else
+        edges([&](int q) { return col[e0 + q]; }, std::false_type{});
       if (ej == 0) DEG[ei] = deg;
     }
+    load_w<4, ABL>(bw, wr, wl, wC);
     __syncthreads();
 
     // ---- C: [gate | u1] over [x_d ; agg]: waves 0-3 the x_d half of K (ring planes), 4-7 the
@@ -437,17 +479,18 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       f32x16 acc[2];
       zero(acc[0]);
       zero(acc[1]);
-      const unsigned short* wc = W.planes + WC_OFF + frag_off(32 * nq, BF * kh, 2 * BF) + 8 * lane;
       constexpr int CAB = (ABL & 4) ? (ABL | 32) : ABL;
       if (kh == 0) {
-        x3_planes<2, 4, CAB>(acc, ring_frag(d0), wc);
+        x3_mfma<2, 4, CAB>(acc, ring_frag(d0), bw);
+        load_w<4, ABL>(bw, wr, wl, wD);
       } else {
-        x3_planes<2, 4, CAB>(acc, [&](int mb, int ks, bf16x8 (&a)[3]) {
+        x3_mfma<2, 4, CAB>(acc, [&](int mb, int ks, bf16x8 (&a)[3]) {
           const unsigned short* row = reinterpret_cast<const unsigned short*>(PT + (32 * mb + lr) * PSS);
 #pragma unroll
           for (int pl = 0; pl < 3; ++pl)
             a[pl] = *reinterpret_cast<const bf16x8*>(row + pl * BF + 8 * (2 * ks + hc));
-        }, wc);
+        }, bw);
+        load_w<4, ABL>(bw, wr, wl, wA);           // waves 4-7 are idle until the next tile's phase A
       }
       __syncthreads();                    // agg planes read: PT takes the partials
       // the two K halves' partials meet in PT (accumulator layout): each wave of a pair keeps
@@ -469,7 +512,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       for (int r = 0; r < 16; ++r) mine[r] += part[(kh * 16 + r) * 64];
       __syncthreads();                    // partials read: PT takes [gate | u1]
       const int n = 32 * nq + lr;         // output column: gate (n < 64) or u1 (n - 64)
-      const float bias = nq < 2 ? W.gb[n] : W.ub1[n - BF];
+      const float bias = BS[n];         // gate.0 (n < 64) | update_net.0
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float v = mine[r] + bias;
@@ -483,7 +526,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       const int mb = wave >> 1, nb = wave & 1;
       f32x16 acc[1];
       zero(acc[0]);
-      x3_planes<1, 4, (ABL & 8) ? (ABL | 32) : ABL>(acc, [&](int, int ks, bf16x8 (&a)[3]) {
+      x3_mfma<1, 4, (ABL & 8) ? (ABL | 32) : ABL>(acc, [&](int, int ks, bf16x8 (&a)[3]) {
         const float* u = PT + (32 * mb + lr) * PSS + BF + 16 * ks + 8 * hc;
         const f32x4 x0 = *reinterpret_cast<const f32x4*>(u);
         const f32x4 x1 = *reinterpret_cast<const f32x4*>(u + 4);
@@ -491,9 +534,10 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         split3(x0, x1, o);
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) a[pl] = __builtin_bit_cast(bf16x8, o[pl]);
-      }, W.planes + WU2_OFF + frag_off(32 * nb, 0, BF) + 8 * lane);
+      }, bw);
+      load_w<4, ABL>(bw, wr, wl, OT ? wD + (OT0_OFF - WU2_OFF) : wA);
       const int n = 32 * nb + lr;
-      const float ub = W.ub2[n];
+      const float ub = BS[2 * BF + n];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = 32 * mb + acc_row(r, lane);
@@ -534,8 +578,9 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       f32x16 acc[1];
       if (wave < 4) {
         zero(acc[0]);
-        x3_planes<1, 4, ABL>(acc, split_rows(0), W.planes + OT0_OFF + frag_off(32 * nb, 0, BF) + 8 * lane);
-        const float bias = W.ob0[n];
+        x3_mfma<1, 4, ABL>(acc, split_rows(0), bw);
+        load_w<4, ABL>(bw, wr, wl, wD + (OT2_OFF - WU2_OFF));
+        const float bias = BS[3 * BF + n];
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           PT[(32 * mb + acc_row(r, lane)) * PSS + BF + n] = relu(acc[0][r] + bias);
@@ -543,8 +588,9 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       __syncthreads();
       if (wave < 4) {
         zero(acc[0]);
-        x3_planes<1, 4, ABL>(acc, split_rows(BF), W.planes + OT2_OFF + frag_off(32 * nb, 0, BF) + 8 * lane);
-        const float bias = W.ob2[n];
+        x3_mfma<1, 4, ABL>(acc, split_rows(BF), bw);
+        load_w<4, ABL>(bw, wr, wl, wA);
+        const float bias = BS[4 * BF + n];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int d = d0 + 32 * mb + acc_row(r, lane);
