@@ -47,6 +47,9 @@ struct GemmArgs {
   // gemm_x3 with A already split (x3_split_kernel): three bf16 planes [3][M][K] at apl
   const unsigned short* apl;
   size_t apl_plane;   // elements per plane (M * K)
+  // gemm_p3: W already split too, three bf16 planes [3][N][K] at bpl (row stride K)
+  const unsigned short* bpl;
+  size_t bpl_plane;   // elements per plane (N * K)
 };
 
 __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int col, float acc) {
@@ -1283,6 +1286,170 @@ __global__ __launch_bounds__(256) void streamk_fixup4_kernel(GemmArgs p, int BM,
   epilogue_store4(p, row, col, v);
 }
 
+// gemm_x3 on operands that are ALREADY split ("p3"): A as three bf16 planes [3][M][K] (p.apl,
+// plane stride p.apl_plane) and W as three planes [3][N][K] (p.bpl, p.bpl_plane), row stride K,
+// K % 32 == 0.  Nothing is converted in the tile: each 32-k stage (three planes of BM + BN rows
+// x 64 B = 72 KB for 256 x 128) goes global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KB per
+// wave-instruction, no VGPR round trip, no VALU, no ds_write), double-buffered, one raw barrier
+// per stage: stage kt + 1 is issued right after the barrier that retires stage kt - 1's reads
+// and has the whole of stage kt's MFMAs to land.  The LDS image is gemm_x3's (plane-major,
+// [row][32 bf16], 16-B chunk c stored at c ^ ((row >> 2) & 3)): the swizzle is applied on the
+// global address, since a DMA's LDS destination is lane-linear.  Same products in the same
+// order as gemm_x3, so the same bits for the same split-K partition.
+template <int BM, int BN, int WGM, int WGN>
+constexpr int p3_smem_bytes() {
+  constexpr int NW = WGM * WGN, WM = BM / WGM;
+  constexpr int BUF = 3 * (BM + BN) * 64, STAGE = NW * WM * 36 * 4;
+  return 2 * BUF > STAGE ? 2 * BUF : STAGE;
+}
+
+template <int BM, int BN, int WGM, int WGN>
+__device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int mt, int nt,
+                                             int sp, int kbeg, int kend) {
+  constexpr int BK = 32;
+  constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TI = WM / 32, TJ = WN / 32;
+  constexpr int ROWS = BM + BN;
+  constexpr int PLANE = ROWS * 64, BUF = 3 * PLANE;
+  constexpr int PIECES = 3 * ROWS / 16;            // 1-KB DMA pieces per stage
+  static_assert(ROWS % 16 == 0 && PIECES % NW == 0 && TI >= 1 && TJ >= 1, "bad p3 tile");
+  constexpr int PPW = PIECES / NW;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+
+  // piece q * NW + wave covers image rows 16 piece .. + 15 (plane-major [3][ROWS]); lane l lands
+  // at byte 16 l of it: row 16 piece + (l >> 2), chunk slot l & 3 = logical chunk (l & 3) ^ key
+  const unsigned short* src[PPW];
+#pragma unroll
+  for (int q = 0; q < PPW; ++q) {
+    const int R = (q * NW + wave) * 16 + (lane >> 2);
+    const int pl = R / ROWS, r = R % ROWS;
+    const int c = (lane & 3) ^ ((r >> 2) & 3);
+    if (r < BM) {
+      const int gr = min(m0 + r, p.M - 1);
+      src[q] = p.apl + pl * p.apl_plane + (size_t)gr * p.K + 8 * c;
+    } else {
+      const int gr = min(n0 + r - BM, p.N - 1);
+      src[q] = p.bpl + pl * p.bpl_plane + (size_t)gr * p.K + 8 * c;
+    }
+  }
+  auto issue = [&](int buf, int k0) {
+#pragma unroll
+    for (int q = 0; q < PPW; ++q)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src[q] + k0),
+          (__attribute__((address_space(3))) void*)(smem + buf * BUF + (q * NW + wave) * 1024),
+          16, 0, 0);
+  };
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  int aoff[TI], akey[TI], boff[TJ], bkey[TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int row = wm * WM + i * 32 + (lane & 31);
+    aoff[i] = row * 64;
+    akey[i] = (row >> 2) & 3;
+  }
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int row = BM + wn * WN + j * 32 + (lane & 31);
+    boff[j] = row * 64;
+    bkey[j] = (row >> 2) & 3;
+  }
+  const int hk = lane >> 5;
+  struct Frags { bf16x8 a[3][TI], b[3][TJ]; };
+  auto read = [&](Frags& f, const char* S, int s) {
+    const int c = 2 * s + hk;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+        f.a[pl][i] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + aoff[i] + ((c ^ akey[i]) << 4));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        f.b[pl][j] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + boff[j] + ((c ^ bkey[j]) << 4));
+    }
+  };
+  auto mfma6 = [&](const Frags& f, int i, int j) {
+    f32x16 t = acc[i][j];
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[2][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[2][i], f.b[0][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[1][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[1][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[0][j], t, 0, 0, 0);
+    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[0][j], t, 0, 0, 0);
+  };
+  constexpr int NG = TI * TJ;
+  const int nk = (kend - kbeg) / BK;
+  if (nk > 0) issue(0, kbeg);
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vm<0>();          // this wave's pieces of stage kt have landed
+    lds_barrier();         // ... everyone's; and every wave is done reading stage kt - 1
+    if (kt + 1 < nk) issue((kt + 1) & 1, kbeg + (kt + 1) * BK);
+    const char* S = smem + (kt & 1) * BUF;
+    Frags f0, f1;
+    read(f0, S, 0);
+#pragma unroll
+    for (int g = 0; g < 2 * NG; ++g) {
+      if (g < NG) mfma6(f0, g / TJ, g % TJ);
+      else mfma6(f1, (g - NG) / TJ, (g - NG) % TJ);
+      if (g == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        read(f1, S, 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
+                            reinterpret_cast<float*>(smem) + wave * (WM * 36));
+}
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[p3_smem_bytes<BM, BN, WGM, WGN>()];
+  const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
+  const int nwg = mt_n * nt_n * p.splits;
+  const int bid = xcd_swizzle(blockIdx.x, nwg);
+  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
+  gemm_p3_body<BM, BN, WGM, WGN>(p, smem, mt, nt, sp, kbeg, kend);
+}
+
+// gemm_p3 in stream-K form (see gemm_x3_sk), pieces summed by streamk_fixup4_kernel
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3_sk(GemmArgs p, int KT, long I) {
+  __shared__ __attribute__((aligned(1024))) char smem[p3_smem_bytes<BM, BN, WGM, WGN>()];
+  const int B = gridDim.x;
+  const int b = xcd_swizzle(blockIdx.x, B);
+  const int mt_n = (p.M + BM - 1) / BM;
+  long i0 = (long)b * I / B;
+  const long i1 = (long)(b + 1) * I / B;
+  while (i0 < i1) {
+    const int t = (int)(i0 / KT);
+    const int k0 = (int)(i0 - (long)t * KT);
+    const int k1 = (int)min((long)KT, k0 + (i1 - i0));
+    GemmArgs q = p;
+    int sp = 0;
+    if (k0 == 0 && k1 == KT) {
+      q.splits = 1;
+    } else {
+      q.splits = 2;
+      sp = b - sk_block_of((long)t * KT, I, B);
+    }
+    gemm_p3_body<BM, BN, WGM, WGN>(q, smem, t % mt_n, t / mt_n, sp, 32 * k0, min(p.K, 32 * k1));
+    i0 += k1 - k0;
+    if (i0 < i1) __syncthreads();
+  }
+}
+
 // gemm_x3 as a two-group ping-pong ("x3pp").  The timing ablations of gemm_x3 (tools/gemm_sweep.py
 // x3, tuning tiles 7-11) showed its MFMAs and its other work do not overlap: M = 4096 takes
 // 518 us, 219 us of it without any MFMA and ~200 us of MFMA alone; the loads are not the
@@ -2474,9 +2641,9 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   if (env && tile == 0) return false;
   if (!env && a.M <= 64) return false;  // tools/gemm_sweep.py x3: fp32 tiles win to M = 64 (27 vs 31 us)
   // 7..11: gemm_x3<256,128> timing ablations (ABL 1, 2, 4, 5, 3), K % 32 == 0 only
-  const int bms[15] = {0, 256, 128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
-  const int bns[15] = {0, 128, 128, 64, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
-  if (tile < 1 || tile > 14 || ((tile >= 7 && tile <= 11) || tile == 13) && a.K % 32 != 0) {
+  const int bms[16] = {0, 256, 128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
+  const int bns[16] = {0, 128, 128, 64, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
+  if (tile < 1 || tile > 15 || ((tile >= 7 && tile <= 11) || tile >= 13) && a.K % 32 != 0) {
     tile = a.M > 256 ? 1 : 2;
   }
   const int bm = bms[tile], bn = bns[tile];
@@ -2540,6 +2707,52 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
     a.apl = pl;
     a.apl_plane = (size_t)a.M * a.K;
     hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 0, true>), grid, dim3(512), 0, s, a);
+    return true;
+  }
+  // tile 15: gemm_p3 -- both operands split into planes first (x3_split_kernel into buffers of
+  // this build); AZ_P3_REUSE=1 splits only on the first call (a probe with fixed operands then
+  // times the tile kernel alone); AZ_P3_SK=1 the stream-K grid
+  if (tile == 15 && whole && a.lda == a.K && a.ldb == a.K) {
+    static unsigned short* pbuf = nullptr;
+    static size_t pcap = 0;
+    static const float *lastA = nullptr, *lastB = nullptr;
+    static const bool reuse = tuning_env("AZ_P3_REUSE") != nullptr;
+    static const bool sk = tuning_env("AZ_P3_SK") != nullptr;
+    const size_t need = (size_t)3 * ((size_t)a.M + a.N) * a.K;
+    if (need > pcap) {
+      if (pbuf) (void)hipFree(pbuf);
+      if (hipMalloc(&pbuf, need * 2) != hipSuccess) return false;
+      pcap = need;
+      lastA = lastB = nullptr;
+    }
+    a.apl = pbuf;
+    a.apl_plane = (size_t)a.M * a.K;
+    a.bpl = pbuf + 3 * a.apl_plane;
+    a.bpl_plane = (size_t)a.N * a.K;
+    if (!reuse || lastA != a.A || lastB != a.B) {
+      const long sa = (long)a.M * (a.K / 8), sb = (long)a.N * (a.K / 8);
+      hipLaunchKernelGGL(x3_split_kernel, dim3((unsigned)((sa + 255) / 256)), dim3(256), 0, s,
+                         a.A, a.lda, a.M, a.K, pbuf, a.apl_plane);
+      hipLaunchKernelGGL(x3_split_kernel, dim3((unsigned)((sb + 255) / 256)), dim3(256), 0, s,
+                         a.B, a.ldb, a.N, a.K, const_cast<unsigned short*>(a.bpl), a.bpl_plane);
+      lastA = a.A;
+      lastB = a.B;
+    }
+    const int KT = a.K / 32;
+    const long I = tiles * (long)KT;
+    const int B = (int)std::min<long>(256, I);
+    const long per = I / B;
+    // slabs: a tile is cut into at most ceil(KT / per) + 1 pieces, each one M x N slab
+    const long smax = per > 0 ? (KT + per - 1) / per + 1 : 0;
+    if (sk && a.slab && a.vec_epi && per >= 1 && (size_t)smax * a.M * a.N * 4 <= ws_bytes) {
+      hipLaunchKernelGGL((gemm_p3_sk<256, 128, 4, 2>), dim3(B), dim3(512), 0, s, a, KT, I);
+      const long n4 = (long)a.M * (a.N / 4);
+      hipLaunchKernelGGL(streamk_fixup4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                         a, 256, 128, KT, I, B);
+      a.splits = 1;
+      return true;
+    }
+    hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2>), grid, dim3(512), 0, s, a);
     return true;
   }
 #endif

@@ -485,6 +485,7 @@ struct az_mcts {
   int use_gnn = 0;
   std::vector<Tree> trees;
   std::vector<int32_t> last_order;             // slots of the last collect, in output order
+  std::vector<int32_t> row_of;                 // feed_collect: slot -> row of the fed batch
   std::vector<int8_t> leafbuf;
   int threads = 1;                             // host threads of the last collect (feed too)
   RowCache cache;
@@ -995,6 +996,45 @@ int az_mcts_episode_targets(const az_mcts* m, int slot, double* init_policy, dou
   return AZM_OK;
 }
 
+int az_mcts_episodes_moves(const az_mcts* m, const int32_t* slots, int n, int32_t* moves) {
+  if (!m || (n > 0 && (!slots || !moves)) || n < 0)
+    return fail(AZM_EINVAL, "az_mcts_episodes_moves: bad args");
+  for (int i = 0; i < n; ++i) {
+    if (!slot_ok(m, slots[i])) return fail(AZM_EINVAL, "az_mcts_episodes_moves: bad slot");
+    moves[i] = (int32_t)m->trees[slots[i]].ep.curs.size();
+  }
+  return AZM_OK;
+}
+
+int az_mcts_episode_records(const az_mcts* m, const int32_t* slots, int n, int8_t* boards,
+                            int8_t* curs, int8_t* temps, int32_t* actions, double* pi,
+                            int32_t* init_nsa, int8_t* init_has, float* std_v, int32_t* exp_nsa,
+                            double* exp_q, int8_t* exp_tag, int* result_tags, double* results,
+                            double* init_policy, double* exp_policy, int8_t* exp_value_tag,
+                            double* exp_value) {
+  if (!m || n < 0 || (n > 0 && !slots)) return fail(AZM_EINVAL, "az_mcts_episode_records: bad args");
+  const bool tg = init_policy != nullptr;
+  if (tg && (!exp_policy || !exp_value_tag || !exp_value))
+    return fail(AZM_EINVAL, "az_mcts_episode_records: partial target pointers");
+  const size_t A = (size_t)m->R.A, C = (size_t)m->R.cells;
+  size_t o = 0;                                 // first move of episode i in the outputs
+  for (int i = 0; i < n; ++i) {
+    const int s = slots[i];
+    if (int rc = az_mcts_episode_record(m, s, boards + o * C, curs + o, temps + o, actions + o,
+                                        pi + o * A, init_nsa + o * A, init_has + o * A, std_v + o,
+                                        exp_nsa + o * A, exp_q + o * A, exp_tag + o * A,
+                                        result_tags + i, results + i))
+      return rc;
+    if (tg) {
+      if (int rc = az_mcts_episode_targets(m, s, init_policy + o * A, exp_policy + o * A,
+                                           exp_value_tag + o, exp_value + o))
+        return rc;
+    }
+    o += m->trees[s].ep.curs.size();
+  }
+  return AZM_OK;
+}
+
 int az_rng_test(uint32_t seed, int op, int n, const double* p, int np_, int64_t* out) {
   // differential-test hook: op 0 = n x next uint32, 1 = n x randint(np_), 2 = n x choice(np_, p)
   MT19937 r;
@@ -1051,13 +1091,43 @@ int az_mcts_remaining_all(const az_mcts* m, int32_t* out) {
   return AZM_OK;
 }
 
-int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int threads) {
-  if (!m || !boards || !slots || cap < 0) return fail(AZM_EINVAL, "az_mcts_collect: bad args");
-  if (m->spec_slot >= 0)
-    return fail(AZM_ESTATE, "az_mcts_collect: a collect_spec request was not fed");
-  for (auto& t : m->trees)
-    if (t.pending_leaf >= 0 && !m->last_order.empty())
-      return fail(AZM_ESTATE, "az_mcts_collect: the previous leaves were not fed");
+}  // extern "C"
+
+namespace {
+
+// One network row for a slot's pending request (az_mcts_feed's body): expand_tree's root
+// predict takes v only; a leaf is expanded and its value backed up.  failed = the reference's
+// uniform priors / v = 0 (MCTS.py:195-200), or an aborted episode for a root predict (unguarded
+// in the reference, MCTS.py:108-113).  Returns 1 when the episode was aborted.
+int feed_row(az_mcts* m, Tree& t, int i, const float* pi, const float* v, const float* gpi,
+             const float* gv, bool failed) {
+  const int A = m->R.A;
+  if (t.pending_std) {
+    t.pending_std = false;
+    if (failed) {
+      t.ep.phase = E_ABORTED;
+      return 1;
+    }
+    Node& nd = t.nodes[t.find_or_add(t.ep.board, m->R)];
+    nd.std_v = v[i];
+    nd.std_epoch = t.epoch;
+    return 0;
+  }
+  expand(m, t, failed ? nullptr : pi + (size_t)i * A, failed ? 0.f : v[i],
+         (failed || !m->use_gnn) ? nullptr : gpi + (size_t)i * A,
+         (failed || !m->use_gnn) ? 0.f : gv[i], failed);
+  return 0;
+}
+
+struct FeedRows {        // rows of the previous collect, fed inside the next one
+  const int32_t* row_of; // slot -> row index, -1 = none
+  const float *pi, *v, *gpi, *gv;
+};
+
+// az_mcts_collect's body; with fr, each group of slots first takes its network rows (the feed
+// and the next descents of a slot run back to back on one thread, in one parallel region).
+int collect_impl(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int threads,
+                 const FeedRows* fr) {
   const int S = (int)m->trees.size();
   std::vector<uint8_t> has(S, 0);
   if (threads < 1) threads = 1;
@@ -1068,6 +1138,11 @@ int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int thr
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
   for (int gi = 0; gi < ngroups; ++gi) {
     const int s0 = gi * kGroup, s1 = std::min(S, s0 + kGroup);
+    if (fr) {
+      for (int s = s0; s < s1; ++s)
+        if (fr->row_of[s] >= 0)
+          feed_row(m, m->trees[s], fr->row_of[s], fr->pi, fr->v, fr->gpi, fr->gv, false);
+    }
     for (;;) {
       Tree* need[kGroup];
       int nn = 0;
@@ -1104,42 +1179,60 @@ int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int thr
   return cnt;
 }
 
-int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const float* gpi,
-                 const float* gv, int failed) {
+// the checks az_mcts_feed / az_mcts_feed_collect share
+int check_feed(const az_mcts* m, int count, const float* pi, const float* v, const float* gpi,
+               const float* gv, int failed, const char* what) {
   if (!m || count != (int)m->last_order.size())
-    return fail(AZM_EINVAL, "az_mcts_feed: count differs from the last collect");
+    return fail(AZM_EINVAL, std::string(what) + ": count differs from the last collect");
   if (!failed && (!pi || !v || (m->use_gnn && (!gpi || !gv))))
-    return fail(AZM_EINVAL, "az_mcts_feed: missing network outputs");
-  const int A = m->R.A;
+    return fail(AZM_EINVAL, std::string(what) + ": missing network outputs");
   for (int i = 0; i < count; ++i) {
     const Tree& t = m->trees[m->last_order[i]];
     if (t.pending_leaf < 0 && !t.pending_std)
-      return fail(AZM_ESTATE, "az_mcts_feed: slot has no pending request");
+      return fail(AZM_ESTATE, std::string(what) + ": slot has no pending request");
   }
+  return AZM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int threads) {
+  if (!m || !boards || !slots || cap < 0) return fail(AZM_EINVAL, "az_mcts_collect: bad args");
+  if (m->spec_slot >= 0)
+    return fail(AZM_ESTATE, "az_mcts_collect: a collect_spec request was not fed");
+  for (auto& t : m->trees)
+    if (t.pending_leaf >= 0 && !m->last_order.empty())
+      return fail(AZM_ESTATE, "az_mcts_collect: the previous leaves were not fed");
+  return collect_impl(m, boards, slots, cap, threads, nullptr);
+}
+
+int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const float* gpi,
+                 const float* gv, int failed) {
+  if (const int rc = check_feed(m, count, pi, v, gpi, gv, failed, "az_mcts_feed")) return rc;
   // every leaf belongs to a different slot's tree: the expansions are independent
   int aborted = 0;
 #pragma omp parallel for schedule(dynamic, 8) num_threads(m->threads) if (count >= 32) \
     reduction(+ : aborted)
-  for (int i = 0; i < count; ++i) {
-    Tree& t = m->trees[m->last_order[i]];
-    if (t.pending_std) {                        // expand_tree's root predict: v only
-      t.pending_std = false;
-      if (failed) {                             // unguarded in the reference (MCTS.py:108-113)
-        t.ep.phase = E_ABORTED;
-        aborted += 1;
-        continue;
-      }
-      Node& nd = t.nodes[t.find_or_add(t.ep.board, m->R)];
-      nd.std_v = v[i];
-      nd.std_epoch = t.epoch;
-      continue;
-    }
-    expand(m, t, failed ? nullptr : pi + (size_t)i * A, failed ? 0.f : v[i],
-           (failed || !m->use_gnn) ? nullptr : gpi + (size_t)i * A,
-           (failed || !m->use_gnn) ? 0.f : gv[i], failed != 0);
-  }
+  for (int i = 0; i < count; ++i)
+    aborted += feed_row(m, m->trees[m->last_order[i]], i, pi, v, gpi, gv, failed != 0);
   m->last_order.clear();
   return aborted;
+}
+
+int az_mcts_feed_collect(az_mcts* m, int count, const float* pi, const float* v,
+                         const float* gpi, const float* gv, int8_t* boards, int32_t* slots,
+                         int cap, int threads) {
+  if (const int rc = check_feed(m, count, pi, v, gpi, gv, 0, "az_mcts_feed_collect")) return rc;
+  if (!boards || !slots || cap < 0) return fail(AZM_EINVAL, "az_mcts_feed_collect: bad args");
+  if (m->spec_slot >= 0)
+    return fail(AZM_ESTATE, "az_mcts_feed_collect: a collect_spec request was not fed");
+  m->row_of.assign(m->trees.size(), -1);
+  for (int i = 0; i < count; ++i) m->row_of[m->last_order[i]] = i;
+  m->last_order.clear();
+  const FeedRows fr{m->row_of.data(), pi, v, gpi, gv};
+  return collect_impl(m, boards, slots, cap, threads, &fr);
 }
 
 int az_mcts_cache_put(az_mcts* m, int count, const int8_t* boards, const float* pi, const float* v,

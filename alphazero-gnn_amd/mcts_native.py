@@ -45,6 +45,8 @@ _SIGS = {
     "az_mcts_remaining_all": (ctypes.c_int, [_P, _P]),
     "az_mcts_collect": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, ctypes.c_int]),
     "az_mcts_feed": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int]),
+    "az_mcts_feed_collect": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P, _P,
+                                            ctypes.c_int, ctypes.c_int]),
     "az_mcts_cache_put": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "az_mcts_cache_clear": (ctypes.c_int, [_P]),
     "az_mcts_collect_spec": (ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.c_int]),
@@ -65,6 +67,8 @@ _SIGS = {
     "az_mcts_episode_moves": (ctypes.c_int, [_P, ctypes.c_int]),
     "az_mcts_episode_record": (ctypes.c_int, [_P, ctypes.c_int] + [_P] * 13),
     "az_mcts_episode_targets": (ctypes.c_int, [_P, ctypes.c_int] + [_P] * 4),
+    "az_mcts_episodes_moves": (ctypes.c_int, [_P, _P, ctypes.c_int, _P]),
+    "az_mcts_episode_records": (ctypes.c_int, [_P, _P, ctypes.c_int] + [_P] * 17),
     "az_rng_test": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int,
                                    _P]),
     "az_rng_doubles": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, _P]),
@@ -202,6 +206,14 @@ class Engine:
         ptrs = self._rows_ptrs("Engine.feed", k, pi, v, gpi, gv, at_least=True)
         return _check(lib().az_mcts_feed(self.h, k, *ptrs, 0), "az_mcts_feed")
 
+    def feed_collect(self, k, pi, v, gpi=None, gv=None, threads=1):
+        """feed(k, pi, v, gpi, gv) then collect(threads) in one native pass (az_mcts_feed_collect);
+        -> the new leaf count, boards in self.leaf_boards[:n]."""
+        ptrs = self._rows_ptrs("Engine.feed_collect", int(k), pi, v, gpi, gv, at_least=True)
+        return _check(lib().az_mcts_feed_collect(self.h, int(k), *ptrs, self._pb, self._ps,
+                                                 self.slots, int(threads)),
+                      "az_mcts_feed_collect")
+
     def _rows_ptrs(self, what, k, pi, v, gpi, gv, at_least):
         """Checked float32 row pointers for pi / v (/ gpi / gv when use_gnn): the C side reads
         pi + i*A for i < k, so shapes are verified before any pointer escapes.  Up to 64 rows
@@ -288,10 +300,54 @@ class Engine:
                "az_mcts_episode_begin")
 
     def episodes_finished(self):
-        out = np.zeros(self.slots, np.int32)
-        k = _check(lib().az_mcts_episode_finished(self.h, _ptr(out), self.slots),
+        if not hasattr(self, "_fin"):
+            self._fin = np.zeros(self.slots, np.int32)
+            self._pfin = _ptr(self._fin)
+        k = _check(lib().az_mcts_episode_finished(self.h, self._pfin, self.slots),
                    "az_mcts_episode_finished")
-        return out[:k].tolist()
+        return self._fin[:k].tolist()
+
+    _REC = (("boards", np.int8, "C"), ("cur", np.int8, 1), ("temp", np.int8, 1),
+            ("action", np.int32, 1), ("pi", np.float64, "A"), ("init_nsa", np.int32, "A"),
+            ("init_has", np.int8, "A"), ("std_v", np.float32, 1), ("exp_nsa", np.int32, "A"),
+            ("exp_q", np.float64, "A"), ("exp_tag", np.int8, "A"))
+    _TGT = (("init_policy", np.float64, "A"), ("exp_policy", np.float64, "A"),
+            ("exp_value_tag", np.int8, 1), ("exp_value", np.float64, 1))
+
+    def episode_records(self, slots):
+        """episode_record for several finished slots with two engine calls: every field of all
+        of them is copied into ONE array per field (az_mcts_episode_records) and each record
+        holds views of its episode's rows."""
+        n = len(slots)
+        if n == 0:
+            return []
+        sl = np.asarray(slots, np.int32)
+        moves = np.zeros(n, np.int32)
+        _check(lib().az_mcts_episodes_moves(self.h, _ptr(sl), n, _ptr(moves)),
+               "az_mcts_episodes_moves")
+        tot = int(moves.sum())
+        A, c = self.A, self.n
+        width = {"C": (c, c), "A": (A,), 1: ()}
+        big = {k: np.empty((tot,) + width[w], dt) for k, dt, w in self._REC}
+        tg = {k: np.empty((tot,) + width[w], dt) for k, dt, w in self._TGT} if self.use_gnn else {}
+        rtag = np.zeros(n, np.intc)
+        rval = np.zeros(n, np.float64)
+        tp = [_ptr(tg[k]) for k, _, _ in self._TGT] if self.use_gnn else [None] * 4
+        _check(lib().az_mcts_episode_records(self.h, _ptr(sl), n,
+                                             *[_ptr(big[k]) for k, _, _ in self._REC],
+                                             _ptr(rtag), _ptr(rval), *tp),
+               "az_mcts_episode_records")
+        out = []
+        o = 0
+        vals = rval.tolist()
+        for i, m in enumerate(moves.tolist()):
+            r = {k: a[o:o + m] for k, a in big.items()}
+            r["result"] = int(vals[i]) if rtag[i] == TAG_INT else float(vals[i])
+            if tg:
+                r.update({k: a[o:o + m] for k, a in tg.items()})
+            out.append(r)
+            o += m
+        return out
 
     def episode_record(self, slot):
         """Per-move records of a finished episode (see include/az_mcts.h)."""

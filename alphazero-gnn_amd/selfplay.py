@@ -340,6 +340,7 @@ class _EpisodeLane:
         self.rounds = self.rows = 0
         self.assemble_s = 0.0
         self.assembler, self.pending = None, []
+        self.fed = None            # rows of the last batch, fed by the next gather
 
     def start(self):
         while self.queue and self.free:
@@ -356,15 +357,17 @@ class _EpisodeLane:
         import time
         from mcts_native import assemble_episode
         t = time.perf_counter()
-        for slot in self.eng.episodes_finished():
-            e = self.running.pop(slot)
-            rec = self.eng.episode_record(slot)
-            if self.assembler is None:
-                self.results[e] = assemble_episode(self.game, self.args, rec)
-            else:
-                self.pending.append((e, self.assembler.submit(assemble_episode, self.game,
-                                                              self.args, rec)))
-            self.free.append(slot)
+        fin = self.eng.episodes_finished()
+        if fin:
+            recs = self.eng.episode_records(fin)
+            for slot, rec in zip(fin, recs):
+                e = self.running.pop(slot)
+                if self.assembler is None:
+                    self.results[e] = assemble_episode(self.game, self.args, rec)
+                else:
+                    self.pending.append((e, self.assembler.submit(assemble_episode, self.game,
+                                                                  self.args, rec)))
+                self.free.append(slot)
         self.assemble_s += time.perf_counter() - t
         self.start()
 
@@ -374,7 +377,12 @@ class _EpisodeLane:
         self.pending = []
 
     def gather(self):
-        self.k = self.eng.collect(self.threads)
+        if self.fed is not None:        # last round's rows are fed inside this collect
+            pi, v, gpi, gv = self.fed
+            self.fed = None
+            self.k = self.eng.feed_collect(self.k, pi, v, gpi, gv, self.threads)
+        else:
+            self.k = self.eng.collect(self.threads)
         if not self.k:
             return None
         self.rounds += 1
@@ -382,6 +390,9 @@ class _EpisodeLane:
         return self.eng.leaf_boards[:self.k]
 
     def deliver(self, pending):
+        """A finished prediction: on success its rows are kept for the next gather
+        (az_mcts_feed_collect: the feed and the next descents in one native pass; episodes only
+        finish inside a collect, so harvesting first sees the same slots as feeding first)."""
         if pending is not None:
             try:
                 pi, v, gpi, gv = pending.result()
@@ -399,7 +410,7 @@ class _EpisodeLane:
                     raise err
                 nn_fallback.record("selfplay.engine", err, self.k)
             else:                     # engine errors (shapes, state) propagate as themselves
-                self.eng.feed(self.k, pi, v, gpi, gv)
+                self.fed = (pi, v, gpi, gv)
         self.harvest()
 
     def live(self):

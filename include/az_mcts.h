@@ -85,6 +85,15 @@ int az_mcts_collect(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int thr
 int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const float* gpi,
                  const float* gv, int failed);
 
+/* az_mcts_feed (network rows for the last collect, never failed) followed by az_mcts_collect, in
+ * ONE parallel pass: each worker thread feeds a group of slots and runs their next descents back
+ * to back.  Same trees and leaves as the two calls (every slot's work is independent of the
+ * others').  Returns the new leaf count like az_mcts_collect.  A failed batch goes through
+ * az_mcts_feed(failed = 1) instead. */
+int az_mcts_feed_collect(az_mcts* m, int count, const float* pi, const float* v,
+                         const float* gpi, const float* gv, int8_t* boards, int32_t* slots,
+                         int cap, int threads);
+
 /* Speculative rows: network outputs of boards the search has not asked for yet (the arena
  * evaluates a leaf together with its children, mcts_native.ArenaPlayer), same layout as
  * az_mcts_feed.  A later search that reaches one of these boards as a new leaf is expanded from
@@ -140,6 +149,16 @@ int az_mcts_episode_record(const az_mcts* m, int slot, int8_t* boards, int8_t* c
  * had no visits before expansion gets valids / sum(valids). */
 int az_mcts_episode_targets(const az_mcts* m, int slot, double* init_policy, double* exp_policy,
                             int8_t* exp_value_tag, double* exp_value);
+/* Batched export for the self-play driver: moves[i] = az_mcts_episode_moves(slots[i]), and the
+ * records (+ the targets when init_policy != NULL) of n finished slots written back to back into
+ * arrays sized for sum(moves) (episode i starts at move sum(moves[:i])), result i at index i. */
+int az_mcts_episodes_moves(const az_mcts* m, const int32_t* slots, int n, int32_t* moves);
+int az_mcts_episode_records(const az_mcts* m, const int32_t* slots, int n, int8_t* boards,
+                            int8_t* curs, int8_t* temps, int32_t* actions, double* pi,
+                            int32_t* init_nsa, int8_t* init_has, float* std_v, int32_t* exp_nsa,
+                            double* exp_q, int8_t* exp_tag, int* result_tags, double* results,
+                            double* init_policy, double* exp_policy, int8_t* exp_value_tag,
+                            double* exp_value);
 /* np.random.RandomState emulation, for tests: op 0 = n raw uint32 draws, 1 = n x randint(0, np_),
  * 2 = n x choice(np_, p=p); az_rng_doubles = n x random_sample(). */
 int az_rng_test(uint32_t seed, int op, int n, const double* p, int np_, int64_t* out);

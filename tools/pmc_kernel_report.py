@@ -29,7 +29,11 @@ for k, cs in vals.items():
     wc = a.get("SQ_WAVE_CYCLES")
     if ns and "GRBM_GUI_ACTIVE" in a:
         gui = a["GRBM_GUI_ACTIVE"]
-        out.append(f"clk_GHz={gui / 8 / ns:.3f}")
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs; the quotient reads high for dispatches shorter
+        # than ~0.3 ms (MI355X_MICROARCH.md, DVFS give-back) and is only a clock below ~2.5 GHz
+        clk = gui / 8 / ns
+        out.append(f"clk_GHz={clk:.3f}" if ns >= 3e5 and clk < 2.6 else
+                   f"clk_GHz=n/a(dispatch {ns / 1e3:.0f} us: GUI_ACTIVE/8/ns = {clk:.2f})")
         if "SQ_VALU_MFMA_BUSY_CYCLES" in a:
             out.append(f"mfma_busy={a['SQ_VALU_MFMA_BUSY_CYCLES'] / (gui / 8 * 1024):.3f}")
     if wc:

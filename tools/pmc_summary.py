@@ -82,7 +82,7 @@ def main(d, tag):
                  "dispatches": nf,
                  "hbm_bytes_per_launch": gemm_tile + gemm_red,
                  "gemm_kernel_bytes": gemm_tile, "reduce_kernel_bytes": gemm_red,
-                 "algorithmic_bytes": 4 * (B * F + F * F + F + B * F)},
+                 "algorithmic_bytes": 4 * (B * F + F * F + F + B * F), "tag": tag},
     }
     if agg and aggw:
         V, E = 512 * 1024, 512 * 3968
@@ -101,7 +101,13 @@ def main(d, tag):
                 ("gnn_layer_fused", lambda n: "gnn_layer_fused_kernel" in n,
                  V * 1024 + 4 * E + 4 * (V + 1)),
                 ("gnn_source_proj", lambda n: "gemm_tall" in n or "gemm_f32" in n,
-                 V * 64 * 4 + 128 * 64 * 4 + V * 128 * 4)):
+                 V * 64 * 4 + 128 * 64 * 4 + V * 128 * 4),
+                # round 3 (tools/band_probe.py): the band-mode layer, one launch per layer (x read
+                # once, x_out written, the CSR); OT = the last layer with output_transform fused
+                ("gnn_layer_band", lambda n: "gnn_layer_band_kernel<0, false>" in n,
+                 V * 64 * 4 * 2 + 4 * E + 4 * (V + 1)),
+                ("gnn_layer_band_ot", lambda n: "gnn_layer_band_kernel<0, true>" in n,
+                 V * 64 * 4 * 2 + 4 * E + 4 * (V + 1))):
             a = [kb for _, n, kb, _ in fe2 if pred(n)]
             b = [kb for _, n, kb, _ in wr2 if pred(n)]
             if a and b:
@@ -109,9 +115,10 @@ def main(d, tag):
                             "hbm_bytes_per_launch": int((2 * sum(a) / len(a) + sum(b) / len(b))
                                                         * 1024),
                             "algorithmic_bytes": alg,
-                            "note": "512 32x32 grids, back-to-back launches (x and Ps partly "
+                            "tag": tag,
+                            "note": "512 32x32 grids, back-to-back launches (x partly "
                                     "Infinity-Cache resident between them)"}
-    res["round"] = 2 if tag.startswith("r02") else res["round"]
+    res["round"] = int(tag[1:3]) if tag[:3] in ("r02", "r03", "r04", "r05", "r06") else res["round"]
     # keep the entries of earlier passes this one did not measure (e.g. the fused-layer probe)
     path = os.path.join(ROOT, "profiles", "pmc.json")
     try:
