@@ -85,8 +85,9 @@ class _DirectBatch:
     be in flight), device scratch is shared (the stream orders the batches).  Replaces ~10
     torch-level launches, a pinned H2D and a D2H copy per lock-step round."""
 
-    def __init__(self, w):
+    def __init__(self, w, stream=None):
         self.w, self.cap, self.ring = w, 0, []
+        self.stream = stream      # None: the current stream; else this stream (own scratch)
         self.fn = _lib.lib().az_c4_eval_fwd
 
     def _grow(self, n):
@@ -139,7 +140,7 @@ class _DirectBatch:
         hin, outs = e["in"], e["out"]
         hin.numpy()[:n] = boards
         pi, v, gpi, gv = outs if both else (outs[0], outs[1], None, None)
-        s = torch.cuda.current_stream(self.w.device)
+        s = self.stream if self.stream is not None else torch.cuda.current_stream(self.w.device)
         P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         rc = self.fn(ctypes.byref(self.desc), ctypes.c_void_p(hin.data_ptr()), n, P(pi), P(v),
                      P(gpi), P(gv), ctypes.c_void_p(s.cuda_stream))
@@ -424,14 +425,20 @@ class NetWrapper:
         pi, v = self._eval(boards, False)
         return pi.cpu().numpy(), v.cpu().numpy()
 
-    def _launch(self, boards, both):
-        """Queue a batched prediction; returns a PendingPrediction (see predict_*_async)."""
+    def _launch(self, boards, both, stream=None):
+        """Queue a batched prediction; returns a PendingPrediction (see predict_*_async).
+        stream: run it on that HIP stream with its own device scratch (the lock-step lanes give
+        each lane a stream, so one lane's batch can overlap the other's on the GPU); the caller
+        orders the stream after any parameter update (play_episodes_engine does)."""
         if self.has_gnn and _direct_ok(self) and len(boards) > 0:
-            if getattr(self, "_direct", None) is None:
-                self._direct = _DirectBatch(self)
+            directs = self.__dict__.setdefault("_directs", {})
+            key = None if stream is None else stream.cuda_stream
+            d = directs.get(key)
+            if d is None:
+                d = directs[key] = _DirectBatch(self, stream)
             self.nnet.eval()
             self.gnn.eval()
-            return self._direct.launch(boards, both)
+            return d.launch(boards, both)
         if not hasattr(self, "_ring"):
             self._ring = _PinnedRing()
         boards = np.asarray(boards)
@@ -626,9 +633,9 @@ class GNNWrapperMixin:
         out = torch.cat([pi, v[:, None], gpi, gv[:, None]], dim=1).cpu().numpy()
         return out[:, :A], out[:, A], out[:, A + 1:2 * A + 1], out[:, 2 * A + 1]
 
-    def predict_both_async(self, boards):
+    def predict_both_async(self, boards, stream=None):
         """predict_both without waiting: .result() -> (pi, v, gnn_pi, gnn_v)."""
-        return self._launch(boards, True)
+        return self._launch(boards, True, stream)
 
     def train(self, examples, gnn_examples=None):
         self._train(examples, gnn_examples)

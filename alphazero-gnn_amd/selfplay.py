@@ -158,11 +158,11 @@ class _Immediate:
         return self.out
 
 
-def _launch(nnet, boards, want_gnn):
+def _launch(nnet, boards, want_gnn, stream=None):
     fn = getattr(nnet, "predict_both_async" if want_gnn else "predict_batch_async", None)
     try:
         if fn is not None:
-            return fn(boards)
+            return fn(boards) if stream is None else fn(boards, stream=stream)
         return _Immediate(_net_call(nnet, boards, want_gnn))
     except Exception as ex:
         return _Immediate(err=ex)
@@ -445,6 +445,7 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
             lane.assembler = pool
     for lane in L:
         lane.start()
+    streams = _lane_streams(nnet, use_gnn, lanes)
     inflight = [None] * lanes
     t0 = time.perf_counter()
     t_wait = 0.0
@@ -464,7 +465,7 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
             if lane.live():
                 boards = lane.gather()
                 if boards is not None:
-                    inflight[i] = _launch(nnet, boards, use_gnn)
+                    inflight[i] = _launch(nnet, boards, use_gnn, streams[i])
                     idle = 0
                 else:
                     lane.deliver(None)
@@ -486,6 +487,28 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
                      net_s=t_wait, host_s=time.perf_counter() - t0 - t_wait, lanes=lanes,
                      assemble_s=sum(ln.assemble_s for ln in L))
     return results
+
+
+def _lane_streams(nnet, use_gnn, lanes):
+    """One HIP stream per lane for nets whose batched predict takes one (wrappers.py: each
+    stream has its own device scratch), so a lane's batch can start while the other lane's is
+    still on the GPU; every stream first waits for the work already queued on the current
+    stream (parameter updates).  [None] * lanes otherwise (everything on the current stream)."""
+    import inspect
+    fn = getattr(nnet, "predict_both_async" if use_gnn else "predict_batch_async", None)
+    if lanes < 2 or fn is None or "stream" not in inspect.signature(fn).parameters:
+        return [None] * lanes
+    import torch
+    if not torch.cuda.is_available():
+        return [None] * lanes
+    cur = torch.cuda.current_stream()
+    held = nnet.__dict__.setdefault("_lane_streams", [])   # reused: each owns device scratch
+    while len(held) < lanes:
+        held.append(torch.cuda.Stream())
+    out = held[:lanes]
+    for st in out:
+        st.wait_stream(cur)
+    return out
 
 
 def _args_val(args, name, default=None):

@@ -47,20 +47,27 @@ int fail(const char* what) {
 }
 
 // Whole episodes in `slots` slots until `episodes` are finished.
+// fused: good batches are fed inside the next collect (az_mcts_feed_collect) and finished
+// episodes exported in one az_mcts_episode_records call per round
 int run_episodes(int game, int n, int slots, int use_gnn, int threads, int episodes, int sims,
-                 uint64_t salt) {
+                 uint64_t salt, bool fused = false) {
   az_mcts* m = az_mcts_create(game, n, slots, 1.25, use_gnn);
   if (!m) return fail("create");
   const int A = az_mcts_action_size(m), cells = n * n;
   std::vector<int8_t> boards((size_t)slots * cells);
   std::vector<int32_t> lslots(slots), fin(slots);
   std::vector<float> pi((size_t)slots * A), v(slots), gpi((size_t)slots * A), gv(slots);
-  int started = 0, finished = 0, rounds = 0;
+  int started = 0, finished = 0, rounds = 0, held = 0;   // held: rows kept for feed_collect
   for (int s = 0; s < slots && started < episodes; ++s, ++started)
     if (az_mcts_episode_begin(m, s, 1000u + (uint32_t)started, sims, 3, 4)) return fail("begin");
   while (finished < episodes) {
     if (++rounds > 200000) return fail("no progress");
-    const int k = az_mcts_collect(m, boards.data(), lslots.data(), slots, threads);
+    const int k = held > 0
+        ? az_mcts_feed_collect(m, held, pi.data(), v.data(), use_gnn ? gpi.data() : nullptr,
+                               use_gnn ? gv.data() : nullptr, boards.data(), lslots.data(), slots,
+                               threads)
+        : az_mcts_collect(m, boards.data(), lslots.data(), slots, threads);
+    held = 0;
     if (k < 0) return fail("collect");
     if (k > 0) {
       for (int i = 0; i < k; ++i) {
@@ -69,6 +76,11 @@ int run_episodes(int game, int n, int slots, int use_gnn, int threads, int episo
       }
       // an occasional failed batch: leaves degrade, an expand_tree root predict aborts
       const bool failed = (mix(salt + rounds) % 97) == 0;
+      if (fused && !failed) {
+        held = k;                        // fed by the next round's feed_collect
+        goto harvest;
+      }
+      {
       const int rc = az_mcts_feed(m, k, pi.data(), v.data(), use_gnn ? gpi.data() : nullptr,
                                   use_gnn ? gv.data() : nullptr, failed ? 1 : 0);
       if (rc < 0) return fail("feed");
@@ -78,9 +90,28 @@ int run_episodes(int game, int n, int slots, int use_gnn, int threads, int episo
           if (mv < 0) return fail("moves");
         }
       }
+      }
     }
+  harvest:
     const int f = az_mcts_episode_finished(m, fin.data(), slots);
     if (f < 0) return fail("finished");
+    if (fused && f > 0) {                // the batched export of all of them
+      std::vector<int32_t> mvs(f);
+      if (az_mcts_episodes_moves(m, fin.data(), f, mvs.data())) return fail("episodes_moves");
+      size_t tot = 0;
+      for (int i = 0; i < f; ++i) tot += (size_t)mvs[i];
+      std::vector<int8_t> b(tot * cells), cur(tot), temp(tot), has(tot * A), tag(tot * A), vt(tot);
+      std::vector<int32_t> act(tot), inn(tot * A), xn(tot * A);
+      std::vector<double> p(tot * A), xq(tot * A), ip(tot * A), xp(tot * A), xv(tot), res(f);
+      std::vector<float> sv(tot);
+      std::vector<int> rt(f);
+      if (az_mcts_episode_records(m, fin.data(), f, b.data(), cur.data(), temp.data(), act.data(),
+                                  p.data(), inn.data(), has.data(), sv.data(), xn.data(), xq.data(),
+                                  tag.data(), rt.data(), res.data(),
+                                  use_gnn ? ip.data() : nullptr, use_gnn ? xp.data() : nullptr,
+                                  use_gnn ? vt.data() : nullptr, use_gnn ? xv.data() : nullptr))
+        return fail("episode_records");
+    }
     for (int i = 0; i < f; ++i) {
       const int s = fin[i];
       const int mv = az_mcts_episode_moves(m, s);
@@ -205,9 +236,10 @@ int main() {
   for (const auto& g : games)
     for (int gnn = 0; gnn <= 1; ++gnn) {
       if (run_search(g[0], g[1], gnn)) return 1;
-      if (run_episodes(g[0], g[1], 5, gnn, 3, 9, g[0] == AZM_GAME_CONNECT4 ? 12 : 8,
-                       (uint64_t)(g[0] * 131 + g[1] * 7 + gnn)))
-        return 1;
+      for (int fused = 0; fused <= 1; ++fused)
+        if (run_episodes(g[0], g[1], 5, gnn, 3, 9, g[0] == AZM_GAME_CONNECT4 ? 12 : 8,
+                         (uint64_t)(g[0] * 131 + g[1] * 7 + gnn), fused != 0))
+          return 1;
     }
   double a[37];
   for (int i = 0; i < 37; ++i) a[i] = i * 0.25;

@@ -314,3 +314,49 @@ def test_engine_episodes_match_python_fuzz(gi, use_gnn):
     for e in eps:
         assert typed(nat[e][0]) == typed(py[e][0]), e
         assert typed(nat[e][1]) == typed(py[e][1]), e
+
+
+@pytest.mark.parametrize("use_gnn", [False, True])
+def test_feed_collect_equals_feed_then_collect(use_gnn):
+    """az_mcts_feed_collect (the feed inside the next collect's parallel pass) hands out the
+    same leaves round by round as az_mcts_feed + az_mcts_collect, and the batched record export
+    (az_mcts_episode_records) equals the per-slot az_mcts_episode_record / _targets."""
+    from connect4.Connect4Game import Connect4Game
+    from mcts_native import Engine
+    game = Connect4Game(7)
+    net = HashNet(game.getActionSize(), 5)
+    S = 12
+    engs = [Engine(game, S, 1.0, use_gnn) for _ in range(2)]
+    for e in engs:
+        for s in range(S):
+            e.episode_begin(s, 900 + s, 9, 3, 6)
+    ks = [e.collect(3) for e in engs]
+    done = [{}, {}]
+    for _ in range(5000):
+        assert ks[0] == ks[1]
+        assert np.array_equal(engs[0].leaf_boards[:ks[0]], engs[1].leaf_boards[:ks[1]])
+        if ks[0] == 0:
+            break
+        out = net.predict_both(engs[0].leaf_boards[:ks[0]])
+        engs[0].feed(ks[0], *out)
+        for j, e in enumerate(engs):
+            fin = e.episodes_finished()
+            if j == 0:
+                for s in fin:
+                    done[0][s] = e.episode_record(s)
+            else:
+                for s, r in zip(fin, e.episode_records(fin)):
+                    done[1][s] = r
+        ks = [engs[0].collect(3), engs[1].feed_collect(ks[1], *out, threads=3)]
+    for e, d in zip(engs, done):
+        for s in e.episodes_finished():
+            d[s] = e.episode_record(s)
+    assert sorted(done[0]) == sorted(done[1]) == list(range(S))
+    for s in range(S):
+        a, b = done[0][s], done[1][s]
+        assert sorted(a) == sorted(b)
+        for key in a:
+            if key == "result":
+                assert type(a[key]) is type(b[key]) and a[key] == b[key]
+            else:
+                assert a[key].dtype == b[key].dtype and np.array_equal(a[key], b[key]), key

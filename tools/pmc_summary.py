@@ -108,6 +108,8 @@ def main(d, tag):
                  V * 64 * 4 * 2 + 4 * E + 4 * (V + 1)),
                 ("gnn_layer_band_ot", lambda n: "gnn_layer_band_kernel<0, true>" in n,
                  V * 64 * 4 * 2 + 4 * E + 4 * (V + 1))):
+            if key == "gnn_source_proj" and tag >= "r03":   # no source projection in band mode
+                continue
             a = [kb for _, n, kb, _ in fe2 if pred(n)]
             b = [kb for _, n, kb, _ in wr2 if pred(n)]
             if a and b:
@@ -126,6 +128,8 @@ def main(d, tag):
     except (OSError, ValueError):
         old = {}
     for k, v in old.items():
+        if k == "gnn_source_proj" and tag >= "r03":
+            continue
         if isinstance(v, dict) and k not in res:
             v.setdefault("tag", old.get("tag"))
             res[k] = v
