@@ -68,7 +68,7 @@ class C4Eval(ctypes.Structure):
                 ("ot0_w", c_void_p), ("ot0_b", c_void_p), ("ot2_w", c_void_p),
                 ("ot2_b", c_void_p), ("max_B", c_int), ("feat", c_void_p), ("hidden", c_void_p),
                 ("y", c_void_p), ("logp", c_void_p), ("glogp", c_void_p), ("ws", c_void_p),
-                ("ws_bytes", c_size_t)]
+                ("ws_bytes", c_size_t), ("sync", c_void_p), ("err", c_void_p)]
 
 
 # name -> (restype, argtypes); every symbol here must be declared in include/az_hip.h
@@ -167,7 +167,7 @@ def load(path=LIB_PATH):
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.az_abi_version() != 1:
+    if L.az_abi_version() != 2:
         raise RuntimeError("libaz_hip.so ABI mismatch")
     _lib = L
     return L

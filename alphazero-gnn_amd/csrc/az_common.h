@@ -34,6 +34,25 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   }
 }
 
+// Bytes handed between the workgroups of ONE launch (c4_leaf_kernel; MI355X_MICROARCH.md,
+// "Hand-offs measured with sc1 loads", row 1): the producer stores them write-through (sc1),
+// every storing wave waits for its stores (vmcnt(0)) before its block counts itself, and EVERY
+// load of them is an sc1 load, which bypasses the CU's L1 (another CU's stores never refresh
+// it) -- no agent-scope fence (buffer_wbl2 / buffer_inv, several us each at 4 blocks per CU).
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16 bytes at byte offset `off` of the wave-uniform `base` (`bytes` addressable from base)
+__device__ __forceinline__ f32x4 ld4_sc1(const float* base, int off, int bytes) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

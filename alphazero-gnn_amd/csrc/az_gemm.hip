@@ -18,6 +18,7 @@
 #include "az_common.h"
 #include "az_x3.h"
 #include "az_heads.h"
+#include "az_trunk_split.h"
 
 namespace az {
 
@@ -1942,7 +1943,7 @@ __global__ __launch_bounds__(256) void gemv_f32(GemmArgs p) {
 // a load phase and an LDS-store phase so that every load of the block is in flight before the
 // first one is waited for: with the loads issued ahead of the weight stream, the store phase
 // waits for A alone (vmcnt is in order), and no load sits next to a branch.
-template <int MG, int S>
+template <int MG, int S, bool SC1 = false>   // SC1: A's rows were stored by other blocks
 struct RowStage {
   static constexpr int T = MG * S * 64;          // float4 slots
   static constexpr int NI = (T + 255) / 256;     // per thread
@@ -1961,6 +1962,10 @@ struct RowStage {
       const int idx = min((int)threadIdx.x + 256 * i, T - 1);
       const int k = (idx % (S * 64)) * 4;
       const int kc = k < p.K ? k : 0;
+      if constexpr (SC1) {                         // no A2 / gathered rows on this path
+        v[i] = ld4_sc1(p.A, (ar[i] * p.lda + kc) * 4, p.M * p.lda * 4);
+        continue;
+      }
       const float* src = (p.A2 && kc >= p.K0) ? p.A2 + (size_t)ar[i] * p.lda2 + (kc - p.K0)
                                               : p.A + (size_t)ar[i] * p.lda + kc;
       v[i] = *reinterpret_cast<const f32x4*>(src);
@@ -1985,12 +1990,23 @@ struct RowStage {
 // the first FMA -- one HBM round trip per wave instead of one per KC chunk.  Loads past K
 // re-read the row start and meet zeros in the staged A; rows past N are clamped to row 0 and
 // never stored.
-template <int MR, int S, int R>
-__device__ __forceinline__ void gemv_full_block(const GemmArgs& p, int bid, float* As) {
+// WF (the batch-1 leaf kernel): the weight rows are loaded FIRST, then pre() runs (a wait for the
+// producer of A, true = go on) and only then A is staged -- same arithmetic.
+struct NoPre {
+  __device__ bool operator()() const { return true; }
+};
+
+// SC1 (with WF): A is read with sc1 loads and C written through with sc1 stores (bias and
+// activation only: epilogue_store's arithmetic for an epilogue without C2 / R / G / beta).
+template <int MR, int S, int R, bool WF = false, class Pre = NoPre, bool SC1 = false,
+          class Pre0 = NoPre>
+__device__ __forceinline__ bool gemv_full_block(const GemmArgs& p, int bid, float* As,
+                                                Pre pre = Pre{}, Pre0 pre0 = Pre0{}) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n_base = (bid * 4 + wave) * R;
-  RowStage<MR, S> st;
-  st.load(p, 0);
+  RowStage<MR, S, SC1> st;
+  if constexpr (!WF) st.load(p, 0);
+  if (!pre0()) return false;                // (tuning experiments: delay the weight stream)
   f32x4 w[R][S];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -2002,6 +2018,10 @@ __device__ __forceinline__ void gemv_full_block(const GemmArgs& p, int bid, floa
     }
   }
   __builtin_amdgcn_sched_barrier(0);        // keep the weight stream issued before A's wait
+  if constexpr (WF) {
+    if (!pre()) return false;
+    st.load(p, 0);
+  }
   st.store(p, 0, As);
   __syncthreads();
   float acc[MR][R];
@@ -2031,8 +2051,17 @@ __device__ __forceinline__ void gemv_full_block(const GemmArgs& p, int bid, floa
     }
   if (lane < MR * R) {
     const int m = lane / R, r = lane % R;
-    if (m < p.M && n_base + r < p.N) epilogue_store(p, m, n_base + r, mine);
+    if (m < p.M && n_base + r < p.N) {
+      if constexpr (SC1) {
+        const int col = n_base + r;
+        st_sc1(p.C + (size_t)m * p.ldc + col,
+               apply_act(mine + (p.bias ? p.bias[col] : 0.f), p.act));
+      } else {
+        epilogue_store(p, m, n_base + r, mine);
+      }
+    }
   }
+  return true;
 }
 
 template <int MR, int S, int R>
@@ -2046,12 +2075,13 @@ __global__ __launch_bounds__(256) void gemv_full(GemmArgs p) {
 // budget: the wave's R weight rows are loaded ONCE into registers, then the rows of A go through
 // LDS MG at a time.  Every output is the same lane-strided fmaf chain + wave_sum as gemv_full,
 // so a row's result does not depend on M (bit-identical to the batch-1 launch).
-template <int S, int R, int MG>
-__device__ __forceinline__ void gemv_rows_block(const GemmArgs& p, int bid, float* As) {
+template <int S, int R, int MG, bool WF = false, class Pre = NoPre>
+__device__ __forceinline__ bool gemv_rows_block(const GemmArgs& p, int bid, float* As,
+                                                Pre pre = Pre{}) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n_base = (bid * 4 + wave) * R;
   RowStage<MG, S> st;
-  st.load(p, 0);
+  if constexpr (!WF) st.load(p, 0);
   f32x4 w[R][S];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -2063,6 +2093,10 @@ __device__ __forceinline__ void gemv_rows_block(const GemmArgs& p, int bid, floa
     }
   }
   __builtin_amdgcn_sched_barrier(0);        // keep the weight stream issued before A's wait
+  if constexpr (WF) {
+    if (!pre()) return false;
+    st.load(p, 0);
+  }
   st.store(p, 0, As);
   for (int m0 = 0; m0 < p.M; m0 += MG) {
     __syncthreads();                        // this group's A is in LDS
@@ -2102,6 +2136,7 @@ __device__ __forceinline__ void gemv_rows_block(const GemmArgs& p, int bid, floa
       if (m < p.M && n_base + r < p.N) epilogue_store(p, m, n_base + r, mine);
     }
   }
+  return true;
 }
 
 template <int S, int R, int MG>
@@ -2133,6 +2168,216 @@ __global__ __launch_bounds__(256) void gemv_side_heads(GemmArgs p, SideHeads h, 
                           h.wv, h.bp, h.bv, row, h.logp, h.pi, h.v, part, sm);
   }
 }
+
+// --------------------------------------------------------------------- the batch-1 leaf kernel
+// az_c4_eval_fwd for B <= 2 boards (the MCTS leaf, MCTS.py:169-173, and the arena's two-row
+// speculative batches) in
+// ONE launch instead of four (trunk, output_transform.0 + standard heads, output_transform.2,
+// GNN heads): every stage is the same device code as in the separate launches -- so every
+// output is bit-identical to them -- and the stages hand over through device-scope counters:
+//   blocks [0, 4B)            the trunk (c4_trunk_split_block), then signal sync[0];
+//   blocks [4B, 5B)           the standard heads of one board, after sync[0] = 4B; signal sync[1];
+//   next ng blocks            output_transform.0: their weight rows are loaded into registers
+//                             FIRST, while the trunk runs, then they wait for sync[0] = 4B,
+//                             stage the features and finish; signal sync[2];
+//   last ng blocks            output_transform.2 the same way behind sync[2] = ng; the last block
+//                             of each 256-column head chunk (ticket sync[4 + c]) forms that
+//                             chunk's head partials, the last chunk (ticket sync[3]) finalizes
+//                             the GNN heads and resets every counter for the next launch.
+// The 78.6 MB of output_transform weights stream in under the trunk instead of after it.  All
+// blocks must be resident at once (a waiting block holds its CU): the launcher checks the
+// occupancy first, workgroups are dispatched in index order (producers before consumers), and
+// every wait gives up after 20 ms, setting *err (host-visible) -- the caller then discards the
+// outputs, zeroes the counters and uses the four-launch path.
+struct HeadsTail {
+  const float* wp; const float* bp; int A; const float* wv; const float* bv;
+  float* logp; float* pi; float* v;
+  float* part;        // [B][chunks][9] device scratch
+};
+
+struct LeafArgs {
+  const int8_t* boards; int B;
+  const float *w1, *b1, *w2, *b2;     // conv1 / conv2
+  float* feat;
+  GemmArgs g1, g2;                    // output_transform.0 (+ ReLU), output_transform.2
+  SideHeads sh;                       // standard heads of feat
+  HeadsTail ht;                       // GNN heads of g2.C
+  int* sync;                          // [4 + chunks] device counters: zero on entry, left zero
+  int* err;                           // host-visible: 1 = a wait timed out, outputs invalid
+  int ng;                             // GEMV blocks per GEMV (8 output columns each)
+  unsigned long long* trace;          // tuning build (AZ_LEAF_TRACE): [event][min, max] stamps
+  int mode;                           // tuning build (AZ_LEAF_MODE): weight-stream experiments
+};
+
+// Timing probe of the tuning build: the earliest and latest 100 MHz wall-clock stamp of each
+// event over the blocks that pass it (tools/leaf_probe.py); compiled out of the product.
+enum LeafEv { LE_START, LE_TRUNK, LE_G1_WEIGHTS, LE_G1_GO, LE_G1_DONE, LE_G2_WEIGHTS, LE_G2_GO,
+              LE_G2_DONE, LE_CHUNK, LE_FINAL, LE_STD, LE_N };
+__device__ __forceinline__ void leaf_stamp(const LeafArgs& a, int ev) {
+#ifdef AZ_TUNING
+  if (a.trace && threadIdx.x == 0) {
+    const unsigned long long t = wall_clock64();
+    atomicMin(&a.trace[2 * ev], t);
+    atomicMax(&a.trace[2 * ev + 1], t);
+  }
+#else
+  (void)a;
+  (void)ev;
+#endif
+}
+
+constexpr uint64_t kLeafTimeoutTicks = 2000000;   // 20 ms of the 100 MHz wall clock
+// sync layout (ints): the two counters hundreds of blocks poll -- trunk done, output_transform.0
+// done -- are kept in kLeafRep replicas, each on a 128-B line of its own, so the polls spread
+// over many L2 channels instead of hammering one (MI355X_MICROARCH.md hand-off table, row 2:
+// each producer adds to every replica with ONE wave instruction, a consumer polls one replica);
+// then the standard-heads counter, the chunk-done ticket and the per-chunk tickets, one line each.
+constexpr int kLeafRep = 32, kLeafLine = 32;
+constexpr int kSyncTrunk = 0, kSyncG1 = kLeafRep * kLeafLine;
+constexpr int kSyncStd = 2 * kLeafRep * kLeafLine, kSyncChunks = kSyncStd + kLeafLine;
+constexpr int kSyncTicket0 = kSyncChunks + kLeafLine;   // + c * kLeafLine for chunk c
+constexpr int kSyncInts = kSyncTicket0 + 16 * kLeafLine;   // 16 chunks at most (K <= 4096)
+
+// wait until *ctr >= target: thread 0 polls with sc1 loads (the block parks at the barrier);
+// the handed-off bytes are then read with sc1 loads only (no acquire fence: see st_sc1)
+__device__ __forceinline__ bool leaf_wait(int* ctr, int target, int* err, int* flag) {
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      // ~0.25 us between polls: hundreds of blocks polling one line back to back slow the
+      // chip's memory traffic -- the weight streams this kernel overlaps (MI355X_MICROARCH.md:
+      // "255 pollers cut chip bandwidth 37-71 %")
+      __builtin_amdgcn_s_sleep(4);
+      if (wall_clock64() - t0 > kLeafTimeoutTicks) {
+        ok = 0;
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    *flag = ok;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// every wave's write-through stores have completed, then ONE lane counts the block (rep: in
+// every replica, lane l of wave 0 adding to replica l)
+__device__ __forceinline__ void leaf_signal(int* ctr, bool rep = false) {
+  drain_stores();
+  __syncthreads();
+  if (rep ? threadIdx.x < kLeafRep : threadIdx.x == 0)
+    __hip_atomic_fetch_add(ctr + threadIdx.x * kLeafLine, 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+// the replica of a replicated counter this block polls
+__device__ __forceinline__ int* leaf_rep(int* ctr) {
+  return ctr + (blockIdx.x % kLeafRep) * kLeafLine;
+}
+
+// leaf_signal that tells the block whether it was the total-th (last) to arrive
+__device__ __forceinline__ bool leaf_ticket(int* ctr, int total, int* flag) {
+  drain_stores();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *flag = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
+  __syncthreads();
+  return *flag != 0;
+}
+
+template <int MK>
+__global__ __launch_bounds__(256, 4) void c4_leaf_kernel(LeafArgs a) {   // <= 128 VGPRs
+  constexpr int S = 13, R = 2;
+  static_assert(MK == 1 || MK == 2, "one or two rows (the 3..8-row GEMV spills at 128 VGPRs)");
+  __shared__ union {
+    TrunkSplitSmem trunk;
+    float As[MK * S * 256];
+    struct { float part[HEADS_ROWS_MAXC * 9]; float sm[9]; } hd;
+  } sm;
+  __shared__ int flag;
+  const int nt = 4 * a.B, id = blockIdx.x;
+  leaf_stamp(a, LE_START);
+  if (id < nt) {
+    c4_trunk_split_block<true>(a.boards, a.w1, a.b1, a.w2, a.b2, a.feat, id >> 2, id & 3,
+                               sm.trunk);
+    leaf_signal(a.sync + kSyncTrunk, true);
+    leaf_stamp(a, LE_TRUNK);
+    return;
+  }
+  if (id < nt + a.B) {
+    const int row = id - nt;
+    if (leaf_wait(leaf_rep(a.sync + kSyncTrunk), nt, a.err, &flag))
+      heads_row_block<8, 4, true>(a.sh.x + (size_t)row * a.sh.ldx, a.sh.x + (size_t)row * a.sh.ldx,
+                            a.sh.K, a.sh.wp, a.sh.A, a.sh.wv, a.sh.bp, a.sh.bv, row, a.sh.logp,
+                            a.sh.pi, a.sh.v, sm.hd.part, sm.hd.sm);
+    leaf_signal(a.sync + kSyncStd);
+    leaf_stamp(a, LE_STD);
+    return;
+  }
+  const int g = id - nt - a.B;
+  const bool second = g >= a.ng;
+  auto gemv = [&](const GemmArgs& p, int bid, int* ctr, int target) {
+    // tuning build, AZ_LEAF_MODE (a.mode): 1 = output_transform.2's weights only after the
+    // trunk, 2 = after output_transform.0, 3 = every weight stream only behind its producer
+    auto pre0 = [&] {
+      if (a.mode == 0) return true;
+      if (a.mode == 1 && second) return leaf_wait(leaf_rep(a.sync + kSyncTrunk), nt, a.err, &flag);
+      if (a.mode == 2 && second) return leaf_wait(leaf_rep(a.sync + kSyncG1), a.ng, a.err, &flag);
+      if (a.mode == 3) return leaf_wait(ctr, target, a.err, &flag);
+      return true;
+    };
+    auto pre = [&] {
+#ifdef AZ_TUNING
+      if (a.trace) {                     // the weights have landed (vmcnt is in order)
+        drain_stores();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        leaf_stamp(a, second ? LE_G2_WEIGHTS : LE_G1_WEIGHTS);
+      }
+#endif
+      const bool go = leaf_wait(ctr, target, a.err, &flag);
+      leaf_stamp(a, second ? LE_G2_GO : LE_G1_GO);
+      return go;
+    };
+    return gemv_full_block<MK, S, R, true, decltype(pre), true, decltype(pre0)>(p, bid, sm.As, pre,
+                                                                                 pre0);
+  };
+  if (!second) {
+    gemv(a.g1, g, leaf_rep(a.sync + kSyncTrunk), nt);
+    leaf_signal(a.sync + kSyncG1, true);
+    leaf_stamp(a, LE_G1_DONE);
+    return;
+  }
+  const int g2 = g - a.ng;
+  const bool ok = gemv(a.g2, g2, leaf_rep(a.sync + kSyncG1), a.ng);
+  leaf_stamp(a, LE_G2_DONE);
+  const int nch = (a.g2.N + HEADS_KC - 1) / HEADS_KC;
+  constexpr int PER = HEADS_KC / (4 * R);           // GEMV blocks per head chunk
+  const int c = g2 / PER;
+  if (!leaf_ticket(a.sync + kSyncTicket0 + c * kLeafLine, min(PER, a.ng - c * PER), &flag))
+    return;
+  const int wave = threadIdx.x >> 6;
+  if (ok) {
+    for (int r = wave; r < a.B; r += 4) {
+      const float* yr = a.g2.C + (size_t)r * a.g2.ldc;
+      heads_chunk_part<8, true>(yr, yr, a.g2.N, a.ht.wp, a.ht.A, a.ht.wv, c,
+                          a.ht.part + ((size_t)r * nch + c) * 9);
+    }
+  }
+  leaf_stamp(a, LE_CHUNK);
+  if (!leaf_ticket(a.sync + kSyncChunks, nch, &flag)) return;
+  if (ok) {
+    for (int r = 0; r < a.B; ++r)
+      heads_finalize_row<8, true>(a.ht.part + (size_t)r * nch * 9, nch, a.ht.A, a.ht.bp, a.ht.bv, r,
+                            a.ht.logp, a.ht.pi, a.ht.v, sm.hd.sm);
+  }
+  leaf_wait(a.sync + kSyncStd, a.B, a.err, &flag);   // the standard heads' waits are over too
+  for (int i = threadIdx.x; i < kSyncInts; i += 256) a.sync[i] = 0;
+  leaf_stamp(a, LE_FINAL);
+}
+
+#ifdef AZ_TUNING
+static unsigned long long* g_leaf_trace = nullptr;
+#endif
 
 // --------------------------------------------------------------------- K-sliced row panels
 // C = epi(A . W^T) for mid-size M (the B = 512 output_transform: 512 x 3136 x 3136).  A tile
@@ -2987,6 +3232,80 @@ int gemv1_with_side_heads(const az_gemm_desc* d, const SideHeads* h, hipStream_t
   const int rc = check_launch("gemv_side_heads");
   return rc == AZ_OK ? 1 : rc;
 }
+
+// The batch <= 2 leaf of az_c4_eval_fwd as ONE c4_leaf_kernel launch (see there).  Returns 1
+// when launched, 0 when it does not apply (shapes, no counters, or the grid would not be
+// resident at once on this device), or a negative AZ_E* code.
+int c4_leaf_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, float* v, float* gpi,
+                float* gv, hipStream_t s) {
+  const int F = 3136, nch = (F + HEADS_KC - 1) / HEADS_KC;
+  if (!(e->sync && e->err && B >= 1 && B <= 2 && v && gv && e->A >= 1 && e->A <= 8 &&
+        e->ot0_w && e->ot0_b && e->ot2_w && e->ot2_b && e->hidden && e->y && e->glogp && e->ws &&
+        e->ws_bytes >= (size_t)B * nch * 9 * 4 && aligned16(e->feat) && aligned16(e->hidden) &&
+        aligned16(e->y) && aligned16(e->ot0_w) && aligned16(e->ot2_w) &&
+        aligned16(e->fc_policy_w) && aligned16(e->fc_value_w)))
+    return 0;
+  static_assert(kSyncInts <= 4096, "az_c4_eval.sync holds 4096 ints");
+  const int mk = B;
+  const int ng = F / 8;
+  const int grid = 4 * B + B + 2 * ng;
+  static int cap[4] = {-1, -1, -1, -1};
+  if (cap[mk] < 0) {
+    int dev = 0, cus = 0, nb = 0;
+    const void* k = mk == 1 ? reinterpret_cast<const void*>(&c4_leaf_kernel<1>)
+                            : reinterpret_cast<const void*>(&c4_leaf_kernel<2>);
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess)
+      cap[mk] = 0;
+    else
+      cap[mk] = nb * cus;
+  }
+  if (grid > cap[mk]) return 0;
+  LeafArgs a = {};
+  a.boards = boards; a.B = B;
+  a.w1 = e->conv1_w; a.b1 = e->conv1_b; a.w2 = e->conv2_w; a.b2 = e->conv2_b;
+  a.feat = e->feat;
+  auto gemv_args = [&](const float* A, const float* W, const float* bias, int act, float* C) {
+    GemmArgs g = {};
+    g.M = B; g.N = F; g.K = F;
+    g.A = A; g.lda = F; g.K0 = F; g.B = W; g.ldb = F;
+    g.bias = bias; g.act = act; g.C = C; g.ldc = F;
+    g.splits = 1; g.kc = F;
+    return g;
+  };
+  a.g1 = gemv_args(e->feat, e->ot0_w, e->ot0_b, AZ_ACT_RELU, e->hidden);
+  a.g2 = gemv_args(e->hidden, e->ot2_w, e->ot2_b, AZ_ACT_NONE, e->y);
+  a.sh = {e->feat, F, F, B, e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,
+          e->logp, pi, v};
+  a.ht = {e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b, e->glogp, gpi, gv,
+          static_cast<float*>(e->ws)};
+  a.sync = e->sync; a.err = e->err; a.ng = ng;
+#ifdef AZ_TUNING
+  static const char* env_mode = tuning_env("AZ_LEAF_MODE");
+  a.mode = env_mode ? atoi(env_mode) : 0;
+  static const bool trace = tuning_env("AZ_LEAF_TRACE") != nullptr;
+  if (trace) {
+    if (!g_leaf_trace && hipMalloc(&g_leaf_trace, 2 * LE_N * 8) != hipSuccess) return 0;
+    unsigned long long init[2 * LE_N];
+    for (int i = 0; i < LE_N; ++i) { init[2 * i] = ~0ull; init[2 * i + 1] = 0; }
+    if (hipMemcpy(g_leaf_trace, init, sizeof(init), hipMemcpyHostToDevice) != hipSuccess) return 0;
+    a.trace = g_leaf_trace;
+  }
+#endif
+  if (mk == 1) hipLaunchKernelGGL(c4_leaf_kernel<1>, dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(c4_leaf_kernel<2>, dim3(grid), dim3(256), 0, s, a);
+  const int rc = check_launch("c4_leaf_kernel");
+  return rc == AZ_OK ? 1 : rc;
+}
+
+#ifdef AZ_TUNING
+// tools/leaf_probe.py: the last traced launch's [event][min, max] stamps (synchronous)
+extern "C" int az_tuning_leaf_trace(unsigned long long* out) {
+  if (!g_leaf_trace) return -1;
+  return hipMemcpy(out, g_leaf_trace, 2 * LE_N * 8, hipMemcpyDeviceToHost) == hipSuccess ? LE_N : -1;
+}
+#endif
 
 int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
   int splits = 1;

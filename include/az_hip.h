@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define AZ_ABI_VERSION 1
+#define AZ_ABI_VERSION 2
 
 #define AZ_OK 0
 #define AZ_EINVAL (-1)     /* bad shape / null pointer / misaligned buffer */
@@ -152,6 +152,12 @@ typedef struct az_c4_eval {
   float* feat; float* hidden; float* y;    /* device [max_B][3136] each (hidden/y: GNN only) */
   float* logp; float* glogp;               /* device [max_B][A] */
   void* ws; size_t ws_bytes;               /* >= az_transform_heads_ws_bytes(max_B, 3136, A) */
+  /* Optional (both NULL: four launches).  The batch <= 2 evaluation in ONE launch
+   * (c4_leaf_kernel, az_gemm.hip): sync = device int[4096], zeroed once by the caller and left
+   * zero by every launch; err = host-visible int (az_host_alloc) the launch sets to 1 if its
+   * in-kernel hand-over timed out -- the outputs are then invalid: zero sync and *err, and call
+   * again without them.  One evaluation at a time per sync buffer. */
+  int* sync; int* err;
 } az_c4_eval;
 /* v != NULL: standard heads into pi [B][A] (may be NULL) and v [B];  gv != NULL: the GNN tail
  * into gpi / gv.  boards, pi, v, gpi, gv may be az_host_alloc memory. */

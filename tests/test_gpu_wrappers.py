@@ -324,6 +324,34 @@ def test_batch1_direct_equals_graph(c4_wrapper, kind):
             np.testing.assert_allclose(a[k:k + 8], z["pi_gnn_b1"][i], atol=TOL)
 
 
+def test_one_launch_leaf_equals_four_launches(c4_wrapper):
+    """az_c4_eval_fwd with hand-over counters runs 1-2 rows as ONE c4_leaf_kernel launch (trunk,
+    both GEMVs, both heads; weights streamed in under the trunk): every output row equals the
+    four-launch path's bits, the counters are left zero, and a timed-out hand-over (simulated
+    by the flag) makes the evaluator drop the outputs, zero the counters and recompute on the
+    four-launch path."""
+    import torch
+    from azhip.wrappers import _Batch1Direct
+    z = golden("c4_gnn.npz")
+    fused, plain = _Batch1Direct(c4_wrapper, "both", cap=8), _Batch1Direct(c4_wrapper, "both", cap=8)
+    plain.desc.sync = plain.desc.err = None
+    plain.err_np = None
+    boards = z["boards"][:24].astype(np.int8)
+    for n in (1, 2, 2, 1, 3):
+        for i in range(0, 24 - n, 5):
+            a = fused.run_rows(boards[i:i + n])
+            c = plain.run_rows(boards[i:i + n])
+            for x, y in zip(a, c):
+                assert np.array_equal(x, y), (n, i)
+            np.testing.assert_allclose(a[2], z["pi_gnn_b1"][i:i + n], atol=TOL)
+            assert int(fused.sync.abs().sum()) == 0
+    fused.err_np[0] = 1                       # as if the last launch's waits had timed out
+    a, c = fused.run_rows(boards[:1]), plain.run_rows(boards[:1])
+    assert all(np.array_equal(x, y) for x, y in zip(a, c))
+    assert fused.leaf_timeouts == 1 and fused.desc.sync is None
+    torch.cuda.synchronize()
+
+
 def test_direct_batch_async_equals_predict_both(c4_wrapper):
     """The lock-step rounds' batched call (predict_both_async -> az_c4_eval_fwd, zero-copy ring
     of host buffers, scratch grown on demand) returns predict_both's bits, several batches in

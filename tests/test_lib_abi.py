@@ -40,7 +40,7 @@ def test_binding_matches_header(built):
     from azhip import _lib
     assert sorted(_lib.SIGNATURES) == declared()
     L = _lib.load()
-    assert L.az_abi_version() == 1
+    assert L.az_abi_version() == 2
     assert L.az_last_error() == b""
 
 
