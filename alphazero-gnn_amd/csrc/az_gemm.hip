@@ -1226,56 +1226,86 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
 }
 
 // Stream-K form of gemm_x3 for grids whose tile count does not fill the chip in whole rounds
-// (M ~ 600 .. 2,000 at N = 3,136: 100 .. 200 tiles of 256 x 128 on 256 CUs).  The I = tiles x KT
-// k-iterations (KT 32-k steps per tile, tiles in (mt fastest, nt) order) are cut into B equal
-// contiguous ranges, one per block: a block finishes the tail of one tile and starts the next.
-// A range that covers a whole tile writes C through the fused epilogue; a piece of a tile writes
-// its raw partial sums to slab[piece] (piece = its index among the tile's blocks), and
+// (M ~ 600 .. 2,000 at N = 3,136: 100 .. 200 tiles of 256 x 128 on 256 CUs).  The tiles' k-steps
+// (KT 32-k steps per tile, tiles in (mt fastest, nt) order) are cut into B contiguous ranges of
+// equal cost, one per block: a block finishes the tail of one tile and starts the next.  A step
+// costs 2 units, or SkPlan::wt for the last, partial row of m-tiles (1 = half: an experiment in
+// which the waves of a tail tile whose rows all lie past M skipped their MFMAs -- measured
+// slower, r03m: a tail step costs a full step at one MFMA wave per SIMD, and the blocks given
+// more tail steps became the critical path; wt = 2 in the product).  A range that
+// covers a whole tile writes C through the fused epilogue; a piece of a tile writes its raw
+// partial sums to slab[piece] (piece = the block's index among the tile's blocks), and
 // streamk_fixup4_kernel sums a split tile's pieces in piece order (deterministic) and runs the
-// epilogue.  Block b's range: [b I / B, (b + 1) I / B); the block holding iteration i is
-// ceil((i + 1) B / I) - 1.
-__device__ __forceinline__ int sk_block_of(long i, long I, int B) {
-  return (int)(((i + 1) * B + I - 1) / I - 1);
+// epilogue.
+struct SkPlan {
+  int mt_n, KT, wt;     // m-tiles, k-steps per tile, cost of a last-row step (1 or 2)
+  long C;               // total cost units
+  int B;                // blocks
+};
+
+// cost units before k-step k of tile t
+__host__ __device__ __forceinline__ long sk_unit(const SkPlan& q, long t, int k) {
+  const long full_rows_done = t / q.mt_n;            // the last-row tiles before t
+  const long before = (t - full_rows_done) * 2L * q.KT + full_rows_done * (long)q.wt * q.KT;
+  return before + (long)k * ((int)(t % q.mt_n) == q.mt_n - 1 ? q.wt : 2);
+}
+// the block that runs k-step k of tile t
+__host__ __device__ __forceinline__ int sk_block(const SkPlan& q, long t, int k) {
+  return (int)(sk_unit(q, t, k) * q.B / q.C);
+}
+// block b's first k-step (flattened t * KT + k): the first whose cost position u satisfies
+// u * B / C >= b, i.e. u >= ceil(b * C / B)
+__device__ __forceinline__ long sk_first(const SkPlan& q, int b) {
+  const long u = ((long)b * q.C + q.B - 1) / q.B;
+  const long G = (long)(q.mt_n - 1) * 2 * q.KT + (long)q.wt * q.KT;   // one n-tile column
+  const long g = u / G, r = u - g * G;
+  long mt, k;
+  if (r < (long)(q.mt_n - 1) * 2 * q.KT) {
+    mt = r / (2L * q.KT);
+    k = (r - mt * 2L * q.KT + 1) / 2;
+  } else {
+    mt = q.mt_n - 1;
+    k = (r - (long)(q.mt_n - 1) * 2 * q.KT + q.wt - 1) / q.wt;
+  }
+  return (g * q.mt_n + mt) * q.KT + k;       // k == KT rolls over to the next tile's step 0
 }
 
 template <int BM, int BN, int WGM, int WGN, bool MASK>
-__global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3_sk(GemmArgs p, int KT, long I) {
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3_sk(GemmArgs p, SkPlan q) {
   __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<BM, BN, WGM, WGN>()];
-  const int B = gridDim.x;
-  const int b = xcd_swizzle(blockIdx.x, B);
-  const int mt_n = (p.M + BM - 1) / BM;
-  long i0 = (long)b * I / B;
-  const long i1 = (long)(b + 1) * I / B;
+  const int b = xcd_swizzle(blockIdx.x, q.B);
+  const int KT = q.KT, mt_n = q.mt_n;
+  long i0 = sk_first(q, b);
+  const long i1 = b + 1 < q.B ? sk_first(q, b + 1) : (long)mt_n * ((p.N + BN - 1) / BN) * KT;
   while (i0 < i1) {
     const int t = (int)(i0 / KT);
     const int k0 = (int)(i0 - (long)t * KT);
     const int k1 = (int)min((long)KT, k0 + (i1 - i0));
-    GemmArgs q = p;
+    GemmArgs g = p;
     int sp = 0;
     if (k0 == 0 && k1 == KT) {
-      q.splits = 1;                       // the whole tile: fused epilogue into C
+      g.splits = 1;                       // the whole tile: fused epilogue into C
     } else {
-      q.splits = 2;                       // a piece: raw partials into slab[piece]
-      sp = b - sk_block_of((long)t * KT, I, B);
+      g.splits = 2;                       // a piece: raw partials into slab[piece]
+      sp = b - sk_block(q, t, 0);
     }
-    gemm_x3_body<BM, BN, WGM, WGN, MASK>(q, smem, t % mt_n, t / mt_n, sp, 32 * k0,
+    gemm_x3_body<BM, BN, WGM, WGN, MASK>(g, smem, t % mt_n, t / mt_n, sp, 32 * k0,
                                          min(p.K, 32 * k1));
     i0 += k1 - k0;
     if (i0 < i1) __syncthreads();         // the next segment's prologue reuses the LDS
   }
 }
 
-// Sums the pieces of every tile gemm_x3_sk split (slab[0 .. np), np = the tile's block count)
-// and runs the epilogue on them; whole tiles were written by their block.  float4 per lane.
-__global__ __launch_bounds__(256) void streamk_fixup4_kernel(GemmArgs p, int BM, int BN, int KT,
-                                                             long I, int B) {
+// Sums the pieces of every tile gemm_x3_sk / gemm_p3_sk split (slab[0 .. np), np = the tile's
+// block count) and runs the epilogue on them; whole tiles were written by their block.  float4
+// per lane.
+__global__ __launch_bounds__(256) void streamk_fixup4_kernel(GemmArgs p, int BM, int BN, SkPlan q) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   const int n4 = p.N >> 2;
   if (idx >= (long)p.M * n4) return;
   const int row = (int)(idx / n4), col = (int)(idx % n4) * 4;
-  const int mt_n = (p.M + BM - 1) / BM;
-  const long t = (long)(col / BN) * mt_n + row / BM;
-  const int bf = sk_block_of(t * KT, I, B), bl = sk_block_of(t * KT + KT - 1, I, B);
+  const long t = (long)(col / BN) * q.mt_n + row / BM;
+  const int bf = sk_block(q, t, 0), bl = sk_block(q, t, q.KT - 1);
   if (bf == bl) return;
   const size_t plane = (size_t)p.M * p.N, off = (size_t)row * p.N + col;
   f32x4 v = *reinterpret_cast<const f32x4*>(p.slab + off);
@@ -1285,6 +1315,28 @@ __global__ __launch_bounds__(256) void streamk_fixup4_kernel(GemmArgs p, int BM,
     for (int c = 0; c < 4; ++c) v[c] += u[c];
   }
   epilogue_store4(p, row, col, v);
+}
+
+// The stream-K plan for a BM x BN tile grid on B blocks (host); weighted: the last row of
+// m-tiles costs half when at most 128 of its rows are real (see gemm_x3_sk; not used).
+static SkPlan sk_plan(int M, int N, int K, int BM, int BN, int B, bool weighted) {
+  SkPlan q;
+  q.mt_n = (M + BM - 1) / BM;
+  q.KT = (K + 31) / 32;
+  const int rows_last = M - (q.mt_n - 1) * BM;
+  q.wt = weighted && rows_last < BM && rows_last <= BM / 2 ? 1 : 2;
+  const long nt_n = (N + BN - 1) / BN;
+  q.C = nt_n * ((long)(q.mt_n - 1) * 2 * q.KT + (long)q.wt * q.KT);
+  q.B = B;
+  return q;
+}
+// the most pieces any tile of plan q is cut into (slabs needed)
+static int sk_max_pieces(const SkPlan& q, int N, int BN) {
+  const long tiles = (long)q.mt_n * ((N + BN - 1) / BN);
+  int mx = 1;
+  for (long t = 0; t < tiles; ++t)
+    mx = std::max(mx, sk_block(q, t, q.KT - 1) - sk_block(q, t, 0) + 1);
+  return mx;
 }
 
 // gemm_x3 on operands that are ALREADY split ("p3"): A as three bf16 planes [3][M][K] (p.apl,
@@ -1426,13 +1478,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3(GemmArgs p) {
 
 // gemm_p3 in stream-K form (see gemm_x3_sk), pieces summed by streamk_fixup4_kernel
 template <int BM, int BN, int WGM, int WGN>
-__global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3_sk(GemmArgs p, int KT, long I) {
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3_sk(GemmArgs p, SkPlan sq) {
   __shared__ __attribute__((aligned(1024))) char smem[p3_smem_bytes<BM, BN, WGM, WGN>()];
-  const int B = gridDim.x;
-  const int b = xcd_swizzle(blockIdx.x, B);
-  const int mt_n = (p.M + BM - 1) / BM;
-  long i0 = (long)b * I / B;
-  const long i1 = (long)(b + 1) * I / B;
+  const int b = xcd_swizzle(blockIdx.x, sq.B);
+  const int mt_n = sq.mt_n, KT = sq.KT;
+  long i0 = sk_first(sq, b);
+  const long i1 = b + 1 < sq.B ? sk_first(sq, b + 1) : (long)mt_n * ((p.N + BN - 1) / BN) * KT;
   while (i0 < i1) {
     const int t = (int)(i0 / KT);
     const int k0 = (int)(i0 - (long)t * KT);
@@ -1443,7 +1494,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3_sk(GemmArgs p, int KT,
       q.splits = 1;
     } else {
       q.splits = 2;
-      sp = b - sk_block_of((long)t * KT, I, B);
+      sp = b - sk_block(sq, t, 0);
     }
     gemm_p3_body<BM, BN, WGM, WGN>(q, smem, t % mt_n, t / mt_n, sp, 32 * k0, min(p.K, 32 * k1));
     i0 += k1 - k0;
@@ -2927,16 +2978,17 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
     const long I = tiles * (long)KT;
     const int B = (int)std::min<long>(cus, I);
     const long per = I / B;
-    const long smax = per > 0 ? (KT + per - 1) / per + 1 : 0;
-    if ((double)blocks / (double)(rounds * cus) < 0.9 && per >= 8 &&
-        (size_t)smax * a.M * a.N * 4 <= ws_bytes) {
-      if (whole) hipLaunchKernelGGL((gemm_x3_sk<256, 128, 4, 2, false>), dim3(B), dim3(512), 0, s, a, KT, I);
-      else hipLaunchKernelGGL((gemm_x3_sk<256, 128, 4, 2, true>), dim3(B), dim3(512), 0, s, a, KT, I);
-      const long n4 = (long)a.M * (a.N / 4);
-      hipLaunchKernelGGL(streamk_fixup4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                         a, 256, 128, KT, I, B);
-      a.splits = 1;
-      return true;
+    if ((double)blocks / (double)(rounds * cus) < 0.9 && per >= 8) {
+      const SkPlan q = sk_plan(a.M, a.N, a.K, 256, 128, B, false);
+      if ((size_t)sk_max_pieces(q, a.N, 128) * a.M * a.N * 4 <= ws_bytes) {
+        if (whole) hipLaunchKernelGGL((gemm_x3_sk<256, 128, 4, 2, false>), dim3(B), dim3(512), 0, s, a, q);
+        else hipLaunchKernelGGL((gemm_x3_sk<256, 128, 4, 2, true>), dim3(B), dim3(512), 0, s, a, q);
+        const long n4 = (long)a.M * (a.N / 4);
+        hipLaunchKernelGGL(streamk_fixup4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0,
+                           s, a, 256, 128, q);
+        a.splits = 1;
+        return true;
+      }
     }
   }
 #ifdef AZ_TUNING
@@ -2990,14 +3042,13 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
     const int KT = a.K / 32;
     const long I = tiles * (long)KT;
     const int B = (int)std::min<long>(256, I);
-    const long per = I / B;
-    // slabs: a tile is cut into at most ceil(KT / per) + 1 pieces, each one M x N slab
-    const long smax = per > 0 ? (KT + per - 1) / per + 1 : 0;
-    if (sk && a.slab && a.vec_epi && per >= 1 && (size_t)smax * a.M * a.N * 4 <= ws_bytes) {
-      hipLaunchKernelGGL((gemm_p3_sk<256, 128, 4, 2>), dim3(B), dim3(512), 0, s, a, KT, I);
+    const SkPlan q = sk_plan(a.M, a.N, a.K, 256, 128, B, false);
+    if (sk && a.slab && a.vec_epi && I / B >= 1 &&
+        (size_t)sk_max_pieces(q, a.N, 128) * a.M * a.N * 4 <= ws_bytes) {
+      hipLaunchKernelGGL((gemm_p3_sk<256, 128, 4, 2>), dim3(B), dim3(512), 0, s, a, q);
       const long n4 = (long)a.M * (a.N / 4);
       hipLaunchKernelGGL(streamk_fixup4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                         a, 256, 128, KT, I, B);
+                         a, 256, 128, q);
       a.splits = 1;
       return true;
     }

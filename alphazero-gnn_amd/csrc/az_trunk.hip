@@ -663,7 +663,9 @@ extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w
              "az_c4_trunk_fwd: null pointer");
   hipStream_t s = as_stream(stream);
   static const char* env = tuning_env("AZ_TRUNK_NB");   // tuning experiments only
-  int nbk = B >= 4096 ? 8 : (B >= 2048 ? 4 : (B >= 256 ? 2 : (B <= 8 ? 0 : 1)));
+  // boards per block by batch (tools/heads_sweep.py, r03m): 8 from B = 1,536 (the self-play
+  // rounds: 47.7 vs 58.2 us at B = 1,576 for 2), 4 from 768 (27.2 vs 31.2 us at 1,024)
+  int nbk = B >= 1536 ? 8 : (B >= 768 ? 4 : (B >= 256 ? 2 : (B <= 8 ? 0 : 1)));
   if (env) nbk = atoi(env);
   switch (nbk) {
     case 8:
@@ -735,12 +737,25 @@ static void launch_heads(const float* hp, int ldhp, const float* hv, int ldhv, i
                        wp, A, wv, bp, bv, logp, pi, v);
     return;
   }
-  if (AMAX == 8 && nchunks <= 16 && !two_pass && B <= 2048) {
-    // one launch, 2 rows per block, one wave per chunk (splitk_heads_rowsw_kernel's body).
-    // Large B stays two-pass: its blocks reuse each weight slice for 16 rows, where rowsw
-    // re-reads all 113 KB of head weights every 2 rows (B = 65,536: 735 us vs ~0.3 ms)
-    hipLaunchKernelGGL((heads_rowsw_kernel<8, 2>), dim3((B + 1) / 2), dim3(64 * nchunks), 0, s,
-                       hp, ldhp, hv, ldhv, B, K, wp, A, wv, bp, bv, logp, pi, v);
+  static const char* env_r = tuning_env("AZ_HEADS_R");   // tuning sweeps (tools/heads_sweep.py)
+  // R rows per block, one wave per chunk holding that chunk's head weights for all R rows: a
+  // block re-reads the 113 KB of head weights, so R grows with B while the grid still covers
+  // the CUs (2 at B = 512: 256 blocks; 4 from the self-play rounds' B ~ 1,600: ~400)
+  int R = B > 768 ? 4 : 2;      // r03m: B = 1,576 21.4 vs 24.2 us, B = 4,096 41.6 vs 47.8
+  if (env_r) R = atoi(env_r);
+  if (AMAX == 8 && nchunks <= 16 && !two_pass && B <= 8192 && (R == 2 || R == 4 || R == 8)) {
+    // one launch (splitk_heads_rowsw_kernel's body); above B = 8192 the two-pass form's
+    // 16-row weight reuse wins (B = 65,536: rowsw at R = 2 took 735 us vs ~0.3 ms)
+    const dim3 blk(64 * nchunks);
+    if (R == 2)
+      hipLaunchKernelGGL((heads_rowsw_kernel<8, 2>), dim3((B + 1) / 2), blk, 0, s, hp, ldhp, hv,
+                         ldhv, B, K, wp, A, wv, bp, bv, logp, pi, v);
+    else if (R == 4)
+      hipLaunchKernelGGL((heads_rowsw_kernel<8, 4>), dim3((B + 3) / 4), blk, 0, s, hp, ldhp, hv,
+                         ldhv, B, K, wp, A, wv, bp, bv, logp, pi, v);
+    else
+      hipLaunchKernelGGL((heads_rowsw_kernel<8, 8>), dim3((B + 7) / 8), blk, 0, s, hp, ldhp, hv,
+                         ldhv, B, K, wp, A, wv, bp, bv, logp, pi, v);
     return;
   }
   dim3 g(nchunks, (B + HEADS_ROWS - 1) / HEADS_ROWS);

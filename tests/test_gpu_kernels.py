@@ -103,7 +103,7 @@ def _x3_check(ops, x, w, b, rows=None, report=None):
     return rep
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 3136, 3136), (800, 3136, 3136), (1576, 3136, 3136),
+@pytest.mark.parametrize("M,N,K", [(512, 3136, 3136), (800, 3136, 3136), (1576, 3136, 3136), (700, 3136, 3136),
                                    (64, 3136, 3136), (37, 1001, 1028), (4096, 1024, 2048)])
 def test_x3_gemm_has_fp32_accuracy(ops, M, N, K):
     """The K-major GEMMs with M > 64, K >= 1024, N >= 256 (output_transform; the self-play
