@@ -7,6 +7,7 @@
 namespace az {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 // conv2's weights in LDS: row co at stride W2S_STRIDE floats.  Stride = 2 (mod 32) makes the
 // conv2 fragment reads (lane: co = 16 consecutive rows, ci = 2 values 9 floats apart per 32-lane
@@ -108,13 +109,34 @@ __device__ __forceinline__ void c4_trunk_split_block(
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(j < 4 ? x[j] : y[j - 4], breg[tap * 8 + j], acc,
                                                  0, 0, 0);
   }
+  if constexpr (SC1) {
+    // the block's 16 channels x 49 positions are ONE contiguous, 16-B aligned run of 784 floats
+    // (feat[b][16q * 49 ..]): staged in LDS (conv1's tile is no longer read) and written through
+    // as 196 16-B stores instead of 784 dword ones (each an own fabric write when write-through)
+    __syncthreads();                                 // every wave is done reading c1
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int p = mt * 16 + h * 4 + r;
-    if (p < P) {
-      const float v = acc[r] + bias;
-      if constexpr (SC1) st_sc1(feat + (size_t)b * 3136 + co * P + p, v > 0.f ? v : 0.f);
-      else feat[(size_t)b * 3136 + co * P + p] = v > 0.f ? v : 0.f;
+    for (int r = 0; r < 4; ++r) {
+      const int p = mt * 16 + h * 4 + r;
+      if (p < P) {
+        const float v = acc[r] + bias;
+        c1[c16 * P + p] = v > 0.f ? v : 0.f;
+      }
+    }
+    __syncthreads();
+    if (tid < 16 * P / 4) {
+      float* dst = feat + (size_t)b * 3136 + (size_t)q * 16 * P;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 16 * P * 4, 0x00020000);
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(c1 + tid * 4);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, tid * 16, 0, 16);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p = mt * 16 + h * 4 + r;
+      if (p < P) {
+        const float v = acc[r] + bias;
+        feat[(size_t)b * 3136 + co * P + p] = v > 0.f ? v : 0.f;
+      }
     }
   }
 }
