@@ -51,8 +51,8 @@ def parse():
     ap.add_argument("--no-b1", action="store_true", help="skip the as-called batch-1 leg")
     ap.add_argument("--large-batch", type=int, default=65536,
                     help="extra leg at this batch (SURVEY §8d config 2); 0 = skip")
-    ap.add_argument("--sp-games", type=int, default=4096,
-                    help="self-play leg: games per GPU, all played in lock step (4096: 'tools/sp_sweep.py' r02s, 779 vs 702 games/s for 2048 with the x3 GEMMs)")
+    ap.add_argument("--sp-games", type=int, default=8192,
+                    help="self-play leg: games per GPU, all played in lock step (8192: 'tools/sp_sweep.py' r03o, 870 vs 762 games/s for 4096 and 848 for 12288 on one box; r02s: 4096 779 vs 2048 702)")
     ap.add_argument("--sp-sims", type=int, default=100, help="numMCTSSims (SURVEY §8d config 3)")
     ap.add_argument("--sp-threads", type=int, default=0,
                     help="host threads for the engine (0: this rank's share of the visible "
@@ -414,10 +414,11 @@ def x3_roofline(kernel, flop, seconds, traffic=None, traffic_run=None):
             "speedup_vs_fp32_mfma_peak": round(fp32_eq / FP32_MFMA_PEAK_TFLOPS, 4)}
 
 
-def gemm_shapes_leg(torch, ops, ev, device, Ms=(800, 1576), reps=20):
+def gemm_shapes_leg(torch, ops, ev, device, Ms=(800, 1576, 3150), reps=20):
     """output_transform.0 (one az_gemm_f32 call, Linear 3136x3136 + ReLU) at the self-play
-    leg's batch sizes: 4096 lock-step games on 2 lanes put ~1,576 rows into each predict_both,
-    the tail of a run ~800 (HIP events around each call, on the launch stream)."""
+    leg's batch sizes: 8192 lock-step games on 2 lanes put ~3,150 rows into each predict_both
+    (4096 games ~1,576), the tail of a run ~800 (HIP events around each call, on the launch
+    stream)."""
     Gn = ev.gnn.params
     out = []
     for M in Ms:
