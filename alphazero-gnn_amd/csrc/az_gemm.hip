@@ -2049,15 +2049,13 @@ struct NoPre {
 
 // SC1 (with WF): A is read with sc1 loads and C written through with sc1 stores (bias and
 // activation only: epilogue_store's arithmetic for an epilogue without C2 / R / G / beta).
-template <int MR, int S, int R, bool WF = false, class Pre = NoPre, bool SC1 = false,
-          class Pre0 = NoPre>
+template <int MR, int S, int R, bool WF = false, class Pre = NoPre, bool SC1 = false>
 __device__ __forceinline__ bool gemv_full_block(const GemmArgs& p, int bid, float* As,
-                                                Pre pre = Pre{}, Pre0 pre0 = Pre0{}) {
+                                                Pre pre = Pre{}) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n_base = (bid * 4 + wave) * R;
   RowStage<MR, S, SC1> st;
   if constexpr (!WF) st.load(p, 0);
-  if (!pre0()) return false;                // (tuning experiments: delay the weight stream)
   f32x4 w[R][S];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -2126,12 +2124,12 @@ __global__ __launch_bounds__(256) void gemv_full(GemmArgs p) {
 // budget: the wave's R weight rows are loaded ONCE into registers, then the rows of A go through
 // LDS MG at a time.  Every output is the same lane-strided fmaf chain + wave_sum as gemv_full,
 // so a row's result does not depend on M (bit-identical to the batch-1 launch).
-template <int S, int R, int MG, bool WF = false, class Pre = NoPre>
+template <int S, int R, int MG, bool WF = false, class Pre = NoPre, bool SC1 = false>
 __device__ __forceinline__ bool gemv_rows_block(const GemmArgs& p, int bid, float* As,
                                                 Pre pre = Pre{}) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n_base = (bid * 4 + wave) * R;
-  RowStage<MG, S> st;
+  RowStage<MG, S, SC1> st;
   if constexpr (!WF) st.load(p, 0);
   f32x4 w[R][S];
 #pragma unroll
@@ -2184,7 +2182,15 @@ __device__ __forceinline__ bool gemv_rows_block(const GemmArgs& p, int bid, floa
     }
     if (lane < MG * R) {
       const int m = m0 + lane / R, r = lane % R;
-      if (m < p.M && n_base + r < p.N) epilogue_store(p, m, n_base + r, mine);
+      if (m < p.M && n_base + r < p.N) {
+        if constexpr (SC1) {
+          const int col = n_base + r;
+          st_sc1(p.C + (size_t)m * p.ldc + col,
+                 apply_act(mine + (p.bias ? p.bias[col] : 0.f), p.act));
+        } else {
+          epilogue_store(p, m, n_base + r, mine);
+        }
+      }
     }
   }
   return true;
@@ -2222,24 +2228,27 @@ __global__ __launch_bounds__(256) void gemv_side_heads(GemmArgs p, SideHeads h, 
 
 // --------------------------------------------------------------------- the batch-1 leaf kernel
 // az_c4_eval_fwd for B <= 2 boards (the MCTS leaf, MCTS.py:169-173, and the arena's two-row
-// speculative batches) in
-// ONE launch instead of four (trunk, output_transform.0 + standard heads, output_transform.2,
-// GNN heads): every stage is the same device code as in the separate launches -- so every
-// output is bit-identical to them -- and the stages hand over through device-scope counters:
-//   blocks [0, 4B)            the trunk (c4_trunk_split_block), then signal sync[0];
-//   blocks [4B, 5B)           the standard heads of one board, after sync[0] = 4B; signal sync[1];
-//   next ng blocks            output_transform.0: their weight rows are loaded into registers
-//                             FIRST, while the trunk runs, then they wait for sync[0] = 4B,
-//                             stage the features and finish; signal sync[2];
-//   last ng blocks            output_transform.2 the same way behind sync[2] = ng; the last block
-//                             of each 256-column head chunk (ticket sync[4 + c]) forms that
-//                             chunk's head partials, the last chunk (ticket sync[3]) finalizes
-//                             the GNN heads and resets every counter for the next launch.
-// The 78.6 MB of output_transform weights stream in under the trunk instead of after it.  All
-// blocks must be resident at once (a waiting block holds its CU): the launcher checks the
-// occupancy first, workgroups are dispatched in index order (producers before consumers), and
-// every wait gives up after 20 ms, setting *err (host-visible) -- the caller then discards the
-// outputs, zeroes the counters and uses the four-launch path.
+// speculative batches; 3-8 rows are faster as four launches) in ONE launch instead of four (trunk, output_transform.0 + standard heads,
+// output_transform.2, GNN heads): every stage is the same device code as in the separate
+// launches -- so every output is bit-identical to them -- and the stages hand over through
+// device-scope counters:
+//   blocks [0, 4B)            the trunk (c4_trunk_split_block), then signal "trunk";
+//   blocks [4B, 5B)           the standard heads of one board behind "trunk"; signal "std";
+//   the next ng = 392 blocks  8 columns of output_transform.0 -- their weight rows loaded into
+//                             registers FIRST, under the trunk, then the features staged behind
+//                             "trunk" -- signal "g1"; then the same 8 columns of
+//                             output_transform.2 (weights loaded right away, hidden behind
+//                             "g1"); the last block of each 256-column head chunk (ticket)
+//                             forms the chunk's head partials, the last chunk (ticket)
+//                             finalizes the GNN heads and zeroes every counter for the next
+//                             launch.
+// All blocks must be resident at once (a waiting block holds its CU): launch bounds of 2 blocks
+// per CU (no spills), the launcher checks the occupancy first, workgroups are
+// dispatched in index order (producers first), and every wait gives up after 20 ms, setting *err
+// (host-visible) -- the caller then discards the outputs, zeroes the counters and uses the
+// four-launch path.  (A first form with separate blocks for the second GEMV, both weight streams
+// under the trunk, 4 blocks per CU and 1-2 rows only, measured the same 29 us at one row:
+// r03n_leaf_ab, the stage chain is the bound, not the weight stream.)
 struct HeadsTail {
   const float* wp; const float* bp; int A; const float* wv; const float* bv;
   float* logp; float* pi; float* v;
@@ -2257,7 +2266,6 @@ struct LeafArgs {
   int* err;                           // host-visible: 1 = a wait timed out, outputs invalid
   int ng;                             // GEMV blocks per GEMV (8 output columns each)
   unsigned long long* trace;          // tuning build (AZ_LEAF_TRACE): [event][min, max] stamps
-  int mode;                           // tuning build (AZ_LEAF_MODE): weight-stream experiments
 };
 
 // Timing probe of the tuning build: the earliest and latest 100 MHz wall-clock stamp of each
@@ -2337,9 +2345,9 @@ __device__ __forceinline__ bool leaf_ticket(int* ctr, int total, int* flag) {
 }
 
 template <int MK>
-__global__ __launch_bounds__(256, 4) void c4_leaf_kernel(LeafArgs a) {   // <= 128 VGPRs
+__global__ __launch_bounds__(256, 2) void c4_leaf_kernel(LeafArgs a) {   // <= 256 VGPRs
   constexpr int S = 13, R = 2;
-  static_assert(MK == 1 || MK == 2, "one or two rows (the 3..8-row GEMV spills at 128 VGPRs)");
+  static_assert(MK == 1 || MK == 2, "one or two rows");
   __shared__ union {
     TrunkSplitSmem trunk;
     float As[MK * S * 256];
@@ -2365,22 +2373,12 @@ __global__ __launch_bounds__(256, 4) void c4_leaf_kernel(LeafArgs a) {   // <= 1
     leaf_stamp(a, LE_STD);
     return;
   }
+  // the GEMV blocks: 8 columns of output_transform.0, then the same 8 of output_transform.2
   const int g = id - nt - a.B;
-  const bool second = g >= a.ng;
-  auto gemv = [&](const GemmArgs& p, int bid, int* ctr, int target) {
-    // tuning build, AZ_LEAF_MODE (a.mode): 1 = output_transform.2's weights only after the
-    // trunk, 2 = after output_transform.0, 3 = every weight stream only behind its producer
-    auto pre0 = [&] {
-      if (a.mode == 0) return true;
-      if (a.mode == 1 && second) return leaf_wait(leaf_rep(a.sync + kSyncTrunk), nt, a.err, &flag);
-      if (a.mode == 2 && second) return leaf_wait(leaf_rep(a.sync + kSyncG1), a.ng, a.err, &flag);
-      if (a.mode == 3) return leaf_wait(ctr, target, a.err, &flag);
-      return true;
-    };
+  auto gemv = [&](const GemmArgs& p, int* ctr, int target, bool second) {
     auto pre = [&] {
 #ifdef AZ_TUNING
       if (a.trace) {                     // the weights have landed (vmcnt is in order)
-        drain_stores();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         leaf_stamp(a, second ? LE_G2_WEIGHTS : LE_G1_WEIGHTS);
       }
@@ -2389,21 +2387,17 @@ __global__ __launch_bounds__(256, 4) void c4_leaf_kernel(LeafArgs a) {   // <= 1
       leaf_stamp(a, second ? LE_G2_GO : LE_G1_GO);
       return go;
     };
-    return gemv_full_block<MK, S, R, true, decltype(pre), true, decltype(pre0)>(p, bid, sm.As, pre,
-                                                                                 pre0);
+    return gemv_full_block<MK, S, R, true, decltype(pre), true>(p, g, sm.As, pre);
   };
-  if (!second) {
-    gemv(a.g1, g, leaf_rep(a.sync + kSyncTrunk), nt);
-    leaf_signal(a.sync + kSyncG1, true);
-    leaf_stamp(a, LE_G1_DONE);
-    return;
-  }
-  const int g2 = g - a.ng;
-  const bool ok = gemv(a.g2, g2, leaf_rep(a.sync + kSyncG1), a.ng);
+  const bool ok1 = gemv(a.g1, leaf_rep(a.sync + kSyncTrunk), nt, false);
+  leaf_signal(a.sync + kSyncG1, true);
+  leaf_stamp(a, LE_G1_DONE);
+  __syncthreads();                       // the staging LDS is reused by the second GEMV
+  const bool ok = gemv(a.g2, leaf_rep(a.sync + kSyncG1), a.ng, true) && ok1;
   leaf_stamp(a, LE_G2_DONE);
   const int nch = (a.g2.N + HEADS_KC - 1) / HEADS_KC;
   constexpr int PER = HEADS_KC / (4 * R);           // GEMV blocks per head chunk
-  const int c = g2 / PER;
+  const int c = g / PER;
   if (!leaf_ticket(a.sync + kSyncTicket0 + c * kLeafLine, min(PER, a.ng - c * PER), &flag))
     return;
   const int wave = threadIdx.x >> 6;
@@ -2411,7 +2405,7 @@ __global__ __launch_bounds__(256, 4) void c4_leaf_kernel(LeafArgs a) {   // <= 1
     for (int r = wave; r < a.B; r += 4) {
       const float* yr = a.g2.C + (size_t)r * a.g2.ldc;
       heads_chunk_part<8, true>(yr, yr, a.g2.N, a.ht.wp, a.ht.A, a.ht.wv, c,
-                          a.ht.part + ((size_t)r * nch + c) * 9);
+                                a.ht.part + ((size_t)r * nch + c) * 9);
     }
   }
   leaf_stamp(a, LE_CHUNK);
@@ -3290,6 +3284,8 @@ int gemv1_with_side_heads(const az_gemm_desc* d, const SideHeads* h, hipStream_t
 int c4_leaf_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, float* v, float* gpi,
                 float* gv, hipStream_t s) {
   const int F = 3136, nch = (F + HEADS_KC - 1) / HEADS_KC;
+  // 1-2 rows: 3 or more take the four launches, faster there (tools/leaf_rows_probe.py, r03p:
+  // 1 row 39.8 vs 45.6 us, 2 rows 44.8 vs 47.9, 3 rows 53.8 vs 50.6, 8 rows 75.0 vs 58.4)
   if (!(e->sync && e->err && B >= 1 && B <= 2 && v && gv && e->A >= 1 && e->A <= 8 &&
         e->ot0_w && e->ot0_b && e->ot2_w && e->ot2_b && e->hidden && e->y && e->glogp && e->ws &&
         e->ws_bytes >= (size_t)B * nch * 9 * 4 && aligned16(e->feat) && aligned16(e->hidden) &&
@@ -3299,7 +3295,7 @@ int c4_leaf_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, flo
   static_assert(kSyncInts <= 4096, "az_c4_eval.sync holds 4096 ints");
   const int mk = B;
   const int ng = F / 8;
-  const int grid = 4 * B + B + 2 * ng;
+  const int grid = 4 * B + B + ng;
   static int cap[4] = {-1, -1, -1, -1};
   if (cap[mk] < 0) {
     int dev = 0, cus = 0, nb = 0;
@@ -3333,8 +3329,6 @@ int c4_leaf_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, flo
           static_cast<float*>(e->ws)};
   a.sync = e->sync; a.err = e->err; a.ng = ng;
 #ifdef AZ_TUNING
-  static const char* env_mode = tuning_env("AZ_LEAF_MODE");
-  a.mode = env_mode ? atoi(env_mode) : 0;
   static const bool trace = tuning_env("AZ_LEAF_TRACE") != nullptr;
   if (trace) {
     if (!g_leaf_trace && hipMalloc(&g_leaf_trace, 2 * LE_N * 8) != hipSuccess) return 0;

@@ -337,7 +337,7 @@ def test_one_launch_leaf_equals_four_launches(c4_wrapper):
     plain.desc.sync = plain.desc.err = None
     plain.err_np = None
     boards = z["boards"][:24].astype(np.int8)
-    for n in (1, 2, 2, 1, 3):
+    for n in (1, 2, 2, 1, 3, 5, 8):
         for i in range(0, 24 - n, 5):
             a = fused.run_rows(boards[i:i + n])
             c = plain.run_rows(boards[i:i + n])
