@@ -13,6 +13,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # and the kernel-variant test only)
 LIB_PATH = os.path.join(HERE, "libaz_hip_tuning.so" if os.environ.get("AZ_TUNING_LIB") == "1"
                         else "libaz_hip.so")
+# AZ_AB_LIB=<file in azhip/>: an A/B build of the same sources at another revision (tools/
+# ab_lib.sh writes libaz_hip_base.so), timed beside the current one in the same GPU session
+if os.environ.get("AZ_AB_LIB"):
+    LIB_PATH = os.path.join(HERE, os.path.basename(os.environ["AZ_AB_LIB"]))
 
 c_int, c_float, c_double, c_void_p, c_int64, c_size_t = (
     ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_void_p, ctypes.c_int64, ctypes.c_size_t)

@@ -45,9 +45,8 @@ def _compile(src, force=False, tuning=False):
     odir = os.path.join(OBJ, "tuning") if tuning else OBJ
     obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
     s = os.path.join(CSRC, src)
-    deps = [s, os.path.join(CSRC, "az_common.h"), os.path.join(CSRC, "az_heads.h"),
-            os.path.join(CSRC, "az_x3.h"),
-            os.path.join(os.path.dirname(PKG), "include", "az_hip.h")]
+    deps = [s, os.path.join(os.path.dirname(PKG), "include", "az_hip.h")] + \
+        [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     if not force and os.path.exists(obj) and \
             all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj

@@ -81,6 +81,23 @@ __device__ __forceinline__ float sigmoid_fast(float v) {
   return __builtin_amdgcn_rcpf(1.f + __expf(-v));
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xF, 0xF, false));
+}
+
+// sum over each aligned group of 8 lanes, the same bits in every lane of the group: quad_perm
+// [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror -- three DPP adds (no LDS round trip, where
+// __shfl_xor with width 8 is a ds_bpermute and a wait per step)
+__device__ __forceinline__ float sum8(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  return v + dpp<0x141>(v);
+}
+
 // 8 consecutive weights -> their three bf16 planes
 __global__ __launch_bounds__(256) void band_split_weights(const float* __restrict__ w1,
                                                           const float* __restrict__ gw,
@@ -230,10 +247,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       *reinterpret_cast<u32x4*>(XR + xr_off(slot, pl, tid & 7)) = o[pl];
   };
   // x of ring row `slot`, features 8c .. 8c + 7, rebuilt exactly from its planes
-  auto x_ring = [&](int slot, int c, f32x4 (&v)[2]) {
-    const u32x4 h = *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 0, c));
-    const u32x4 m = *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 1, c));
-    const u32x4 l = *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 2, c));
+  auto x_planes = [](const u32x4& h, const u32x4& m, const u32x4& l, f32x4 (&v)[2]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float lo = (__uint_as_float(h[q] << 16) + __uint_as_float(m[q] << 16)) +
@@ -243,6 +257,11 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       v[q >> 1][2 * (q & 1)] = lo;
       v[q >> 1][2 * (q & 1) + 1] = hi;
     }
+  };
+  auto x_ring = [&](int slot, int c, f32x4 (&v)[2]) {
+    x_planes(*reinterpret_cast<const u32x4*>(XR + xr_off(slot, 0, c)),
+             *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 1, c)),
+             *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 2, c)), v);
   };
   // A fragments straight from the ring planes: rows r0 + 32 mb + (lane & 31)
   auto ring_frag = [&](int r0) {
@@ -373,13 +392,21 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         auto alpha_of = [&](int s) {
           float acc = 0.f;
           if (FAST || (unsigned)(s - lo) < (unsigned)RING) {
+            // two interleaved partial sums (even / odd hidden unit): the adds and FMAs go out
+            // as packed v_pk_add_f32 / v_pk_fma_f32, half the instructions of the scalar chain
             const float* ps = PSR + (s & (RING - 1)) * PSRS + 4 * ej;
+            f32x2 acc2 = {0.f, 0.f};
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               const f32x4 p = *reinterpret_cast<const f32x4*>(ps + 32 * (c ^ par));
 #pragma unroll
-              for (int u = 0; u < 4; ++u) acc = fmaf(relu(pt[c][u] + p[u]), ww[c][u], acc);
+              for (int u = 0; u < 4; u += 2) {
+                f32x2 t = f32x2{pt[c][u], pt[c][u + 1]} + f32x2{p[u], p[u + 1]};
+                t = f32x2{relu(t.x), relu(t.y)};
+                acc2 = __builtin_elementwise_fma(t, f32x2{ww[c][u], ww[c][u + 1]}, acc2);
+              }
             }
+            acc = acc2.x + acc2.y;
           } else {    // source outside the window: its Ps from global memory, on the VALU
             const float* xs = x + (size_t)s * BF;
 #pragma unroll 1
@@ -392,9 +419,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
               acc = fmaf(relu(PT[ei * PSS + h] + p), B1W2[BH + h], acc);
             }
           }
-#pragma unroll
-          for (int o = 4; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 8);
-          return sigmoid_fast(acc + b2);
+          return sigmoid_fast(sum8(acc) + b2);
         };
         auto x_of = [&](int s, f32x4 (&v)[2]) {
           if (FAST || (unsigned)(s - lo) < (unsigned)RING) {
@@ -408,38 +433,96 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         float a[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) src[q] = q < deg ? col_of(q) : d;
+        // FAST: the four edges straight-line, a missing edge (q >= deg) scored on the
+        // destination's own row and given weight 0 (S + 0 and g + 0 * x are exact for finite x):
+        // all 16 Ps reads go out before the first use, and the four score reductions and
+        // sigmoids interleave instead of each edge waiting behind its own branch and LDS reads
         float S = 0.f;
+        if constexpr (FAST) {
+          f32x4 p[4][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          a[q] = 0.f;
-          if (q < deg) {
-            a[q] = alpha_of(src[q]);
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              p[q][c] = *reinterpret_cast<const f32x4*>(PSR + (src[q] & (RING - 1)) * PSRS +
+                                                        4 * ej + 32 * (c ^ par));
+          float z[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f32x2 acc2 = {0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+              for (int u = 0; u < 4; u += 2) {
+                f32x2 t = f32x2{pt[c][u], pt[c][u + 1]} + f32x2{p[q][c][u], p[q][c][u + 1]};
+                t = f32x2{relu(t.x), relu(t.y)};
+                acc2 = __builtin_elementwise_fma(t, f32x2{ww[c][u], ww[c][u + 1]}, acc2);
+              }
+            z[q] = acc2.x + acc2.y;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) z[q] = sum8(z[q]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float aq = sigmoid_fast(z[q] + b2);
+            a[q] = q < deg ? aq : 0.f;
             S += a[q];
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            a[q] = 0.f;
+            if (q < deg) {
+              a[q] = alpha_of(src[q]);
+              S += a[q];
+            }
           }
         }
         if constexpr (!FAST) {
 #pragma unroll 1
           for (int q = 4; q < deg; ++q) S += alpha_of(col_of(q));
         }
+        // alpha / S as alpha * (1 / S): one IEEE division per destination instead of one per
+        // edge (<= 1.5 ulp apart; the layer is held to 2e-6 of the training path)
         const bool norm = S > 0.f;
+        const float rS = norm ? 1.f / S : 1.f;
         f32x4 g[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+        if constexpr (FAST) {
+          u32x4 xp[4][3];                   // the four sources' planes, all reads in flight
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (q < deg) {
-            const float wq = norm ? a[q] / S : a[q];
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+              xp[q][pl] = *reinterpret_cast<const u32x4*>(XR + xr_off(src[q] & (RING - 1), pl, ej));
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float wq = a[q] * rS;
             f32x4 v[2];
-            x_of(src[q], v);
+            x_planes(xp[q][0], xp[q][1], xp[q][2], v);
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               g[0][c] = fmaf(wq, v[0][c], g[0][c]);
               g[1][c] = fmaf(wq, v[1][c], g[1][c]);
             }
           }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (q < deg) {
+              const float wq = a[q] * rS;
+              f32x4 v[2];
+              x_of(src[q], v);
+#pragma unroll
+              for (int c = 0; c < 4; ++c) {
+                g[0][c] = fmaf(wq, v[0][c], g[0][c]);
+                g[1][c] = fmaf(wq, v[1][c], g[1][c]);
+              }
+            }
+        }
 #pragma unroll 1
         for (int q = FAST ? deg : 4; q < deg; ++q) {
           const int s = col_of(q);
-          const float aq = alpha_of(s);
-          const float wq = norm ? aq / S : aq;
+          const float wq = alpha_of(s) * rS;
           f32x4 v[2];
           x_of(s, v);
 #pragma unroll
@@ -492,11 +575,13 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         }, bw);
         load_w<4, ABL>(bw, wr, wl, wA);           // waves 4-7 are idle until the next tile's phase A
       }
-      __syncthreads();                    // agg planes read: PT takes the partials
-      // the two K halves' partials meet in PT (accumulator layout): each wave of a pair keeps
-      // m-block kh, hands the other to its partner, and finishes its own (sum = x_d half + agg
-      // half either way round: fp32 addition commutes)
-      float* part = PT + nq * 2048 + lane;
+      // the two K halves' partials meet in the Ps ring's dead half (accumulator layout, 16 rows
+      // per quarter): the slots of rows [d0 - 32, d0 + 32), read for the last time in phase B and
+      // written next by the next tile's phase A -- so no barrier is needed before the partials
+      // are stored, nor between reading them and storing [gate | u1] over the agg planes in PT.
+      // Each wave of a pair keeps m-block kh, hands the other to its partner, and finishes its
+      // own (sum = x_d half + agg half either way round: fp32 addition commutes)
+      float* part = PSR + ((d0 - BR + 16 * nq) & (RING - 1)) * PSRS + lane;
       f32x16 mine;
       if (kh == 0) {
 #pragma unroll
@@ -507,10 +592,9 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         for (int r = 0; r < 16; ++r) part[r * 64] = acc[0][r];
         mine = acc[1];
       }
-      __syncthreads();
+      __syncthreads();                    // partials stored; every wave's agg-plane reads done
 #pragma unroll
       for (int r = 0; r < 16; ++r) mine[r] += part[(kh * 16 + r) * 64];
-      __syncthreads();                    // partials read: PT takes [gate | u1]
       const int n = 32 * nq + lr;         // output column: gate (n < 64) or u1 (n - 64)
       const float bias = BS[n];         // gate.0 (n < 64) | update_net.0
 #pragma unroll
