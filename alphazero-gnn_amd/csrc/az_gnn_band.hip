@@ -196,6 +196,21 @@ __device__ __forceinline__ void zero(f32x16& a) {
 
 }  // namespace
 
+#ifdef AZ_TUNING
+// ABL & 256 (tuning build): wall-clock stamps of block 0's waves 0 and 4 at the phase boundaries
+// of its first 64 tiles, [wave group][tile][event] (tools/band_trace.py)
+constexpr int BT_EV = 12, BT_TILES = 64;
+__device__ unsigned long long g_band_trace[2 * BT_TILES * BT_EV];
+#define BSTAMP(ev)                                                                            \
+  do {                                                                                        \
+    if constexpr ((ABL & 256) != 0)                                                           \
+      if (blockIdx.x == 0 && lane == 0 && (wave & 3) == 0 && tile - t0 < BT_TILES)            \
+        g_band_trace[((wave >> 2) * BT_TILES + (tile - t0)) * BT_EV + (ev)] = wall_clock64(); \
+  } while (0)
+#else
+#define BSTAMP(ev) do {} while (0)
+#endif
+
 // ABL != 0 only in the tuning build: timing ablations, results wrong by design (bits 1 / 2 / 4 /
 // 8 = no phase A / B / C / D math, 16 = no weight loads, 64 = no x_out stores, 128 = no x loads)
 // OT: the layer is the network's last -- output_transform (gnn_utils.py:101-105,115: Linear +
@@ -283,7 +298,11 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   const int wl = 16 * lane;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   const int wA = W1_OFF + frag_off(32 * (wv & 3), wv < 4 ? 0 : BF, 2 * BF);
-  const int wC = WC_OFF + frag_off(32 * (wv & 3), BF * (wv >> 2), 2 * BF);
+  // C's column quarter of a wave: the agg-half waves (4-7) take the quarters of the x-half waves
+  // on the other SIMDs' partner (quarter ^ 2), so each SIMD (waves w, w + 4) finishes one gate
+  // quarter (sigmoid: two transcendentals per element) and one update_net.0 quarter (ReLU)
+  const int cq = (wv & 3) ^ (wv < 4 ? 0 : 2);
+  const int wC = WC_OFF + frag_off(32 * cq, BF * (wv >> 2), 2 * BF);
   const int wD = WU2_OFF + frag_off(32 * (wv & 1), 0, BF);
   bf16x8 bw[4][3];
   constexpr int AAB = (ABL & 1) ? (ABL | 32) : ABL;
@@ -326,6 +345,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   __syncthreads();
 
   for (int tile = t0; tile < t1; ++tile) {
+    BSTAMP(0);
     const int d0 = tile * BT;
     const int lo = d0 - BR;               // the window: nodes [lo, lo + RING)
     const bool has_next = tile + 1 < t1;
@@ -357,7 +377,9 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     } else {
       ps_rows(d0 + BR);
     }
+    BSTAMP(1);
     __syncthreads();
+    BSTAMP(2);
 
     // ---- B: attention scores and normalised aggregation (gnn_utils.py:48-65); each
     //      destination's agg replaces its Pt row, as three planes.  The prefetch goes out first:
@@ -553,12 +575,14 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       if (ej == 0) DEG[ei] = deg;
     }
     load_w<4, ABL>(bw, wr, wl, wC);
+    BSTAMP(3);
     __syncthreads();
+    BSTAMP(4);
 
     // ---- C: [gate | u1] over [x_d ; agg]: waves 0-3 the x_d half of K (ring planes), 4-7 the
     //      agg half (planes in the Pt rows); wave & 3 = 32-column quarter (0-1 gate, 2-3 u1)
     {
-      const int nq = wave & 3, kh = wave >> 2;
+      const int nq = cq, kh = wave >> 2;
       f32x16 acc[2];
       zero(acc[0]);
       zero(acc[1]);
@@ -575,6 +599,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         }, bw);
         load_w<4, ABL>(bw, wr, wl, wA);           // waves 4-7 are idle until the next tile's phase A
       }
+      BSTAMP(5);
       // the two K halves' partials meet in the Ps ring's dead half (accumulator layout, 16 rows
       // per quarter): the slots of rows [d0 - 32, d0 + 32), read for the last time in phase B and
       // written next by the next tile's phase A -- so no barrier is needed before the partials
@@ -593,6 +618,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         mine = acc[1];
       }
       __syncthreads();                    // partials stored; every wave's agg-plane reads done
+      BSTAMP(6);
 #pragma unroll
       for (int r = 0; r < 16; ++r) mine[r] += part[(kh * 16 + r) * 64];
       const int n = 32 * nq + lr;         // output column: gate (n < 64) or u1 (n - 64)
@@ -604,8 +630,15 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       }
     }
     __syncthreads();
+    BSTAMP(7);
 
-    // ---- D: x_out = x_d + gate * (u1 Wu2^T + bu2)  (waves 0-3: 32 x 32 each; u1 split here)
+    // ---- D: x_out = x_d + gate * (u1 Wu2^T + bu2)  (waves 0-3: 32 x 32 each; u1 split here).
+    //      The MFMA waves park u2 = u1 Wu2^T + bu2 in the Ps ring's dead slots [d0 - 32, d0)
+    //      (contiguous, [64][64]); then all 8 waves apply the residual row by row: a thread per
+    //      (row, 8 features) reads x_d as three plane chunks, gate and u2 as float4s, and stores
+    //      x_out as two float4s (the MFMA layout would need 48 16-bit plane reads and 16 scattered
+    //      4-byte stores per lane, on half the waves)
+    float* const u2s = PSR + ((d0 - BR) & (RING - 1)) * PSRS;
     if (wave < 4) {
       const int mb = wave >> 1, nb = wave & 1;
       f32x16 acc[1];
@@ -623,25 +656,40 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       const int n = 32 * nb + lr;
       const float ub = BS[2 * BF + n];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = 32 * mb + acc_row(r, lane);
-        const int slot = (d0 + row) & (RING - 1);
-        const int k = xr_off(slot, 0, n >> 3) + (n & 7);
-        const float xd = (__uint_as_float((unsigned)XR[k] << 16) +
-                          __uint_as_float((unsigned)XR[k + BF] << 16)) +
-                         __uint_as_float((unsigned)XR[k + 2 * BF] << 16);
-        const float o = DEG[row] > 0 ? xd + PT[row * PSS + n] * (acc[0][r] + ub) : xd;
-        if constexpr (OT) {
-          PT[row * PSS + n] = o;          // in place of the gate element it consumed
-        } else {
-          const int d = d0 + row;
-          if (d < V) {
-            if constexpr ((ABL & 64) == 0) x_out[(size_t)d * BF + n] = o;
-            else if (o == 12345.f) x_out[0] = o;
+      for (int r = 0; r < 16; ++r) u2s[(32 * mb + acc_row(r, lane)) * BF + n] = acc[0][r] + ub;
+    }
+    __syncthreads();                      // u2 complete
+    {
+      const int i = tid >> 3, c = tid & 7;   // row, features 8c .. 8c + 7
+      f32x4 xv[2];
+      x_ring((d0 + i) & (RING - 1), c, xv);
+      const f32x4* gp = reinterpret_cast<const f32x4*>(PT + i * PSS + 8 * c);
+      const f32x4* up = reinterpret_cast<const f32x4*>(u2s + i * BF + 8 * c);
+      const bool upd = DEG[i] > 0;
+      f32x4 o[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 gv = gp[h], uv = up[h];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[h][e] = upd ? xv[h][e] + gv[e] * uv[e] : xv[h][e];
+      }
+      if constexpr (OT) {
+        float* dst = PT + i * PSS + 8 * c;    // in place of the gate elements it consumed
+        *reinterpret_cast<f32x4*>(dst) = o[0];
+        *reinterpret_cast<f32x4*>(dst + 4) = o[1];
+      } else {
+        const int d = d0 + i;
+        if (d < V) {
+          if constexpr ((ABL & 64) == 0) {
+            *reinterpret_cast<f32x4*>(x_out + (size_t)d * BF + 8 * c) = o[0];
+            *reinterpret_cast<f32x4*>(x_out + (size_t)d * BF + 8 * c + 4) = o[1];
+          } else if (o[0][0] == 12345.f) {
+            x_out[0] = o[0][0];
           }
         }
       }
     }
+    BSTAMP(8);
     if constexpr (OT) {
       // ---- E: h = relu(x_out W0^T + b0) -> PT[:, 64:128] (u1's, free once every wave's D
       //      MFMAs are done);  F: y = h W2^T + b2 -> HBM  (waves 0-3, 32 x 32 each; x_out / h
@@ -683,12 +731,14 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       }
     }
     __syncthreads();                      // x_d rows read: their slots take the next rows
+    BSTAMP(9);
     if (has_next) {
       store_rows(d0 + BT + BR, nextx);
       CLS[nxt][tid] = cln;                // used only when the next tile has <= 512 edges
     }
     if (tile + 2 < t1 && tid <= BT) RPS[cur][tid] = rp2;   // tile + 2 has this tile's parity
     __syncthreads();
+    BSTAMP(10);
   }
 }
 
@@ -745,6 +795,7 @@ int gnn_layer_band(const az_graph* g, const float* x, const az_gnn_layer_w* w, f
     case 15: AZ_BAND(15); break;
     case 31: AZ_BAND(31); break;
     case 223: AZ_BAND(223); break;
+    case 256: AZ_BAND(256); break;
     default: AZ_BAND(0); break;
   }
 #else
@@ -753,5 +804,14 @@ int gnn_layer_band(const az_graph* g, const float* x, const az_gnn_layer_w* w, f
 #undef AZ_BAND
   return check_launch("gnn_layer_band_kernel");
 }
+
+#ifdef AZ_TUNING
+// tools/band_trace.py: the last traced launch's stamps (synchronous)
+extern "C" int az_tuning_band_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_band_trace), sizeof(g_band_trace)) == hipSuccess
+             ? (int)(sizeof(g_band_trace) / 8)
+             : -1;
+}
+#endif
 
 }  // namespace az
