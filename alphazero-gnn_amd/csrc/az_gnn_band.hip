@@ -189,6 +189,16 @@ __device__ __forceinline__ int xr_off(int slot, int pl, int c) {
   return slot * XRS + pl * BF + ((c ^ ((slot >> 1) & 7)) << 3);
 }
 
+// the accumulator rows of register r relative to the lane's first (acc_row(r, lane) - acc_row(0,
+// lane)), and an opaque copy of a lane's base offset: the per-register stores then use base +
+// constant (the DS immediate offset) instead of 16 loop-invariant addresses hoisted out of the
+// tile loop (which spill at 256 VGPRs)
+__device__ __forceinline__ constexpr int acc_drow(int r) { return (r & 3) + 8 * (r >> 2); }
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 __device__ __forceinline__ void zero(f32x16& a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) a[r] = 0.f;
@@ -713,9 +723,9 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         x3_mfma<1, 4, ABL>(acc, split_rows(0), bw);
         load_w<4, ABL>(bw, wr, wl, wD + (OT2_OFF - WU2_OFF));
         const float bias = BS[3 * BF + n];
+        float* const pe = PT + opaque((32 * mb + acc_row(0, lane)) * PSS + BF + n);
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          PT[(32 * mb + acc_row(r, lane)) * PSS + BF + n] = relu(acc[0][r] + bias);
+        for (int r = 0; r < 16; ++r) pe[acc_drow(r) * PSS] = relu(acc[0][r] + bias);
       }
       __syncthreads();
       if (wave < 4) {
@@ -723,14 +733,22 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         x3_mfma<1, 4, ABL>(acc, split_rows(BF), bw);
         load_w<4, ABL>(bw, wr, wl, wA);
         const float bias = BS[4 * BF + n];
+        float* const pf = PT + opaque((32 * mb + acc_row(0, lane)) * PSS + n);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int d = d0 + 32 * mb + acc_row(r, lane);
-          if (d < V) x_out[(size_t)d * BF + n] = acc[0][r] + bias;
-        }
+        for (int r = 0; r < 16; ++r)      // y over x_out's rows in PT (read by E, before F)
+          pf[acc_drow(r) * PSS] = acc[0][r] + bias;
       }
     }
     __syncthreads();                      // x_d rows read: their slots take the next rows
+    if constexpr (OT) {                   // y leaves row by row, two float4 per thread
+      const int i = tid >> 3, c = tid & 7, d = d0 + i;
+      if (d < V) {
+        const float* src = PT + i * PSS + 8 * c;
+        *reinterpret_cast<f32x4*>(x_out + (size_t)d * BF + 8 * c) = *reinterpret_cast<const f32x4*>(src);
+        *reinterpret_cast<f32x4*>(x_out + (size_t)d * BF + 8 * c + 4) =
+            *reinterpret_cast<const f32x4*>(src + 4);
+      }
+    }
     BSTAMP(9);
     if (has_next) {
       store_rows(d0 + BT + BR, nextx);
