@@ -82,7 +82,7 @@ _WS = {}
 _WS_PINNED = {}
 
 
-def workspace(device, nbytes=96 << 20):
+def workspace(device, nbytes=256 << 20):
     """Per-device split-K workspace (kept for the process lifetime; grows on demand, which
     frees the previous buffer -- so a captured hipGraph must not reference it: see
     `pinned_workspace`)."""
