@@ -46,12 +46,17 @@ def run(env, B, tag):
 
 if __name__ == "__main__":
     import numpy as np
-    for B in (512, 1024, 1576, 2048, 4096):
+    # python tools/heads_sweep.py [B,B,...] [all|twopass]
+    Bs = [int(b) for b in sys.argv[1].split(",")] if len(sys.argv) > 1 else [512, 1024, 1576, 2048, 4096]
+    which = sys.argv[2] if len(sys.argv) > 2 else "all"
+    envs = ([{"AZ_HEADS_TWOPASS": "1"}] if which == "twopass" else
+            [{"AZ_HEADS_R": "2"}, {"AZ_HEADS_R": "4"}, {"AZ_HEADS_R": "8"}, {"AZ_TRUNK_NB": "1"},
+             {"AZ_TRUNK_NB": "2"}, {"AZ_TRUNK_NB": "4"}, {"AZ_TRUNK_NB": "8"},
+             {"AZ_HEADS_TWOPASS": "1"}])
+    for B in Bs:
         base, ref = run({}, B, "base")
         print(json.dumps({"B": B, "variant": "default", **base}), flush=True)
-        for env in ({"AZ_HEADS_R": "2"}, {"AZ_HEADS_R": "4"}, {"AZ_HEADS_R": "8"},
-                    {"AZ_TRUNK_NB": "1"}, {"AZ_TRUNK_NB": "2"}, {"AZ_TRUNK_NB": "4"},
-                    {"AZ_TRUNK_NB": "8"}):
+        for env in envs:
             res, out = run(env, B, "v")
             same = bool(out is not None and ref is not None and np.array_equal(out, ref))
             print(json.dumps({"B": B, "variant": env, "bit_identical": same, **res}), flush=True)
