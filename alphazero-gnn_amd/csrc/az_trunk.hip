@@ -741,14 +741,11 @@ static void launch_heads(const float* hp, int ldhp, const float* hv, int ldhv, i
   // R rows per block, one wave per chunk holding that chunk's head weights for all R rows: a
   // block re-reads the 113 KB of head weights, so R grows with B while the grid still covers
   // the CUs (2 at B = 512: 256 blocks; 4 from the self-play rounds' B ~ 1,600: ~400)
-  int R = B > 768 ? 4 : 2;      // r03m: B = 1,024 15.0 vs 15.3 us
+  int R = B > 768 ? 4 : 2;      // r03m: B = 1,576 21.4 vs 24.2 us, B = 4,096 41.6 vs 47.8
   if (env_r) R = atoi(env_r);
-  if (AMAX == 8 && nchunks <= 16 && !two_pass && (B <= 1024 || env_r) &&
-      (R == 2 || R == 4 || R == 8)) {
-    // one launch (splitk_heads_rowsw_kernel's body); above B = 1,024 the two-pass form's
-    // 16-row weight reuse wins (profiles/r03t_heads_twopass_sweep.jsonl, bit-identical:
-    // B = 512 15.5 vs 17.8 us one-pass; 1,576 21.4 vs 18.6; 3,150 39.9 vs 28.7; 4,096 41.4 vs
-    // 33.7; 8,192 77.2 vs 52.6)
+  if (AMAX == 8 && nchunks <= 16 && !two_pass && B <= 8192 && (R == 2 || R == 4 || R == 8)) {
+    // one launch (splitk_heads_rowsw_kernel's body); above B = 8192 the two-pass form's
+    // 16-row weight reuse wins (B = 65,536: rowsw at R = 2 took 735 us vs ~0.3 ms)
     const dim3 blk(64 * nchunks);
     if (R == 2)
       hipLaunchKernelGGL((heads_rowsw_kernel<8, 2>), dim3((B + 1) / 2), blk, 0, s, hp, ldhp, hv,
