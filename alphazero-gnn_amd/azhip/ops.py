@@ -197,7 +197,7 @@ def c4_trunk(boards_i8, W, out=None):
 
 def c4_trunk_heads(boards_i8, W, feat=None, logp=None, pi=None, v=None, want_pi=True):
     """Trunk + policy/value heads (Connect4Net.py:42-60) -> (feat, logp, pi, v); one launch
-    for B <= 32, bit-identical to c4_trunk then heads."""
+    for B <= 320, bit-identical to c4_trunk then heads."""
     _need(boards_i8, torch.int8, "boards")
     B = boards_i8.shape[0]
     dev = _dev(boards_i8)

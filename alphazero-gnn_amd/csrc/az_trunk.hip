@@ -802,7 +802,23 @@ extern "C" int az_c4_trunk_heads_fwd(const int8_t* boards, int B, const float* c
   AZ_REQUIRE(aligned16(feat) && aligned16(wp) && aligned16(wv), AZ_EINVAL,
              "az_c4_trunk_heads_fwd: operands need 16B alignment");
   static const bool split = tuning_env("AZ_TRUNK_HEADS_SPLIT") != nullptr;   // A/B experiments
-  if (B <= HEADS_ROWS_MAXB && A <= 8 && !split) {
+  static const char* fused_nb = tuning_env("AZ_TRUNK_HEADS_FUSED");        // A/B: any B, NB 1/2
+  if (fused_nb && A <= 8) {
+    if (atoi(fused_nb) == 2)
+      hipLaunchKernelGGL(c4_trunk_heads_kernel<2>, dim3((B + 1) / 2), dim3(512), 0,
+                         as_stream(stream), boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat,
+                         wp, bp, A, wv, bv, logp, pi, v);
+    else
+      hipLaunchKernelGGL(c4_trunk_heads_kernel<1>, dim3(B), dim3(512), 0, as_stream(stream),
+                         boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, wp, bp, A, wv, bv,
+                         logp, pi, v);
+    return check_launch("c4_trunk_heads_kernel");
+  }
+  // one launch up to B = 320 (profiles/r03t_trunk_heads_probe.jsonl, bit-identical: B = 64
+  // 17.2 vs 19.9 us for trunk + heads, 256 17.1 vs 23.8; at 512 the two launches win, 25.5 vs
+  // 28.9): the self-play lanes' shrinking batches as their games finish
+  constexpr int TRUNK_HEADS_MAXB = 320;
+  if (B <= TRUNK_HEADS_MAXB && A <= 8 && !split) {
     hipLaunchKernelGGL(c4_trunk_heads_kernel<1>, dim3(B), dim3(512), 0, as_stream(stream), boards,
                        B, conv1_w, conv1_b, conv2_w, conv2_b, feat, wp, bp, A, wv, bv, logp, pi,
                        v);

@@ -127,7 +127,7 @@ int az_heads_fwd(const float* hp, int ldhp, const float* hv, int ldhv, int B, in
 
 /* Connect4 trunk and policy/value heads in one call: az_c4_trunk_fwd then az_heads_fwd on the
  * feature rows (Connect4Net.py:42-60; Connect4GNN.py:48-57), bit-identical to that pair.  For
- * B <= 32 and A <= 8 it is ONE launch (the heads read the features from the trunk's LDS tile);
+ * B <= 320 and A <= 8 it is ONE launch (the heads read the features from the trunk's LDS tile);
  * otherwise the two launches, with ws >= az_heads_ws_bytes(B, 3136, A).  feat [B][3136] is
  * written either way; boards may be az_host_alloc memory (read in place). */
 int az_c4_trunk_heads_fwd(const int8_t* boards, int B, const float* conv1_w, const float* conv1_b,
