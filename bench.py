@@ -36,8 +36,11 @@ HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec peak
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    # 200 + 200 steps of the B = 512 step take ~70 ms; fewer warmup steps time the chip while its
+    # clock is still ramping (profiles/r03v_warmup_probe.jsonl: warmup 10 / steps 50 -> 177 us per
+    # step, warmup 200 -> 156 us, unchanged at 500 timed steps)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample (rank 0, N=1 only)")
@@ -414,7 +417,7 @@ def x3_roofline(kernel, flop, seconds, traffic=None, traffic_run=None):
             "speedup_vs_fp32_mfma_peak": round(fp32_eq / FP32_MFMA_PEAK_TFLOPS, 4)}
 
 
-def gemm_shapes_leg(torch, ops, ev, device, Ms=(800, 1576, 3150), reps=20):
+def gemm_shapes_leg(torch, ops, ev, device, Ms=(800, 1576, 3150), reps=50, warm=30):
     """output_transform.0 (one az_gemm_f32 call, Linear 3136x3136 + ReLU) at the self-play
     leg's batch sizes: 8192 lock-step games on 2 lanes put ~3,150 rows into each predict_both
     (4096 games ~1,576), the tail of a run ~800 (HIP events around each call, on the launch
@@ -424,7 +427,7 @@ def gemm_shapes_leg(torch, ops, ev, device, Ms=(800, 1576, 3150), reps=20):
     for M in Ms:
         x = torch.empty((M, F), device=device).uniform_(0, 1)
         y = torch.empty((M, F), device=device)
-        for _ in range(3):
+        for _ in range(warm):             # the clock settles over tens of ms (main step note)
             ops.linear(x, Gn["output_transform.0.weight"], Gn["output_transform.0.bias"],
                        act=ops.ACT_RELU, out=y)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]

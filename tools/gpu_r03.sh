@@ -12,5 +12,5 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --durations=30 --timeou
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
 timeout -k 10 200 python -u tools/band_probe.py 512 20 > $O/band_probe.log 2>&1 || exit $?
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-selfplay --no-train --no-agg-extra --large-batch 0 > $O/kt.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 200 --warmup 200 --no-cpu --no-selfplay --no-train --no-agg-extra --large-batch 0 > $O/kt.log 2>&1 || exit $?
 echo done > $O/done
