@@ -663,17 +663,52 @@ extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w
              "az_c4_trunk_fwd: null pointer");
   hipStream_t s = as_stream(stream);
   static const char* env = tuning_env("AZ_TRUNK_NB");   // tuning experiments only
-  // boards per block by batch (tools/heads_sweep.py, r03m): 8 from B = 1,536 (the self-play
-  // rounds: 47.7 vs 58.2 us at B = 1,576 for 2), 4 from 768 (27.2 vs 31.2 us at 1,024)
-  int nbk = B >= 1536 ? 8 : (B >= 768 ? 4 : (B >= 256 ? 2 : (B <= 8 ? 0 : 1)));
+  // boards per block: the time is whole rounds of blocks over the CUs, each round t(NB) (one
+  // block per CU at a time in effect; measured on MI355X, profiles/r03w_trunk_nb_sweep.jsonl:
+  // t = 9, 16, 22, 25, 28.5, 33, 42, 47 us for NB = 1..8, every NB bit-identical), so pick the
+  // NB with the fewest rounds x t(NB): B = 512 -> 2, 1,024 -> 4, 1,576 -> 7, 2,048 -> 8,
+  // 2,560 -> 5 (56 vs 89 us for 8), 3,150 -> 7 (85 vs 90), 4,096 -> 8
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0, n = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+           n > 0) ? n : 256;
+  }
+  int nbk = 0;
+  if (B > 8) {
+    static const float t_nb[9] = {0.f, 9.f, 16.f, 22.f, 25.f, 28.5f, 33.f, 42.f, 47.f};
+    float best = 0.f;
+    for (int nb = 1; nb <= 8; ++nb) {
+      const long rounds = ((long)(B + nb - 1) / nb + cus - 1) / cus;
+      const float t = (float)rounds * t_nb[nb];
+      if (nb == 1 || t < best) best = t, nbk = nb;
+    }
+  }
   if (env) nbk = atoi(env);
   switch (nbk) {
     case 8:
       hipLaunchKernelGGL(c4_trunk_kernel<8>, dim3((B + 7) / 8), dim3(512), 0, s, boards, B,
                          conv1_w, conv1_b, conv2_w, conv2_b, feat);
       break;
+    case 7:
+      hipLaunchKernelGGL(c4_trunk_kernel<7>, dim3((B + 6) / 7), dim3(512), 0, s, boards, B,
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+      break;
+    case 6:
+      hipLaunchKernelGGL(c4_trunk_kernel<6>, dim3((B + 5) / 6), dim3(512), 0, s, boards, B,
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+      break;
+    case 5:
+      hipLaunchKernelGGL(c4_trunk_kernel<5>, dim3((B + 4) / 5), dim3(512), 0, s, boards, B,
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+      break;
     case 4:
       hipLaunchKernelGGL(c4_trunk_kernel<4>, dim3((B + 3) / 4), dim3(512), 0, s, boards, B,
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+      break;
+    case 3:
+      hipLaunchKernelGGL(c4_trunk_kernel<3>, dim3((B + 2) / 3), dim3(512), 0, s, boards, B,
                          conv1_w, conv1_b, conv2_w, conv2_b, feat);
       break;
     case 2:

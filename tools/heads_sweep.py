@@ -46,10 +46,11 @@ def run(env, B, tag):
 
 if __name__ == "__main__":
     import numpy as np
-    # python tools/heads_sweep.py [B,B,...] [all|twopass]
+    # python tools/heads_sweep.py [B,B,...] [all|twopass|trunk]
     Bs = [int(b) for b in sys.argv[1].split(",")] if len(sys.argv) > 1 else [512, 1024, 1576, 2048, 4096]
     which = sys.argv[2] if len(sys.argv) > 2 else "all"
     envs = ([{"AZ_HEADS_TWOPASS": "1"}] if which == "twopass" else
+            [{"AZ_TRUNK_NB": str(n)} for n in (1, 2, 3, 4, 5, 6, 7, 8)] if which == "trunk" else
             [{"AZ_HEADS_R": "2"}, {"AZ_HEADS_R": "4"}, {"AZ_HEADS_R": "8"}, {"AZ_TRUNK_NB": "1"},
              {"AZ_TRUNK_NB": "2"}, {"AZ_TRUNK_NB": "4"}, {"AZ_TRUNK_NB": "8"},
              {"AZ_HEADS_TWOPASS": "1"}])
