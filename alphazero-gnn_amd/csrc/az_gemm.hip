@@ -9,7 +9,9 @@
 // of its A row / B column with one ds_read_b128 and feeds 4 MFMAs; the k order inside an
 // 8-k group is permuted (lane half h owns k = 4h..4h+3, MFMA t sums k = t and 4+t), which
 // changes only the fp32 summation order.
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <type_traits>
@@ -999,12 +1001,20 @@ constexpr int x3_smem_bytes() {
 
 // One (tile, k range) of gemm_x3: C tile (mt, nt) over k in [kbeg, kend); sp = the split-K
 // slab it writes when p.splits > 1 (raw partial sums), else the fused epilogue.
-template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false, int MF = 32>
+// FLEX (stream-K tail rows): the tile shape is chosen at run time from the 384 LDS rows of the
+// 256 x 128 / 8-wave body: bma = 256 (256 x 128, waves 4 x 2) or bma = 128 (128 x 256, waves
+// 2 x 4); every wave keeps its 64 x 64 sub-tile, so the loop, its MFMAs and its LDS traffic are
+// the same, and only the loader's row split, the fragment row offsets and the epilogue origin
+// change (all computed once, before the k loop).  mt / nt count tiles of that shape.
+template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false, int MF = 32,
+          bool FLEX = false>
 __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int mt, int nt,
-                                             int sp, int kbeg, int kend) {
+                                             int sp, int kbeg, int kend, int bma = BM) {
   static_assert(!APL || !MASK, "pre-split A needs whole 32-k tiles");
+  static_assert(!FLEX || (BM == 256 && BN == 128 && WGM == 4 && WGN == 2 && MF == 32 && !APL),
+                "FLEX reshapes the 256 x 128 8-wave tile");
   constexpr int BK = 32;
-  constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
+  constexpr int NT = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TI = WM / MF, TJ = WN / MF;
   constexpr int NSTEP = MF == 32 ? 2 : 1;
@@ -1015,26 +1025,29 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
                 (BN * 4) % NT == 0, "bad x3 tile");
   constexpr int PLANE = (BM + BN) * 64;          // bytes of one bf16 plane (A rows, then W rows)
   constexpr int BUF = 3 * PLANE;
-  const int m0 = mt * BM, n0 = nt * BN;
+  const int tbm = FLEX ? bma : BM, tbn = FLEX ? BM + BN - bma : BN;
+  const int wgn = FLEX ? tbn / WN : WGN;
+  const int m0 = mt * tbm, n0 = nt * tbn;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave / WGN, wn = wave % WGN;
+  const int wm = wave / wgn, wn = wave % wgn;
 
-  // loader: segment q covers row idx >> 2 (A rows first, then W rows), k = 8 * (idx & 3) ..+7
+  // loader: segment q covers image row (tid + q NT) >> 2 (A rows first, then W rows),
+  // k = 8 * (idx & 3) ..+7
   const float* src[NSEG];
   int soff[NSEG], sk[NSEG];
 #pragma unroll
   for (int q = 0; q < NSEG; ++q) {
-    const bool isa = q < ASEG;
-    const int idx = threadIdx.x + (isa ? q : q - ASEG) * NT;
-    const int r = idx >> 2, c = idx & 3;
+    const int idx = threadIdx.x + q * NT;
+    const int row = idx >> 2, c = idx & 3;
+    const bool isa = FLEX ? row < tbm : q < ASEG;
     if (isa) {
-      const int gr = m0 + r < p.M ? m0 + r : 0;     // clamped rows feed outputs never stored
+      const int gr = m0 + row < p.M ? m0 + row : 0;     // clamped rows feed outputs never stored
       src[q] = p.A + (size_t)gr * p.lda;
     } else {
+      const int r = row - tbm;
       const int gr = n0 + r < p.N ? n0 + r : 0;
       src[q] = p.B + (size_t)gr * p.ldb;
     }
-    const int row = isa ? r : BM + r;
     soff[q] = row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
     sk[q] = c * 8;
   }
@@ -1108,7 +1121,7 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
   }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    const int row = BM + wn * WN + j * MF + (lane & (MF - 1));
+    const int row = tbm + wn * WN + j * MF + (lane & (MF - 1));
     boff[j] = row * 64;
     bkey[j] = (row >> 2) & 3;
   }
@@ -1296,6 +1309,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3_sk(GemmArgs p, SkPlan 
   }
 }
 
+#ifdef AZ_TUNING   // round 3's stream-K (gemm_x3_sk, gemm_p3_sk): A/B runs only
 // Sums the pieces of every tile gemm_x3_sk / gemm_p3_sk split (slab[0 .. np), np = the tile's
 // block count) and runs the epilogue on them; whole tiles were written by their block.  float4
 // per lane.
@@ -1317,6 +1331,8 @@ __global__ __launch_bounds__(256) void streamk_fixup4_kernel(GemmArgs p, int BM,
   epilogue_store4(p, row, col, v);
 }
 
+#endif
+
 // The stream-K plan for a BM x BN tile grid on B blocks (host); weighted: the last row of
 // m-tiles costs half when at most 128 of its rows are real (see gemm_x3_sk; not used).
 static SkPlan sk_plan(int M, int N, int K, int BM, int BN, int B, bool weighted) {
@@ -1337,6 +1353,230 @@ static int sk_max_pieces(const SkPlan& q, int N, int BN) {
   for (long t = 0; t < tiles; ++t)
     mx = std::max(mx, sk_block(q, t, q.KT - 1) - sk_block(q, t, 0) + 1);
   return mx;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Cycled stream-K ("csk"): gemm_x3_sk with the tile order and the block -> XCD placement chosen
+// for L2 reuse, and a short tile for a mostly padded last m-row.
+//
+// gemm_x3_sk walks the whole (tile, k) sequence with B equal ranges, so the blocks that need the
+// same A panel (same m-tile) or W panel (same n-tile) at the same k run 16-36 k-steps apart: on
+// one XCD that is ~25 MB of other loads in between, far beyond its 4 MB L2, and every k-slab of
+// A and W is fetched again from the Infinity Cache by each of its consumers (980 MB per dispatch
+// at the self-play shapes against ~86 MB algorithmic, L2 hit 0.29; r03x).
+//
+// Here the tiles are grouped into CYCLES, macro tiles of am x an tiles (slot f = fm + am * fn
+// holds tile (cm * am + fm, cn * an + fn) of cycle (cm, cn)), and every cycle's am * an * KT
+// k-steps are cut the same way into b equal ranges, one per block.  Block r of every cycle thus
+// runs the same (slot, k) sequence at the same time: in phase.  Logical block ids run r-major,
+// cycle fastest, so the in-phase blocks of all cycles are neighbours on one XCD; at slot f they
+// hold a 2-D set of tiles (every cm, every cn), in which each A k-slab is read by the cycles
+// along n and each W k-slab by the cycles along m at the same k, out of that XCD's L2.
+// Measured (tools/csk_probe.py, profiles/r04a_csk.jsonl): M = 1,536 with am x an = 1 x 5 on 240
+// blocks runs 62 steps per block in 200 us, gemm_x3_sk 58 steps on 256 blocks in 203 us:
+// 3.22 vs 3.49 us per step.
+//
+// A last m-row with at most 128 real rows runs 128 x 256 tiles instead of mostly padded
+// 256 x 128 ones (the FLEX body: the same waves, MFMAs and LDS image, half the rows, twice the
+// columns): half the steps, in cycles of its own (`at` wide tiles each, bt blocks per cycle).
+// Pieces of a tile (a slot split between blocks) write raw partials to slab[r - first block of
+// the slot] and csk_fixup4_kernel sums them in that order: deterministic.
+struct CskPlan {
+  int mt_n, nt_n, KT;  // 256 x 128 tile grid, 32-k steps per tile
+  int am, an;          // macro tile of a full cycle (am | full m-rows, an | nt_n)
+  int cm;              // cycles along m (full rows / am); along n: nt_n / an
+  int tail;            // 1: the last m-row runs 128 x 256 tiles
+  int at, ct;          // wide tiles per tail cycle, tail cycles (at * ct = ceil(N / 256))
+  int bf, bt;          // blocks per full / tail cycle
+  int Cf, Ct;          // full / tail cycles
+  int B;               // blocks: Cf * bf + Ct * bt
+};
+
+// the block of a b-block cycle of W steps that runs cycle step u (ranges [r W / b, (r+1) W / b))
+__host__ __device__ __forceinline__ int csk_block_of(int u, int b, int W) {
+  return ((u + 1) * b - 1) / W;
+}
+
+template <bool MASK>
+__global__ __launch_bounds__(512) void gemm_x3_csk(GemmArgs p, CskPlan q) {
+  __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<256, 128, 4, 2>()];
+  const int L = xcd_swizzle(blockIdx.x, q.B);
+  int r, b, am, an, mt0, nt0, bma;
+  if (L < q.Cf * q.bf) {                  // r-major, cycle fastest: in-phase blocks adjacent
+    r = L / q.Cf;
+    const int c = L - r * q.Cf, cn = c / q.cm;
+    b = q.bf;
+    am = q.am;
+    an = q.an;
+    mt0 = (c - cn * q.cm) * q.am;
+    nt0 = cn * q.an;
+    bma = 256;
+  } else {
+    const int l = L - q.Cf * q.bf;
+    r = l / q.Ct;
+    b = q.bt;
+    am = 1;
+    an = q.at;
+    mt0 = (q.mt_n - 1) * 2;               // in 128-row units
+    nt0 = (l - r * q.Ct) * q.at;          // in 256-column units
+    bma = 128;
+  }
+  const int W = am * an * q.KT;           // <= 256 x 98 steps: int arithmetic throughout
+  int i0 = r * W / b;
+  const int i1 = (r + 1) * W / b;
+  while (i0 < i1) {
+    const int f = i0 / q.KT;
+    const int k0 = i0 - f * q.KT;
+    const int k1 = min(q.KT, k0 + (i1 - i0));
+    GemmArgs g = p;
+    int sp = 0;
+    if (k0 == 0 && k1 == q.KT) {
+      g.splits = 1;                       // the whole tile: fused epilogue into C
+    } else {
+      g.splits = 2;                       // a piece: raw partials into slab[piece]
+      sp = r - csk_block_of(f * q.KT, b, W);
+    }
+    const int fn = f / am;
+    int mt_i = mt0 + (f - fn * am), bma_i = bma;   // opaque per segment: keeps the body's
+    asm volatile("" : "+s"(mt_i), "+s"(bma_i));    // address setup in the loop (hoisted, it spills)
+    gemm_x3_body<256, 128, 4, 2, MASK, 0, false, 32, true>(g, smem, mt_i, nt0 + fn, sp, 32 * k0,
+                                                          min(p.K, 32 * k1), bma_i);
+    i0 += k1 - k0;
+    if (i0 < i1) __syncthreads();         // the next segment's prologue reuses the LDS
+  }
+}
+
+// Sums the pieces of every tile gemm_x3_csk split, in piece (= k) order, and runs the epilogue;
+// whole tiles were written by their block.  float4 per lane.
+__global__ __launch_bounds__(256) void csk_fixup4_kernel(GemmArgs p, CskPlan q) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const int n4 = p.N >> 2;
+  if (idx >= (long)p.M * n4) return;
+  const int row = (int)(idx / n4), col = (int)(idx % n4) * 4;
+  const int mt = row >> 8;
+  const bool tail = q.tail && mt == q.mt_n - 1;
+  int f, b, W;
+  if (tail) {
+    f = (col >> 8) % q.at;
+    b = q.bt;
+    W = q.at * q.KT;
+  } else {
+    f = mt % q.am + q.am * ((col >> 7) % q.an);
+    b = q.bf;
+    W = q.am * q.an * q.KT;
+  }
+  const int bf = csk_block_of(f * q.KT, b, W), bl = csk_block_of((f + 1) * q.KT - 1, b, W);
+  if (bf == bl) return;
+  const size_t plane = (size_t)p.M * p.N, off = (size_t)row * p.N + col;
+  f32x4 v = *reinterpret_cast<const f32x4*>(p.slab + off);
+  for (int s = 1; s <= bl - bf; ++s) {
+    const f32x4 u = *reinterpret_cast<const f32x4*>(p.slab + s * plane + off);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += u[e];
+  }
+  epilogue_store4(p, row, col, v);
+}
+
+static int csk_max_pieces(const CskPlan& q) {
+  int mx = 1;
+  for (int t = 0; t < 2; ++t) {
+    const int b = t ? q.bt : q.bf, per = t ? q.at : q.am * q.an;
+    if (b <= 0 || per <= 0) continue;
+    const int W = per * q.KT;
+    for (int f = 0; f < per; ++f)
+      mx = std::max(mx, csk_block_of((f + 1) * q.KT - 1, b, W) - csk_block_of(f * q.KT, b, W) + 1);
+  }
+  return mx;
+}
+
+// Fills the derived fields of a plan from (am, an, bf) and the tail's (at, bt); false if the
+// plan does not tile this M x N or needs more than `cus` blocks.
+static bool csk_make(int M, int N, int K, int cus, int am, int an, int bf, int at, int bt,
+                     CskPlan& q) {
+  q = CskPlan{};
+  q.mt_n = (M + 255) / 256;
+  q.nt_n = (N + 127) / 128;
+  q.KT = (K + 31) / 32;
+  const int ntw = (N + 255) / 256, rows_last = M - (q.mt_n - 1) * 256;
+  q.tail = at > 0 ? 1 : 0;
+  if (q.tail && (q.mt_n < 2 || rows_last > 128 || ntw % at || bt < 1)) return false;
+  const int rows_full = q.mt_n - q.tail;
+  if (am < 1 || an < 1 || bf < 1 || rows_full % am || q.nt_n % an) return false;
+  q.am = am;
+  q.an = an;
+  q.cm = rows_full / am;
+  q.bf = bf;
+  q.Cf = q.cm * (q.nt_n / an);
+  q.at = at;
+  q.ct = q.tail ? ntw / at : 0;
+  q.bt = q.tail ? bt : 0;
+  q.Ct = q.ct;
+  q.B = q.Cf * q.bf + q.Ct * q.bt;
+  return q.B >= 1 && q.B <= cus;
+}
+
+// Chooses the plan for an M x N x K GEMM on `cus` CUs: every (am, an) macro tile and block count
+// bf for the full rows, the fastest (at, bt) for a wide-tile tail row in the CUs left.  A cycle
+// of `per` tiles on b blocks takes ceil(per KT / b) steps (the wide tile's step costs what the
+// 256 x 128 one's does), the launch the slowest cycle.  The per-step cost grows with the k-slab
+// bytes each block fetches past the XCD's L2: (ua * 32 KB + un * 16 KB) / (ua * un) for the ua
+// m-tiles x un n-tiles that the in-phase blocks on one XCD hold at a slot (an estimate; 48 KB
+// when nothing is shared).  Fitted to tools/csk_probe.py at M = 1,536 .. 4,096
+// (profiles/r04a_csk.jsonl): a step costs ~1 + miss_cost x (KB - 9) / 39 relative to a fully
+// shared one, miss_cost ~0.1 (3.16 vs 3.53 us per step at M = 1,536, 2.80 vs 3.08 at 4,096).
+constexpr double CSK_MISS_COST = 0.12;
+static bool csk_plan(int M, int N, int K, int cus, double miss_cost, CskPlan& out) {
+  const int mt_n = (M + 255) / 256, nt_n = (N + 127) / 128, KT = (K + 31) / 32;
+  const int ntw = (N + 255) / 256;
+  const int rows_last = M - (mt_n - 1) * 256;
+  const int tail = mt_n > 1 && rows_last <= 128 ? 1 : 0;
+  const int rows_full = mt_n - tail;
+  double best = 1e30;
+  bool found = false;
+  for (int am = 1; am <= rows_full; ++am) {
+    if (rows_full % am) continue;
+    for (int an = 1; an <= nt_n; ++an) {
+      if (nt_n % an) continue;
+      const int Cm = rows_full / am, Cn = nt_n / an, Cf = Cm * Cn;
+      const int W = am * an * KT;
+      // in-phase cycles on one XCD: up to 32 / (cycles per XCD) of them, m-fastest
+      const int on_xcd = std::min(Cf, 32);
+      const int ua = std::min(Cm, on_xcd), un = (on_xcd + Cm - 1) / Cm;
+      const double miss_kb = (ua * 32.0 + un * 16.0) / (double)(ua * un);
+      const double step = 1.0 + miss_cost * std::max(0.0, std::min(1.0, (miss_kb - 9.0) / 39.0));
+      for (int bf = 1; Cf * bf <= cus && W / bf >= 8; ++bf) {   // >= 8 steps per block
+        const int tf = (W + bf - 1) / bf;
+        int at = 0, bt = 0, tt = 0;
+        if (tail) {
+          // the tail row: per cycle width, the fewest blocks that finish within tf, else all
+          // the CUs left; the earliest finish, ties to the narrower cycles (more in phase)
+          const int room = cus - Cf * bf;
+          int tt_best = 1 << 30;
+          for (int a = 1; a <= ntw; ++a) {
+            if (ntw % a || room < ntw / a) continue;
+            const int ct = ntw / a, Wt = a * KT;
+            const int b = std::min(room / ct, (Wt + tf - 1) / tf);
+            const int t = std::max(tf, (Wt + b - 1) / b);
+            if (t < tt_best) {
+              tt_best = t;
+              at = a;
+              bt = b;
+            }
+          }
+          if (!at) break;
+          tt = tt_best;
+        }
+        const double cost = std::max(tf, tt) * step;
+        CskPlan q;
+        if (cost < best - 1e-9 && csk_make(M, N, K, cus, am, an, bf, at, bt, q)) {
+          best = cost;
+          out = q;
+          found = true;
+        }
+      }
+    }
+  }
+  return found;
 }
 
 // gemm_x3 on operands that are ALREADY split ("p3"): A as three bf16 planes [3][M][K] (p.apl,
@@ -2937,7 +3177,7 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   // 7..11: gemm_x3<256,128> timing ablations (ABL 1, 2, 4, 5, 3), K % 32 == 0 only
   const int bms[16] = {0, 256, 128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
   const int bns[16] = {0, 128, 128, 64, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
-  if (tile < 1 || tile > 15 || ((tile >= 7 && tile <= 11) || tile >= 13) && a.K % 32 != 0) {
+  if (tile < 1 || tile > 15 || (((tile >= 7 && tile <= 11) || tile >= 13) && a.K % 32 != 0)) {
     tile = a.M > 256 ? 1 : 2;
   }
   const int bm = bms[tile], bn = bns[tile];
@@ -2973,6 +3213,38 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
     const int B = (int)std::min<long>(cus, I);
     const long per = I / B;
     if ((double)blocks / (double)(rounds * cus) < 0.9 && per >= 8) {
+      // cycled stream-K (gemm_x3_csk).  Tuning build: AZ_CSK = "off" runs round 3's gemm_x3_sk,
+      // "am,an,bf,at,bt" forces a plan (csk_make), AZ_CSK_MISS sets the planner's miss cost,
+      // AZ_CSK_PRINT prints the plan
+      CskPlan cq{};
+      bool use_csk = true, ok = false, forced = false;
+#ifdef AZ_TUNING
+      static const char* env_csk = tuning_env("AZ_CSK");
+      static const char* env_miss = tuning_env("AZ_CSK_MISS");
+      int am = 0, an = 0, bf = 0, at = 0, bt = 0;
+      use_csk = !env_csk || strcmp(env_csk, "off") != 0;
+      if (use_csk && env_csk && sscanf(env_csk, "%d,%d,%d,%d,%d", &am, &an, &bf, &at, &bt) == 5) {
+        forced = true;
+        ok = csk_make(a.M, a.N, a.K, cus, am, an, bf, at, bt, cq);
+      }
+      if (use_csk && !forced)
+        ok = csk_plan(a.M, a.N, a.K, cus, env_miss ? atof(env_miss) : CSK_MISS_COST, cq);
+      if (ok && tuning_env("AZ_CSK_PRINT"))
+        fprintf(stderr, "csk M=%d: am=%d an=%d cycles=%d bf=%d tail=%d at=%d ct=%d bt=%d B=%d pieces=%d\n",
+                a.M, cq.am, cq.an, cq.Cf, cq.bf, cq.tail, cq.at, cq.ct, cq.bt, cq.B, csk_max_pieces(cq));
+#else
+      ok = csk_plan(a.M, a.N, a.K, cus, CSK_MISS_COST, cq);
+#endif
+      if (use_csk && ok && (size_t)csk_max_pieces(cq) * a.M * a.N * 4 <= ws_bytes) {
+        if (whole) hipLaunchKernelGGL((gemm_x3_csk<false>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        else hipLaunchKernelGGL((gemm_x3_csk<true>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        const long n4 = (long)a.M * (a.N / 4);
+        hipLaunchKernelGGL(csk_fixup4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                           a, cq);
+        a.splits = 1;
+        return true;
+      }
+#ifdef AZ_TUNING
       const SkPlan q = sk_plan(a.M, a.N, a.K, 256, 128, B, false);
       if ((size_t)sk_max_pieces(q, a.N, 128) * a.M * a.N * 4 <= ws_bytes) {
         if (whole) hipLaunchKernelGGL((gemm_x3_sk<256, 128, 4, 2, false>), dim3(B), dim3(512), 0, s, a, q);
@@ -2983,6 +3255,7 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
         a.splits = 1;
         return true;
       }
+#endif
     }
   }
 #ifdef AZ_TUNING
