@@ -440,10 +440,27 @@ def gemm_shapes_leg(torch, ops, ev, device, Ms=(800, 1576, 3150), reps=50, warm=
         us = float(np.mean([e[2 * i].elapsed_time(e[2 * i + 1]) for i in range(reps)])) * 1e3
         r = x3_roofline("az_gemm_f32 output_transform.0 at M = %d" % M, 2.0 * M * F * F,
                         us * 1e-6)
-        out.append({"M": M, "avg_call_us": r["avg_launch_us"], "frac": r["frac"],
-                    "fp32_equiv_tflops": r["fp32_equiv_tflops"]})
+        row = {"M": M, "avg_call_us": r["avg_launch_us"], "frac": r["frac"],
+               "fp32_equiv_tflops": r["fp32_equiv_tflops"]}
+        pm = _pmc_selfplay_gemm(M)
+        if pm:
+            row.update(pm)
+        out.append(row)
         del x, y
     return out
+
+
+def _pmc_selfplay_gemm(M):
+    """The committed PMC pass of the self-play GEMM at this M (profiles/pmc.json gemm_selfplay,
+    tools/gpu_csk_pmc.sh): HBM bytes per dispatch of the GEMM kernel, its L2 hit rate and the
+    algorithmic bytes (A + W read, C written)."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc.json")))["gemm_selfplay"]
+        r = d["by_M"][str(M)]["csk"]
+        return {"traffic": r["hbm_bytes_per_dispatch"], "traffic_algorithmic": r["algorithmic_bytes"],
+                "l2_hit": r.get("l2_hit"), "traffic_run": d.get("tag")}
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def selfplay_args(sims):
