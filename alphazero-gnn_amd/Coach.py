@@ -31,6 +31,8 @@ class ExamplesUnpickler(Unpickler):
         ("numpy", "ndarray"), ("numpy", "dtype"),
         ("numpy.core.multiarray", "_reconstruct"), ("numpy.core.multiarray", "scalar"),
         ("numpy._core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "scalar"),
+        # protocol 5 (Python 3.14's default) rebuilds contiguous arrays from their buffer
+        ("numpy.core.numeric", "_frombuffer"), ("numpy._core.numeric", "_frombuffer"),
         ("builtins", "list"), ("builtins", "tuple"), ("builtins", "dict"), ("builtins", "set"),
         ("builtins", "frozenset"), ("builtins", "int"), ("builtins", "float"),
         ("builtins", "bool"), ("builtins", "str"), ("builtins", "bytes"),

@@ -8,6 +8,7 @@ torch.save dict ({'state_dict': ..., 'gnn': ...}) with the same keys, so files m
 between the reference and this implementation.
 """
 import ctypes
+import logging
 import os
 
 import numpy as np
@@ -15,6 +16,16 @@ import torch
 
 from . import _lib, nets, ops, train as T
 from .nets import boards_to_device
+
+log = logging.getLogger(__name__)
+# one-launch leaf hand-over timeouts in this process (each switches one evaluator to the
+# four-launch path for good); bench.py reports it, so a degraded arena cannot go unnoticed
+_LEAF_TIMEOUTS = [0]
+
+
+def leaf_timeouts():
+    """How many one-launch leaf evaluations timed out in this process (_Batch1Direct._call)."""
+    return _LEAF_TIMEOUTS[0]
 
 
 def _dev_array(rows, dtype, device):
@@ -350,6 +361,10 @@ class _Batch1Direct:
             self.desc.err = None
             self.err_np = None
             self.leaf_timeouts = getattr(self, "leaf_timeouts", 0) + 1
+            _LEAF_TIMEOUTS[0] += 1
+            log.warning("az_c4_eval_fwd: the one-launch leaf kernel's hand-over timed out (not "
+                        "all its blocks were resident); this evaluator uses the four-launch path "
+                        "from now on (%d timeout(s) in this process)", _LEAF_TIMEOUTS[0])
             rc = self.fn(*self.args, n, *self.outs, self.sptr)
             if rc:
                 _lib.check(rc, "az_c4_eval_fwd")

@@ -1230,6 +1230,19 @@ int az_mcts_feed_collect(az_mcts* m, int count, const float* pi, const float* v,
     return fail(AZM_ESTATE, "az_mcts_feed_collect: a collect_spec request was not fed");
   m->row_of.assign(m->trees.size(), -1);
   for (int i = 0; i < count; ++i) m->row_of[m->last_order[i]] = i;
+  // the rows are applied inside the collect, so a cap the collect would overflow must fail
+  // here, while nothing has changed yet (a later plain az_mcts_feed still matches last_order):
+  // every slot that is fed, searching or inside an episode can hand out one leaf
+  int may = 0;
+  for (size_t s = 0; s < m->trees.size(); ++s) {
+    const Tree& t = m->trees[s];
+    may += m->row_of[s] >= 0 || t.ep.phase != E_IDLE || searching(t) || t.pending_leaf >= 0 ||
+           t.pending_std;
+  }
+  if (cap < may)
+    return fail(AZM_EINVAL, "az_mcts_feed_collect: cap " + std::to_string(cap) +
+                                " smaller than the " + std::to_string(may) +
+                                " slots that may hand out a leaf (nothing was fed)");
   m->last_order.clear();
   const FeedRows fr{m->row_of.data(), pi, v, gpi, gv};
   return collect_impl(m, boards, slots, cap, threads, &fr);

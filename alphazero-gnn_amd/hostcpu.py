@@ -57,12 +57,25 @@ def local_world_size():
         return 1
 
 
+# True once pin_rank_to_gpu_numa has narrowed this process's affinity mask to the rank's own share
+# of the cores: the mask is then per rank, and only node-wide limits are split among the ranks.
+_MASK_PER_RANK = False
+
+
 def threads_per_rank(local_world=None, cap=16):
-    """Engine threads for this rank: its share of the visible cores (the ranks of one node
-    split them evenly, LOCAL_WORLD_SIZE), at most `cap` (16: on a 16-core share, 32 threads
-    halved games/s, profiles/r02s_selfplay_sweep.jsonl)."""
+    """Engine threads for this rank, at most `cap` (16: on a 16-core share, 32 threads halved
+    games/s, profiles/r02s_selfplay_sweep.jsonl).  The node-wide limits -- an affinity mask
+    that was not narrowed per rank, a cgroup CPU quota -- are split evenly among the
+    LOCAL_WORLD_SIZE ranks; a mask pin_rank_to_gpu_numa already narrowed to this rank's share
+    is used as it is (dividing it again gave 8 ranks on two 64-core nodes 2 threads each)."""
     lw = local_world or local_world_size()
-    return max(1, min(cap, host_cpus() // lw))
+    n = len(affinity())
+    if not _MASK_PER_RANK:
+        n //= lw
+    q = cgroup_cpu_quota()
+    if q:
+        n = min(n, q // lw)
+    return max(1, min(cap, n))
 
 
 def _cpulist(s):
@@ -152,5 +165,7 @@ def pin_rank_to_gpu_numa(local_rank, local_world=None):
         os.sched_setaffinity(0, cpus)
     except (AttributeError, OSError):
         return info
+    global _MASK_PER_RANK
+    _MASK_PER_RANK = True
     info.update(cpus=len(cpus), pinned=True)
     return info

@@ -399,12 +399,13 @@ class _EpisodeLane:
             except Exception as err:  # the reference's per-leaf degradation (MCTS.py:195-200)
                 aborted = self.eng.feed(self.k, failed=True)
                 if aborted:
-                    # an expand_tree root predict was in the batch: unguarded in the reference
-                    # (MCTS.py:108-113), so the failure propagates out of the episode -- after
-                    # counting the batch's other leaves, which the same feed degraded
-                    if self.k > 1:
+                    # expand_tree root predicts were in the batch: unguarded in the reference
+                    # (MCTS.py:108-113), so the failure propagates out of those episodes -- after
+                    # counting the batch's other leaves, which the same feed degraded (the feed
+                    # returns how many of the k requests were aborted roots)
+                    if self.k > aborted:
                         try:
-                            nn_fallback.record("selfplay.engine", err, self.k - 1)
+                            nn_fallback.record("selfplay.engine", err, self.k - aborted)
                         except Exception:     # AZ_STRICT_NN: the original error wins
                             pass
                     raise err

@@ -701,6 +701,11 @@ def pmc_run(key):
         return None
 
 
+def _leaf_timeouts():
+    from azhip import wrappers
+    return wrappers.leaf_timeouts()
+
+
 def main():
     args = parse()
     # before any GPU call: this rank on its GPU's NUMA node (best effort; hostcpu.py)
@@ -895,6 +900,9 @@ def main():
             "selfplay": sp,
             "train": tr,
             "cpu_baseline": cpu,
+            # one-launch leaf kernel hand-over timeouts (azhip/wrappers.py; each switches an
+            # evaluator to the four-launch path): non-zero means degraded batch-1 / arena legs
+            "leaf_timeouts": _leaf_timeouts(),
         }
         print(json.dumps(out))
     if world > 1:

@@ -89,7 +89,9 @@ int az_mcts_feed(az_mcts* m, int count, const float* pi, const float* v, const f
  * ONE parallel pass: each worker thread feeds a group of slots and runs their next descents back
  * to back.  Same trees and leaves as the two calls (every slot's work is independent of the
  * others').  Returns the new leaf count like az_mcts_collect.  A failed batch goes through
- * az_mcts_feed(failed = 1) instead. */
+ * az_mcts_feed(failed = 1) instead.  cap must cover every slot that may hand out a leaf (fed,
+ * searching or inside an episode; the slot count always does): a smaller cap fails with
+ * AZM_EINVAL before any row is applied, so the same rows can still go through az_mcts_feed. */
 int az_mcts_feed_collect(az_mcts* m, int count, const float* pi, const float* v,
                          const float* gpi, const float* gv, int8_t* boards, int32_t* slots,
                          int cap, int threads);

@@ -328,10 +328,11 @@ def test_c4_trunk_and_heads_vs_oracle(ops):
     np.testing.assert_allclose(v.cpu().numpy()[:256], z["v_b1"], atol=1e-5)
 
 
-@pytest.mark.parametrize("B", [1, 3, 8, 32, 33, 100])
+@pytest.mark.parametrize("B", [1, 3, 8, 32, 33, 100, 320, 321])
 def test_c4_trunk_heads_fused_bit_identical(ops, B):
-    """az_c4_trunk_heads_fwd (one launch for B <= 32) == az_c4_trunk_fwd + az_heads_fwd bit for
-    bit, and the oracle within 1e-5 (Connect4Net.py:42-60)."""
+    """az_c4_trunk_heads_fwd (one launch for B <= 320, the unfused pair above) ==
+    az_c4_trunk_fwd + az_heads_fwd bit for bit, and the oracle within 1e-5
+    (Connect4Net.py:42-60)."""
     from oracle import nets as O
     z = golden("c4_net.npz")
     W = split_weights(z, "w/")
@@ -347,6 +348,24 @@ def test_c4_trunk_heads_fused_bit_identical(ops, B):
     rlp, rv = O.c4_heads(O.c4_features(boards, W), W)
     np.testing.assert_allclose(lp.cpu().numpy(), rlp, atol=1e-5)
     np.testing.assert_allclose(v.cpu().numpy(), np.asarray(rv).reshape(-1), atol=1e-5)
+
+
+def test_c4_trunk_every_boards_per_block_variant_bit_identical(ops):
+    """az_c4_trunk_fwd picks boards per block NB = 1..8 from a rounds model (az_trunk.hip); on
+    256 CUs the batch sizes below select NB = 1, 2, 3, 4, 5, 6, 7, 8.  A board's arithmetic does
+    not depend on NB, so every row of every batch equals (torch.equal) the same board's row in
+    the B = 2,000 (NB = 8) batch, and the first rows match the oracle within 1e-5."""
+    from oracle import nets as O
+    z = golden("c4_net.npz")
+    W = split_weights(z, "w/")
+    Wd = {k: cu(v) for k, v in W.items()}
+    boards = np.random.default_rng(11).integers(-1, 2, size=(2000, 7, 7)).astype(np.int8)
+    full = ops.c4_trunk(cu(boards), Wd)
+    for B in (200, 500, 600, 1000, 1200, 1500, 1700, 1999):
+        f = ops.c4_trunk(cu(boards[:B]), Wd)
+        assert torch.equal(f, full[:B]), B
+    np.testing.assert_allclose(full[:16].cpu().numpy(), O.c4_features(boards[:16], W),
+                               atol=1e-5, rtol=1e-5)
 
 
 def test_c4_trunk_large_batches(ops):

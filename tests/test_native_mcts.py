@@ -360,3 +360,30 @@ def test_feed_collect_equals_feed_then_collect(use_gnn):
                 assert type(a[key]) is type(b[key]) and a[key] == b[key]
             else:
                 assert a[key].dtype == b[key].dtype and np.array_equal(a[key], b[key]), key
+
+
+def test_feed_collect_small_cap_fails_before_feeding():
+    """az_mcts_feed_collect with a cap below the slots that may hand out a leaf
+    fails with nothing applied, so the same rows still go through a plain az_mcts_feed and the
+    next collect hands out what a clean feed + collect would."""
+    from connect4.Connect4Game import Connect4Game
+    from mcts_native import Engine, lib
+    game = Connect4Game(7)
+    net = HashNet(game.getActionSize(), 5)
+    S = 6
+    engs = [Engine(game, S, 1.0, True) for _ in range(2)]
+    for e in engs:
+        for s in range(S):
+            e.episode_begin(s, 300 + s, 9, 3, 6)
+    k = [e.collect(2) for e in engs]
+    assert k[0] == k[1] == S
+    out = net.predict_both(engs[0].leaf_boards[:k[0]])
+    e = engs[1]
+    ptrs = e._rows_ptrs("test", k[1], *out, at_least=True)
+    rc = lib().az_mcts_feed_collect(e.h, k[1], *ptrs, e._pb, e._ps, 1, 2)
+    assert rc < 0
+    assert "nothing was fed" in lib().az_mcts_last_error().decode()
+    for x in engs:
+        x.feed(S, *out)
+    a, b = engs[0].collect(2), engs[1].collect(2)
+    assert a == b and np.array_equal(engs[0].leaf_boards[:a], engs[1].leaf_boards[:b])

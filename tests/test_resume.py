@@ -81,6 +81,12 @@ def test_examples_unpickler_refuses_foreign_globals(tmp_path):
     coach.loadTrainExamples()
     (std, gnn), = coach.trainExamplesHistory
     assert np.array_equal(std[0][0], hist[0][0][0][0]) and gnn[0][3] == np.float32(0.25)
+    # a history pickled with protocol 5 (numpy rebuilds contiguous arrays via _frombuffer)
+    p5 = tmp_path / "p5.pth.tar.examples"
+    p5.write_bytes(pickle.dumps([deque(hist[0][0]), deque(hist[0][1])], protocol=5))
+    with open(p5, "rb") as f:
+        got = ExamplesUnpickler(f).load()
+    assert np.array_equal(got[0][0][0], hist[0][0][0][0]) and got[1][0][3] == np.float32(0.25)
 
 
 @pytest.mark.gpu

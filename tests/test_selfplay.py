@@ -136,6 +136,36 @@ def test_host_thread_budget(monkeypatch):
         assert hostcpu.affinity() == before
 
 
+def test_host_thread_budget_divides_node_limits_once(monkeypatch):
+    """with 8 ranks on two 64-core NUMA nodes each rank is pinned to its 16-core
+    share; that mask is already per rank and must not be divided by the rank count again, while
+    a node-wide mask or cgroup quota is split among the ranks."""
+    import hostcpu
+    monkeypatch.setattr(hostcpu, "affinity", lambda: list(range(16)))
+    monkeypatch.setattr(hostcpu, "cgroup_cpu_quota", lambda: None)
+    monkeypatch.setattr(hostcpu, "_MASK_PER_RANK", True)        # pinned: a per-rank mask
+    assert hostcpu.threads_per_rank(local_world=8) == 16
+    monkeypatch.setattr(hostcpu, "cgroup_cpu_quota", lambda: 64)  # node quota: 64 / 8 ranks
+    assert hostcpu.threads_per_rank(local_world=8) == 8
+    monkeypatch.setattr(hostcpu, "cgroup_cpu_quota", lambda: None)
+    monkeypatch.setattr(hostcpu, "affinity", lambda: list(range(128)))
+    monkeypatch.setattr(hostcpu, "_MASK_PER_RANK", False)       # unpinned: the node's mask
+    assert hostcpu.threads_per_rank(local_world=8) == 16
+    assert hostcpu.threads_per_rank(local_world=16) == 8
+    # the pin itself marks the mask per rank, with several local ranks on one node
+    monkeypatch.setattr(hostcpu, "gpu_numa_nodes", lambda: [0] * 8)
+    monkeypatch.setattr(hostcpu, "_read", lambda p: "0-127" if p.endswith("cpulist") else None)
+    got = {}
+    monkeypatch.setattr(hostcpu.os, "sched_setaffinity", lambda pid, c: got.setdefault("cpus", c))
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    info = hostcpu.pin_rank_to_gpu_numa(3, 8)
+    assert info["pinned"] and info["cpus"] == 16 and got["cpus"] == list(range(48, 64))
+    assert hostcpu._MASK_PER_RANK
+    monkeypatch.setattr(hostcpu, "affinity", lambda: got["cpus"])
+    assert hostcpu.threads_per_rank(local_world=8) == 16
+
+
 def test_engine_assembler_thread_equals_inline():
     """Examples assembled on the assembler thread equal the inline assembly, episode by
     episode (recorded reference outputs, so both equal the reference's examples too)."""
