@@ -152,6 +152,8 @@ SIGNATURES = {
                             c_size_t, c_void_p]),
     "az_adam_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_double, c_double,
                             c_double, c_double, c_int, c_void_p]),
+    "az_weights_changed": (c_int, []),
+    "az_gemm_form": (c_int, [c_int, c_int, c_int, c_size_t]),
 }
 
 _lib = None

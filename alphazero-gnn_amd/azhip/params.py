@@ -8,6 +8,16 @@ import numpy as np
 import torch
 
 
+def weights_changed():
+    """Tell libaz_hip.so that parameter values changed (az_weights_changed): the fp16 GEMM form
+    recomputes its cached per-row weight scales before their next use.  Every in-place write of
+    a parameter buffer outside az_adam_f32 must call this (load_state_dict, copy_flat_ do)."""
+    if not torch.cuda.is_available():
+        return
+    from . import _lib
+    _lib.check(_lib.load().az_weights_changed(), "az_weights_changed")
+
+
 def _align4(n):
     return (n + 3) & ~3
 
@@ -75,6 +85,12 @@ class FlatParams:
                                    f"{tuple(src.shape)}, the shape in current model is "
                                    f"{tuple(dst.shape)}")
             dst.copy_(src.to(torch.float32), non_blocking=False)
+        weights_changed()
+
+    def copy_flat_(self, src):
+        """Overwrite the whole parameter buffer (a snapshot restore) and say so to the library."""
+        self.flat.copy_(src)
+        weights_changed()
 
     # -- training buffers -------------------------------------------------------------------
     @property

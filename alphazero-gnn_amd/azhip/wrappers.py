@@ -623,9 +623,9 @@ class NetWrapper:
         return snap
 
     def restore(self, snap):
-        self.nnet.params.flat.copy_(snap["nnet"])
+        self.nnet.params.copy_flat_(snap["nnet"])
         if self.has_gnn:
-            self.gnn.params.flat.copy_(snap["gnn"])
+            self.gnn.params.copy_flat_(snap["gnn"])
 
 
 class GNNWrapperMixin:

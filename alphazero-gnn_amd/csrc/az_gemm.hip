@@ -14,8 +14,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <type_traits>
 #include <utility>
+#include <vector>
 
 #include "az_common.h"
 #include "az_x3.h"
@@ -53,6 +56,10 @@ struct GemmArgs {
   // gemm_p3: W already split too, three bf16 planes [3][N][K] at bpl (row stride K)
   const unsigned short* bpl;
   size_t bpl_plane;   // elements per plane (N * K)
+  // gemm_x3 in its fp16 form (H3): per-row power-of-two scales of A ([2][M]: s, then 1/s) and of
+  // W ([2][N]), row_scale_kernel
+  const float* sa;
+  const float* sw;
 };
 
 __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int col, float acc) {
@@ -992,10 +999,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f32_glds2(GemmArgs p) {
 // == 0): the tile copies them into the LDS image without any VALU, only W is split here.
 // MF = 16 (tuning build): v_mfma_f32_16x16x32_bf16 blocks, one k step per 32-k tile (lane l
 // holds row l & 15, k chunk l >> 4), against two 32x32x16 steps for MF = 32.
-template <int BM, int BN, int WGM, int WGN, int MF = 32>
+template <int BM, int BN, int WGM, int WGN, int MF = 32, int PL = 3>
 constexpr int x3_smem_bytes() {
   constexpr int NW = WGM * WGN, WM = BM / WGM;
-  constexpr int BUF = 3 * (BM + BN) * 64, STAGE = NW * WM * 36 * 4;
+  constexpr int BUF = PL * (BM + BN) * 64, STAGE = NW * WM * 36 * 4;
   return 2 * BUF > STAGE ? 2 * BUF : STAGE;
 }
 
@@ -1006,11 +1013,18 @@ constexpr int x3_smem_bytes() {
 // 2 x 4); every wave keeps its 64 x 64 sub-tile, so the loop, its MFMAs and its LDS traffic are
 // the same, and only the loader's row split, the fragment row offsets and the epilogue origin
 // change (all computed once, before the k loop).  mt / nt count tiles of that shape.
+//
+// H3: the fp16 form (see az_x3.h split2s): every operand row scaled by its power-of-two factor
+// (p.sa / p.sw, from row_scale_kernel), split into two fp16 terms, a*b as the three products
+// ah*bl + al*bh + ah*bh on v_mfma_f32_32x32x16_f16 (two LDS planes instead of three, half the
+// MFMAs), and the accumulators multiplied back by 1 / (sa[row] sw[col]) (exact) before the
+// epilogue.
 template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false, int MF = 32,
-          bool FLEX = false>
+          bool FLEX = false, bool H3 = false>
 __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int mt, int nt,
                                              int sp, int kbeg, int kend, int bma = BM) {
   static_assert(!APL || !MASK, "pre-split A needs whole 32-k tiles");
+  static_assert(!H3 || (!APL && ABL == 0 && MF == 32), "H3: the product form only");
   static_assert(!FLEX || (BM == 256 && BN == 128 && WGM == 4 && WGN == 2 && MF == 32 && !APL),
                 "FLEX reshapes the 256 x 128 8-wave tile");
   constexpr int BK = 32;
@@ -1023,8 +1037,9 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
   constexpr int ASEG = BM * 4 / NT, BSEG = BN * 4 / NT, NSEG = ASEG + BSEG;
   static_assert(TI >= 1 && TJ >= 1 && ASEG >= 1 && BSEG >= 1 && (BM * 4) % NT == 0 &&
                 (BN * 4) % NT == 0, "bad x3 tile");
-  constexpr int PLANE = (BM + BN) * 64;          // bytes of one bf16 plane (A rows, then W rows)
-  constexpr int BUF = 3 * PLANE;
+  constexpr int PL = H3 ? 2 : 3;                 // operand planes (fp16 h, l / bf16 h, m, l)
+  constexpr int PLANE = (BM + BN) * 64;          // bytes of one 16-bit plane (A rows, then W rows)
+  constexpr int BUF = PL * PLANE;
   const int tbm = FLEX ? bma : BM, tbn = FLEX ? BM + BN - bma : BN;
   const int wgn = FLEX ? tbn / WN : WGN;
   const int m0 = mt * tbm, n0 = nt * tbn;
@@ -1035,6 +1050,7 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
   // k = 8 * (idx & 3) ..+7
   const float* src[NSEG];
   int soff[NSEG], sk[NSEG];
+  float ssc[H3 ? NSEG : 1];                      // H3: the segment's row scale
 #pragma unroll
   for (int q = 0; q < NSEG; ++q) {
     const int idx = threadIdx.x + q * NT;
@@ -1043,10 +1059,12 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
     if (isa) {
       const int gr = m0 + row < p.M ? m0 + row : 0;     // clamped rows feed outputs never stored
       src[q] = p.A + (size_t)gr * p.lda;
+      if constexpr (H3) ssc[q] = p.sa[gr];
     } else {
       const int r = row - tbm;
       const int gr = n0 + r < p.N ? n0 + r : 0;
       src[q] = p.B + (size_t)gr * p.ldb;
+      if constexpr (H3) ssc[q] = p.sw[gr];
     }
     soff[q] = row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
     sk[q] = c * 8;
@@ -1085,6 +1103,19 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
           *reinterpret_cast<u32x4*>(base + pl * PLANE + soff[q]) = ld.pa[q][pl];
         return;
       }
+    }
+    if constexpr (H3) {
+      u32x4 o2[2];
+      if constexpr (decltype(mask)::value) {
+        const int k = k0 + sk[q];
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        split2s(k < kend ? ld.f[q][0] : z, k + 4 < kend ? ld.f[q][1] : z, ssc[q], o2);
+      } else {
+        split2s(ld.f[q][0], ld.f[q][1], ssc[q], o2);
+      }
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) *reinterpret_cast<u32x4*>(base + pl * PLANE + soff[q]) = o2[pl];
+      return;
     }
     if constexpr (decltype(mask)::value) {
       const int k = k0 + sk[q];
@@ -1126,11 +1157,11 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
     bkey[j] = (row >> 2) & 3;
   }
   const int hk = MF == 32 ? lane >> 5 : lane >> 4;
-  struct Frags { bf16x8 a[3][TI], b[3][TJ]; };
+  struct Frags { bf16x8 a[PL][TI], b[PL][TJ]; };
   auto read = [&](Frags& f, const char* S, int s) {
     const int c = MF == 32 ? 2 * s + hk : hk;
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
+    for (int pl = 0; pl < PL; ++pl) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
         f.a[pl][i] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + aoff[i] + ((c ^ akey[i]) << 4));
@@ -1146,7 +1177,14 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
       return;
     }
     acc_t t = acc[i][j];
-    if constexpr (MF == 32) {
+    if constexpr (H3) {
+      // fp16 terms (h = plane 0, l = plane 1), the dropped al*bl smallest; smallest first
+      const f16x8 ah = __builtin_bit_cast(f16x8, f.a[0][i]), al = __builtin_bit_cast(f16x8, f.a[PL - 1][i]);
+      const f16x8 bh = __builtin_bit_cast(f16x8, f.b[0][j]), bl = __builtin_bit_cast(f16x8, f.b[PL - 1][j]);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, t, 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, t, 0, 0, 0);
+    } else if constexpr (MF == 32) {
       t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[2][j], t, 0, 0, 0);
       t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[2][i], f.b[0][j], t, 0, 0, 0);
       t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[1][j], t, 0, 0, 0);
@@ -1223,19 +1261,37 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
     step(kt, r1, r0);                 // tile kt + 1 in r1, tile kt + 2 -> r0
     if (kt + 1 < nk) step(kt + 1, r0, r1);
   }
+  if constexpr (H3) {
+    // back to the operands' units: acc(row, col) / (sa[row] sw[col]), powers of two (exact);
+    // the inverses sit after the scales (p.sa + M, p.sw + N)
+    float iw[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+      iw[j] = p.sw[p.N + min(n0 + wn * WN + j * MF + (lane & (MF - 1)), p.N - 1)];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < NACC; ++r) {
+        const int row = m0 + wm * WM + i * MF + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const float ia = p.sa[p.M + min(row, p.M - 1)];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j][r] *= ia * iw[j];
+      }
+  }
   tile_epilogue<MF, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
 }
 
-template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false, int MF = 32>
+template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false, int MF = 32,
+          bool H3 = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
-  __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<BM, BN, WGM, WGN, MF>()];
+  __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<BM, BN, WGM, WGN, MF, H3 ? 2 : 3>()];
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
   const int nwg = mt_n * nt_n * p.splits;
   const int bid = xcd_swizzle(blockIdx.x, nwg);
   const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
   const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
-  gemm_x3_body<BM, BN, WGM, WGN, MASK, ABL, APL, MF>(p, smem, mt, nt, sp, kbeg, kend);
+  gemm_x3_body<BM, BN, WGM, WGN, MASK, ABL, APL, MF, false, H3>(p, smem, mt, nt, sp, kbeg, kend);
 }
 
 // Stream-K form of gemm_x3 for grids whose tile count does not fill the chip in whole rounds
@@ -1397,9 +1453,9 @@ __host__ __device__ __forceinline__ int csk_block_of(int u, int b, int W) {
   return ((u + 1) * b - 1) / W;
 }
 
-template <bool MASK>
+template <bool MASK, bool H3>
 __global__ __launch_bounds__(512) void gemm_x3_csk(GemmArgs p, CskPlan q) {
-  __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<256, 128, 4, 2>()];
+  __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<256, 128, 4, 2, 32, H3 ? 2 : 3>()];
   const int L = xcd_swizzle(blockIdx.x, q.B);
   int r, b, am, an, mt0, nt0, bma;
   if (L < q.Cf * q.bf) {                  // r-major, cycle fastest: in-phase blocks adjacent
@@ -1439,8 +1495,8 @@ __global__ __launch_bounds__(512) void gemm_x3_csk(GemmArgs p, CskPlan q) {
     const int fn = f / am;
     int mt_i = mt0 + (f - fn * am), bma_i = bma;   // opaque per segment: keeps the body's
     asm volatile("" : "+s"(mt_i), "+s"(bma_i));    // address setup in the loop (hoisted, it spills)
-    gemm_x3_body<256, 128, 4, 2, MASK, 0, false, 32, true>(g, smem, mt_i, nt0 + fn, sp, 32 * k0,
-                                                          min(p.K, 32 * k1), bma_i);
+    gemm_x3_body<256, 128, 4, 2, MASK, 0, false, 32, true, H3>(g, smem, mt_i, nt0 + fn, sp,
+                                                              32 * k0, min(p.K, 32 * k1), bma_i);
     i0 += k1 - k0;
     if (i0 < i1) __syncthreads();         // the next segment's prologue reuses the LDS
   }
@@ -3163,6 +3219,90 @@ static int splits_256x128(int M, int N, int K, size_t ws_bytes) {
   return S;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row scales of the fp16 form (H3, az_x3.h split2s): one wave per row, s[r] = 2^e with
+// max_k |X[r][k]| * s in [2^(T-1), 2^T) (s = 1 for an all-zero or non-finite row: a NaN / inf then
+// reaches the outputs as in fp32), out[rows + r] = 1 / s (exact).  e is kept within +-120 so s
+// and 1/s are normal floats.
+__global__ __launch_bounds__(256) void row_scale_kernel(const float* __restrict__ X, int rows,
+                                                        int cols, int ld, int T,
+                                                        float* __restrict__ out) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float* x = X + (size_t)r * ld;
+  float m = 0.f;
+  const int c4 = cols & ~3;
+  for (int c = lane * 4; c < c4; c += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + c);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  for (int c = c4 + lane; c < cols; c += 64) m = fmaxf(m, fabsf(x[c]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (lane == 0) {
+    int e = 0;
+    if (m > 0.f && m <= 3.4e38f) {
+      int ex;
+      (void)frexpf(m, &ex);
+      e = min(120, max(-120, T - ex));
+    }
+    out[r] = ldexpf(1.f, e);
+    out[rows + r] = ldexpf(1.f, -e);
+  }
+}
+
+// A's rows are scaled into [2^13, 2^14) (fp16 max 65504); W's into [2^9, 2^10): its scales are
+// cached between weight updates (below) and stay safe while the weights grow up to 64x.
+constexpr int H3_TA = 14, H3_TW = 10;
+
+// W row-scale cache: weights change only between calls that say so (az_weights_changed, which
+// az_adam_f32 also calls; the Python parameter store calls it on every load / copy), so a
+// weight matrix's scales are computed once per weight update.  Each entry has two buffers: a
+// recompute writes the other one and synchronises its stream before publishing it, so a GEMM
+// launched earlier on another stream keeps reading consistent scales, and one launched later on
+// any stream sees finished ones.
+static std::atomic<long> g_wgen{1};
+struct WScaleEntry {
+  const float* w;
+  int n, k, ld;
+  long gen;
+  float* buf[2];
+  int cur;
+};
+static std::mutex g_wmu;
+static std::vector<WScaleEntry> g_wcache;
+
+}  // namespace az
+extern "C" int az_weights_changed(void) {
+  az::g_wgen.fetch_add(1);
+  return AZ_OK;
+}
+namespace az {
+
+static const float* w_row_scales(const float* w, int n, int k, int ld, hipStream_t s) {
+  const long gen = g_wgen.load();
+  std::lock_guard<std::mutex> lk(g_wmu);
+  WScaleEntry* e = nullptr;
+  for (auto& x : g_wcache)
+    if (x.w == w && x.n == n && x.k == k && x.ld == ld) e = &x;
+  if (e && e->gen == gen) return e->buf[e->cur];
+  if (!e) {
+    WScaleEntry x{w, n, k, ld, 0, {nullptr, nullptr}, 0};
+    if (hipMalloc(&x.buf[0], (size_t)4 * n * sizeof(float)) != hipSuccess) return nullptr;
+    x.buf[1] = x.buf[0] + 2 * n;
+    x.cur = 1;
+    g_wcache.push_back(x);
+    e = &g_wcache.back();
+  }
+  const int nxt = e->cur ^ 1;
+  hipLaunchKernelGGL(row_scale_kernel, dim3((n + 3) / 4), dim3(256), 0, s, w, n, k, ld, H3_TW,
+                     e->buf[nxt]);
+  if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+  e->cur = nxt;
+  e->gen = gen;
+  return e->buf[nxt];
+}
+
 // gemm_x3 launch for a K-major A and W (no A2 / gathered rows), M > 64: 256x128 (8 waves) above
 // M = 256, else 128x128 (4 waves); split-K so the grid nears one block per CU (measured on
 // MI355X, tools/gemm_sweep.py x3: M = 512 75 us vs 103 us for the fp32 MFMA tile, M = 800 147 vs
@@ -3171,6 +3311,24 @@ static int splits_256x128(int M, int N, int K, size_t ws_bytes) {
 static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   static const char* env = tuning_env("AZ_GEMM_X3");
   static const char* env_split = tuning_env("AZ_GEMM_SPLITS");
+  // the fp16 form (H3) for the product tiles when the workspace can hold A's row scales (taken
+  // from its end, after every split-K slab); tuning build: AZ_GEMM_PREC=x3 keeps the bf16 form
+  static const char* env_prec = tuning_env("AZ_GEMM_PREC");
+  const size_t sa_bytes = ((size_t)2 * a.M * sizeof(float) + 255) / 256 * 256;
+  bool h3 = !(env_prec && strcmp(env_prec, "x3") == 0) && a.slab && ws_bytes >= sa_bytes + 256;
+  if (h3) ws_bytes = (ws_bytes - sa_bytes) / 256 * 256;
+  float* const sa_buf = h3 ? reinterpret_cast<float*>(reinterpret_cast<char*>(a.slab) + ws_bytes)
+                           : nullptr;
+  // A's row scales and W's (cached) just before the launch that uses them
+  auto h3_scales = [&]() {
+    const float* sw = w_row_scales(a.B, a.N, a.K, a.ldb, s);
+    if (!sw) return false;
+    hipLaunchKernelGGL(row_scale_kernel, dim3((a.M + 3) / 4), dim3(256), 0, s, a.A, a.M, a.K,
+                       a.lda, H3_TA, sa_buf);
+    a.sa = sa_buf;
+    a.sw = sw;
+    return true;
+  };
   int tile = env ? atoi(env) : 0;
   if (env && tile == 0) return false;
   if (!env && a.M <= 64) return false;  // tools/gemm_sweep.py x3: fp32 tiles win to M = 64 (27 vs 31 us)
@@ -3217,8 +3375,9 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
       // "am,an,bf,at,bt" forces a plan (csk_make), AZ_CSK_MISS sets the planner's miss cost,
       // AZ_CSK_PRINT prints the plan
       CskPlan cq{};
-      bool use_csk = true, ok = false, forced = false;
+      bool use_csk = true, ok = false;
 #ifdef AZ_TUNING
+      bool forced = false;
       static const char* env_csk = tuning_env("AZ_CSK");
       static const char* env_miss = tuning_env("AZ_CSK_MISS");
       int am = 0, an = 0, bf = 0, at = 0, bt = 0;
@@ -3236,8 +3395,11 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
       ok = csk_plan(a.M, a.N, a.K, cus, CSK_MISS_COST, cq);
 #endif
       if (use_csk && ok && (size_t)csk_max_pieces(cq) * a.M * a.N * 4 <= ws_bytes) {
-        if (whole) hipLaunchKernelGGL((gemm_x3_csk<false>), dim3(cq.B), dim3(512), 0, s, a, cq);
-        else hipLaunchKernelGGL((gemm_x3_csk<true>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        if (h3) h3 = h3_scales();
+        if (h3 && whole) hipLaunchKernelGGL((gemm_x3_csk<false, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        else if (h3) hipLaunchKernelGGL((gemm_x3_csk<true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        else if (whole) hipLaunchKernelGGL((gemm_x3_csk<false, false>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        else hipLaunchKernelGGL((gemm_x3_csk<true, false>), dim3(cq.B), dim3(512), 0, s, a, cq);
         const long n4 = (long)a.M * (a.N / 4);
         hipLaunchKernelGGL(csk_fixup4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
                            a, cq);
@@ -3327,6 +3489,16 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   if (whole) hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, false>), grid, dim3(64 * WM_ * WN_), \
                                 0, s, a);                                                      \
   else hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, true>), grid, dim3(64 * WM_ * WN_), 0, s, a);
+#define AZ_H3(BM_, BN_, WM_, WN_)                                                              \
+  if (whole) hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, false, 0, false, 32, true>), grid,  \
+                                dim3(64 * WM_ * WN_), 0, s, a);                                \
+  else hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, true, 0, false, 32, true>), grid,         \
+                          dim3(64 * WM_ * WN_), 0, s, a);
+  if (h3 && (tile == 1 || tile == 2) && h3_scales()) {
+    if (tile == 1) { AZ_H3(256, 128, 4, 2) }
+    else { AZ_H3(128, 128, 2, 2) }
+    return true;
+  }
   switch (tile) {
     case 1: AZ_X3(256, 128, 4, 2) break;
 #ifdef AZ_TUNING
@@ -3636,4 +3808,14 @@ int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
 
 extern "C" int az_gemm_f32(const az_gemm_desc* d, void* stream) {
   return az::gemm_f32(d, az::as_stream(stream));
+}
+
+// The MFMA products per fp32 product az_gemm_f32 uses for a plain K-major M x N x K GEMM with
+// ws_bytes of workspace (the dispatch rules of gemm_f32 / launch_x3, product build): 3 = the
+// fp16 form (h3), 6 = the bf16 form (x3), 1 = an fp32 MFMA tile, 0 = the fp32 GEMV (M <= 8).
+extern "C" int az_gemm_form(int M, int N, int K, size_t ws_bytes) {
+  if (M <= 8) return 0;
+  if (!(M > 64 && K >= 1024 && N >= 256)) return 1;
+  const size_t sa_bytes = ((size_t)2 * M * sizeof(float) + 255) / 256 * 256;
+  return ws_bytes >= sa_bytes + 256 ? 3 : 6;
 }

@@ -72,6 +72,7 @@ extern "C" int az_adam_f32(float* p, const float* g, float* m, float* v, int64_t
   AZ_REQUIRE(p && g && m && v, AZ_EINVAL, "az_adam_f32: null");
   AZ_REQUIRE(aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v), AZ_EINVAL,
              "az_adam_f32: buffers need 16B alignment");
+  az_weights_changed();   // the GEMMs' cached weight scales (az_gemm.hip) are stale now
   const double bc1 = 1.0 - pow(beta1, step);
   const double bc2 = 1.0 - pow(beta2, step);
   const double step_size = lr / bc1;

@@ -45,6 +45,37 @@ __device__ __forceinline__ void split3(const f32x4& x0, const f32x4& x1, u32x4 (
 }
 
 
+// ---------------------------------------------------------------------------------------------
+// fp32 on the fp16 matrix cores ("h3"): an fp32 x times its row's power-of-two scale s (so the
+// row's largest |x s| lies in [2^13, 2^14)) is split into two fp16 terms h = rne(x s),
+// l = rne(x s - h) (x s - h is exact in fp32); |x s - h - l| <= 2^-22 |x s| while l is a normal
+// fp16, and <= 2^-25 absolutely below that, i.e. <= 2^-39 of the row's largest |x s|.  a*b is the
+// sum of the three products ah*bl + al*bh + ah*bh (each exact in fp32); the dropped al*bl is
+// <= 2^-22 |a s_a||b s_b|.  Per product that is <= 3 * 2^-22 |a||b| (+ the 2^-39 floors), an order
+// of magnitude below the fp32 accumulation's own rounding over K = 3136 products
+// (tests/test_gpu_kernels.py x3_bound).  v_mfma_f32_32x32x16_f16 runs at the bf16 rate: half the
+// MFMAs of the six-product bf16 form and two LDS planes instead of three.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned pk_f16(float a, float b) {
+  const f16x2 h = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(unsigned, h);
+}
+
+// 8 consecutive floats of one row, scaled by s -> two planes of 8 fp16 (element j in bits 16j..)
+__device__ __forceinline__ void split2s(const f32x4& x0, const f32x4& x1, float s, u32x4 (&o)[2]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float a = (q < 2 ? x0[2 * q] : x1[2 * q - 4]) * s;
+    const float b = (q < 2 ? x0[2 * q + 1] : x1[2 * q - 3]) * s;
+    const unsigned h = pk_f16(a, b);
+    const f16x2 hh = __builtin_bit_cast(f16x2, h);
+    o[0][q] = h;
+    o[1][q] = pk_f16(a - (float)hh[0], b - (float)hh[1]);
+  }
+}
+
 // acc += A . B over one 16-k step of v_mfma_f32_32x32x16_bf16 with both operands as three bf16
 // planes (a[0..2] = h, m, l of A's fragment, b[0..2] of B's), the dropped terms smallest first
 __device__ __forceinline__ f32x16 mfma6_32x32x16(const bf16x8 (&a)[3], const bf16x8 (&b)[3],

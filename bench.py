@@ -397,23 +397,36 @@ def large_batch_leg(torch, ops, ev, device, B=65536, reps=5):
     torch.cuda.empty_cache()
     return {"batch": B, "ms_per_batch": round(ms, 3), "boards_per_s": round(B / (ms * 1e-3), 1),
             "gemm": x3_roofline("az_gemm_f32 output_transform.0 at M = %d" % B,
-                                2.0 * B * F * F, gemm_ms * 1e-3)}
+                                2.0 * B * F * F, gemm_ms * 1e-3, products=gemm_products(B))}
 
 
-def x3_roofline(kernel, flop, seconds, traffic=None, traffic_run=None):
-    """Roofline of a gemm_x3 call: it runs every fp32 product as 6 bf16 MFMA products, so the
-    pipe it is bound by is the bf16 one -- achieved = 6 x 2MNK / time against the dense bf16
-    MFMA peak (frac <= 1 by construction).  The fp32-equivalent rate (2MNK / time, whose
-    ceiling on this pipe is x3_peak = bf16 peak / 6) is kept beside it, and so is its ratio to
-    the fp32 MFMA peak (a speed-up over the native fp32 pipe, not a fraction: it exceeds 1 at
-    large M, where the emulation outruns v_mfma_f32_*_f32)."""
+def gemm_products(M, N=F, K=F):
+    """MFMA products per fp32 product of the product dispatch for this GEMM (az_gemm_form with
+    ops.workspace's 256 MB): 3 = fp16 form, 6 = bf16 form, 1 = fp32 MFMA tile."""
+    from azhip import _lib
+    return int(_lib.load().az_gemm_form(M, N, K, 256 << 20))
+
+
+def x3_roofline(kernel, flop, seconds, traffic=None, traffic_run=None, products=6):
+    """Roofline of a split-operand GEMM call: every fp32 product runs as `products` 16-bit MFMA
+    products -- 3 in the fp16 form (two fp16 terms per operand, v_mfma_f32_32x32x16_f16), 6 in the
+    bf16 form (three bf16 terms, v_mfma_f32_32x32x16_bf16) -- so the pipe it is bound by is the
+    dense fp16 / bf16 one (the same 2516.6 TF/s): achieved = products x 2MNK / time against that
+    peak (frac <= 1 by construction).  The fp32-equivalent rate (2MNK / time, whose ceiling on
+    this pipe is peak / products) is kept beside it, and so is its ratio to the fp32 MFMA peak (a
+    speed-up over the native fp32 pipe, not a fraction: it exceeds 1 where the split form
+    outruns v_mfma_f32_*_f32)."""
     fp32_eq = flop / seconds / 1e12
-    return {"kernel": kernel, "bound": "mfma", "pipe": "bf16 (v_mfma_f32_32x32x16_bf16)",
-            "achieved": round(6 * fp32_eq, 2), "peak": BF16_MFMA_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(6 * fp32_eq / BF16_MFMA_PEAK_TFLOPS, 4),
+    pipe = ("fp16 (v_mfma_f32_32x32x16_f16, 3 products per fp32 product)" if products == 3 else
+            "bf16 (v_mfma_f32_32x32x16_bf16, 6 products per fp32 product)")
+    return {"kernel": kernel, "bound": "mfma", "pipe": pipe, "products": products,
+            "achieved": round(products * fp32_eq, 2), "peak": BF16_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(products * fp32_eq / BF16_MFMA_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_run": traffic_run,
-            "avg_launch_us": round(seconds * 1e6, 2), "flop_per_launch_fp32": flop, "bf16_flop_per_launch": 6 * flop,
-            "fp32_equiv_tflops": round(fp32_eq, 2), "x3_peak_fp32_equiv": X3_PEAK_TFLOPS,
+            "avg_launch_us": round(seconds * 1e6, 2), "flop_per_launch_fp32": flop,
+            "mfma_flop_per_launch": products * flop,
+            "fp32_equiv_tflops": round(fp32_eq, 2),
+            "split_peak_fp32_equiv": round(BF16_MFMA_PEAK_TFLOPS / products, 1),
             "speedup_vs_fp32_mfma_peak": round(fp32_eq / FP32_MFMA_PEAK_TFLOPS, 4)}
 
 
@@ -439,7 +452,7 @@ def gemm_shapes_leg(torch, ops, ev, device, Ms=(800, 1576, 3150), reps=50, warm=
         torch.cuda.synchronize()
         us = float(np.mean([e[2 * i].elapsed_time(e[2 * i + 1]) for i in range(reps)])) * 1e3
         r = x3_roofline("az_gemm_f32 output_transform.0 at M = %d" % M, 2.0 * M * F * F,
-                        us * 1e-6)
+                        us * 1e-6, products=gemm_products(M))
         row = {"M": M, "avg_call_us": r["avg_launch_us"], "frac": r["frac"],
                "fp32_equiv_tflops": r["fp32_equiv_tflops"]}
         pm = _pmc_selfplay_gemm(M)
@@ -887,9 +900,12 @@ def main():
                        "global_batch": B * world, "batch_per_gpu": B, "feature_dim": F,
                        "parallelism": f"dp{world} (independent shards, no collective)"},
             "roofline": x3_roofline(
-                "az_gemm_f32 output_transform.0 call (gemm_x3 tile kernel + its split-K reduce), "
-                "Linear 3136x3136 at M = %d: fp32 operands split into 3 bf16 terms, 6 cross "
-                "products on the bf16 MFMA" % B, flop, avg_gemm_s, traffic, pmc_run("gemm")),
+                "az_gemm_f32 output_transform.0 call (row scales + gemm_x3 tile kernel + its "
+                "split-K reduce), Linear 3136x3136 at M = %d: fp32 operands split into 16-bit "
+                "terms (%s), their cross products on the matrix cores"
+                % (B, "2 fp16 terms per row-scaled operand, 3 products"
+                   if gemm_products(B) == 3 else "3 bf16 terms, 6 products"),
+                flop, avg_gemm_s, traffic, pmc_run("gemm"), products=gemm_products(B)),
             "gemm_shapes": shapes,
             "layer_roofline": layer,
             "cnn_b512": cnn,

@@ -95,6 +95,13 @@ typedef struct az_gemm_desc {
 
 int az_gemm_f32(const az_gemm_desc* d, void* stream);
 
+/* MFMA products per fp32 product that az_gemm_f32 runs for a plain K-major M x N x K GEMM with
+ * ws_bytes of workspace: 3 = the fp16 form (each operand row scaled by a power of two and split
+ * into two fp16 terms, three products on v_mfma_f32_32x32x16_f16: M > 64, K >= 1024, N >= 256,
+ * room for A's row scales), 6 = the bf16 form (three bf16 terms, six products), 1 = an fp32
+ * MFMA tile, 0 = the fp32 GEMV (M <= 8).  For rooflines and reports; no GPU work. */
+int az_gemm_form(int M, int N, int K, size_t ws_bytes);
+
 /* ---------------------------------------------------------------------------------
  * Connect4Net trunk, connect4/Connect4Net.py:42-49 (== Connect4GNNWrapper.extract_features,
  * connect4/Connect4GNN.py:31-46 in eval mode): conv1 3x3 p1 + ReLU -> conv2 3x3 p1 + ReLU ->
@@ -352,6 +359,12 @@ int az_mlp2_bwd(const float* x, int M, int F, const float* w0, const float* w2,
  * --------------------------------------------------------------------------------- */
 int az_adam_f32(float* p, const float* g, float* m, float* v, int64_t n,
                 double lr, double beta1, double beta2, double eps, int step, void* stream);
+
+/* Parameters changed: every cached per-row weight scale of the fp16 GEMM form (az_gemm_f32's
+ * large K-major GEMMs, az_gemm.hip row_scale_kernel) is recomputed before its next use.
+ * az_adam_f32 calls it; a caller that writes weights any other way (loading a checkpoint,
+ * copying buffers) must call it before the next GEMM on those weights. */
+int az_weights_changed(void);
 
 #ifdef __cplusplus
 }

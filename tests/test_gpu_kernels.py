@@ -64,20 +64,27 @@ U32 = 2.0 ** -24          # fp32 unit roundoff
 
 
 def x3_bound(K, lam=8.0):
-    """Per-element error bound of an x3 GEMM (az_gemm.hip gemm_x3), as a multiple of
-    sum_k |a_k b_k| (+ |bias|), derived from the algorithm, not from observed errors:
-    * split: a = h + m + l (round-to-nearest-even bf16 terms) leaves |a - (h+m+l)| <= 2^-24 |a|,
-      and the three dropped cross terms m l', l m', l l' are <= 2^-23 (1 + 2^-8)^2 |a||b|: with
-      the representation error of both operands, <= 2^-22 |a||b| per product, rigorously;
-    * the six kept bf16 x bf16 products are exact in fp32 (8 + 8 significand bits);
-    * accumulation: one output element is a chain of 6 * ceil(K / 16) MFMA accumulations (one
-      fp32 rounding each; S <= 8 chains for split-K, whose reduce adds <= 8 + 2 more; 16 more
+    """Per-element error bound of the large K-major GEMMs (az_gemm.hip gemm_x3 in either form),
+    as a multiple of sum_k |a_k b_k| (+ |bias|), derived from the algorithm, not from observed
+    errors:
+    * bf16 form (x3, tuning build AZ_GEMM_PREC=x3): a = h + m + l (round-to-nearest-even bf16
+      terms) leaves |a - (h+m+l)| <= 2^-24 |a|, and the three dropped cross terms m l', l m', l l'
+      are <= 2^-23 (1 + 2^-8)^2 |a||b|: <= 2^-22 |a||b| per product, rigorously;
+    * fp16 form (h3, the product): each row is scaled by a power of two s so its largest |a s|
+      lies in [2^13, 2^14) (W's rows in [2^9, 2^10)), a s = h + l + r with |r| <= 2^-22 |a s|
+      while l is a normal fp16 (|a s| >= 2^-2) and |r| <= 2^-25 otherwise (<= 2^-38 of the row's
+      largest |a s|); with the dropped l l' <= 2^-22 |a s||b s'|, <= 3 * 2^-22 |a||b| per product
+      plus that floor (az_x3.h split2s);
+    * the kept bf16 x bf16 / fp16 x fp16 products are exact in fp32 (8 + 8 / 11 + 11 bits);
+    * accumulation: one output element is a chain of (6 or 3) * ceil(K / 16) MFMA accumulations
+      (one fp32 rounding each; S <= 8 chains for split-K, whose reduce adds <= 8 + 2 more; 16 more
       for a rounding inside each MFMA).  For n roundings the probabilistic bound of Higham and
       Mary (SIAM J. Sci. Comput. 41(5), 2019) is |err| <= lam sqrt(n) u sum|terms|, failing with
       probability <= 2 n exp(-lam^2 / 2) per element (lam = 8: < 1e-10 for n < 1e4).
-    The chain is taken at S = 1 (longest, so the largest sqrt(n))."""
+    The chain is taken at its longest (x3, S = 1: the largest sqrt(n)) and the representation
+    term at the larger (h3's 3 * 2^-22), so one bound covers both forms."""
     n = 6 * ((K + 15) // 16) + 16 + 8 + 2
-    return 2.0 ** -22 + lam * np.sqrt(n) * U32
+    return 3 * 2.0 ** -22 + lam * np.sqrt(n) * U32
 
 
 def _x3_check(ops, x, w, b, rows=None, report=None):
@@ -199,8 +206,8 @@ def test_x3_gemm_keeps_all_six_products(ops):
     """A discriminating case for the split itself: every operand is 1 + 2^-9 + d with
     d in [1.5, 2) * 2^-18 (exact in fp32), so its bf16 terms are h = 1, m = 2^-9, l = d > 0: the
     l cross terms are positive and add up over K instead of averaging out.  A scheme without
-    them (four products) misses x3_bound(1024) on EVERY element (checked in float64 here);
-    the six-product x3 GEMM must stay inside it."""
+    them (four bf16 products) misses x3_bound(1024) on EVERY element (checked in float64 here);
+    the GEMM (the fp16 form: 11 + 11 bits per operand) must stay inside it."""
     M, N, K = 256, 512, 1024
     g = torch.Generator().manual_seed(6)
 
@@ -220,6 +227,71 @@ def test_x3_gemm_keeps_all_six_products(ops):
     ref = x.double() @ w.double().T
     e4 = ((four - ref).abs() / (x.double().abs() @ w.double().abs().T)).numpy()
     assert e4.min() > x3_bound(K) > rep["x3_max"], (float(e4.min()), rep)
+
+
+def test_h3_gemm_keeps_the_cross_products(ops):
+    """The fp16 form's split: every operand is (1 + 2^-12 (1 + j / 32)) * 2^e with j in [16, 32)
+    (exact in fp32), so after the row scaling its fp16 terms are h = 2^e' and l = the 2^-12 part:
+    the h*l cross products are positive and add up over K.  Without them (h*h only) every element
+    misses x3_bound(1024) (checked in float64); the GEMM must stay inside it."""
+    M, N, K = 256, 512, 1024
+    g = torch.Generator().manual_seed(7)
+
+    def operand(r, c):
+        j = torch.randint(16, 32, (r, c), generator=g).double()
+        return (1 + 2.0 ** -12 * (1 + j / 32)).float()
+
+    x = operand(M, K)
+    w = operand(N, K) / K
+    b = torch.zeros((N,))
+    rep = _x3_check(ops, x, w, b, report={"operands": "1 + 2^-12 d: positive fp16 l terms"})
+    hh = x.half().double() @ (w * 1024).half().double().T / 1024    # h*h only (W row scale 2^10)
+    ref = x.double() @ w.double().T
+    e1 = ((hh - ref).abs() / (x.double().abs() @ w.double().abs().T)).numpy()
+    assert e1.min() > x3_bound(K) > rep["x3_max"], (float(e1.min()), rep)
+
+
+def test_h3_gemm_wide_dynamic_range(ops):
+    """Rows whose values span 2^-30 .. 2^30 (and all-zero / single-value rows): the per-row
+    power-of-two scaling keeps every row inside the bound; the fp16 range alone would overflow
+    the large values and flush the small ones."""
+    M, N, K = 300, 512, 1536
+    g = torch.Generator().manual_seed(8)
+    mag = 2.0 ** (torch.randint(-30, 31, (M, 1), generator=g).double()
+                  + torch.randn((M, K), generator=g).double() * 3)
+    x = (mag * torch.sign(torch.randn((M, K), generator=g).double())).float()
+    x[0] = 0.0
+    x[1] = 0.0
+    x[1, 7] = 3.0e-30
+    w = (torch.rand((N, K), generator=g) * 2 - 1) * 2.0 ** 20
+    b = torch.zeros((N,))
+    _x3_check(ops, x, w, b, report={"operands": "rows spanning 2^-30 .. 2^30, W ~ 2^20"})
+
+
+def test_h3_weight_scales_follow_weight_updates(ops):
+    """The fp16 form caches each weight matrix's row scales between weight updates
+    (az_weights_changed; az_adam_f32 and the parameter store call it).  Growing W 4096x in place
+    -- far past the scales' 64x headroom -- and announcing it gives the right result again; the
+    same GEMM before the update is right too."""
+    from azhip import params as P
+    M, N, K = 512, 3136, 3136
+    g = torch.Generator().manual_seed(9)
+    x = torch.rand((M, K), generator=g) * 2 - 1
+    w = ((torch.rand((N, K), generator=g) * 2 - 1) / K ** 0.5)
+    b = torch.rand((N,), generator=g) - 0.5
+    wd = w.cuda()
+    _x3_check_dev(ops, x, wd, w, b)
+    wd.mul_(4096.0)
+    P.weights_changed()
+    _x3_check_dev(ops, x, wd, w * 4096.0, b)
+
+
+def _x3_check_dev(ops, x, wd, w, b):
+    y = ops.linear(x.cuda(), wd, b.cuda(), act=0).cpu().double()
+    ref = x.double() @ w.double().T + b.double()
+    bound = (x.double().abs() @ w.double().abs().T + b.double().abs()).numpy()
+    e = (y - ref).abs().numpy() / bound
+    assert np.isfinite(y.numpy()).all() and e.max() <= x3_bound(x.shape[1]), float(e.max())
 
 
 @pytest.mark.parametrize("K", [3136, 2500, 100])
