@@ -69,7 +69,7 @@ def parse():
 
 
 CALIBRATION = "profiles/r02_cpu_calibration.json"   # tools/cpu_calibration.py, build container
-CPU_THREADS = 8        # the thread count of the reference measurements
+CPU_CHILD = "--cpu-baselines-child"
 
 
 def _calibration():
@@ -79,38 +79,91 @@ def _calibration():
         return {}
 
 
-def cpu_baseline(W, G, seconds, B):
-    """The reference CPU path's workload on this host: the per-board GNN forward of B-board
-    batches (extract_features -> output_transform -> heads, Connect4GNN.py:31-57 +
-    gnn_utils.py:115) as oracle/torch_ref.py's restatement -- the same torch CPU ops as the
-    reference, fp32, eval, no_grad, CPU_THREADS torch threads -- repeated for ~`seconds`.
-    profiles/r02_cpu_calibration.json records its time against the imported reference's on
-    identical inputs and threads in the build container (ratio within a few %)."""
+def cpu_baseline(W, G, seconds, B, threads, gnn=True):
+    """The reference CPU path's workload on this host: the per-board forward of B-board batches
+    -- GNN: extract_features -> output_transform -> heads (Connect4GNN.py:31-57 +
+    gnn_utils.py:115); CNN: Connect4Net.forward (Connect4Net.py:30-60) -- as oracle/torch_ref.py's
+    restatement (the same torch CPU ops as the reference, fp32, eval, no_grad) on `threads`
+    torch threads, repeated for ~`seconds`.  profiles/r02_cpu_calibration.json records its time
+    against the imported reference's on identical inputs and threads in the build container
+    (ratio within a few %)."""
     import torch
     from oracle import torch_ref as TR
-    torch.set_num_threads(CPU_THREADS)
+    torch.set_num_threads(threads)
     rng = np.random.default_rng(1)
     boards = torch.from_numpy(rng.integers(-1, 2, size=(B, 7, 7)).astype(np.float32))
     Wt = TR.params(W, torch.float32, requires_grad=False)
     Gt = TR.params({k: v for k, v in G.items() if k.startswith("output_transform")},
-                   torch.float32, requires_grad=False)
+                   torch.float32, requires_grad=False) if gnn else None
 
     def run():
         with torch.no_grad():
-            return TR.c4_heads(TR.output_transform(TR.c4_features(boards, Wt), Gt), Wt)
+            f = TR.c4_features(boards, Wt)
+            return TR.c4_heads(TR.output_transform(f, Gt) if gnn else f, Wt)
     run()
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         run()
         n += 1
     dt = time.perf_counter() - t0
-    cal = _calibration().get("gnn_b512", {})
-    return {"value": n * B / dt, "unit": "board evals/s", "cores": CPU_THREADS, "kind": "port",
+    cal = _calibration().get("gnn_b512" if gnn else "cnn_b512", {})
+    what = "c4_features -> output_transform -> heads" if gnn else "c4_features -> heads (CNN)"
+    return {"value": n * B / dt, "unit": "board evals/s", "cores": threads, "kind": "port",
             "sample": f"{n} batches x {B} random boards, {dt:.1f} s: oracle/torch_ref.py "
-                      f"(the reference's torch CPU ops: c4_features -> output_transform -> heads), "
-                      f"fp32, {CPU_THREADS} threads; calibration {CALIBRATION}: port / reference "
-                      f"time = {cal.get('ratio_port_torch_over_reference')} on the build "
-                      f"container"}
+                      f"(the reference's torch CPU ops: {what}), fp32, {threads} threads; "
+                      f"calibration {CALIBRATION}: port / reference time = "
+                      f"{cal.get('ratio_port_torch_over_reference')} on the build container"}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baselines_child(spec):
+    """The CPU baselines, in a fresh process (bench.py --cpu-baselines-child SPEC): started with
+    the rank's full visible core set (the mask before pin_rank_to_gpu_numa narrowed it), no GPU
+    context, no engine threads, torch on every visible core.  Prints one
+    JSON object: gnn / cnn board baselines, the self-play loop's moves, the config-5 oracle."""
+    import hostcpu
+    try:
+        os.sched_setaffinity(0, spec["cpus"])
+    except (AttributeError, OSError):
+        pass
+    threads = hostcpu.host_cpus()
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    from azhip.weights import connect4_net_spec, gnn_spec, synthetic_state_dict
+    W = synthetic_state_dict(connect4_net_spec(7), 1)
+    G = synthetic_state_dict(gnn_spec(F, 2), 2)
+    sec, B = spec["seconds"], spec["B"]
+    out = {"host": {"cores": threads, "affinity_cpus": len(hostcpu.affinity()),
+                    "cgroup_quota": hostcpu.cgroup_cpu_quota(), "cpu_model": _cpu_model(),
+                    "process": "fresh child of the bench rank, full visible mask, no GPU"}}
+    out["gnn_b512"] = cpu_baseline(W, G, sec, B, threads)
+    out["cnn_b512"] = cpu_baseline(W, G, min(sec, 5.0), B, threads, gnn=False)
+    if spec.get("selfplay"):
+        out["selfplay"] = selfplay_cpu_baseline(W, G, spec["sims"], sec, threads)
+    if spec.get("grid_seconds"):
+        out["grid"] = grid_cpu_baseline(spec["grid_seconds"], threads)
+    print(json.dumps(out), flush=True)
+
+
+def run_cpu_baselines(cpus, seconds, B, sims, selfplay, grid_seconds):
+    """Runs cpu_baselines_child in a child process (see there) and returns its results."""
+    import subprocess
+    spec = {"cpus": list(cpus), "seconds": seconds, "B": B, "sims": sims, "selfplay": selfplay,
+            "grid_seconds": grid_seconds}
+    env = dict(os.environ, OMP_NUM_THREADS=str(len(cpus)))
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), CPU_CHILD, json.dumps(spec)],
+                       env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError("CPU baseline child failed:\n" + r.stderr[-2000:])
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def cnn_b512_leg(torch, ev, device, B=512, reps=50):
@@ -127,12 +180,11 @@ def cnn_b512_leg(torch, ev, device, B=512, reps=50):
     e[1].record()
     torch.cuda.synchronize()
     ms = e[0].elapsed_time(e[1]) / reps
-    cal = _calibration().get("cnn_b512", {})
     return {"batch": B, "ms_per_batch": round(ms, 4), "boards_per_s": round(B / (ms * 1e-3), 1),
             "flop_per_board": 1891008,
             "tflops": round(1891008 * B / (ms * 1e-3) / 1e12, 2),
-            "reference_cpu_boards_per_s": cal.get("reference_boards_per_s"),
-            "note": "trunk (c4_trunk_kernel) + heads; reference figure from " + CALIBRATION}
+            "note": "trunk (c4_trunk_kernel) + heads; cpu_baseline: the torch restatement "
+                    "timed on this host (bench.py cpu_baselines_child)"}
 
 
 def as_called_b1_leg(W, G, leaves=2000):
@@ -308,7 +360,7 @@ def layer_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True)
     return out
 
 
-def grid_forward_leg(torch, ops, device, graphs=512, cpu_seconds=0.0):
+def grid_forward_leg(torch, ops, device, graphs=512):
     """Config 5 end to end: PolicyValueGNN(64, 2 layers) forward over `graphs`
     32x32 grids (the per-destination generalisation of gnn_utils.py:34-117: factored attention
     GEMM, per-edge scores, CSR aggregate, gate/update GEMMs with the gated residual, then
@@ -345,27 +397,30 @@ def grid_forward_leg(torch, ops, device, graphs=512, cpu_seconds=0.0):
            "ms_per_forward": round(ms, 3), "node_updates_per_s": round(2 * g.V / (ms * 1e-3), 1),
            "unit": "node-updates/s", "gflop_per_forward": round(flop / 1e9, 2),
            "tflops": round(flop / (ms * 1e-3) / 1e12, 2), "max_abs_err_vs_oracle_grid0": err}
-    if cpu_seconds > 0:
-        n_g = 8
-        xs = x[:1024 * n_g].cpu().numpy()
-        cg = _grid_graph(ops, "cpu", n_g, build=False)
-        G32 = {k: np.asarray(v, np.float32) for k, v in Gw.items()}
-        O.policy_value_gnn_csr(xs, cg[0], cg[1], G32, dtype=np.float32)
-        n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < cpu_seconds:
-            O.policy_value_gnn_csr(xs, cg[0], cg[1], G32, dtype=np.float32)
-            n += 1
-        dt = time.perf_counter() - t0
-        try:
-            from threadpoolctl import threadpool_info
-            threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-        except Exception:  # pragma: no cover
-            threads = os.cpu_count()
-        out["cpu_baseline"] = {"value": round(n * 2 * 1024 * n_g / dt, 1),
-                               "unit": "node-updates/s", "cores": int(threads), "kind": "port",
-                               "sample": f"{n} forwards of {n_g} grids (numpy fp32 oracle, "
-                                         f"vectorised CSR restatement), {dt:.1f} s"}
     return out
+
+
+def grid_cpu_baseline(seconds, threads):
+    """Config 5's CPU baseline: the numpy oracle's vectorised CSR restatement of
+    PolicyValueGNN(64, 2 layers) over 8 32x32 grids (oracle/nets.py), fp32, for ~`seconds`."""
+    from azhip.weights import gnn_spec, synthetic_state_dict
+    from oracle import nets as O
+    Gw = synthetic_state_dict(gnn_spec(64, 2), 3)
+    n_g = 8
+    rng = np.random.default_rng(0)
+    xs = (rng.random((1024 * n_g, 64), dtype=np.float32) * 2 - 1)
+    cg = _grid_graph(None, "cpu", n_g, build=False)
+    G32 = {k: np.asarray(v, np.float32) for k, v in Gw.items()}
+    O.policy_value_gnn_csr(xs, cg[0], cg[1], G32, dtype=np.float32)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        O.policy_value_gnn_csr(xs, cg[0], cg[1], G32, dtype=np.float32)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * 2 * 1024 * n_g / dt, 1), "unit": "node-updates/s",
+            "cores": threads, "kind": "port",
+            "sample": f"{n} forwards of {n_g} grids (numpy fp32 oracle, vectorised CSR "
+                      f"restatement), {dt:.1f} s, BLAS on {threads} threads"}
 
 
 def large_batch_leg(torch, ops, ev, device, B=65536, reps=5):
@@ -635,11 +690,11 @@ def train_leg(W, G, device):
                               "frac": round(gbs / HBM_PEAK_GBS, 4)}}
 
 
-def selfplay_cpu_baseline(W, G, sims, seconds):
+def selfplay_cpu_baseline(W, G, sims, seconds, threads):
     """The reference's sequential loop on the host: Coach.executeEpisode over this repo's Python
     MCTS (bit-exact with the reference's, tests/test_mcts_golden.py) with oracle/torch_ref.py as
     the network behind the reference's batch-1 predict plumbing (Connect4GNN.py:59-120), torch
-    on CPU_THREADS threads (the reference measurement's count): moves finished in `seconds`.
+    on `threads` threads: moves finished in `seconds`.
     tools/cpu_calibration.py measured this loop against the imported reference's loop on the
     same episode (profiles/r02_cpu_calibration.json: selfplay)."""
     import torch
@@ -647,7 +702,7 @@ def selfplay_cpu_baseline(W, G, sims, seconds):
     import MCTS as M
     from connect4.Connect4Game import Connect4Game
     from oracle import torch_ref as TR
-    torch.set_num_threads(CPU_THREADS)
+    torch.set_num_threads(threads)
     Wt = TR.params(W, torch.float32, requires_grad=False)
     Gt = TR.params({k: v for k, v in G.items() if k.startswith("output_transform")},
                    torch.float32, requires_grad=False)
@@ -721,8 +776,10 @@ def _leaf_timeouts():
 
 def main():
     args = parse()
-    # before any GPU call: this rank on its GPU's NUMA node (best effort; hostcpu.py)
+    # before any GPU call: this rank on its GPU's NUMA node (best effort; hostcpu.py); the mask
+    # before the pin is what the CPU baselines' child process gets back
     import hostcpu
+    visible_cpus = hostcpu.affinity()
     pin = hostcpu.pin_rank_to_gpu_numa(int(os.environ.get("LOCAL_RANK", "0")))
     if not args.sp_threads:
         args.sp_threads = hostcpu.threads_per_rank()
@@ -810,9 +867,7 @@ def main():
 
     grid = None
     if not args.no_grid:
-        grid = grid_forward_leg(torch, ops, device,
-                                cpu_seconds=(5.0 if (rank == 0 and world == 1 and not args.no_cpu)
-                                             else 0.0))
+        grid = grid_forward_leg(torch, ops, device)
         if world > 1:
             t = torch.tensor([grid["ms_per_forward"]], device=red_dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -867,23 +922,32 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(W, G, args.cpu_seconds, B)
+        # the reference CPU path's workloads on this host's visible cores, in a fresh
+        # process (no GPU context, no engine threads, the mask before the NUMA pin)
+        cb = run_cpu_baselines(visible_cpus, args.cpu_seconds, B, args.sp_sims,
+                               sp is not None, 5.0 if grid is not None else 0.0)
+        host = cb["host"]
+        cpu = dict(cb["gnn_b512"], host=host)
+        cnn["cpu_baseline"] = cb["cnn_b512"]
+        if grid is not None:
+            grid["cpu_baseline"] = cb["grid"]
         if sp is not None:
-            b = selfplay_cpu_baseline(W, G, args.sp_sims, args.cpu_seconds)
+            b = cb["selfplay"]
             mean_moves = sp["moves"] / max(1, sp["games"])
             games = b["moves"] / mean_moves
             ratio = _calibration().get("selfplay", {}).get("ratio_port_over_reference_time")
             rate = games / b["seconds"]
             sp["cpu_baseline"] = {
-                "value": round(rate, 4), "unit": "games/s", "cores": CPU_THREADS, "kind": "port",
+                "value": round(rate, 4), "unit": "games/s", "cores": host["cores"], "kind": "port",
                 "reference_equivalent": round(rate * ratio, 4) if ratio else None,
                 "sample": f"reference sequential loop (this repo's bit-exact Python MCTS, batch-1 "
                           f"predict + predict_with_gnn through oracle/torch_ref.py with the "
-                          f"reference's predict plumbing, {CPU_THREADS} torch threads): "
-                          f"{b['moves']} moves in {b['seconds']} s = {games:.2f} games at the "
-                          f"GPU leg's mean {mean_moves:.1f} moves/game; {CALIBRATION}: this loop "
-                          f"takes {ratio} of the imported reference loop's time on the same "
-                          f"episode -> reference_equivalent"}
+                          f"reference's predict plumbing, {host['cores']} torch threads, fresh "
+                          f"process): {b['moves']} moves in {b['seconds']} s = {games:.2f} games "
+                          f"at the GPU leg's mean {mean_moves:.1f} moves/game; {CALIBRATION}: "
+                          f"this loop takes {ratio} of the imported reference loop's time on the "
+                          f"same episode (8 threads, build container) -> reference_equivalent",
+                "host": host}
 
     if rank == 0:
         value = world * B * args.steps / elapsed
@@ -926,4 +990,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[1] == CPU_CHILD:
+        cpu_baselines_child(json.loads(sys.argv[2]))
+    else:
+        main()

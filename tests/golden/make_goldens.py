@@ -23,6 +23,8 @@ Fixtures:
      mcts_ttt3.npz/json  TicTacToe 3x3 GNN self-play episodes with expand_tree
      mcts_c4_gnn.npz/json  Connect4 GNN self-play at the north-star setting (sims 100, use_gnn,
                          expand_tree; G1 CNN weights + G2 GNN weights), episodes 0-2
+     mcts_c4_gnn_trace.npz G6c: the same setting, episodes 0-15: every UCB selection of the
+                         reference's search (state crc32, action, score gap, Ns) + the examples
   G7 coach_ttt3.json     one full TicTacToe 3x3 GNN Coach iteration (seeds 0): counts, arena W/L/D
   G8 rules.npz           game rules on random-play positions (Connect4 n=7,5; TicTacToe n=3,4):
                          getGameEnded for both players, getValidMoves, every legal next state,
@@ -462,6 +464,86 @@ def g6b():
     print(f"  G6b episodes {time.time() - t0:.1f}s")
 
 
+def g6c(episodes=range(16)):
+    """G6c mcts_c4_gnn_trace.npz: the reference's own search trace at the G6b setting (same
+    network, seed = e) for episodes 0-15, for the lock-step parity test at production batch
+    sizes (tests/test_gpu_selfplay.py): every UCB selection the reference's MCTS.search makes --
+    crc32 of the state bytes, the chosen action, the best-minus-second score gap and Ns[s] -- and
+    the episode's std / GNN examples.  The selection is inline in MCTS.search (MCTS.py:202-218),
+    so it is read from inside the reference's own frame when search calls game.getNextState
+    right after choosing (MCTS.py:223): the scores are recomputed there from the same Qsa / Ps /
+    Ns / Nsa with the same float expressions."""
+    import math
+    import zlib
+    z = np.load(out("c4_net.npz"))
+    c4sd = {k[2:]: z[k] for k in z.files if k.startswith("w/")}
+    game = Connect4Game(7)
+    torch.manual_seed(0)
+    g = Connect4GNNWrapper(game, base_args(use_gnn=True))
+    g.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in c4sd.items()})
+    gsd = W.synthetic_state_dict(W.gnn_spec(3136, 2), GNN_C4_SEED)
+    g.gnn.load_state_dict({k: torch.from_numpy(v) for k, v in gsd.items()})
+    del gsd
+    args = base_args(numMCTSSims=100, use_gnn=True)
+    A = game.getActionSize()
+    sel = []
+    orig_next = game.getNextState
+
+    def rec_next(board, player, action):
+        f = sys._getframe(1)
+        if f.f_code.co_name == "search" and f.f_code.co_filename == ref_mcts.__file__:
+            mc, st = f.f_locals["self"], f.f_locals["s"]
+            us = []
+            for b in range(A):
+                if not mc.Vs[st][b]:
+                    continue
+                if (st, b) in mc.Qsa:
+                    u = mc.Qsa[(st, b)] + mc.args.cpuct * mc.Ps[st][b] * math.sqrt(mc.Ns[st]) / (
+                        1 + mc.Nsa[(st, b)])
+                else:
+                    u = mc.args.cpuct * mc.Ps[st][b] * math.sqrt(mc.Ns[st] + ref_mcts.EPS)
+                us.append(float(u))
+            us.sort(reverse=True)
+            sel.append((zlib.crc32(st), int(action), us[0] - us[1] if len(us) > 1 else math.inf,
+                        int(mc.Ns[st])))
+        return orig_next(board, player, action)
+
+    game.getNextState = rec_next
+    coach = ref_coach.Coach.__new__(ref_coach.Coach)
+    coach.game, coach.args, coach.nnet = game, args, g
+    off, std, gnn, soff, goff = [0], [], [], [0], [0]
+    t0 = time.time()
+    for e in episodes:
+        np.random.seed(e)
+        coach.mcts = ref_mcts.MCTS(game, g, args)
+        s_ex, g_ex = coach.executeEpisode()
+        std += [(np.asarray(b).astype(np.int8), np.asarray(p, np.float64), float(r))
+                for b, p, r in s_ex]
+        gnn += [(np.asarray(x[0]).astype(np.int8), int(x[1]), np.asarray(x[2], np.float64),
+                 np.float32(x[3]), np.asarray(x[4], np.float64), float(x[5]), float(x[6]))
+                for x in g_ex]
+        off.append(len(sel))
+        soff.append(len(std))
+        goff.append(len(gnn))
+        print(f"  G6c episode {e}: {len(s_ex) // 2} moves, {off[-1] - off[-2]} selections, "
+              f"{time.time() - t0:.1f}s", flush=True)
+    game.getNextState = orig_next
+    np.savez_compressed(
+        out("mcts_c4_gnn_trace.npz"), episodes=np.array(list(episodes)),
+        args=json.dumps(dict(args)),
+        sel_off=np.array(off, np.int64), sel_state_crc32=np.array([x[0] for x in sel], np.uint32),
+        sel_action=np.array([x[1] for x in sel], np.int8),
+        sel_gap=np.array([x[2] for x in sel], np.float64),
+        sel_ns=np.array([x[3] for x in sel], np.int32),
+        std_off=np.array(soff, np.int64), std_board=np.stack([x[0] for x in std]),
+        std_pi=np.stack([x[1] for x in std]), std_z=np.array([x[2] for x in std]),
+        gnn_off=np.array(goff, np.int64), gnn_board=np.stack([x[0] for x in gnn]),
+        gnn_player=np.array([x[1] for x in gnn], np.int8),
+        gnn_init_pi=np.stack([x[2] for x in gnn]), gnn_init_v=np.array([x[3] for x in gnn]),
+        gnn_exp_pi=np.stack([x[4] for x in gnn]), gnn_exp_v=np.array([x[5] for x in gnn]),
+        gnn_reward=np.array([x[6] for x in gnn]))
+
+
 # ----------------------------------------------------------------------------------- G7
 def g7():
     """main.py:158-285 wiring for: --game tictactoe --board_size 3 --use_gnn --numIters 1."""
@@ -642,6 +724,10 @@ def main():
     if want == {"g6b"}:
         g6b()
         print(f"G6b done {time.time() - t0:.1f}s")
+        return
+    if want == {"g6c"}:
+        g6c()
+        print(f"G6c done {time.time() - t0:.1f}s")
         return
     if want == {"g9"}:
         g9()

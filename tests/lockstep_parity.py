@@ -23,6 +23,7 @@ This module proves that for every compared episode:
    margin).  A divergence with a larger gap is a search bug, not rounding.
 """
 import math
+import zlib
 from collections import defaultdict
 
 import numpy as np
@@ -183,6 +184,28 @@ def _gnn_close(x, y, tol):
     return True
 
 
+def _state_key(s):
+    """A selection's state as the reference trace stores it (tests/golden/make_goldens.py g6c:
+    crc32 of the state bytes), so live runs (bytes) compare with the recorded trace (ints)."""
+    return zlib.crc32(s) if isinstance(s, (bytes, bytearray)) else int(s)
+
+
+def reference_trace(z, e):
+    """Episode e of the reference's recorded search (G6c, mcts_c4_gnn_trace.npz) in the form
+    `sequential` returns: selects (state crc32, action, gap, Ns), std and GNN examples."""
+    i = int(np.flatnonzero(z["episodes"] == e)[0])
+    a, b = int(z["sel_off"][i]), int(z["sel_off"][i + 1])
+    selects = list(zip(z["sel_state_crc32"][a:b].tolist(), z["sel_action"][a:b].tolist(),
+                       z["sel_gap"][a:b].tolist(), z["sel_ns"][a:b].tolist()))
+    a, b = int(z["std_off"][i]), int(z["std_off"][i + 1])
+    std = [(z["std_board"][j], z["std_pi"][j], float(z["std_z"][j])) for j in range(a, b)]
+    a, b = int(z["gnn_off"][i]), int(z["gnn_off"][i + 1])
+    gnn = [(z["gnn_board"][j], int(z["gnn_player"][j]), z["gnn_init_pi"][j],
+            np.float32(z["gnn_init_v"][j]), z["gnn_exp_pi"][j], float(z["gnn_exp_v"][j]),
+            float(z["gnn_reward"][j])) for j in range(a, b)]
+    return dict(selects=selects, std=std, gnn=gnn)
+
+
 def first_divergence(seq, rep, tol, cpuct):
     """Compare two recorded runs of one episode.  Returns None when they agree (identical UCB
     selections, identical std examples, GNN examples equal up to `tol` in their network-valued
@@ -191,7 +214,7 @@ def first_divergence(seq, rep, tol, cpuct):
     same_std = norm_std(seq["std"]) == norm_std(rep["std"])
     same_gnn = _gnn_close(norm_gnn(seq["gnn"]), norm_gnn(rep["gnn"]), tol)
     k = next((j for j, (x, y) in enumerate(zip(seq["selects"], rep["selects"]))
-              if x[:2] != y[:2]), None)
+              if (_state_key(x[0]), x[1]) != (_state_key(y[0]), y[1])), None)
     # examples carry the game's final reward: compare (board, pi) to find the first move apart
     a = [x[:2] for x in norm_std(seq["std"])]
     b = [x[:2] for x in norm_std(rep["std"])]

@@ -219,24 +219,29 @@ def test_engine_one_slot_equals_sequential_hip(c4, meta):
         assert _norm_gnn(out[e][1]) == _norm_gnn(hip["gnn"]), e
 
 
-N_COMPARED = 16      # the three G6b episodes + 13 more, same weights and seeds (seed = e)
+N_COMPARED = 16      # G6c: the reference's own trace of episodes 0-15, same weights, seed = e
 
 
 @pytest.mark.parametrize("G", [16, 256, 4096])
 def test_lockstep_engine_parity_at_production_batches(c4, meta, G):
     """Lock-step engine self-play at G slots (2 lanes: leaf batches of ~G/2 .. G rows, the
-    bench plays 4096) against the sequential reference loop with the same HIP network, for 16
-    episodes, move by move (tests/lockstep_parity.py):
+    bench plays 4096) against the REFERENCE's own search trace of episodes 0-15 (G6c: the
+    reference's MCTS.search / Coach.executeEpisode with its CPU torch network, same weights,
+    seed = e; every UCB selection recorded), move by move (tests/lockstep_parity.py):
     * every compared episode's engine rows, replayed through Coach.executeEpisode, reproduce
       the engine's examples exactly (the engine's search == the reference search);
     * the rows are within 1e-5 of the batch-1 network on the same boards;
-    * an episode may leave the sequential one only at a UCB near tie the 1e-5 network
-      tolerance can flip (first differing selection, gap <= near_tie_bound) -- a larger gap
-      fails the test.  Agreement per episode is reported."""
+    * an episode may leave the reference's trace only at a UCB near tie the 1e-5 network
+      tolerance can flip (first differing selection, the reference's own gap there <=
+      near_tie_bound) -- a larger gap fails the test.  The same check against this repo's
+      sequential loop with the batch-1 HIP network is kept beside it.  Agreement per episode
+      with both is reported."""
     import lockstep_parity as LP
     from connect4.Connect4Game import Connect4Game
     game = Connect4Game(7)
     args = Args(meta["args"])
+    trace = golden("mcts_c4_gnn_trace.npz")
+    assert sorted(trace["episodes"].tolist()) == list(range(N_COMPARED))
     n = max(G, N_COMPARED)
     eps = list(range(n))
     st = {}
@@ -251,13 +256,15 @@ def test_lockstep_engine_parity_at_production_batches(c4, meta, G):
             d = max(float(np.abs(r[1] - o[0][0]).max()), abs(float(r[2]) - float(o[1][0])),
                     float(np.abs(r[3] - o[2][0]).max()), abs(float(r[4]) - float(o[3][0])))
             worst = max(worst, d)
-        seq = _hip_sequential(c4, meta, e)
-        rep = LP.compare_episode(game, args, e, seq, rs, out[e], TOL)
-        rep["rows"] = len(rs)
-        report.append(rep)
+        ref = LP.compare_episode(game, args, e, LP.reference_trace(trace, e), rs, out[e], TOL)
+        hip = LP.compare_episode(game, args, e, _hip_sequential(c4, meta, e), rs, out[e], TOL)
+        ref["rows"] = len(rs)
+        ref["vs_hip_sequential"] = {k: hip[k] for k in ("agreeing_moves", "divergence")}
+        report.append(ref)
     moves = sum(r["moves"] for r in report)
     agree = sum(r["agreeing_moves"] for r in report)
     summary = {"G": G, "episodes_played": n, "compared": N_COMPARED,
+               "against": "reference trace (G6c, mcts_c4_gnn_trace.npz)",
                "batch_rows": {"max": max(st["batch_rows"]),
                               "mean": float(np.mean(st["batch_rows"]))},
                "max_row_diff_vs_batch1": worst, "move_agreement": agree / moves,
@@ -268,6 +275,8 @@ def test_lockstep_engine_parity_at_production_batches(c4, meta, G):
     for r in report:
         assert r["replay_equals_engine"], r
         d = r["divergence"]
+        assert d is None or d["near_tie"], r
+        d = r["vs_hip_sequential"]["divergence"]
         assert d is None or d["near_tie"], r
     if G >= 256:
         assert max(st["batch_rows"]) > 64       # really ran the large-batch (x3 GEMM) path

@@ -85,3 +85,38 @@ def test_large_batch_noise_is_caught():
     assert all(r["replay_equals_engine"] for r in reps)
     divs = [r["divergence"] for r in reps if r["divergence"] is not None]
     assert divs and any(not d["near_tie"] for d in divs), reps
+
+
+def test_reference_trace_pinned_by_recorded_outputs():
+    """G6c (mcts_c4_gnn_trace.npz, the reference's selection trace of episodes 0-15) against G6b
+    (mcts_c4_gnn.npz: every network output the reference's episodes 0-2 requested): this repo's
+    reference-shaped loop, fed G6b's recorded outputs, makes the same UCB selections -- state,
+    action, Ns, and the score gap to 1e-6 -- as G6c recorded inside the reference's search, and
+    the same examples, so the trace the GPU lock-step test compares against is the reference's
+    search."""
+    import json
+    import os
+    import lockstep_parity as LP
+    from connect4.Connect4Game import Connect4Game
+    from conftest import GOLDEN, golden
+    from test_mcts_golden import Args, RecordedNet
+    meta = json.load(open(os.path.join(GOLDEN, "mcts_c4_gnn.json")))
+    trace = golden("mcts_c4_gnn_trace.npz")
+    assert json.loads(str(trace["args"])) == meta["args"]
+    net = RecordedNet(golden("mcts_c4_gnn.npz"), 7)
+    game = Connect4Game(7)
+    for ep in meta["episodes"]:
+        e = ep["episode"]
+        got = LP.sequential(game, net, Args(meta["args"]), e)
+        ref = LP.reference_trace(trace, e)
+        assert len(got["selects"]) == len(ref["selects"]), e
+        for x, y in zip(got["selects"], ref["selects"]):
+            assert (LP._state_key(x[0]), x[1], x[3]) == (y[0], y[1], y[3]), e
+            # G6b stores the outputs as float32 (the GNN prior loses a few ulps of the
+            # reference's value): the gaps agree to ~1e-8, far inside any near-tie bound
+            assert x[2] == y[2] or abs(x[2] - y[2]) <= 1e-6, e
+        assert LP.norm_std(got["std"]) == LP.norm_std(ref["std"]), e
+        # init_v / exp_v / init_pi are network values and Q averages: G6b's float32 outputs
+        # move them by ulps; board, player, visit-count targets and reward are exact
+        assert LP._gnn_close(LP.norm_gnn(got["gnn"]), LP.norm_gnn(ref["gnn"]), 1e-6), e
+        assert LP.first_divergence(ref, got, 1e-6, meta["args"]["cpuct"]) is None, e

@@ -45,7 +45,7 @@ int main(int argc, char** argv) {
   int finished = 0, held = 0;
   long rows = 0, rounds = 0;
   const auto t0 = std::chrono::steady_clock::now();
-  double tc = 0.0;
+  double tc = 0.0, tn = 0.0, tf = 0.0;
   while (finished < E) {
     const auto c0 = std::chrono::steady_clock::now();
     const int k = held > 0 ? az_mcts_feed_collect(m, held, pi.data(), v.data(), gpi.data(),
@@ -53,21 +53,29 @@ int main(int argc, char** argv) {
                            : az_mcts_collect(m, boards.data(), sl.data(), E, threads);
     tc += std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
     if (k < 0) { fprintf(stderr, "collect: %s\n", az_mcts_last_error()); return 1; }
+    // the stand-in network runs on all threads (timed apart: it is not engine work -- serial,
+    // it was 2.1-2.5 s of every 2,048-episode run and looked like an engine serial part)
+    const auto n0 = std::chrono::steady_clock::now();
+#pragma omp parallel for num_threads(threads) schedule(static)
     for (int i = 0; i < k; ++i) {
       fake_net(&boards[(size_t)i * cells], cells, A, 7, &pi[(size_t)i * A], &v[i]);
       fake_net(&boards[(size_t)i * cells], cells, A, 9, &gpi[(size_t)i * A], &gv[i]);
     }
+    tn += std::chrono::duration<double>(std::chrono::steady_clock::now() - n0).count();
     held = k;
     rows += k;
     ++rounds;
+    const auto f0 = std::chrono::steady_clock::now();
     const int f = az_mcts_episode_finished(m, fin.data(), E);
+    tf += std::chrono::duration<double>(std::chrono::steady_clock::now() - f0).count();
     if (f < 0) { fprintf(stderr, "finished: %s\n", az_mcts_last_error()); return 1; }
     finished += f;
     if (k == 0 && f == 0 && held == 0) break;
   }
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  printf("episodes %d threads %d rounds %ld rows %ld seconds %.3f (in collect %.3f) episodes/s %.1f\n",
-         E, threads, rounds, rows, dt, tc, E / dt);
+  printf("episodes %d threads %d rounds %ld rows %ld seconds %.3f (in collect %.3f, stand-in net "
+         "%.3f, episode_finished %.3f) episodes/s %.1f; engine-only (collect) episodes/s %.1f\n",
+         E, threads, rounds, rows, dt, tc, tn, tf, E / dt, E / tc);
   az_mcts_destroy(m);
   return 0;
 }
