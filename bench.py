@@ -68,7 +68,7 @@ def parse():
     return ap.parse_args()
 
 
-CALIBRATION = "profiles/r02_cpu_calibration.json"   # tools/cpu_calibration.py, build container
+CALIBRATION = "profiles/r04_cpu_calibration.json"   # tools/cpu_calibration.py, build container
 CPU_CHILD = "--cpu-baselines-child"
 
 
@@ -135,7 +135,7 @@ def cpu_baselines_child(spec):
         os.sched_setaffinity(0, spec["cpus"])
     except (AttributeError, OSError):
         pass
-    threads = hostcpu.host_cpus()
+    threads = int(spec.get("threads") or hostcpu.host_cpus())
     os.environ["OMP_NUM_THREADS"] = str(threads)
     from azhip.weights import connect4_net_spec, gnn_spec, synthetic_state_dict
     W = synthetic_state_dict(connect4_net_spec(7), 1)
