@@ -5,8 +5,9 @@
 //
 //   per tile of 64 consecutive destination nodes [d0, d0 + 64), one 512-thread block per CU,
 //   persistent over a contiguous run of tiles:
-//     A  Pt = X[d0, d0+64) W1[:, :F]^T           (waves 0-3)   } x3 MFMAs: fp32 operands as three
-//        Ps = X[d0+32, d0+96) W1[:, F:]^T         (waves 4-7)   } bf16 terms, six products
+//     A  Pt = X[d0, d0+64) W1[:, :F]^T           (waves 0-3)   } fp16-form MFMAs: fp32 operands,
+//        Ps = X[d0+32, d0+96) W1[:, F:]^T         (waves 4-7)   } row-scaled, as two fp16 terms
+//                                                                  (az_x3.h), three products
 //     B  alpha_e = sigmoid(w2 . relu(Pt[d] + Ps[s] + b1) + b2), agg_d = sum_e alpha_e / S x_s
 //        (8 lanes per destination, edges in CSR order, S = sum alpha > 0: gnn_utils.py:48-65)
 //     C  [gate | u1] = [x_d ; agg_d] [Wg ; Wu1]^T + b   (K split over the two wave halves)
@@ -16,14 +17,18 @@
 //   tile's window [d0 - 32, d0 + 96): each tile adds 64 new rows (their x and Ps) and drops 64,
 //   so every node's x is read from HBM once and its Ps computed once per block run -- the
 //   separate Ps projection GEMM (and its 268 MB write + gather at 512 grids) is gone.  Nothing
-//   but x_out leaves the CU.  The weights (three bf16 planes in MFMA fragment order, split once
-//   per launch) stream from L2.
+//   but x_out leaves the CU.  The weights (two fp16 planes in MFMA fragment order, each row scaled
+//   by its power of two, split once per launch) stream from L2.
 //
-//   MFMA operands that come from LDS are stored ALREADY split: x rows enter the ring as their
-//   three bf16 planes (split once, when the row arrives), and each destination's agg is written
-//   as planes over its own (consumed) Pt row -- the split is exact (x = h + m + l), so the
-//   aggregation and the residual rebuild x from the planes bit for bit.  Only update_net.0's
-//   output (u1, the last GEMM's A) is split in the waves.
+//   MFMA operands that come from LDS are stored ALREADY split: x rows enter the ring as three fp16
+//   planes of x s (s the row's power-of-two scale, 1/s kept per ring slot; the first two planes
+//   are the MFMA's two terms), and each destination's agg is written as its two planes over its
+//   own (consumed) Pt row.  (h + m + l) / s rebuilds x exactly while l is a normal fp16, and
+//   within 2^-39 of the row's largest |x| otherwise: the aggregation and the residual use that;
+//   a destination without in-edges copies x from HBM, so its output is x bit for bit
+//   (gnn_utils.py:35-36).  update_net.0's output (u1) and output_transform's operands are split
+//   in the waves, scaled per 64-row tile.  Every GEMM's accumulators are multiplied back by
+//   1 / (s_row s_w) (exact) before use.
 //
 // Edges are never dropped: a destination with any in-degree is aggregated completely, and a
 // source outside the window (a graph that is not banded as the caller claimed) takes a slow
@@ -45,11 +50,11 @@ constexpr int BNT = 512;      // threads: 8 waves, one block per CU
 constexpr int PSS = 132;      // Pt / agg-plane / [gate | u1] row stride (floats), = 4 (mod 64)
 constexpr int PSRS = 128;     // Ps ring row stride: every row starts on bank 0, and the two
                               // destinations of a 16-lane read group take opposite halves
-constexpr int XRS = 3 * BF;   // ring row: three planes of 64 bf16 (384 B), 16-B chunks swizzled
+constexpr int XRS = 3 * BF;   // ring row: three planes of 64 fp16 (384 B), 16-B chunks swizzled
 
-// weight planes [3][WTOT] bf16 in MFMA-fragment order: a matrix W [N][K] (nn.Linear [out][in])
-// is stored as (N / 32) x (K / 16) blocks of 512 bf16, block (nb, ks) holding the B operand of
-// one v_mfma_f32_32x32x16_bf16 step lane by lane (lane l: row 32 nb + (l & 31), k = 16 ks +
+// weight planes [2][WTOT] fp16 in MFMA-fragment order: a matrix W [N][K] (nn.Linear [out][in])
+// is stored as (N / 32) x (K / 16) blocks of 512 fp16, block (nb, ks) holding the B operand of
+// one v_mfma_f32_32x32x16_f16 step lane by lane (lane l: row 32 nb + (l & 31), k = 16 ks +
 // 8 (l >> 5) .. + 7), so a wave reads its fragment as ONE contiguous 1 KB (row-major planes
 // made every lane touch its own cache line: 4x the L2 traffic)
 constexpr int W1_OFF = 0;                    // attention.0    [128][128]
@@ -59,7 +64,9 @@ constexpr int OT0_OFF = WU2_OFF + BF * BF;  // output_transform.0 [64][64] (fuse
 constexpr int OT2_OFF = OT0_OFF + BF * BF;   // output_transform.2 [64][64]
 constexpr int WLAYER = OT0_OFF;              // the layer's own weights
 constexpr int WTOT = OT2_OFF + BF * BF;      // plane stride
-constexpr int FRAG = 512;                    // bf16 per fragment block
+constexpr int FRAG = 512;                    // fp16 per fragment block
+// 1 / s of every weight row (after the planes): W1 rows, [Wg ; Wu1] rows, Wu2, OT.0, OT.2
+constexpr int WI_W1 = 0, WI_WC = 128, WI_WU2 = 256, WI_OT0 = 320, WI_OT2 = 384, WI_N = 448;
 
 // offset of W[n][k .. k + 7] (k % 8 == 0) in a fragment-ordered matrix of K columns
 __host__ __device__ constexpr int frag_off(int n, int k, int K) {
@@ -67,7 +74,8 @@ __host__ __device__ constexpr int frag_off(int n, int k, int K) {
 }
 
 struct BandW {
-  const unsigned short* planes;              // [3][WTOT]
+  const unsigned short* planes;              // [2][WTOT]
+  const float* winv;                         // [WI_N] 1 / s per weight row
   const float *w1, *b1, *w2, *b2, *gb, *ub1, *ub2;
   const float *ob0, *ob2;                    // output_transform biases (OT only)
 };
@@ -98,7 +106,32 @@ __device__ __forceinline__ float sum8(float v) {
   return v + dpp<0x141>(v);
 }
 
-// 8 consecutive weights -> their three bf16 planes
+// the same for the maximum (row scales of the fp16 planes)
+__device__ __forceinline__ float max8(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  return fmaxf(v, dpp<0x141>(v));
+}
+
+__device__ __forceinline__ float absmax8(const f32x4 (&v)[2]) {
+  float m = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m = fmaxf(m, fabsf(v[h][e]));
+  return m;
+}
+
+// maximum over the 64 lanes of a wave
+__device__ __forceinline__ float wave_absmax(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// 8 consecutive weights of one row -> their two fp16 planes, the row scaled by its power of two
+// (max |w s| in [2^13, 2^14): every thread reads its row's <= 128 weights for the maximum); the
+// row's first chunk also stores 1 / s in winv
 __global__ __launch_bounds__(256) void band_split_weights(const float* __restrict__ w1,
                                                           const float* __restrict__ gw,
                                                           const float* __restrict__ uw1,
@@ -106,48 +139,66 @@ __global__ __launch_bounds__(256) void band_split_weights(const float* __restric
                                                           const float* __restrict__ ow0,
                                                           const float* __restrict__ ow2,
                                                           unsigned short* __restrict__ planes,
-                                                          int n) {
+                                                          float* __restrict__ winv, int n) {
   const int i = (blockIdx.x * 256 + threadIdx.x) * 8;   // element of [W1 | Wg ; Wu1 | Wu2 | ..]
   if (i >= n) return;
   const float* src;
-  int dst;
+  int dst, len, wrow, pos;
   if (i < WC_OFF) {                       // W1 [128][128]
     src = w1 + i;
     dst = W1_OFF + frag_off(i >> 7, i & 127, 2 * BF);
+    len = 2 * BF;
+    wrow = WI_W1 + (i >> 7);
+    pos = i & 127;
   } else if (i < WU2_OFF) {               // [Wg ; Wu1] [128][128]
     const int j = i - WC_OFF;
     src = j < BF * 2 * BF ? gw + j : uw1 + (j - BF * 2 * BF);
     dst = WC_OFF + frag_off(j >> 7, j & 127, 2 * BF);
+    len = 2 * BF;
+    wrow = WI_WC + (j >> 7);
+    pos = j & 127;
   } else {                                // Wu2, then output_transform.0 / .2: [64][64] each
     const int m = (i - WU2_OFF) / (BF * BF), j = (i - WU2_OFF) % (BF * BF);
     src = (m == 0 ? uw2 : m == 1 ? ow0 : ow2) + j;
     dst = WU2_OFF + m * BF * BF + frag_off(j >> 6, j & 63, BF);
+    len = BF;
+    wrow = WI_WU2 + m * BF + (j >> 6);
+    pos = j & 63;
   }
+  const float* row = src - pos;
+  float mx = 0.f;
+  for (int k = 0; k < len; k += 4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(row + k);
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  float inv;
+  const float sc = h3_scale(mx, 14, &inv);
+  if (pos == 0) winv[wrow] = inv;
   const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
   const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
-  u32x4 o[3];
-  split3(x0, x1, o);
+  u32x4 o[2];
+  split2s(x0, x1, sc, o);
 #pragma unroll
-  for (int pl = 0; pl < 3; ++pl)
+  for (int pl = 0; pl < 2; ++pl)
     *reinterpret_cast<u32x4*>(planes + (size_t)pl * WTOT + dst) = o[pl];
 }
 
-// acc[mb] += A[32 rows of m-block mb][K = 16 KS] . W[32 rows][K]^T on x3 MFMAs, both operands
-// as bf16 planes.  a(mb, ks, pl) -> this lane's A fragment (plane pl of step ks); w: plane 0 of
-// the first weight fragment block (frag_off(n0, k0, K) + 8 lane; the KS blocks of a row block
-// are consecutive).
-// this lane's weight fragments of KS k steps (3 planes each), requested from L2: issued a phase
+// acc[mb] += A[32 rows of m-block mb][K = 16 KS] . W[32 rows][K]^T on fp16-form MFMAs, both
+// operands as two fp16 planes.  a(mb, ks, pl) -> this lane's A fragment (plane pl of step ks); w:
+// plane 0 of the first weight fragment block (frag_off(n0, k0, K) + 8 lane; the KS blocks of a
+// row block are consecutive).
+// this lane's weight fragments of KS k steps (2 planes each), requested from L2: issued a phase
 // ahead of their MFMAs, so no GEMM of the tile starts by waiting for its weights.  Buffer loads
 // off one descriptor: the lane part (16 B x lane) is the only VGPR, the fragment block's offset
-// `w` (bf16 elements, wave-uniform) rides in an SGPR -- flat pointers per fragment would hold
-// 24 VGPRs of addresses per weight set across the whole tile loop.
+// `w` (fp16 elements, wave-uniform) rides in an SGPR -- flat pointers per fragment would hold
+// 16 VGPRs of addresses per weight set across the whole tile loop.
 template <int KS, int ABL = 0>
-__device__ __forceinline__ void load_w(bf16x8 (&b)[KS][3], __amdgpu_buffer_rsrc_t planes,
+__device__ __forceinline__ void load_w(bf16x8 (&b)[KS][2], __amdgpu_buffer_rsrc_t planes,
                                        int lane_off, int w) {
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
+    for (int pl = 0; pl < 2; ++pl) {
       if constexpr ((ABL & 16) != 0) {
         b[ks][pl] = bf16x8{};             // tuning ablation: no weight loads
       } else {
@@ -160,11 +211,11 @@ __device__ __forceinline__ void load_w(bf16x8 (&b)[KS][3], __amdgpu_buffer_rsrc_
 
 // acc[mb] += A . W^T with the weight fragments already in registers (load_w)
 template <int MB, int KS, int ABL, typename AFrag>
-__device__ __forceinline__ void x3_mfma(f32x16 (&acc)[MB], const AFrag& afrag,
-                                        const bf16x8 (&b)[KS][3]) {
+__device__ __forceinline__ void h3_mfma(f32x16 (&acc)[MB], const AFrag& afrag,
+                                        const bf16x8 (&b)[KS][2]) {
   if constexpr ((ABL & 32) != 0) return;  // tuning ablation: no A reads / MFMAs
   // A fragments one k step ahead of their MFMAs (LDS latency behind the previous step's)
-  bf16x8 a[2][MB][3];
+  bf16x8 a[2][MB][2];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) afrag(mb, 0, a[0][mb]);
 #pragma unroll
@@ -174,7 +225,7 @@ __device__ __forceinline__ void x3_mfma(f32x16 (&acc)[MB], const AFrag& afrag,
       for (int mb = 0; mb < MB; ++mb) afrag(mb, ks + 1, a[(ks + 1) & 1][mb]);
     }
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) acc[mb] = mfma6_32x32x16(a[ks & 1][mb], b[ks], acc[mb]);
+    for (int mb = 0; mb < MB; ++mb) acc[mb] = mfma3_32x32x16_f16(a[ks & 1][mb], b[ks], acc[mb]);
   }
 }
 
@@ -238,6 +289,9 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   __shared__ int DEG[BT];
   __shared__ int RPS[2][BT + 1];          // rowptr of the tile's destinations (+1), prefetched
   __shared__ int CLS[2][BNT];             // the tile's sources (col), when it has <= 512 edges
+  __shared__ float XSI[RING];             // 1 / s of each ring row's fp16 planes
+  __shared__ float AGSI[BT];              // 1 / s of each destination's agg planes
+  __shared__ float TMX[2][8];             // per-wave maxima: u1 (C -> D), x_out / h (OT)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 31, hc = lane >> 5;          // fragment row, k half (8-element chunk)
   const int t0 = blockIdx.x * per, t1 = min(ntiles, t0 + per);
@@ -265,35 +319,39 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   };
   auto store_rows = [&](int r0, const f32x4 (&v)[2]) {
     const int slot = (r0 + (tid >> 3)) & (RING - 1);
+    float inv;
+    const float sc = h3_scale(max8(absmax8(v)), 14, &inv);   // the row's 8 threads agree
     u32x4 o[3];
-    split3(v[0], v[1], o);
+    split3h(v[0], v[1], sc, o);
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
       *reinterpret_cast<u32x4*>(XR + xr_off(slot, pl, tid & 7)) = o[pl];
+    if ((tid & 7) == 0) XSI[slot] = inv;
   };
-  // x of ring row `slot`, features 8c .. 8c + 7, rebuilt exactly from its planes
-  auto x_planes = [](const u32x4& h, const u32x4& m, const u32x4& l, f32x4 (&v)[2]) {
+  // x of a ring row, features 8c .. 8c + 7, rebuilt from its three fp16 planes and 1 / s
+  auto x_planes = [](const u32x4& h, const u32x4& m, const u32x4& l, float inv, f32x4 (&v)[2]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float lo = (__uint_as_float(h[q] << 16) + __uint_as_float(m[q] << 16)) +
-                       __uint_as_float(l[q] << 16);
-      const float hi = (__uint_as_float(h[q] & 0xFFFF0000u) + __uint_as_float(m[q] & 0xFFFF0000u)) +
-                       __uint_as_float(l[q] & 0xFFFF0000u);
-      v[q >> 1][2 * (q & 1)] = lo;
-      v[q >> 1][2 * (q & 1) + 1] = hi;
+      // the dwords go through scalars: __builtin_bit_cast of an ext-vector ELEMENT (h[q])
+      // compiles to a bit cast of element 0 for every q on this toolchain (ROCm 7.2 clang)
+      const unsigned hq = h[q], mq = m[q], lq = l[q];
+      const f16x2 hh = __builtin_bit_cast(f16x2, hq), mm = __builtin_bit_cast(f16x2, mq),
+                  ll = __builtin_bit_cast(f16x2, lq);
+      v[q >> 1][2 * (q & 1)] = (((float)hh[0] + (float)mm[0]) + (float)ll[0]) * inv;
+      v[q >> 1][2 * (q & 1) + 1] = (((float)hh[1] + (float)mm[1]) + (float)ll[1]) * inv;
     }
   };
   auto x_ring = [&](int slot, int c, f32x4 (&v)[2]) {
     x_planes(*reinterpret_cast<const u32x4*>(XR + xr_off(slot, 0, c)),
              *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 1, c)),
-             *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 2, c)), v);
+             *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 2, c)), XSI[slot], v);
   };
   // A fragments straight from the ring planes: rows r0 + 32 mb + (lane & 31)
   auto ring_frag = [&](int r0) {
-    return [=](int mb, int ks, bf16x8 (&a)[3]) {
+    return [=](int mb, int ks, bf16x8 (&a)[2]) {
       const int slot = (r0 + 32 * mb + lr) & (RING - 1);
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < 2; ++pl)
         a[pl] = *reinterpret_cast<const bf16x8*>(XR + xr_off(slot, pl, 2 * ks + hc));
     };
   };
@@ -304,7 +362,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   //   C  [gate ; update_net.0]: n quarter wave & 3, K half wave >> 2
   //   D  update_net.2 (waves 0-3: n-block wave & 1); OT: output_transform.0 / .2 likewise
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned short*>(W.planes), 0, 3 * WTOT * 2, 0x00020000);
+      const_cast<unsigned short*>(W.planes), 0, 2 * WTOT * 2, 0x00020000);
   const int wl = 16 * lane;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   const int wA = W1_OFF + frag_off(32 * (wv & 3), wv < 4 ? 0 : BF, 2 * BF);
@@ -314,7 +372,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   const int cq = (wv & 3) ^ (wv < 4 ? 0 : 2);
   const int wC = WC_OFF + frag_off(32 * cq, BF * (wv >> 2), 2 * BF);
   const int wD = WU2_OFF + frag_off(32 * (wv & 1), 0, BF);
-  bf16x8 bw[4][3];
+  bf16x8 bw[4][2];
   constexpr int AAB = (ABL & 1) ? (ABL | 32) : ABL;
   load_w<4, ABL>(bw, wr, wl, wA);
 
@@ -324,12 +382,15 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     f32x16 acc[2];
     zero(acc[0]);
     zero(acc[1]);
-    x3_mfma<2, 4, AAB>(acc, ring_frag(r0), bw);
+    h3_mfma<2, 4, AAB>(acc, ring_frag(r0), bw);
+    const float wi = W.winv[WI_W1 + 32 * nb + lr];   // attention.0 row (hidden unit) scale
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        PSR[((r0 + 32 * mb + acc_row(r, lane)) & (RING - 1)) * PSRS + 32 * nb + lr] = acc[mb][r];
+      for (int r = 0; r < 16; ++r) {
+        const int slot = (r0 + 32 * mb + acc_row(r, lane)) & (RING - 1);
+        PSR[slot * PSRS + 32 * nb + lr] = acc[mb][r] * (XSI[slot] * wi);
+      }
   };
 
   // prologue: the first tile's window [d0 - 32, d0 + 96) and the Ps of its first 64 rows
@@ -377,13 +438,16 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       f32x16 acc[2];
       zero(acc[0]);
       zero(acc[1]);
-      x3_mfma<2, 4, AAB>(acc, ring_frag(d0), bw);
+      h3_mfma<2, 4, AAB>(acc, ring_frag(d0), bw);
       const float b1n = B1W2[32 * wave + lr];     // attention.0's bias, folded into Pt
+      const float wi = W.winv[WI_W1 + 32 * wave + lr];
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          PT[(32 * mb + acc_row(r, lane)) * PSS + 32 * wave + lr] = acc[mb][r] + b1n;
+        for (int r = 0; r < 16; ++r) {
+          const int row = 32 * mb + acc_row(r, lane);
+          PT[row * PSS + 32 * wave + lr] = acc[mb][r] * (XSI[(d0 + row) & (RING - 1)] * wi) + b1n;
+        }
     } else {
       ps_rows(d0 + BR);
     }
@@ -521,16 +585,19 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         f32x4 g[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
         if constexpr (FAST) {
           u32x4 xp[4][3];                   // the four sources' planes, all reads in flight
+          float xi[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
+          for (int q = 0; q < 4; ++q) {
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
               xp[q][pl] = *reinterpret_cast<const u32x4*>(XR + xr_off(src[q] & (RING - 1), pl, ej));
+            xi[q] = XSI[src[q] & (RING - 1)];
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float wq = a[q] * rS;
             f32x4 v[2];
-            x_planes(xp[q][0], xp[q][1], xp[q][2], v);
+            x_planes(xp[q][0], xp[q][1], xp[q][2], xi[q], v);
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               g[0][c] = fmaf(wq, v[0][c], g[0][c]);
@@ -564,12 +631,16 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
           }
         }
         // the group's 8 lanes read their Pt row above (same wave, in order): the row now takes
-        // agg's planes, plane pl at byte 128 pl, 16-B chunk ej
-        u32x4 o[3];
-        split3(g[0], g[1], o);
+        // agg's two fp16 planes (scaled by the row's power of two), plane pl at byte 128 pl,
+        // 16-B chunk ej
+        float ainv;
+        const float asc = h3_scale(max8(absmax8(g)), 14, &ainv);
+        u32x4 o[2];
+        split2s(g[0], g[1], asc, o);
         unsigned short* arow = reinterpret_cast<unsigned short*>(PT + ei * PSS);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(arow + pl * BF + 8 * ej) = o[pl];
+        for (int pl = 0; pl < 2; ++pl) *reinterpret_cast<u32x4*>(arow + pl * BF + 8 * ej) = o[pl];
+        if (ej == 0) AGSI[ei] = ainv;
       };
       bool ok = deg <= 4 && ne <= BNT;
 #pragma unroll
@@ -598,16 +669,26 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       zero(acc[1]);
       constexpr int CAB = (ABL & 4) ? (ABL | 32) : ABL;
       if (kh == 0) {
-        x3_mfma<2, 4, CAB>(acc, ring_frag(d0), bw);
+        h3_mfma<2, 4, CAB>(acc, ring_frag(d0), bw);
         load_w<4, ABL>(bw, wr, wl, wD);
       } else {
-        x3_mfma<2, 4, CAB>(acc, [&](int mb, int ks, bf16x8 (&a)[3]) {
+        h3_mfma<2, 4, CAB>(acc, [&](int mb, int ks, bf16x8 (&a)[2]) {
           const unsigned short* row = reinterpret_cast<const unsigned short*>(PT + (32 * mb + lr) * PSS);
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
+          for (int pl = 0; pl < 2; ++pl)
             a[pl] = *reinterpret_cast<const bf16x8*>(row + pl * BF + 8 * (2 * ks + hc));
         }, bw);
         load_w<4, ABL>(bw, wr, wl, wA);           // waves 4-7 are idle until the next tile's phase A
+      }
+      {   // each K half back to fp32 units with its own row scales (x_d's / agg's) before the sum
+        const float wi = W.winv[WI_WC + 32 * nq + lr];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = 32 * mb + acc_row(r, lane);
+            acc[mb][r] *= (kh == 0 ? XSI[(d0 + row) & (RING - 1)] : AGSI[row]) * wi;
+          }
       }
       BSTAMP(5);
       // the two K halves' partials meet in the Ps ring's dead half (accumulator layout, 16 rows
@@ -633,11 +714,16 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       for (int r = 0; r < 16; ++r) mine[r] += part[(kh * 16 + r) * 64];
       const int n = 32 * nq + lr;         // output column: gate (n < 64) or u1 (n - 64)
       const float bias = BS[n];         // gate.0 (n < 64) | update_net.0
+      float um = 0.f;                     // the largest u1 (phase D's tile scale)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float v = mine[r] + bias;
-        PT[(32 * kh + acc_row(r, lane)) * PSS + n] = nq < 2 ? sigmoid_fast(v) : relu(v);
+        const float o = nq < 2 ? sigmoid_fast(v) : relu(v);
+        PT[(32 * kh + acc_row(r, lane)) * PSS + n] = o;
+        um = fmaxf(um, nq < 2 ? 0.f : o);
       }
+      um = wave_absmax(um);
+      if (lane == 0) TMX[0][wave] = um;
     }
     __syncthreads();
     BSTAMP(7);
@@ -651,22 +737,28 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     float* const u2s = PSR + ((d0 - BR) & (RING - 1)) * PSRS;
     if (wave < 4) {
       const int mb = wave >> 1, nb = wave & 1;
+      float uinv;                         // u1's tile scale (the u1 waves' maxima, phase C)
+      float um = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) um = fmaxf(um, TMX[0][w]);
+      const float usc = h3_scale(um, 14, &uinv);
       f32x16 acc[1];
       zero(acc[0]);
-      x3_mfma<1, 4, (ABL & 8) ? (ABL | 32) : ABL>(acc, [&](int, int ks, bf16x8 (&a)[3]) {
+      h3_mfma<1, 4, (ABL & 8) ? (ABL | 32) : ABL>(acc, [&](int, int ks, bf16x8 (&a)[2]) {
         const float* u = PT + (32 * mb + lr) * PSS + BF + 16 * ks + 8 * hc;
         const f32x4 x0 = *reinterpret_cast<const f32x4*>(u);
         const f32x4 x1 = *reinterpret_cast<const f32x4*>(u + 4);
-        u32x4 o[3];
-        split3(x0, x1, o);
+        u32x4 o[2];
+        split2s(x0, x1, usc, o);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) a[pl] = __builtin_bit_cast(bf16x8, o[pl]);
+        for (int pl = 0; pl < 2; ++pl) a[pl] = __builtin_bit_cast(bf16x8, o[pl]);
       }, bw);
       load_w<4, ABL>(bw, wr, wl, OT ? wD + (OT0_OFF - WU2_OFF) : wA);
       const int n = 32 * nb + lr;
       const float ub = BS[2 * BF + n];
+      const float ui = uinv * W.winv[WI_WU2 + n];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) u2s[(32 * mb + acc_row(r, lane)) * BF + n] = acc[0][r] + ub;
+      for (int r = 0; r < 16; ++r) u2s[(32 * mb + acc_row(r, lane)) * BF + n] = acc[0][r] * ui + ub;
     }
     __syncthreads();                      // u2 complete
     {
@@ -677,11 +769,21 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       const f32x4* up = reinterpret_cast<const f32x4*>(u2s + i * BF + 8 * c);
       const bool upd = DEG[i] > 0;
       f32x4 o[2];
+      if (!upd) {                         // no in-edges: x itself, bit for bit (gnn_utils.py:35)
+        const size_t xo = (size_t)min(d0 + i, V - 1) * BF + 8 * c;
+        o[0] = *reinterpret_cast<const f32x4*>(x + xo);
+        o[1] = *reinterpret_cast<const f32x4*>(x + xo + 4);
+      } else {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f32x4 gv = gp[h], uv = up[h];
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 gv = gp[h], uv = up[h];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[h][e] = upd ? xv[h][e] + gv[e] * uv[e] : xv[h][e];
+          for (int e = 0; e < 4; ++e) o[h][e] = xv[h][e] + gv[e] * uv[e];
+        }
+      }
+      if constexpr (OT) {                 // x_out's tile maximum: phase E's scale
+        const float om = wave_absmax(absmax8(o));
+        if (lane == 0) TMX[1][wave] = om;
       }
       if constexpr (OT) {
         float* dst = PT + i * PSS + 8 * c;    // in place of the gate elements it consumed
@@ -706,37 +808,54 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       //      are split in the waves)
       __syncthreads();
       const int mb = (wave >> 1) & 1, nb = wave & 1, n = 32 * nb + lr;
-      auto split_rows = [&](int col0) {
-        return [=](int, int ks, bf16x8 (&a)[3]) {
+      auto split_rows = [&](int col0, float sc) {
+        return [=](int, int ks, bf16x8 (&a)[2]) {
           const float* u = PT + (32 * mb + lr) * PSS + col0 + 16 * ks + 8 * hc;
           const f32x4 x0 = *reinterpret_cast<const f32x4*>(u);
           const f32x4 x1 = *reinterpret_cast<const f32x4*>(u + 4);
-          u32x4 t[3];
-          split3(x0, x1, t);
+          u32x4 t[2];
+          split2s(x0, x1, sc, t);
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl) a[pl] = __builtin_bit_cast(bf16x8, t[pl]);
+          for (int pl = 0; pl < 2; ++pl) a[pl] = __builtin_bit_cast(bf16x8, t[pl]);
         };
       };
       f32x16 acc[1];
       if (wave < 4) {
+        float m = 0.f, inv;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) m = fmaxf(m, TMX[1][w]);
+        const float sc = h3_scale(m, 14, &inv);
         zero(acc[0]);
-        x3_mfma<1, 4, ABL>(acc, split_rows(0), bw);
+        h3_mfma<1, 4, ABL>(acc, split_rows(0, sc), bw);
         load_w<4, ABL>(bw, wr, wl, wD + (OT2_OFF - WU2_OFF));
         const float bias = BS[3 * BF + n];
+        const float wi = inv * W.winv[WI_OT0 + n];
         float* const pe = PT + opaque((32 * mb + acc_row(0, lane)) * PSS + BF + n);
+        float hm = 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) pe[acc_drow(r) * PSS] = relu(acc[0][r] + bias);
-      }
+        for (int r = 0; r < 16; ++r) {
+          const float h = relu(acc[0][r] * wi + bias);
+          pe[acc_drow(r) * PSS] = h;
+          hm = fmaxf(hm, h);
+        }
+        hm = wave_absmax(hm);
+        if (lane == 0) TMX[0][wave] = hm;   // h's tile maximum (phase F's scale); TMX[0] (u1's)
+      }                                     // was last read in phase D, two barriers ago
       __syncthreads();
       if (wave < 4) {
+        float m = 0.f, inv;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) m = fmaxf(m, TMX[0][w]);
+        const float sc = h3_scale(m, 14, &inv);
         zero(acc[0]);
-        x3_mfma<1, 4, ABL>(acc, split_rows(BF), bw);
+        h3_mfma<1, 4, ABL>(acc, split_rows(BF, sc), bw);
         load_w<4, ABL>(bw, wr, wl, wA);
         const float bias = BS[4 * BF + n];
+        const float wi = inv * W.winv[WI_OT2 + n];
         float* const pf = PT + opaque((32 * mb + acc_row(0, lane)) * PSS + n);
 #pragma unroll
         for (int r = 0; r < 16; ++r)      // y over x_out's rows in PT (read by E, before F)
-          pf[acc_drow(r) * PSS] = acc[0][r] + bias;
+          pf[acc_drow(r) * PSS] = acc[0][r] * wi + bias;
       }
     }
     __syncthreads();                      // x_d rows read: their slots take the next rows
@@ -765,17 +884,19 @@ bool gnn_layer_band_ok(const az_graph* g, int F, int H) {
   return F == BF && H == BH && g->V > 0 && g->band > 0 && g->band <= BR;
 }
 
-size_t gnn_layer_band_ws_bytes() { return ((size_t)3 * WTOT * 2 + 255) / 256 * 256; }
+constexpr size_t band_planes_bytes() { return ((size_t)2 * WTOT * 2 + 255) / 256 * 256; }
+size_t gnn_layer_band_ws_bytes() { return band_planes_bytes() + ((size_t)WI_N * 4 + 255) / 256 * 256; }
 
 // One eval-mode GNNLayer on a band graph; with `ot` (output_transform.{0,2}.{weight,bias}: w0,
 // b0, w2, b2) the layer is the network's last and x_out receives output_transform's output.
 int gnn_layer_band(const az_graph* g, const float* x, const az_gnn_layer_w* w, float* x_out,
                    void* ws, hipStream_t s, const float* const* ot) {
   unsigned short* planes = static_cast<unsigned short*>(ws);
+  float* winv = reinterpret_cast<float*>(static_cast<char*>(ws) + band_planes_bytes());
   const int n = ot ? WTOT : WLAYER;
   hipLaunchKernelGGL(band_split_weights, dim3((n / 8 + 255) / 256), dim3(256), 0, s,
                      w->att_w1, w->gate_w, w->upd_w1, w->upd_w2, ot ? ot[0] : nullptr,
-                     ot ? ot[2] : nullptr, planes, n);
+                     ot ? ot[2] : nullptr, planes, winv, n);
   int rc = check_launch("band_split_weights");
   if (rc) return rc;
   static int cus = 0;                     // queried once per process
@@ -791,8 +912,8 @@ int gnn_layer_band(const az_graph* g, const float* x, const az_gnn_layer_w* w, f
   const int ntiles = (g->V + BT - 1) / BT;
   const int per = (ntiles + cus - 1) / cus;
   const int blocks = (ntiles + per - 1) / per;
-  const BandW bw = {planes, w->att_w1, w->att_b1, w->att_w2, w->att_b2, w->gate_b, w->upd_b1,
-                    w->upd_b2, ot ? ot[1] : nullptr, ot ? ot[3] : nullptr};
+  const BandW bw = {planes, winv, w->att_w1, w->att_b1, w->att_w2, w->att_b2, w->gate_b,
+                    w->upd_b1, w->upd_b2, ot ? ot[1] : nullptr, ot ? ot[3] : nullptr};
 #define AZ_BAND(A_)                                                                          \
   do {                                                                                       \
     if (ot)                                                                                  \

@@ -76,6 +76,50 @@ __device__ __forceinline__ void split2s(const f32x4& x0, const f32x4& x1, float 
   }
 }
 
+// The same fp16 terms three deep: h, m = rne(x s - h), l = rne(x s - h - m) (both differences
+// exact in fp32).  (h + m) + l rebuilds x s exactly while l is a normal fp16 (|x s| >= 2^8 for
+// |x s| < 2^15), and within 2^-25 absolutely below that; h, m are the two-term split above.
+__device__ __forceinline__ void split3h(const f32x4& x0, const f32x4& x1, float s, u32x4 (&o)[3]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float a = (q < 2 ? x0[2 * q] : x1[2 * q - 4]) * s;
+    const float b = (q < 2 ? x0[2 * q + 1] : x1[2 * q - 3]) * s;
+    const unsigned h = pk_f16(a, b);
+    const f16x2 hh = __builtin_bit_cast(f16x2, h);
+    const float ra = a - (float)hh[0], rb = b - (float)hh[1];
+    const unsigned m = pk_f16(ra, rb);
+    const f16x2 mm = __builtin_bit_cast(f16x2, m);
+    o[0][q] = h;
+    o[1][q] = m;
+    o[2][q] = pk_f16(ra - (float)mm[0], rb - (float)mm[1]);
+  }
+}
+
+// power-of-two scale s with max |x s| in [2^(T-1), 2^T) for a row / tile maximum m (1 when m is 0
+// or not finite), and its inverse
+__device__ __forceinline__ float h3_scale(float m, int T, float* inv) {
+  int e = 0;
+  if (m > 0.f && m <= 3.4e38f) {
+    int ex;
+    (void)frexpf(m, &ex);
+    e = min(120, max(-120, T - ex));
+  }
+  *inv = ldexpf(1.f, -e);
+  return ldexpf(1.f, e);
+}
+
+// acc += A . B over one 16-k step of v_mfma_f32_32x32x16_f16, both operands as their two fp16
+// terms (bit patterns in bf16x8 registers: a[0] = h, a[1] = l), the dropped l*l smallest;
+// smallest first
+__device__ __forceinline__ f32x16 mfma3_32x32x16_f16(const bf16x8 (&a)[2], const bf16x8 (&b)[2],
+                                                    f32x16 t) {
+  const f16x8 ah = __builtin_bit_cast(f16x8, a[0]), al = __builtin_bit_cast(f16x8, a[1]);
+  const f16x8 bh = __builtin_bit_cast(f16x8, b[0]), bl = __builtin_bit_cast(f16x8, b[1]);
+  t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, t, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, t, 0, 0, 0);
+}
+
 // acc += A . B over one 16-k step of v_mfma_f32_32x32x16_bf16 with both operands as three bf16
 // planes (a[0..2] = h, m, l of A's fragment, b[0..2] of B's), the dropped terms smallest first
 __device__ __forceinline__ f32x16 mfma6_32x32x16(const bf16x8 (&a)[3], const bf16x8 (&b)[3],
