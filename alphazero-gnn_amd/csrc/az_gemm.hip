@@ -3220,26 +3220,40 @@ static int splits_256x128(int M, int N, int K, size_t ws_bytes) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Row scales of the fp16 form (H3, az_x3.h split2s): one wave per row, s[r] = 2^e with
-// max_k |X[r][k]| * s in [2^(T-1), 2^T) (s = 1 for an all-zero or non-finite row: a NaN / inf then
-// reaches the outputs as in fp32), out[rows + r] = 1 / s (exact).  e is kept within +-120 so s
-// and 1/s are normal floats.
+// Row scales of the fp16 form (H3, az_x3.h split2s): one 256-thread block per row, s[r] = 2^e
+// with max_k |X[r][k]| * s in [2^(T-1), 2^T) (s = 1 for an all-zero or non-finite row: a NaN / inf
+// then reaches the outputs as in fp32), out[rows + r] = 1 / s (exact).  e is kept within +-120 so
+// s and 1/s are normal floats.  Every lane issues its (up to 4) float4 loads of a 4096-column
+// chunk before the first maximum: one HBM round trip per chunk (a wave per row walking the row
+// one float4 per lane at a time took 5.7 us at M = 512, K = 3136 -- 13 dependent round trips).
 __global__ __launch_bounds__(256) void row_scale_kernel(const float* __restrict__ X, int rows,
                                                         int cols, int ld, int T,
                                                         float* __restrict__ out) {
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  __shared__ float wm[4];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   if (r >= rows) return;
   const float* x = X + (size_t)r * ld;
   float m = 0.f;
-  const int c4 = cols & ~3;
-  for (int c = lane * 4; c < c4; c += 256) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(x + c);
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  const int c4 = (reinterpret_cast<uintptr_t>(x) & 15) == 0 ? cols & ~3 : 0;
+  constexpr int U = 4;
+  for (int c0 = tid * 4; c0 < c4; c0 += 256 * 4 * U) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u * 256 * 4;
+      v[u] = c < c4 ? *reinterpret_cast<const f32x4*>(x + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u][0]), fabsf(v[u][1])), fmaxf(fabsf(v[u][2]), fabsf(v[u][3]))));
   }
-  for (int c = c4 + lane; c < cols; c += 64) m = fmaxf(m, fabsf(x[c]));
+  for (int c = c4 + tid; c < cols; c += 256) m = fmaxf(m, fabsf(x[c]));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if (lane == 0) {
+  if (lane == 0) wm[tid >> 6] = m;
+  __syncthreads();
+  if (tid == 0) {
+    m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
     int e = 0;
     if (m > 0.f && m <= 3.4e38f) {
       int ex;
@@ -3295,7 +3309,7 @@ static const float* w_row_scales(const float* w, int n, int k, int ld, hipStream
     e = &g_wcache.back();
   }
   const int nxt = e->cur ^ 1;
-  hipLaunchKernelGGL(row_scale_kernel, dim3((n + 3) / 4), dim3(256), 0, s, w, n, k, ld, H3_TW,
+  hipLaunchKernelGGL(row_scale_kernel, dim3(n), dim3(256), 0, s, w, n, k, ld, H3_TW,
                      e->buf[nxt]);
   if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
   e->cur = nxt;
@@ -3323,7 +3337,7 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   auto h3_scales = [&]() {
     const float* sw = w_row_scales(a.B, a.N, a.K, a.ldb, s);
     if (!sw) return false;
-    hipLaunchKernelGGL(row_scale_kernel, dim3((a.M + 3) / 4), dim3(256), 0, s, a.A, a.M, a.K,
+    hipLaunchKernelGGL(row_scale_kernel, dim3(a.M), dim3(256), 0, s, a.A, a.M, a.K,
                        a.lda, H3_TA, sa_buf);
     a.sa = sa_buf;
     a.sw = sw;

@@ -3,7 +3,7 @@
 set -e
 tag=${1:-ab_bench}
 mkdir -p gpurun_out/$tag
-F="--steps 100 --warmup 20 --no-cpu --no-selfplay --no-train --no-b1 --no-grid --no-aggregate --no-agg-extra --large-batch 0"
+F="--steps 200 --warmup 200 --no-cpu --no-selfplay --no-train --no-b1 --no-grid --no-aggregate --no-agg-extra --large-batch 0"
 for i in 1 2 3; do
   for lib in base new; do
     if [ $lib = base ]; then export AZ_AB_LIB=libaz_hip_base.so; else unset AZ_AB_LIB; fi
