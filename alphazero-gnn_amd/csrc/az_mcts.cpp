@@ -3,7 +3,7 @@
 // One tree per game slot: an open-addressing table from the 128-bit board key (two 64-bit
 // occupancy masks, +1 and -1 stones) to nodes; per-node edge arrays (prior, visit count,
 // typed Q) are allocated when a node first becomes a leaf (Vs, MCTS.py:163-165).  A search is
-// a descent recorded as a path of (node, action) and backed up once its value is known
+// a descent recorded as a path of (node, edge) and backed up once its value is known
 // (terminal: immediately; new leaf: when the batched network result is fed back).
 //
 // Numeric parity with the reference (MCTS.py under NumPy 2 / NEP 50):
@@ -16,6 +16,7 @@
 #include "../../include/az_mcts.h"
 
 #include <algorithm>
+#include <new>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -313,7 +314,9 @@ struct Episode {
 };
 
 // ----------------------------------------------------------------------------- trees
-struct Node {
+// One cache line per node (alignas): a 56-byte node straddled two lines at most indices, and the
+// descent's prefetch brought in only the first.
+struct alignas(64) Node {
   Key key;
   Val es;            // Es[s]
   int32_t edge;      // offset / A into the edge pools; -1 until Vs[s] exists
@@ -335,11 +338,37 @@ struct Edge {
   uint8_t V;       // valid move
 };
 
+// 64-byte aligned storage for the edge pool: a node's A edges (8 x 32 B for Connect4 7x7) then
+// occupy whole cache lines instead of one more, straddled, line per node.
+template <class T>
+struct Aligned64 {
+  using value_type = T;
+  Aligned64() = default;
+  template <class U>
+  Aligned64(const Aligned64<U>&) {}
+  T* allocate(size_t n) {
+    return static_cast<T*>(::operator new(n * sizeof(T), std::align_val_t(64)));
+  }
+  void deallocate(T* p, size_t) { ::operator delete(p, std::align_val_t(64)); }
+  template <class U>
+  bool operator==(const Aligned64<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const Aligned64<U>&) const { return false; }
+};
+
+// Transposition table slot: the key is stored beside the node id, so a probe compares keys in
+// the slot's own cache line instead of loading the node (a second dependent miss per probe).
+struct HSlot {
+  Key key;
+  int32_t id;      // -1 = empty
+  int32_t pad;
+};
+
 struct Tree {
   std::vector<Node> nodes;
-  std::vector<int32_t> table;   // open addressing, -1 = empty
+  std::vector<HSlot> table;     // open addressing
   uint64_t mask = 0;
-  std::vector<Edge> EP;         // edge pool, A entries per allocated node
+  std::vector<Edge, Aligned64<Edge>> EP;   // edge pool, A entries per allocated node
   int32_t edges = 0;
   int32_t epoch = 1;
   // search state
@@ -347,7 +376,7 @@ struct Tree {
   int32_t root_id = -1;         // node of `root` once looked up (set_root invalidates it)
   int remaining = 0;
   int pending_leaf = -1;                      // node waiting for the network
-  std::vector<std::pair<int32_t, int32_t>> path;
+  std::vector<std::pair<int32_t, int32_t>> path;   // (node, its chosen edge's index in EP)
   int64_t nsa_total = 0, ps_count = 0;
   int64_t cache_hits = 0;                     // leaves expanded from az_mcts_cache_put rows
   bool pending_std = false;                   // episode mode: waiting for the root's predict
@@ -355,7 +384,7 @@ struct Tree {
 
   void clear() {
     nodes.clear();
-    table.assign(1024, -1);
+    table.assign(1024, HSlot{{0, 0}, -1, 0});
     mask = 1023;
     EP.clear();
     edges = 0;
@@ -376,19 +405,22 @@ struct Tree {
   int32_t find(const Key& k) const {
     if (table.empty()) return -1;
     for (uint64_t h = khash(k) & mask;; h = (h + 1) & mask) {
-      int32_t i = table[h];
-      if (i < 0) return -1;
-      if (nodes[i].key == k) return i;
+      const HSlot& e = table[h];
+      if (e.id < 0) return -1;
+      if (e.key == k) return e.id;
     }
   }
 
+  // the slot a lookup of k starts at (advance_group prefetches it a step ahead)
+  const HSlot* home(const Key& k) const { return table.empty() ? nullptr : &table[khash(k) & mask]; }
+
   void grow() {
-    std::vector<int32_t> t(table.size() * 2, -1);
+    std::vector<HSlot> t(table.size() * 2, HSlot{{0, 0}, -1, 0});
     uint64_t m = t.size() - 1;
     for (int32_t i = 0; i < (int32_t)nodes.size(); ++i) {
       uint64_t h = khash(nodes[i].key) & m;
-      while (t[h] >= 0) h = (h + 1) & m;
-      t[h] = i;
+      while (t[h].id >= 0) h = (h + 1) & m;
+      t[h] = HSlot{nodes[i].key, i, 0};
     }
     table.swap(t);
     mask = m;
@@ -398,9 +430,9 @@ struct Tree {
     if (table.empty()) clear();
     uint64_t h = khash(k) & mask;
     for (;; h = (h + 1) & mask) {
-      int32_t i = table[h];
-      if (i < 0) break;
-      if (nodes[i].key == k) return i;
+      const HSlot& e = table[h];
+      if (e.id < 0) break;
+      if (e.key == k) return e.id;
     }
     Node nd;
     nd.key = k;
@@ -412,7 +444,7 @@ struct Tree {
     nd.has_ns = nd.expanded = 0;
     int32_t id = (int32_t)nodes.size();
     nodes.push_back(nd);
-    table[h] = id;
+    table[h] = HSlot{k, id, 0};
     if ((uint64_t)nodes.size() * 2 > table.size()) grow();
     return id;
   }
@@ -522,12 +554,10 @@ int select_action(const az_mcts* m, const Tree& t, const Node& nd) {
 }
 
 void backup(az_mcts* m, Tree& t, Val v) {
-  const int A = m->R.A;
+  (void)m;
   for (size_t i = t.path.size(); i-- > 0;) {
     Node& nd = t.nodes[t.path[i].first];
-    int a = t.path[i].second;
-    size_t e = (size_t)nd.edge * A + a;
-    Edge& ed = t.EP[e];
+    Edge& ed = t.EP[(size_t)t.path[i].second];
     if (ed.qtag != T_NONE) {
       const Val q = div_n(add(mul_n(ed.N, Val{ed.qx, ed.qtag}), v), (long)ed.N + 1);
       ed.qx = q.x;
@@ -568,9 +598,11 @@ inline void prefetch_edges(const Tree& t, int32_t edge, int A) {
 }
 
 void advance_group(az_mcts* m, Tree* const* ts, int n) {
-  enum : uint8_t { START, NODE, SELECT, DONE };
+  enum : uint8_t { START, NODE, SELECT, LOOKUP, DONE };
   const int A = m->R.A;
   int32_t id[kGroup];
+  Key nkey[kGroup];        // LOOKUP: the child state whose table slot was prefetched
+  int32_t eidx[kGroup];    // ... and the edge that will point at it
   uint8_t ph[kGroup];
   int live = 0;
   for (int i = 0; i < n; ++i) {
@@ -617,22 +649,31 @@ void advance_group(az_mcts* m, Tree* const* ts, int n) {
           }
           break;
         }
-        default: {                               // SELECT
+        case SELECT: {
           const Node& nd = t.nodes[id[i]];
           const int a = select_action(m, t, nd);
           if (a < 0) {                           // MCTS.py:220-221
             finish(i, t, vint(0));
             break;
           }
-          t.path.emplace_back(id[i], a);
           const size_t e = (size_t)nd.edge * A + a;
-          int32_t child = t.EP[e].C;
-          if (child < 0) {
-            Key nk;
-            m->R.next(nd.key, a, &nk);
-            child = t.find_or_add(nk, m->R);     // may grow t.nodes: nd is not used after this
-            t.EP[e].C = child;
+          t.path.emplace_back(id[i], (int32_t)e);
+          const int32_t child = t.EP[e].C;
+          if (child < 0) {                       // first visit of this edge: look the child state
+            m->R.next(nd.key, a, &nkey[i]);      // up next pass, its table slot prefetched now
+            eidx[i] = (int32_t)e;
+            if (const HSlot* h = t.home(nkey[i])) __builtin_prefetch(h);
+            ph[i] = LOOKUP;
+            break;
           }
+          id[i] = child;
+          prefetch_node(t, child);
+          ph[i] = NODE;
+          break;
+        }
+        default: {                               // LOOKUP
+          const int32_t child = t.find_or_add(nkey[i], m->R);   // may grow t.nodes
+          t.EP[(size_t)eidx[i]].C = child;
           id[i] = child;
           prefetch_node(t, child);
           ph[i] = NODE;
@@ -1139,6 +1180,17 @@ int collect_impl(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int thread
   for (int gi = 0; gi < ngroups; ++gi) {
     const int s0 = gi * kGroup, s1 = std::min(S, s0 + kGroup);
     if (fr) {
+      // the group's backups touch every node and edge on each fed slot's path, last written a
+      // round ago (often by another thread): their lines are requested for all slots first
+      for (int s = s0; s < s1; ++s)
+        if (fr->row_of[s] >= 0) {
+          const Tree& t = m->trees[s];
+          if (t.pending_leaf >= 0) prefetch_node(t, t.pending_leaf);
+          for (const auto& pe : t.path) {
+            prefetch_node(t, pe.first);
+            __builtin_prefetch(&t.EP[(size_t)pe.second]);
+          }
+        }
       for (int s = s0; s < s1; ++s)
         if (fr->row_of[s] >= 0)
           feed_row(m, m->trees[s], fr->row_of[s], fr->pi, fr->v, fr->gpi, fr->gv, false);
@@ -1234,11 +1286,12 @@ int az_mcts_feed_collect(az_mcts* m, int count, const float* pi, const float* v,
   // here, while nothing has changed yet (a later plain az_mcts_feed still matches last_order):
   // every slot that is fed, searching or inside an episode can hand out one leaf
   int may = 0;
-  for (size_t s = 0; s < m->trees.size(); ++s) {
-    const Tree& t = m->trees[s];
-    may += m->row_of[s] >= 0 || t.ep.phase != E_IDLE || searching(t) || t.pending_leaf >= 0 ||
-           t.pending_std;
-  }
+  if (cap < (int)m->trees.size())          // (a cap of every slot needs no count)
+    for (size_t s = 0; s < m->trees.size(); ++s) {
+      const Tree& t = m->trees[s];
+      may += m->row_of[s] >= 0 || t.ep.phase != E_IDLE || searching(t) || t.pending_leaf >= 0 ||
+             t.pending_std;
+    }
   if (cap < may)
     return fail(AZM_EINVAL, "az_mcts_feed_collect: cap " + std::to_string(cap) +
                                 " smaller than the " + std::to_string(may) +

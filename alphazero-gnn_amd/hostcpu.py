@@ -36,6 +36,39 @@ def cgroup_cpu_quota():
     return None
 
 
+# True when engine_omp_defaults set OMP_WAIT_POLICY (the CPU baselines' child drops it again)
+_SET_WAIT_POLICY = False
+
+
+def engine_omp_defaults():
+    """OpenMP settings for the self-play engine's thread pool, set only where the user set
+    nothing, and only effective before the OpenMP runtime starts (call before importing torch):
+    OMP_WAIT_POLICY=PASSIVE -- idle workers sleep instead of spinning between the engine's
+    parallel regions.  Measured on the GPU box (profiles/r04i_spwait.jsonl): the self-play leg
+    used 90 CPU-s and was throttled by the 16-CPU cgroup quota in ~35 of ~70 periods with
+    spinning workers, 35 CPU-s and never throttled with sleeping ones, at the same games/s --
+    cores another rank of the node can use."""
+    global _SET_WAIT_POLICY
+    if "OMP_WAIT_POLICY" not in os.environ:
+        os.environ["OMP_WAIT_POLICY"] = "PASSIVE"
+        _SET_WAIT_POLICY = True
+
+
+def cgroup_cpu_stat():
+    """The cgroup's CPU accounting (v2 cpu.stat: usage_usec, nr_periods, nr_throttled,
+    throttled_usec ...) as ints, {} when not readable.  Deltas around a run show whether a CPU
+    quota throttled it (every thread of the cgroup stops for the rest of a period once the
+    quota is spent)."""
+    out = {}
+    for line in (_read("/sys/fs/cgroup/cpu.stat") or "").splitlines():
+        k, _, v = line.partition(" ")
+        try:
+            out[k] = int(v)
+        except ValueError:
+            pass
+    return out
+
+
 def affinity():
     try:
         return sorted(os.sched_getaffinity(0))

@@ -25,6 +25,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 if HERE not in sys.path:
     sys.path.insert(0, HERE)
 
+import hostcpu  # noqa: E402
+
+hostcpu.engine_omp_defaults()    # before the OpenMP runtime starts (torch, the engine)
+
 from Arena import Arena  # noqa: E402
 from Coach import Coach  # noqa: E402
 from MCTS import MCTS  # noqa: E402

@@ -24,6 +24,9 @@ import nn_fallback
 EPS = 1e-8
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "azhip", "libaz_mcts.so")
+# AZ_AB_MCTS_LIB=<file in azhip/>: an A/B build of the engine at another revision (tools/)
+if os.environ.get("AZ_AB_MCTS_LIB"):
+    LIB_PATH = os.path.join(HERE, "azhip", os.path.basename(os.environ["AZ_AB_MCTS_LIB"]))
 
 GAME_CONNECT4, GAME_TICTACTOE = 0, 1
 TAG_NONE, TAG_INT, TAG_FLOAT, TAG_F32 = -1, 0, 1, 2

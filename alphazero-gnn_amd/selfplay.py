@@ -339,6 +339,7 @@ class _EpisodeLane:
         self.k = 0
         self.rounds = self.rows = 0
         self.assemble_s = 0.0
+        self.collect_s = 0.0       # main-thread time inside the engine's (feed_)collect calls
         self.assembler, self.pending = None, []
         self.fed = None            # rows of the last batch, fed by the next gather
 
@@ -377,12 +378,15 @@ class _EpisodeLane:
         self.pending = []
 
     def gather(self):
+        import time
+        t = time.perf_counter()
         if self.fed is not None:        # last round's rows are fed inside this collect
             pi, v, gpi, gv = self.fed
             self.fed = None
             self.k = self.eng.feed_collect(self.k, pi, v, gpi, gv, self.threads)
         else:
             self.k = self.eng.collect(self.threads)
+        self.collect_s += time.perf_counter() - t
         if not self.k:
             return None
         self.rounds += 1
@@ -449,7 +453,7 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
     streams = _lane_streams(nnet, use_gnn, lanes)
     inflight = [None] * lanes
     t0 = time.perf_counter()
-    t_wait = 0.0
+    t_wait = t_launch = 0.0
     idle = 0
     i = 0
     try:
@@ -466,7 +470,9 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
             if lane.live():
                 boards = lane.gather()
                 if boards is not None:
+                    tl = time.perf_counter()
                     inflight[i] = _launch(nnet, boards, use_gnn, streams[i])
+                    t_launch += time.perf_counter() - tl
                     idle = 0
                 else:
                     lane.deliver(None)
@@ -486,7 +492,8 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
         stats["assemble_drain_s"] = drain_s
         stats.update(rounds=sum(ln.rounds for ln in L), rows=sum(ln.rows for ln in L),
                      net_s=t_wait, host_s=time.perf_counter() - t0 - t_wait, lanes=lanes,
-                     assemble_s=sum(ln.assemble_s for ln in L))
+                     assemble_s=sum(ln.assemble_s for ln in L),
+                     collect_s=sum(ln.collect_s for ln in L), launch_s=t_launch)
     return results
 
 
@@ -496,8 +503,10 @@ def _lane_streams(nnet, use_gnn, lanes):
     still on the GPU; every stream first waits for the work already queued on the current
     stream (parameter updates).  [None] * lanes otherwise (everything on the current stream)."""
     import inspect
+    import os
     fn = getattr(nnet, "predict_both_async" if use_gnn else "predict_batch_async", None)
-    if lanes < 2 or fn is None or "stream" not in inspect.signature(fn).parameters:
+    if lanes < 2 or fn is None or "stream" not in inspect.signature(fn).parameters or \
+            os.environ.get("AZ_SP_ONE_STREAM") == "1":
         return [None] * lanes
     import torch
     if not torch.cuda.is_available():

@@ -41,6 +41,9 @@ def parse():
     # step, warmup 200 -> 156 us, unchanged at 500 timed steps)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--settle-ms", type=float, default=60.0,
+                    help="untimed full steps before the warmup until this much wall time has "
+                         "passed (GPU clock ramp); 0 = none")
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample (rank 0, N=1 only)")
@@ -159,6 +162,9 @@ def run_cpu_baselines(cpus, seconds, B, sims, selfplay, grid_seconds):
     spec = {"cpus": list(cpus), "seconds": seconds, "B": B, "sims": sims, "selfplay": selfplay,
             "grid_seconds": grid_seconds}
     env = dict(os.environ, OMP_NUM_THREADS=str(len(cpus)))
+    import hostcpu
+    if hostcpu._SET_WAIT_POLICY:      # the engine's setting, not the user's: torch's default
+        env.pop("OMP_WAIT_POLICY", None)
     r = subprocess.run([sys.executable, os.path.abspath(__file__), CPU_CHILD, json.dumps(spec)],
                        env=env, capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
@@ -542,6 +548,7 @@ def selfplay_leg(W, G, args, device, rank):
     """Self-play games/s: `sp_games` Connect4 GNN games per GPU played in lock step (native
     MCTS engine on the host, one batched predict_both per round on the GPU)."""
     import torch
+    import hostcpu
     from connect4.Connect4GNN import Connect4GNNWrapper
     from connect4.Connect4Game import Connect4Game
     from selfplay import play_episodes_engine
@@ -557,10 +564,14 @@ def selfplay_leg(W, G, args, device, rank):
     import nn_fallback
     nn_fallback.reset()
     st = {}
+    cg0 = hostcpu.cgroup_cpu_stat()
     t0 = time.perf_counter()
     out = play_episodes_engine(Connect4Game(7), net, sa, eps, seeds, args.sp_games,
                                threads=args.sp_threads, stats=st, lanes=lanes)
     dt = time.perf_counter() - t0
+    cg1 = hostcpu.cgroup_cpu_stat()
+    cg = {k: cg1[k] - cg0.get(k, 0) for k in ("usage_usec", "nr_periods", "nr_throttled",
+                                              "throttled_usec") if k in cg1}
     failures = nn_fallback.total()
     if failures:     # degraded play (uniform priors, v = 0) is not a throughput to report
         raise RuntimeError(f"self-play leg: {failures} network fallbacks {nn_fallback.counts()}")
@@ -569,7 +580,10 @@ def selfplay_leg(W, G, args, device, rank):
     return dt, {"games": len(out), "moves": moves, "evals": st["rows"], "rounds": st["rounds"],
                 "nn_failures": failures, "agreement": agreement,
                 "net_wait_s": round(st["net_s"], 3), "host_s": round(st["host_s"], 3),
-                "assemble_s": round(st.get("assemble_s", 0.0), 3)}
+                "assemble_s": round(st.get("assemble_s", 0.0), 3),
+                "collect_s": round(st.get("collect_s", 0.0), 3),
+                "launch_s": round(st.get("launch_s", 0.0), 3),
+                "cgroup_cpu": cg or None}
 
 
 class _HostOnlyNet:
@@ -781,6 +795,7 @@ def main():
     import hostcpu
     visible_cpus = hostcpu.affinity()
     pin = hostcpu.pin_rank_to_gpu_numa(int(os.environ.get("LOCAL_RANK", "0")))
+    hostcpu.engine_omp_defaults()
     if not args.sp_threads:
         args.sp_threads = hostcpu.threads_per_rank()
     import torch
@@ -839,6 +854,17 @@ def main():
     torch.cuda.synchronize()
     assert torch.equal(pi, pi_ref) and torch.equal(v, v_ref)
 
+    # the GPU's clock ramps over the first tens of ms of sustained work (DPM): before the W
+    # warmup steps, full steps run until `--settle-ms` of wall time has passed, so that even a
+    # short run (the driver's --warmup 5 --steps 20) times the steady state a loaded evaluator
+    # runs at (profiles/r03v_warmup_probe.jsonl: 10 warmup steps -> 177 us per step, 200 -> 156)
+    settle_steps, ts = 0, time.perf_counter()
+    while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
+        for _ in range(20):
+            step()
+        settle_steps += 20
+        torch.cuda.synchronize()
+    settle_ms = (time.perf_counter() - ts) * 1e3
     for _ in range(args.warmup):
         step()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
@@ -954,6 +980,8 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "board evals/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "clock_settle": {"ms": round(settle_ms, 1), "steps": settle_steps,
+                             "note": "untimed full steps before the warmup (GPU clock ramp)"},
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (uniform random {-1,0,1} 7x7 boards; PCG64 random-init weights "

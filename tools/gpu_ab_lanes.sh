@@ -1,0 +1,14 @@
+# Self-play leg vs the number of lock-step lanes (and engine base/new), one GPU session.
+#   bash tools/gpu_ab_lanes.sh <tag>
+set -e
+tag=${1:-ab_lanes}
+mkdir -p gpurun_out/$tag
+F="--steps 5 --warmup 2 --no-cpu --no-train --no-b1 --no-grid --no-aggregate --no-agg-extra --large-batch 0"
+for i in 1 2; do
+  for lanes in 2 3 4; do
+    for lib in base new; do
+      if [ $lib = base ]; then export AZ_AB_MCTS_LIB=libaz_mcts_base.so; else unset AZ_AB_MCTS_LIB; fi
+      timeout -k 10 200 python -u bench.py $F --sp-lanes $lanes 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); s=d['selfplay']; print(json.dumps({'lanes':$lanes,'lib':'$lib','games_per_s':s['games_per_s'],'net_wait_s':s['net_wait_s'],'host_s':s['host_s'],'collect_s':s.get('collect_s'),'launch_s':s.get('launch_s'),'rounds':s['rounds']}))" >> gpurun_out/$tag/ab.jsonl
+    done
+  done
+done
