@@ -44,7 +44,7 @@ def engine_omp_defaults():
     """OpenMP settings for the self-play engine's thread pool, set only where the user set
     nothing, and only effective before the OpenMP runtime starts (call before importing torch):
     OMP_WAIT_POLICY=PASSIVE -- idle workers sleep instead of spinning between the engine's
-    parallel regions.  Measured on the GPU box (profiles/r04i_spwait.jsonl): the self-play leg
+    parallel regions.  Measured on the GPU box (profiles/r04i/spwait_ab.jsonl): the self-play leg
     used 90 CPU-s and was throttled by the 16-CPU cgroup quota in ~35 of ~70 periods with
     spinning workers, 35 CPU-s and never throttled with sleeping ones, at the same games/s --
     cores another rank of the node can use."""

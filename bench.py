@@ -532,7 +532,7 @@ def _pmc_selfplay_gemm(M):
         d = json.load(open(os.path.join(ROOT, "profiles", "pmc.json")))["gemm_selfplay"]
         r = d["by_M"][str(M)]["csk"]
         return {"traffic": r["hbm_bytes_per_dispatch"], "traffic_algorithmic": r["algorithmic_bytes"],
-                "l2_hit": r.get("l2_hit"), "traffic_run": d.get("tag")}
+                "l2_hit": r.get("l2_hit"), "traffic_run": r.get("tag", d.get("tag"))}
     except (OSError, KeyError, ValueError):
         return None
 

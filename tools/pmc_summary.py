@@ -46,24 +46,28 @@ def main(d, tag):
             w.writerow([name, len(fe), round(fa, 1), round(wa, 1), int((2 * fa + wa) * 1024)])
 
     def call_bytes(rows, tile_pred):
-        """per az_gemm_f32 call: the tile kernel + the reduce that immediately follows it"""
-        tile, red = [], []
+        """per az_gemm_f32 call: the tile kernel + the reduce that immediately follows it (+ from
+        round 4 the A row-scale launch right before it: the fp16 form, az_gemm.hip)"""
+        tile, red, scl = [], [], []
         for i, (_, name, kb, _) in enumerate(rows):
             nxt = rows[i + 1][1] if i + 1 < len(rows) else ""
+            prv = rows[i - 1][1] if i > 0 else ""
             # output_transform.0 = the tile kernel followed by its splitk_reduce_kernel (the
             # second GEMM's slabs go to splitk_heads_partial_kernel instead)
             if tile_pred(name) and "splitk_reduce" in nxt:
                 tile.append(kb)
                 red.append(rows[i + 1][2])
+                scl.append(rows[i - 1][2] if "row_scale_kernel" in prv else 0.0)
         n = max(1, len(tile))
-        return sum(tile) / n, sum(red) / n, len(tile)
+        return sum(tile) / n, sum(red) / n, len(tile), sum(scl) / n
 
     # the forward Linear path of the bench GEMMs (gemm_x3 from r02m on)
     is_fwd_gemm = lambda n: "gemm_f32_glds" in n or "gemm_x3" in n
-    ft, fr, nf = call_bytes(fetch, is_fwd_gemm)
-    wt, wr, _ = call_bytes(write, is_fwd_gemm)
+    ft, fr, nf, fs = call_bytes(fetch, is_fwd_gemm)
+    wt, wr, _, ws = call_bytes(write, is_fwd_gemm)
     gemm_tile = int((2 * ft + wt) * 1024)
     gemm_red = int((2 * fr + wr) * 1024)
+    gemm_scale = int((2 * fs + ws) * 1024)
     # the 512-grid shard launches (grid = V * 8 lanes); the 4096-grid full-config ones excluded
     shard = 512 * 1024 * 8
     agg = [kb for _, n, kb, gs in fetch if "aggregate_small_kernel" in n and gs == shard]
@@ -76,12 +80,15 @@ def main(d, tag):
                   f"(tools/gpu_profile.sh {tag}); per-kernel averages over all dispatches; "
                   f"bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE reports "
                   f"half of wide reads, MI355X_MICROARCH.md HBM section)",
-        "gemm": {"kernel": "az_gemm_f32 output_transform.0 call (%s tile kernel + "
-                           "splitk_reduce4_kernel)" % ("gemm_x3" if any(
-                               "gemm_x3" in r[1] for r in fetch) else "gemm_f32_glds2"),
+        "gemm": {"kernel": "az_gemm_f32 output_transform.0 call (%s%s tile kernel + "
+                           "splitk_reduce4_kernel)" % (
+                               "row_scale_kernel + " if gemm_scale else "",
+                               "gemm_x3" if any("gemm_x3" in r[1] for r in fetch)
+                               else "gemm_f32_glds2"),
                  "dispatches": nf,
-                 "hbm_bytes_per_launch": gemm_tile + gemm_red,
+                 "hbm_bytes_per_launch": gemm_tile + gemm_red + gemm_scale,
                  "gemm_kernel_bytes": gemm_tile, "reduce_kernel_bytes": gemm_red,
+                 "row_scale_kernel_bytes": gemm_scale,
                  "algorithmic_bytes": 4 * (B * F + F * F + F + B * F), "tag": tag},
     }
     if agg and aggw:
