@@ -20,15 +20,15 @@
 //   but x_out leaves the CU.  The weights (two fp16 planes in MFMA fragment order, each row scaled
 //   by its power of two, split once per launch) stream from L2.
 //
-//   MFMA operands that come from LDS are stored ALREADY split: x rows enter the ring as three fp16
-//   planes of x s (s the row's power-of-two scale, 1/s kept per ring slot; the first two planes
-//   are the MFMA's two terms), and each destination's agg is written as its two planes over its
-//   own (consumed) Pt row.  (h + m + l) / s rebuilds x exactly while l is a normal fp16, and
-//   within 2^-39 of the row's largest |x| otherwise: the aggregation and the residual use that;
-//   a destination without in-edges copies x from HBM, so its output is x bit for bit
-//   (gnn_utils.py:35-36).  update_net.0's output (u1) and output_transform's operands are split
-//   in the waves, scaled per 64-row tile.  Every GEMM's accumulators are multiplied back by
-//   1 / (s_row s_w) (exact) before use.
+//   MFMA operands that come from LDS are stored ALREADY split: x rows enter the ring as the two
+//   fp16 planes of x s (s the row's power-of-two scale, 1/s kept per ring slot), and each
+//   destination's agg is written as its two planes over its own (consumed) Pt row.  The
+//   aggregation takes its sources from the planes ((h + l) / s, within 2^-22 |x|); the residual
+//   x + gate * u2 reads x itself (global memory, L2-resident: the rows entered the ring a tile
+//   earlier), so a destination without in-edges gets x bit for bit (gnn_utils.py:35-36).
+//   update_net.0's output (u1) and output_transform's operands are split in the waves, scaled
+//   per 64-row tile.  Every GEMM's accumulators are multiplied back by 1 / (s_row s_w) (exact)
+//   before use.
 //
 // Edges are never dropped: a destination with any in-degree is aggregated completely, and a
 // source outside the window (a graph that is not banded as the caller claimed) takes a slow
@@ -50,7 +50,7 @@ constexpr int BNT = 512;      // threads: 8 waves, one block per CU
 constexpr int PSS = 132;      // Pt / agg-plane / [gate | u1] row stride (floats), = 4 (mod 64)
 constexpr int PSRS = 128;     // Ps ring row stride: every row starts on bank 0, and the two
                               // destinations of a 16-lane read group take opposite halves
-constexpr int XRS = 3 * BF;   // ring row: three planes of 64 fp16 (384 B), 16-B chunks swizzled
+constexpr int XRS = 2 * BF;   // ring row: two planes of 64 fp16 (256 B), 16-B chunks swizzled
 
 // weight planes [2][WTOT] fp16 in MFMA-fragment order: a matrix W [N][K] (nn.Linear [out][in])
 // is stored as (N / 32) x (K / 16) blocks of 512 fp16, block (nb, ks) holding the B operand of
@@ -122,11 +122,20 @@ __device__ __forceinline__ float absmax8(const f32x4 (&v)[2]) {
   return m;
 }
 
-// maximum over the 64 lanes of a wave
+// maximum over the 64 lanes of a wave (values >= 0): DPP within each 16-lane row (quad_perm
+// [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the four rows' results by readlane --
+// no LDS round trips (__shfl_xor is a ds_bpermute and a wait per step)
 __device__ __forceinline__ float wave_absmax(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  v = fmaxf(v, dpp<0x140>(v));
+  const int b = __builtin_bit_cast(int, v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
 
 // 8 consecutive weights of one row -> their two fp16 planes, the row scaled by its power of two
@@ -234,10 +243,12 @@ __device__ __forceinline__ int acc_row(int r, int lane) {
   return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
 }
 
-// ring row `slot`, plane pl, 16-B chunk c (8 features) -> bf16 offset; the chunk index is
-// XOR-swizzled by (slot >> 1) & 7 so the 32 rows of an MFMA fragment read hit distinct banks
+// ring row `slot`, plane pl, 16-B chunk c (8 features) -> fp16 offset; the row's 16 chunk
+// positions (both planes) are XOR-swizzled by slot & 15, so the 16 rows a 16-lane group of an
+// MFMA fragment read touches (one plane, one chunk) land on 16 distinct 16-B bank positions of
+// the 256-B row stride
 __device__ __forceinline__ int xr_off(int slot, int pl, int c) {
-  return slot * XRS + pl * BF + ((c ^ ((slot >> 1) & 7)) << 3);
+  return slot * XRS + ((((pl << 3) | c) ^ (slot & 15)) << 3);
 }
 
 // the accumulator rows of register r relative to the lane's first (acc_row(r, lane) - acc_row(0,
@@ -321,30 +332,30 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     const int slot = (r0 + (tid >> 3)) & (RING - 1);
     float inv;
     const float sc = h3_scale(max8(absmax8(v)), 14, &inv);   // the row's 8 threads agree
-    u32x4 o[3];
-    split3h(v[0], v[1], sc, o);
+    u32x4 o[2];
+    split2s(v[0], v[1], sc, o);
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < 2; ++pl)
       *reinterpret_cast<u32x4*>(XR + xr_off(slot, pl, tid & 7)) = o[pl];
     if ((tid & 7) == 0) XSI[slot] = inv;
   };
-  // x of a ring row, features 8c .. 8c + 7, rebuilt from its three fp16 planes and 1 / s
-  auto x_planes = [](const u32x4& h, const u32x4& m, const u32x4& l, float inv, f32x4 (&v)[2]) {
+  // x of a ring row, features 8c .. 8c + 7, from its two fp16 planes and 1 / s: (h + l) / s is
+  // within 2^-22 |x| (2^-39 of the row maximum below l's normal range) -- the aggregation's
+  // sources; the residual reads x itself from global memory
+  auto x_planes = [](const u32x4& h, const u32x4& l, float inv, f32x4 (&v)[2]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       // the dwords go through scalars: __builtin_bit_cast of an ext-vector ELEMENT (h[q])
       // compiles to a bit cast of element 0 for every q on this toolchain (ROCm 7.2 clang)
-      const unsigned hq = h[q], mq = m[q], lq = l[q];
-      const f16x2 hh = __builtin_bit_cast(f16x2, hq), mm = __builtin_bit_cast(f16x2, mq),
-                  ll = __builtin_bit_cast(f16x2, lq);
-      v[q >> 1][2 * (q & 1)] = (((float)hh[0] + (float)mm[0]) + (float)ll[0]) * inv;
-      v[q >> 1][2 * (q & 1) + 1] = (((float)hh[1] + (float)mm[1]) + (float)ll[1]) * inv;
+      const unsigned hq = h[q], lq = l[q];
+      const f16x2 hh = __builtin_bit_cast(f16x2, hq), ll = __builtin_bit_cast(f16x2, lq);
+      v[q >> 1][2 * (q & 1)] = ((float)hh[0] + (float)ll[0]) * inv;
+      v[q >> 1][2 * (q & 1) + 1] = ((float)hh[1] + (float)ll[1]) * inv;
     }
   };
   auto x_ring = [&](int slot, int c, f32x4 (&v)[2]) {
     x_planes(*reinterpret_cast<const u32x4*>(XR + xr_off(slot, 0, c)),
-             *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 1, c)),
-             *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 2, c)), XSI[slot], v);
+             *reinterpret_cast<const u32x4*>(XR + xr_off(slot, 1, c)), XSI[slot], v);
   };
   // A fragments straight from the ring planes: rows r0 + 32 mb + (lane & 31)
   auto ring_frag = [&](int r0) {
@@ -584,12 +595,12 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         const float rS = norm ? 1.f / S : 1.f;
         f32x4 g[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
         if constexpr (FAST) {
-          u32x4 xp[4][3];                   // the four sources' planes, all reads in flight
+          u32x4 xp[4][2];                   // the four sources' planes, all reads in flight
           float xi[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
+            for (int pl = 0; pl < 2; ++pl)
               xp[q][pl] = *reinterpret_cast<const u32x4*>(XR + xr_off(src[q] & (RING - 1), pl, ej));
             xi[q] = XSI[src[q] & (RING - 1)];
           }
@@ -597,7 +608,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
           for (int q = 0; q < 4; ++q) {
             const float wq = a[q] * rS;
             f32x4 v[2];
-            x_planes(xp[q][0], xp[q][1], xp[q][2], xi[q], v);
+            x_planes(xp[q][0], xp[q][1], xi[q], v);
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               g[0][c] = fmaf(wq, v[0][c], g[0][c]);
@@ -735,6 +746,15 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     //      x_out as two float4s (the MFMA layout would need 48 16-bit plane reads and 16 scattered
     //      4-byte stores per lane, on half the waves)
     float* const u2s = PSR + ((d0 - BR) & (RING - 1)) * PSRS;
+    // the residual's x rows, requested now (L2: they entered the ring a tile ago) and used after
+    // the u2 barrier: x_out is x + gate * u2 with x itself, not its fp16 planes
+    const int ri = tid >> 3, rc = tid & 7;     // row, features 8 rc .. 8 rc + 7
+    f32x4 xres[2];
+    {
+      const size_t xo = (size_t)min(d0 + ri, V - 1) * BF + 8 * rc;
+      xres[0] = *reinterpret_cast<const f32x4*>(x + xo);
+      xres[1] = *reinterpret_cast<const f32x4*>(x + xo + 4);
+    }
     if (wave < 4) {
       const int mb = wave >> 1, nb = wave & 1;
       float uinv;                         // u1's tile scale (the u1 waves' maxima, phase C)
@@ -762,23 +782,20 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     }
     __syncthreads();                      // u2 complete
     {
-      const int i = tid >> 3, c = tid & 7;   // row, features 8c .. 8c + 7
-      f32x4 xv[2];
-      x_ring((d0 + i) & (RING - 1), c, xv);
+      const int i = ri, c = rc;
       const f32x4* gp = reinterpret_cast<const f32x4*>(PT + i * PSS + 8 * c);
       const f32x4* up = reinterpret_cast<const f32x4*>(u2s + i * BF + 8 * c);
       const bool upd = DEG[i] > 0;
       f32x4 o[2];
       if (!upd) {                         // no in-edges: x itself, bit for bit (gnn_utils.py:35)
-        const size_t xo = (size_t)min(d0 + i, V - 1) * BF + 8 * c;
-        o[0] = *reinterpret_cast<const f32x4*>(x + xo);
-        o[1] = *reinterpret_cast<const f32x4*>(x + xo + 4);
+        o[0] = xres[0];
+        o[1] = xres[1];
       } else {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const f32x4 gv = gp[h], uv = up[h];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[h][e] = xv[h][e] + gv[e] * uv[e];
+          for (int e = 0; e < 4; ++e) o[h][e] = xres[h][e] + gv[e] * uv[e];
         }
       }
       if constexpr (OT) {                 // x_out's tile maximum: phase E's scale
