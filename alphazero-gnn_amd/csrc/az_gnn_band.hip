@@ -303,6 +303,10 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   __shared__ float XSI[RING];             // 1 / s of each ring row's fp16 planes
   __shared__ float AGSI[BT];              // 1 / s of each destination's agg planes
   __shared__ float TMX[2][8];             // per-wave maxima: u1 (C -> D), x_out / h (OT)
+  // update_net.2's two fp16 planes (fragment order), copied once per block: phase D reads its B
+  // fragments here, so waves 0-3 request the next phase's weights from L2 a phase earlier and
+  // the four D waves no longer fetch the same fragments twice
+  __shared__ __attribute__((aligned(16))) unsigned short WU2L[2 * BF * BF];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 31, hc = lane >> 5;          // fragment row, k half (8-element chunk)
   const int t0 = blockIdx.x * per, t1 = min(ntiles, t0 + per);
@@ -406,6 +410,12 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
 
   // prologue: the first tile's window [d0 - 32, d0 + 96) and the Ps of its first 64 rows
   {
+#pragma unroll
+    for (int j = tid; j < 2 * BF * BF / 8; j += BNT) {   // 16-B chunks of the two Wu2 planes
+      const int pl = j / (BF * BF / 8), o = (j % (BF * BF / 8)) * 8;
+      *reinterpret_cast<u32x4*>(WU2L + pl * BF * BF + o) =
+          *reinterpret_cast<const u32x4*>(W.planes + (size_t)pl * WTOT + WU2_OFF + o);
+    }
     const int d0 = t0 * BT;
     f32x4 v[2];
     load_rows(d0 - BR, v);
@@ -681,7 +691,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       constexpr int CAB = (ABL & 4) ? (ABL | 32) : ABL;
       if (kh == 0) {
         h3_mfma<2, 4, CAB>(acc, ring_frag(d0), bw);
-        load_w<4, ABL>(bw, wr, wl, wD);
+        load_w<4, ABL>(bw, wr, wl, OT ? wD + (OT0_OFF - WU2_OFF) : wA);   // D's come from LDS
       } else {
         h3_mfma<2, 4, CAB>(acc, [&](int mb, int ks, bf16x8 (&a)[2]) {
           const unsigned short* row = reinterpret_cast<const unsigned short*>(PT + (32 * mb + lr) * PSS);
@@ -764,6 +774,13 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       const float usc = h3_scale(um, 14, &uinv);
       f32x16 acc[1];
       zero(acc[0]);
+      bf16x8 bd[4][2];                    // update_net.2's fragments of this wave, from LDS
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          bd[ks][pl] = *reinterpret_cast<const bf16x8*>(WU2L + pl * BF * BF + (wD - WU2_OFF) +
+                                                         FRAG * ks + 8 * lane);
       h3_mfma<1, 4, (ABL & 8) ? (ABL | 32) : ABL>(acc, [&](int, int ks, bf16x8 (&a)[2]) {
         const float* u = PT + (32 * mb + lr) * PSS + BF + 16 * ks + 8 * hc;
         const f32x4 x0 = *reinterpret_cast<const f32x4*>(u);
@@ -772,8 +789,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         split2s(x0, x1, usc, o);
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl) a[pl] = __builtin_bit_cast(bf16x8, o[pl]);
-      }, bw);
-      load_w<4, ABL>(bw, wr, wl, OT ? wD + (OT0_OFF - WU2_OFF) : wA);
+      }, bd);
       const int n = 32 * nb + lr;
       const float ub = BS[2 * BF + n];
       const float ui = uinv * W.winv[WI_WU2 + n];

@@ -2,9 +2,9 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r04l
+O=gpurun_out/${TAG:-r04l}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -x -q -k "band or grid or layer_ot or fused or synth" --timeout 300 --timeout-method thread > $O/band_tests.log 2>&1 || { tail -30 $O/band_tests.log; exit 1; }
 tail -2 $O/band_tests.log
-bash tools/gpu_ab_band.sh r04l_band || exit 1
-cat gpurun_out/r04l_band/ab.log
+bash tools/gpu_ab_band.sh ${TAG:-r04l_band} || exit 1
+cat gpurun_out/${TAG:-r04l_band}/ab.log
