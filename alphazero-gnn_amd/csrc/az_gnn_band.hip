@@ -429,7 +429,10 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     __syncthreads();
     const int eb = RPS[t0 & 1][0], ne = RPS[t0 & 1][BT] - eb;
     if (tid < ne && ne <= BNT) CLS[t0 & 1][tid] = col[eb + tid];
-    if (wave >= 4) ps_rows(d0 - BR);
+    if (wave >= 4) {                      // the window's first 128 rows; later tiles' new
+      ps_rows(d0 - BR);                   // rows get theirs in the previous tile's phase D
+      ps_rows(d0 + BR);
+    }
   }
 
   // edge-phase lane roles: destination i (8 lanes), hidden units 4j + 32c (+0..3), features 8j..
@@ -454,7 +457,8 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       rp2 = rowptr[min(d0 + 2 * BT + min(tid, BT), V)];
     };
 
-    // ---- A: Pt (waves 0-3: wave = n-block) | Ps of rows [d0 + 32, d0 + 96) (waves 4-7)
+    // ---- A: Pt (waves 0-3: wave = n-block); the Ps of the window's new rows [d0 + 32, d0 + 96)
+    //      were computed by waves 4-7 during the previous tile's phase D
     if (wave < 4) {
       f32x16 acc[2];
       zero(acc[0]);
@@ -469,8 +473,6 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
           const int row = 32 * mb + acc_row(r, lane);
           PT[row * PSS + 32 * wave + lr] = acc[mb][r] * (XSI[(d0 + row) & (RING - 1)] * wi) + b1n;
         }
-    } else {
-      ps_rows(d0 + BR);
     }
     BSTAMP(1);
     __syncthreads();
@@ -745,17 +747,20 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       }
       um = wave_absmax(um);
       if (lane == 0) TMX[0][wave] = um;
+      // the next tile's new x rows [d0 + 96, d0 + 160) into the ring: their slots (rows
+      // [d0 - 32, d0 + 32)) were read for the last time by this phase's MFMAs, before the
+      // barrier above
+      if (has_next) store_rows(d0 + BT + BR, nextx);
     }
     __syncthreads();
     BSTAMP(7);
 
     // ---- D: x_out = x_d + gate * (u1 Wu2^T + bu2)  (waves 0-3: 32 x 32 each; u1 split here).
-    //      The MFMA waves park u2 = u1 Wu2^T + bu2 in the Ps ring's dead slots [d0 - 32, d0)
-    //      (contiguous, [64][64]); then all 8 waves apply the residual row by row: a thread per
-    //      (row, 8 features) reads x_d as three plane chunks, gate and u2 as float4s, and stores
-    //      x_out as two float4s (the MFMA layout would need 48 16-bit plane reads and 16 scattered
-    //      4-byte stores per lane, on half the waves)
-    float* const u2s = PSR + ((d0 - BR) & (RING - 1)) * PSRS;
+    //      Each MFMA wave replaces its gate elements in PT by gate * u2 (every element has one
+    //      owner); then all 8 waves apply the residual row by row: a thread per (row, 8 features)
+    //      adds x (global) to the products and stores x_out as two float4s (the MFMA layout would
+    //      need 16 scattered 4-byte loads and stores per lane, on half the waves).  Meanwhile
+    //      waves 4-7 compute the next tile's Ps rows into the ring's dead slots.
     // the residual's x rows, requested now (L2: they entered the ring a tile ago) and used after
     // the u2 barrier: x_out is x + gate * u2 with x itself, not its fp16 planes
     const int ri = tid >> 3, rc = tid & 7;     // row, features 8 rc .. 8 rc + 7
@@ -793,14 +798,16 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       const int n = 32 * nb + lr;
       const float ub = BS[2 * BF + n];
       const float ui = uinv * W.winv[WI_WU2 + n];
+      float* const pg = PT + opaque((32 * mb + acc_row(0, lane)) * PSS + n);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) u2s[(32 * mb + acc_row(r, lane)) * BF + n] = acc[0][r] * ui + ub;
+      for (int r = 0; r < 16; ++r) pg[acc_drow(r) * PSS] *= acc[0][r] * ui + ub;   // gate * u2
+    } else if (has_next) {
+      ps_rows(d0 + BT + BR);              // the next tile's new rows (their x stored in C)
     }
-    __syncthreads();                      // u2 complete
+    __syncthreads();                      // gate * u2 complete
     {
       const int i = ri, c = rc;
-      const f32x4* gp = reinterpret_cast<const f32x4*>(PT + i * PSS + 8 * c);
-      const f32x4* up = reinterpret_cast<const f32x4*>(u2s + i * BF + 8 * c);
+      const f32x4* gp = reinterpret_cast<const f32x4*>(PT + i * PSS + 8 * c);   // gate * u2
       const bool upd = DEG[i] > 0;
       f32x4 o[2];
       if (!upd) {                         // no in-edges: x itself, bit for bit (gnn_utils.py:35)
@@ -809,9 +816,9 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       } else {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x4 gv = gp[h], uv = up[h];
+          const f32x4 gu = gp[h];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[h][e] = xres[h][e] + gv[e] * uv[e];
+          for (int e = 0; e < 4; ++e) o[h][e] = xres[h][e] + gu[e];
         }
       }
       if constexpr (OT) {                 // x_out's tile maximum: phase E's scale
@@ -891,7 +898,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
           pf[acc_drow(r) * PSS] = acc[0][r] * wi + bias;
       }
     }
-    __syncthreads();                      // x_d rows read: their slots take the next rows
+    if constexpr (OT) __syncthreads();    // F's y rows in PT complete
     if constexpr (OT) {                   // y leaves row by row, two float4 per thread
       const int i = tid >> 3, c = tid & 7, d = d0 + i;
       if (d < V) {
@@ -902,10 +909,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       }
     }
     BSTAMP(9);
-    if (has_next) {
-      store_rows(d0 + BT + BR, nextx);
-      CLS[nxt][tid] = cln;                // used only when the next tile has <= 512 edges
-    }
+    if (has_next) CLS[nxt][tid] = cln;    // used only when the next tile has <= 512 edges
     if (tile + 2 < t1 && tid <= BT) RPS[cur][tid] = rp2;   // tile + 2 has this tile's parity
     __syncthreads();
     BSTAMP(10);
