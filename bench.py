@@ -150,7 +150,12 @@ def cpu_baselines_child(spec):
     out["gnn_b512"] = cpu_baseline(W, G, sec, B, threads)
     out["cnn_b512"] = cpu_baseline(W, G, min(sec, 5.0), B, threads, gnn=False)
     if spec.get("selfplay"):
-        out["selfplay"] = selfplay_cpu_baseline(W, G, spec["sims"], sec, threads)
+        # the batch-1 loop is latency-bound: timed on every visible core AND on one torch thread
+        # (the faster of the two is the baseline; profiles/r04_cpu_calibration.json
+        # selfplay_by_threads: one thread is as fast or faster for the reference too)
+        sps = max(sec, 20.0)              # room for one whole episode (~8-11 s on one core)
+        out["selfplay"] = {str(t): selfplay_cpu_baseline(W, G, spec["sims"], sps, t)
+                           for t in sorted({threads, 1}, reverse=True)}
     if spec.get("grid_seconds"):
         out["grid"] = grid_cpu_baseline(spec["grid_seconds"], threads)
     print(json.dumps(out), flush=True)
@@ -752,16 +757,21 @@ def selfplay_cpu_baseline(W, G, sims, seconds, threads):
 
     coach = C.Coach.__new__(C.Coach)
     coach.game, coach.args, coach.nnet = game, sa, PortNet()
+    t_done = moves_done = 0
     try:
         while True:
             np.random.seed(done)
             coach.mcts = Counting(game, coach.nnet, sa)
             coach.executeEpisode()
             done += 1
+            t_done, moves_done = time.perf_counter() - t0, moves
     except TimeoutError:
         pass
     dt = time.perf_counter() - t0
-    return {"games_done": done, "moves": moves, "seconds": round(dt, 1)}
+    # whole episodes when at least one finished (an episode's first moves cost the most, so a
+    # partial one would understate the rate); else the moves of the unfinished first episode
+    return {"games_done": done, "moves": moves, "seconds": round(dt, 1),
+            "whole_games_seconds": round(t_done, 2), "whole_games_moves": moves_done}
 
 
 def pmc_traffic(key):
@@ -958,21 +968,33 @@ def main():
         if grid is not None:
             grid["cpu_baseline"] = cb["grid"]
         if sp is not None:
-            b = cb["selfplay"]
             mean_moves = sp["moves"] / max(1, sp["games"])
-            games = b["moves"] / mean_moves
-            ratio = _calibration().get("selfplay", {}).get("ratio_port_over_reference_time")
-            rate = games / b["seconds"]
+            by = {int(t): r for t, r in cb["selfplay"].items()}
+            rates = {t: (r["games_done"] / r["whole_games_seconds"] if r["games_done"] else
+                         r["moves"] / mean_moves / r["seconds"]) for t, r in by.items()}
+            t_best = max(rates, key=rates.get)
+            b, rate = by[t_best], rates[t_best]
+            measured = (f"{b['games_done']} whole episodes ({b['whole_games_moves']} moves) in "
+                        f"{b['whole_games_seconds']} s" if b["games_done"] else
+                        f"{b['moves']} moves in {b['seconds']} s = {b['moves'] / mean_moves:.2f} "
+                        f"games at the GPU leg's mean {mean_moves:.1f} moves/game")
+            cal = _calibration()
+            ratio = (cal.get("selfplay_by_threads", {}).get(str(t_best), {})
+                     .get("ratio_port_over_reference_time")
+                     or cal.get("selfplay", {}).get("ratio_port_over_reference_time"))
             sp["cpu_baseline"] = {
-                "value": round(rate, 4), "unit": "games/s", "cores": host["cores"], "kind": "port",
+                "value": round(rate, 4), "unit": "games/s", "cores": t_best, "kind": "port",
                 "reference_equivalent": round(rate * ratio, 4) if ratio else None,
+                "by_threads": {str(t): round(r, 4) for t, r in sorted(rates.items())},
                 "sample": f"reference sequential loop (this repo's bit-exact Python MCTS, batch-1 "
                           f"predict + predict_with_gnn through oracle/torch_ref.py with the "
-                          f"reference's predict plumbing, {host['cores']} torch threads, fresh "
-                          f"process): {b['moves']} moves in {b['seconds']} s = {games:.2f} games "
-                          f"at the GPU leg's mean {mean_moves:.1f} moves/game; {CALIBRATION}: "
-                          f"this loop takes {ratio} of the imported reference loop's time on the "
-                          f"same episode (8 threads, build container) -> reference_equivalent",
+                          f"reference's predict plumbing, fresh process), timed on "
+                          f"{' and '.join(str(t) for t in sorted(by, reverse=True))} torch "
+                          f"threads, the faster reported ({t_best}): {measured}; "
+                          f"{CALIBRATION}: this loop "
+                          f"takes {ratio} of the imported reference loop's time on the same "
+                          f"episode at that thread count (build container) -> "
+                          f"reference_equivalent",
                 "host": host}
 
     if rank == 0:

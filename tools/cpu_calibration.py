@@ -3,7 +3,7 @@ container, time the imported reference and this repo's CPU restatements on ident
 thread counts, and record the ratios.  bench.py's cpu_baseline (run on the GPU box, where the
 reference does not exist) uses the restatement whose ratio is recorded here.
 
-    PYTHONDONTWRITEBYTECODE=1 python tools/cpu_calibration.py > profiles/r02_cpu_calibration.json
+    PYTHONDONTWRITEBYTECODE=1 python tools/cpu_calibration.py > profiles/r04_cpu_calibration.json
 
 Legs (8 torch threads, fp32, eval mode, torch.no_grad, median of >= 10 after 3 warm-ups):
   gnn_b512  predict_with_gnn per-row semantics at B = 512 (Connect4GNN.py:31-57 +
@@ -169,8 +169,14 @@ def main():
             setattr(mcts_mod.MCTS, name, orig)
         return count[0] / (time.perf_counter() - t)
 
-    ref_rate = episode_rate(ref_coach, ref_mcts, ref)
-    ref_rate = max(ref_rate, episode_rate(ref_coach, ref_mcts, ref))
+    # the batch-1 loop is latency-bound: also timed on ONE torch thread (faster than 8 here)
+    sp_threads = (THREADS, 1)
+    ref_rates = {}
+    for t in sp_threads:
+        torch.set_num_threads(t)
+        ref_rates[t] = max(episode_rate(ref_coach, ref_mcts, ref),
+                           episode_rate(ref_coach, ref_mcts, ref))
+    ref_rate = ref_rates[THREADS]
     # this repo's MCTS / Coach (MCTS.getActionProb drives the generator) with the torch_ref net
     for m in [m for m in sys.modules if m.split(".")[0] in ("connect4", "Coach", "MCTS",
                                                             "gnn_utils", "Arena")]:
@@ -198,13 +204,23 @@ def main():
         def predict_with_gnn(self, board):
             return self._run(board, True)
 
-    port_rate = episode_rate(my_coach, my_mcts, PortNet(), generator=True)
-    port_rate = max(port_rate, episode_rate(my_coach, my_mcts, PortNet(), generator=True))
+    port_rates = {}
+    for t in sp_threads:
+        torch.set_num_threads(t)
+        port_rates[t] = max(episode_rate(my_coach, my_mcts, PortNet(), generator=True),
+                            episode_rate(my_coach, my_mcts, PortNet(), generator=True))
+    port_rate = port_rates[THREADS]
+    torch.set_num_threads(THREADS)
     out["selfplay"] = {"config": "Connect4 7x7, use_gnn, numMCTSSims 100, expand_by 5, episode "
                                  f"seed 0, first {moves_cap} moves",
                        "reference_moves_per_s": round(ref_rate, 3),
                        "port_moves_per_s": round(port_rate, 3),
                        "ratio_port_over_reference_time": round(ref_rate / port_rate, 3)}
+    out["selfplay_by_threads"] = {
+        str(t): {"reference_moves_per_s": round(ref_rates[t], 3),
+                 "port_moves_per_s": round(port_rates[t], 3),
+                 "ratio_port_over_reference_time": round(ref_rates[t] / port_rates[t], 3)}
+        for t in sp_threads}
     print(json.dumps(out, indent=1))
 
 
