@@ -300,17 +300,21 @@ def aggregate_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=T
     return out
 
 
+BAND_PRODUCTS = 3     # gnn_layer_band_kernel's MFMA products per fp32 product (fp16 form, r04)
+
+
 def layer_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True):
     """The eval-mode GNN layer exactly as az_gnn_layer_infer runs it on the config-5 grid (what
-    PolicyValueGNN.forward_graph launches): band_split_weights (221 KB of bf16 weight planes)
+    PolicyValueGNN.forward_graph launches): band_split_weights (147 KB of fp16 weight planes)
     + gnn_layer_band_kernel (projections, attention, normalised aggregation, gate / update MLPs,
     gated residual; x and each node's source projection once, in a rolling LDS window; nothing
     but x_out reaches HBM).  Timed per layer call with HIP events on the launch stream, Infinity
     Cache flushed before each (the headline) and back-to-back.  Algorithmic work (SURVEY.md §8d
     config 5, per layer): 73,728 FLOP per node on the matrix cores (target + source projections
     2 x 16,384, gate / update_net.0 32,768, update_net.2 8,192) + 640 FLOP per edge; bytes = x
-    read (V * 256) + x_out written (V * 256) + col (4E) + rowptr (4(V+1)).  The MFMAs run fp32
-    as 6 bf16 products (x3), so the pipe is the bf16 one."""
+    read (V * 256) + x_out written (V * 256) + col (4E) + rowptr (4(V+1)).  The MFMAs run fp32 in
+    the fp16 form (row-scaled operands as two fp16 terms, 3 products per fp32 product on
+    v_mfma_f32_32x32x16_f16, az_x3.h), so the pipe is the fp16 one (the bf16 rate)."""
     from azhip.weights import gnn_spec, synthetic_state_dict
     Gw = synthetic_state_dict(gnn_spec(64, 2), 3)
     Wl = {k[len("layers.0."):]: torch.from_numpy(v).to(device) for k, v in Gw.items()
@@ -338,7 +342,7 @@ def layer_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True)
         nbytes = V * 512 + 4 * E + 4 * (V + 1)
         del x, out
         return {"V": V, "E": E, "us": us, "flop": flop, "bytes": nbytes,
-                "bf16_tflops": 6 * mflop / (us * 1e-6) / 1e12,
+                "mfma_tflops": BAND_PRODUCTS * mflop / (us * 1e-6) / 1e12,
                 "fp32_equiv_tflops": flop / (us * 1e-6) / 1e12,
                 "gbs": nbytes / (us * 1e-6) / 1e9, "band": g.band}
 
@@ -347,9 +351,11 @@ def layer_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True)
     del flush
     out = {"kernel": "gnn_layer_band_kernel + band_split_weights (az_gnn_layer_infer, eval-mode "
                      "GNNLayer, band %d graph)" % c["band"],
-           "bound": "mfma", "pipe": "bf16 (x3: 6 bf16 products per fp32 product)",
-           "achieved": round(c["bf16_tflops"], 2), "peak": BF16_MFMA_PEAK_TFLOPS,
-           "unit": "TFLOP/s", "frac": round(c["bf16_tflops"] / BF16_MFMA_PEAK_TFLOPS, 4),
+           "bound": "mfma",
+           "pipe": "fp16 (v_mfma_f32_32x32x16_f16, %d products per fp32 product)" % BAND_PRODUCTS,
+           "products": BAND_PRODUCTS,
+           "achieved": round(c["mfma_tflops"], 2), "peak": BF16_MFMA_PEAK_TFLOPS,
+           "unit": "TFLOP/s", "frac": round(c["mfma_tflops"] / BF16_MFMA_PEAK_TFLOPS, 4),
            "fp32_equiv_tflops": round(c["fp32_equiv_tflops"], 2),
            "traffic": pmc_traffic("gnn_layer_band"), "traffic_run": pmc_run("gnn_layer_band"),
            "avg_launch_us": round(c["us"], 2), "flop_per_launch": c["flop"],
@@ -360,12 +366,12 @@ def layer_roofline(torch, ops, device, graphs=512, full_graphs=4096, extra=True)
            "layer_us": round(c["us"], 2)}
     if extra:
         w = run(graphs)
-        out["warm"] = {"us": round(w["us"], 2), "bf16_tflops": round(w["bf16_tflops"], 2),
+        out["warm"] = {"us": round(w["us"], 2), "mfma_tflops": round(w["mfma_tflops"], 2),
                        "note": "back-to-back launches, x cache-warm"}
         if full_graphs:
             f = run(full_graphs, reps=5)
-            out["full_config"] = {"us": round(f["us"], 2), "bf16_tflops": round(f["bf16_tflops"], 2),
-                                  "frac": round(f["bf16_tflops"] / BF16_MFMA_PEAK_TFLOPS, 4),
+            out["full_config"] = {"us": round(f["us"], 2), "mfma_tflops": round(f["mfma_tflops"], 2),
+                                  "frac": round(f["mfma_tflops"] / BF16_MFMA_PEAK_TFLOPS, 4),
                                   "workload": f"{full_graphs} grids, V={f['V']} (all of config 5 "
                                               f"on one GPU)"}
     return out

@@ -37,7 +37,7 @@ def main():
     torch.cuda.synchronize()
     us = e[0].elapsed_time(e[1]) / reps * 1e3
     print(f"graphs={graphs} V={g.V} band={g.band} layer_us={us:.1f} "
-          f"bf16_tflops={6 * 73728 * g.V / us / 1e6:.1f} max_diff_vs_training={err:.3g}", flush=True)
+          f"fp32eq_tflops={73728 * g.V / us / 1e6:.1f} max_diff_vs_training={err:.3g}", flush=True)
     # the whole eval forward (PolicyValueGNN.forward_graph: layer, then layer + output_transform
     # fused) vs the training-mode forward (unfused kernels)
     from azhip.nets import PolicyValueGNN
