@@ -124,7 +124,10 @@ def gemm(desc, device=None):
 def linear(x, w, b=None, act=ACT_NONE, out=None, x2=None, a_rows=None, R=None, G=None,
            c_rows=None, beta=0.0, M=None, C2=None):
     """out = act(cat(x, x2) @ w.T + b) (optionally gated residual R + G*(...)), nn.Linear layout.
-    x: [M, K1] (row stride taken from the tensor), x2: [M, K2] or None, w: [N, K1+K2]."""
+    x: [M, K1] (row stride taken from the tensor), x2: [M, K2] or None, w: [N, K1+K2].
+    Large GEMMs cache w's per-row fp16-form scales by pointer and shape: after writing new
+    values into w -- or passing a different tensor that reuses a freed w's memory -- call
+    params.weights_changed() (include/az_hip.h az_weights_changed)."""
     _need(x, name="x")
     _need(w, name="w")
     K1 = x.shape[1]

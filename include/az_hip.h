@@ -361,9 +361,11 @@ int az_adam_f32(float* p, const float* g, float* m, float* v, int64_t n,
                 double lr, double beta1, double beta2, double eps, int step, void* stream);
 
 /* Parameters changed: every cached per-row weight scale of the fp16 GEMM form (az_gemm_f32's
- * large K-major GEMMs, az_gemm.hip row_scale_kernel) is recomputed before its next use.
- * az_adam_f32 calls it; a caller that writes weights any other way (loading a checkpoint,
- * copying buffers) must call it before the next GEMM on those weights. */
+ * large K-major GEMMs, az_gemm.hip row_scale_kernel) is recomputed before its next use.  The
+ * cache is keyed by the weight pointer and shape, so a caller that writes weights any other way
+ * (loading a checkpoint, copying buffers, or freeing a weight buffer and passing new weights at
+ * the same address) must call it before the next GEMM on those weights; az_adam_f32 calls it.
+ * A stale scale cannot overflow (64x headroom) but costs precision as the weights move. */
 int az_weights_changed(void);
 
 #ifdef __cplusplus
