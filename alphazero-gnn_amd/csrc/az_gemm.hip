@@ -1645,23 +1645,27 @@ static bool csk_plan(int M, int N, int K, int cus, double miss_cost, CskPlan& ou
 // [row][32 bf16], 16-B chunk c stored at c ^ ((row >> 2) & 3)): the swizzle is applied on the
 // global address, since a DMA's LDS destination is lane-linear.  Same products in the same
 // order as gemm_x3, so the same bits for the same split-K partition.
-template <int BM, int BN, int WGM, int WGN>
+// H3 (tile 16 of the tuning build): the fp16 form on pre-split planes -- two fp16 planes of the
+// row-scaled operands (h3_split_kernel), three products per step, accumulators unscaled by
+// 1 / (sa sw) before the epilogue.
+template <int BM, int BN, int WGM, int WGN, bool H3 = false>
 constexpr int p3_smem_bytes() {
   constexpr int NW = WGM * WGN, WM = BM / WGM;
-  constexpr int BUF = 3 * (BM + BN) * 64, STAGE = NW * WM * 36 * 4;
+  constexpr int BUF = (H3 ? 2 : 3) * (BM + BN) * 64, STAGE = NW * WM * 36 * 4;
   return 2 * BUF > STAGE ? 2 * BUF : STAGE;
 }
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, bool H3 = false>
 __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int mt, int nt,
                                              int sp, int kbeg, int kend) {
+  constexpr int PL = H3 ? 2 : 3;
   constexpr int BK = 32;
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TI = WM / 32, TJ = WN / 32;
   constexpr int ROWS = BM + BN;
-  constexpr int PLANE = ROWS * 64, BUF = 3 * PLANE;
-  constexpr int PIECES = 3 * ROWS / 16;            // 1-KB DMA pieces per stage
+  constexpr int PLANE = ROWS * 64, BUF = PL * PLANE;
+  constexpr int PIECES = PL * ROWS / 16;           // 1-KB DMA pieces per stage
   static_assert(ROWS % 16 == 0 && PIECES % NW == 0 && TI >= 1 && TJ >= 1, "bad p3 tile");
   constexpr int PPW = PIECES / NW;
   const int m0 = mt * BM, n0 = nt * BN;
@@ -1714,11 +1718,11 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
     bkey[j] = (row >> 2) & 3;
   }
   const int hk = lane >> 5;
-  struct Frags { bf16x8 a[3][TI], b[3][TJ]; };
+  struct Frags { bf16x8 a[PL][TI], b[PL][TJ]; };
   auto read = [&](Frags& f, const char* S, int s) {
     const int c = 2 * s + hk;
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
+    for (int pl = 0; pl < PL; ++pl) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
         f.a[pl][i] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + aoff[i] + ((c ^ akey[i]) << 4));
@@ -1729,8 +1733,16 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
   };
   auto mfma6 = [&](const Frags& f, int i, int j) {
     f32x16 t = acc[i][j];
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[2][j], t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[2][i], f.b[0][j], t, 0, 0, 0);
+    if constexpr (H3) {
+      const f16x8 ah = __builtin_bit_cast(f16x8, f.a[0][i]), al = __builtin_bit_cast(f16x8, f.a[PL - 1][i]);
+      const f16x8 bh = __builtin_bit_cast(f16x8, f.b[0][j]), bl = __builtin_bit_cast(f16x8, f.b[PL - 1][j]);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, t, 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, t, 0, 0, 0);
+      return;
+    }
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[PL - 1][j], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[PL - 1][i], f.b[0][j], t, 0, 0, 0);
     t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[1][j], t, 0, 0, 0);
     t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[1][j], t, 0, 0, 0);
     t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][i], f.b[0][j], t, 0, 0, 0);
@@ -1757,19 +1769,35 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
       }
     }
   }
+  if constexpr (H3) {
+    float iw[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+      iw[j] = p.sw[p.N + min(n0 + wn * WN + j * 32 + (lane & 31), p.N - 1)];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const float ia = p.sa[p.M + min(row, p.M - 1)];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j][r] *= ia * iw[j];
+      }
+    __syncthreads();           // the epilogue's staging reuses the stage buffers
+  }
   tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
 }
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, bool H3 = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3(GemmArgs p) {
-  __shared__ __attribute__((aligned(1024))) char smem[p3_smem_bytes<BM, BN, WGM, WGN>()];
+  __shared__ __attribute__((aligned(1024))) char smem[p3_smem_bytes<BM, BN, WGM, WGN, H3>()];
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
   const int nwg = mt_n * nt_n * p.splits;
   const int bid = xcd_swizzle(blockIdx.x, nwg);
   const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
   const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
-  gemm_p3_body<BM, BN, WGM, WGN>(p, smem, mt, nt, sp, kbeg, kend);
+  gemm_p3_body<BM, BN, WGM, WGN, H3>(p, smem, mt, nt, sp, kbeg, kend);
 }
 
 // gemm_p3 in stream-K form (see gemm_x3_sk), pieces summed by streamk_fixup4_kernel
@@ -2179,6 +2207,23 @@ __global__ __launch_bounds__(256) void x3_split_kernel(const float* __restrict__
   unsigned short* d = out + (size_t)r * K + c * 8;
 #pragma unroll
   for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(d + pl * plane) = o[pl];
+}
+
+// the fp16 form's two planes of a row-scaled operand (sc[r] = the row's power of two)
+__global__ __launch_bounds__(256) void h3_split_kernel(const float* __restrict__ A, int lda, int M,
+                                                       int K, const float* __restrict__ sc,
+                                                       unsigned short* __restrict__ out,
+                                                       size_t plane) {
+  const long idx = blockIdx.x * 256L + threadIdx.x;
+  const int segs = K >> 3;
+  if (idx >= (long)M * segs) return;
+  const int r = (int)(idx / segs), c = (int)(idx % segs);
+  const float* s = A + (size_t)r * lda + c * 8;
+  u32x4 o[2];
+  split2s(*reinterpret_cast<const f32x4*>(s), *reinterpret_cast<const f32x4*>(s + 4), sc[r], o);
+  unsigned short* d = out + (size_t)r * K + c * 8;
+#pragma unroll
+  for (int pl = 0; pl < 2; ++pl) *reinterpret_cast<u32x4*>(d + pl * plane) = o[pl];
 }
 #endif
 
@@ -3347,9 +3392,9 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   if (env && tile == 0) return false;
   if (!env && a.M <= 64) return false;  // tools/gemm_sweep.py x3: fp32 tiles win to M = 64 (27 vs 31 us)
   // 7..11: gemm_x3<256,128> timing ablations (ABL 1, 2, 4, 5, 3), K % 32 == 0 only
-  const int bms[16] = {0, 256, 128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
-  const int bns[16] = {0, 128, 128, 64, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
-  if (tile < 1 || tile > 15 || (((tile >= 7 && tile <= 11) || tile >= 13) && a.K % 32 != 0)) {
+  const int bms[17] = {0, 256, 128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
+  const int bns[17] = {0, 128, 128, 64, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
+  if (tile < 1 || tile > 16 || (((tile >= 7 && tile <= 11) || tile >= 13) && a.K % 32 != 0)) {
     tile = a.M > 256 ? 1 : 2;
   }
   const int bm = bms[tile], bn = bns[tile];
@@ -3496,6 +3541,52 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
       return true;
     }
     hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2>), grid, dim3(512), 0, s, a);
+    return true;
+  }
+  // tile 16: the fp16 form on pre-split planes (row scales as the product computes them, both
+  // operands split by h3_split_kernel into this build's buffers; AZ_P3_REUSE=1 splits only on
+  // the first call, so a probe with fixed operands times the tile kernel alone)
+  if (tile == 16 && whole && a.lda == a.K && a.ldb == a.K && h3) {
+    static unsigned short* pbuf = nullptr;
+    static float* sbuf = nullptr;
+    static size_t pcap = 0, scap = 0;
+    static const float *lastA = nullptr, *lastB = nullptr;
+    static const bool reuse = tuning_env("AZ_P3_REUSE") != nullptr;
+    const size_t need = (size_t)2 * ((size_t)a.M + a.N) * a.K;
+    if (need > pcap) {
+      if (pbuf) (void)hipFree(pbuf);
+      if (hipMalloc(&pbuf, need * 2) != hipSuccess) return false;
+      pcap = need;
+      lastA = lastB = nullptr;
+    }
+    const size_t sneed = (size_t)2 * (a.M + a.N);
+    if (sneed > scap) {
+      if (sbuf) (void)hipFree(sbuf);
+      if (hipMalloc(&sbuf, sneed * 4) != hipSuccess) return false;
+      scap = sneed;
+      lastA = lastB = nullptr;
+    }
+    a.apl = pbuf;
+    a.apl_plane = (size_t)a.M * a.K;
+    a.bpl = pbuf + 2 * a.apl_plane;
+    a.bpl_plane = (size_t)a.N * a.K;
+    a.sa = sbuf;
+    a.sw = sbuf + 2 * a.M;
+    if (!reuse || lastA != a.A || lastB != a.B) {
+      hipLaunchKernelGGL(row_scale_kernel, dim3(a.M), dim3(256), 0, s, a.A, a.M, a.K, a.lda,
+                         H3_TA, sbuf);
+      hipLaunchKernelGGL(row_scale_kernel, dim3(a.N), dim3(256), 0, s, a.B, a.N, a.K, a.ldb,
+                         H3_TW, sbuf + 2 * a.M);
+      const long sa = (long)a.M * (a.K / 8), sb = (long)a.N * (a.K / 8);
+      hipLaunchKernelGGL(h3_split_kernel, dim3((unsigned)((sa + 255) / 256)), dim3(256), 0, s,
+                         a.A, a.lda, a.M, a.K, sbuf, pbuf, a.apl_plane);
+      hipLaunchKernelGGL(h3_split_kernel, dim3((unsigned)((sb + 255) / 256)), dim3(256), 0, s,
+                         a.B, a.ldb, a.N, a.K, sbuf + 2 * a.M, const_cast<unsigned short*>(a.bpl),
+                         a.bpl_plane);
+      lastA = a.A;
+      lastB = a.B;
+    }
+    hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true>), grid, dim3(512), 0, s, a);
     return true;
   }
 #endif

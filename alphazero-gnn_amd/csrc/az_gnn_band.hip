@@ -26,9 +26,9 @@
 //   aggregation takes its sources from the planes ((h + l) / s, within 2^-22 |x|); the residual
 //   x + gate * u2 reads x itself (global memory, L2-resident: the rows entered the ring a tile
 //   earlier), so a destination without in-edges gets x bit for bit (gnn_utils.py:35-36).
-//   update_net.0's output (u1) and output_transform's operands are split in the waves, scaled
-//   per 64-row tile.  Every GEMM's accumulators are multiplied back by 1 / (s_row s_w) (exact)
-//   before use.
+//   update_net.0's output (u1) and output_transform's operands (x_out, h) become fp16 planes in
+//   place in PT, each row with its own scale.  Every GEMM's accumulators are multiplied back by
+//   1 / (s_row s_w) (exact) before use.
 //
 // Edges are never dropped: a destination with any in-degree is aggregated completely, and a
 // source outside the window (a graph that is not banded as the caller claimed) takes a slow
@@ -84,8 +84,12 @@ __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
 
 // 1 / (1 + e^-v) with the hardware exp2 and reciprocal (~1 ulp each) instead of expf and an IEEE
 // division: a few instructions instead of ~20, within 3e-7 relative of torch.sigmoid -- far
-// inside the 2e-6 the layer is held to against the training path (tests/test_gpu_kernels.py)
+// inside the 2e-6 the layer is held to against the training path (tests/test_gpu_kernels.py).
+// Below v = -80 the result nears fp32's denormal range, which the reciprocal flushes to zero:
+// there the exact form (torch's 1 / (1 + exp(-v)): denormal, then 0 below -88.7), because a
+// destination whose every score is that small is still normalised by S > 0 (gnn_utils.py:58).
 __device__ __forceinline__ float sigmoid_fast(float v) {
+  if (v < -80.f) return 1.f / (1.f + expf(-v));
   return __builtin_amdgcn_rcpf(1.f + __expf(-v));
 }
 
@@ -120,22 +124,6 @@ __device__ __forceinline__ float absmax8(const f32x4 (&v)[2]) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) m = fmaxf(m, fabsf(v[h][e]));
   return m;
-}
-
-// maximum over the 64 lanes of a wave (values >= 0): DPP within each 16-lane row (quad_perm
-// [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the four rows' results by readlane --
-// no LDS round trips (__shfl_xor is a ds_bpermute and a wait per step)
-__device__ __forceinline__ float wave_absmax(float v) {
-  v = fmaxf(v, dpp<0xB1>(v));
-  v = fmaxf(v, dpp<0x4E>(v));
-  v = fmaxf(v, dpp<0x141>(v));
-  v = fmaxf(v, dpp<0x140>(v));
-  const int b = __builtin_bit_cast(int, v);
-  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0));
-  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16));
-  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32));
-  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
-  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
 
 // 8 consecutive weights of one row -> their two fp16 planes, the row scaled by its power of two
@@ -302,7 +290,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   __shared__ int CLS[2][BNT];             // the tile's sources (col), when it has <= 512 edges
   __shared__ float XSI[RING];             // 1 / s of each ring row's fp16 planes
   __shared__ float AGSI[BT];              // 1 / s of each destination's agg planes
-  __shared__ float TMX[2][8];             // per-wave maxima: u1 (C -> D), x_out / h (OT)
+  __shared__ float RSI[BT];               // 1 / s of each row's u1 (D) / x_out (E) / h (F) planes
   // update_net.2's two fp16 planes (fragment order), copied once per block: phase D reads its B
   // fragments here, so waves 0-3 request the next phase's weights from L2 a phase earlier and
   // the four D waves no longer fetch the same fragments twice
@@ -368,6 +356,36 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl)
         a[pl] = *reinterpret_cast<const bf16x8*>(XR + xr_off(slot, pl, 2 * ks + hc));
+    };
+  };
+  // A row segment of PT (64 floats from column col0: u1, h) -> its two fp16 planes IN PLACE
+  // (plane pl at fp16 offset 64 pl of the segment, 16-B chunk c), scaled by the row's power of
+  // two, 1 / s into RSI -- per row, not per tile, so rows of very different magnitudes keep
+  // their own precision.  Thread = (row tid >> 3, chunk tid & 7): a row's 8 threads sit in one
+  // wave and read their chunks before any of them writes (the row maximum needs all of them).
+  auto split_pass = [&](int col0) {
+    const int i = tid >> 3, c = tid & 7;
+    float* const rowp = PT + i * PSS + col0;
+    f32x4 v[2];
+    v[0] = *reinterpret_cast<const f32x4*>(rowp + 8 * c);
+    v[1] = *reinterpret_cast<const f32x4*>(rowp + 8 * c + 4);
+    float inv;
+    const float sc = h3_scale(max8(absmax8(v)), 14, &inv);
+    u32x4 t[2];
+    split2s(v[0], v[1], sc, t);
+    unsigned short* pp = reinterpret_cast<unsigned short*>(rowp);
+    *reinterpret_cast<u32x4*>(pp + 8 * c) = t[0];
+    *reinterpret_cast<u32x4*>(pp + BF + 8 * c) = t[1];
+    if (c == 0) RSI[i] = inv;
+  };
+  // A fragments from such planes: rows 32 mb + (lane & 31) of the segment at column col0
+  auto plane_frag = [&](int mb, int col0) {
+    return [=](int, int ks, bf16x8 (&a)[2]) {
+      const unsigned short* row =
+          reinterpret_cast<const unsigned short*>(PT + (32 * mb + lr) * PSS + col0);
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+        a[pl] = *reinterpret_cast<const bf16x8*>(row + pl * BF + 8 * (2 * ks + hc));
     };
   };
   // Each wave's weight fragments for the GEMM of the NEXT phase are requested as soon as the
@@ -602,9 +620,11 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
           for (int q = 4; q < deg; ++q) S += alpha_of(col_of(q));
         }
         // alpha / S as alpha * (1 / S): one IEEE division per destination instead of one per
-        // edge (<= 1.5 ulp apart; the layer is held to 2e-6 of the training path)
+        // edge (<= 1.5 ulp apart; the layer is held to 2e-6 of the training path); a tiny S
+        // (1 / S would overflow: every alpha near fp32's denormal range) divides per edge
         const bool norm = S > 0.f;
         const float rS = norm ? 1.f / S : 1.f;
+        const bool tiny = norm && S < 0x1p-100f;
         f32x4 g[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
         if constexpr (FAST) {
           u32x4 xp[4][2];                   // the four sources' planes, all reads in flight
@@ -618,7 +638,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float wq = a[q] * rS;
+            const float wq = tiny ? a[q] / S : a[q] * rS;
             f32x4 v[2];
             x_planes(xp[q][0], xp[q][1], xi[q], v);
 #pragma unroll
@@ -631,7 +651,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             if (q < deg) {
-              const float wq = a[q] * rS;
+              const float wq = tiny ? a[q] / S : a[q] * rS;
               f32x4 v[2];
               x_of(src[q], v);
 #pragma unroll
@@ -644,7 +664,8 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
 #pragma unroll 1
         for (int q = FAST ? deg : 4; q < deg; ++q) {
           const int s = col_of(q);
-          const float wq = alpha_of(s) * rS;
+          const float aq = alpha_of(s);
+          const float wq = tiny ? aq / S : aq * rS;
           f32x4 v[2];
           x_of(s, v);
 #pragma unroll
@@ -737,16 +758,11 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       for (int r = 0; r < 16; ++r) mine[r] += part[(kh * 16 + r) * 64];
       const int n = 32 * nq + lr;         // output column: gate (n < 64) or u1 (n - 64)
       const float bias = BS[n];         // gate.0 (n < 64) | update_net.0
-      float um = 0.f;                     // the largest u1 (phase D's tile scale)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float v = mine[r] + bias;
-        const float o = nq < 2 ? sigmoid_fast(v) : relu(v);
-        PT[(32 * kh + acc_row(r, lane)) * PSS + n] = o;
-        um = fmaxf(um, nq < 2 ? 0.f : o);
+        PT[(32 * kh + acc_row(r, lane)) * PSS + n] = nq < 2 ? sigmoid_fast(v) : relu(v);
       }
-      um = wave_absmax(um);
-      if (lane == 0) TMX[0][wave] = um;
       // the next tile's new x rows [d0 + 96, d0 + 160) into the ring: their slots (rows
       // [d0 - 32, d0 + 32)) were read for the last time by this phase's MFMAs, before the
       // barrier above
@@ -770,13 +786,10 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       xres[0] = *reinterpret_cast<const f32x4*>(x + xo);
       xres[1] = *reinterpret_cast<const f32x4*>(x + xo + 4);
     }
+    split_pass(BF);                       // u1 -> its fp16 planes, a scale per row
+    __syncthreads();
     if (wave < 4) {
       const int mb = wave >> 1, nb = wave & 1;
-      float uinv;                         // u1's tile scale (the u1 waves' maxima, phase C)
-      float um = 0.f;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) um = fmaxf(um, TMX[0][w]);
-      const float usc = h3_scale(um, 14, &uinv);
       f32x16 acc[1];
       zero(acc[0]);
       bf16x8 bd[4][2];                    // update_net.2's fragments of this wave, from LDS
@@ -786,21 +799,15 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         for (int pl = 0; pl < 2; ++pl)
           bd[ks][pl] = *reinterpret_cast<const bf16x8*>(WU2L + pl * BF * BF + (wD - WU2_OFF) +
                                                          FRAG * ks + 8 * lane);
-      h3_mfma<1, 4, (ABL & 8) ? (ABL | 32) : ABL>(acc, [&](int, int ks, bf16x8 (&a)[2]) {
-        const float* u = PT + (32 * mb + lr) * PSS + BF + 16 * ks + 8 * hc;
-        const f32x4 x0 = *reinterpret_cast<const f32x4*>(u);
-        const f32x4 x1 = *reinterpret_cast<const f32x4*>(u + 4);
-        u32x4 o[2];
-        split2s(x0, x1, usc, o);
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl) a[pl] = __builtin_bit_cast(bf16x8, o[pl]);
-      }, bd);
+      h3_mfma<1, 4, (ABL & 8) ? (ABL | 32) : ABL>(acc, plane_frag(mb, BF), bd);
       const int n = 32 * nb + lr;
       const float ub = BS[2 * BF + n];
-      const float ui = uinv * W.winv[WI_WU2 + n];
-      float* const pg = PT + opaque((32 * mb + acc_row(0, lane)) * PSS + n);
+      const float wi = W.winv[WI_WU2 + n];
+      const int r0 = opaque(32 * mb + acc_row(0, lane));
+      float* const pg = PT + r0 * PSS + n;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) pg[acc_drow(r) * PSS] *= acc[0][r] * ui + ub;   // gate * u2
+      for (int r = 0; r < 16; ++r)                                    // gate * u2
+        pg[acc_drow(r) * PSS] *= acc[0][r] * (RSI[r0 + acc_drow(r)] * wi) + ub;
     } else if (has_next) {
       ps_rows(d0 + BT + BR);              // the next tile's new rows (their x stored in C)
     }
@@ -821,14 +828,15 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
           for (int e = 0; e < 4; ++e) o[h][e] = xres[h][e] + gu[e];
         }
       }
-      if constexpr (OT) {                 // x_out's tile maximum: phase E's scale
-        const float om = wave_absmax(absmax8(o));
-        if (lane == 0) TMX[1][wave] = om;
-      }
-      if constexpr (OT) {
-        float* dst = PT + i * PSS + 8 * c;    // in place of the gate elements it consumed
-        *reinterpret_cast<f32x4*>(dst) = o[0];
-        *reinterpret_cast<f32x4*>(dst + 4) = o[1];
+      if constexpr (OT) {                 // x_out's fp16 planes (phase E's A), scaled per row,
+        float inv;                        // in place of the gate * u2 row the group just read
+        const float sc = h3_scale(max8(absmax8(o)), 14, &inv);
+        u32x4 t[2];
+        split2s(o[0], o[1], sc, t);
+        unsigned short* pp = reinterpret_cast<unsigned short*>(PT + i * PSS);
+        *reinterpret_cast<u32x4*>(pp + 8 * c) = t[0];
+        *reinterpret_cast<u32x4*>(pp + BF + 8 * c) = t[1];
+        if (c == 0) RSI[i] = inv;
       } else {
         const int d = d0 + i;
         if (d < V) {
@@ -843,59 +851,38 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     }
     BSTAMP(8);
     if constexpr (OT) {
-      // ---- E: h = relu(x_out W0^T + b0) -> PT[:, 64:128] (u1's, free once every wave's D
-      //      MFMAs are done);  F: y = h W2^T + b2 -> HBM  (waves 0-3, 32 x 32 each; x_out / h
-      //      are split in the waves)
+      // ---- E: h = relu(x_out W0^T + b0) -> PT[:, 64:128] (u1's planes, free once every wave's
+      //      D MFMAs are done);  F: y = h W2^T + b2 -> HBM  (waves 0-3, 32 x 32 each; x_out's and
+      //      h's fp16 planes scaled per row)
       __syncthreads();
       const int mb = (wave >> 1) & 1, nb = wave & 1, n = 32 * nb + lr;
-      auto split_rows = [&](int col0, float sc) {
-        return [=](int, int ks, bf16x8 (&a)[2]) {
-          const float* u = PT + (32 * mb + lr) * PSS + col0 + 16 * ks + 8 * hc;
-          const f32x4 x0 = *reinterpret_cast<const f32x4*>(u);
-          const f32x4 x1 = *reinterpret_cast<const f32x4*>(u + 4);
-          u32x4 t[2];
-          split2s(x0, x1, sc, t);
-#pragma unroll
-          for (int pl = 0; pl < 2; ++pl) a[pl] = __builtin_bit_cast(bf16x8, t[pl]);
-        };
-      };
       f32x16 acc[1];
       if (wave < 4) {
-        float m = 0.f, inv;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) m = fmaxf(m, TMX[1][w]);
-        const float sc = h3_scale(m, 14, &inv);
         zero(acc[0]);
-        h3_mfma<1, 4, ABL>(acc, split_rows(0, sc), bw);
+        h3_mfma<1, 4, ABL>(acc, plane_frag(mb, 0), bw);
         load_w<4, ABL>(bw, wr, wl, wD + (OT2_OFF - WU2_OFF));
         const float bias = BS[3 * BF + n];
-        const float wi = inv * W.winv[WI_OT0 + n];
-        float* const pe = PT + opaque((32 * mb + acc_row(0, lane)) * PSS + BF + n);
-        float hm = 0.f;
+        const float wi = W.winv[WI_OT0 + n];
+        const int r0 = opaque(32 * mb + acc_row(0, lane));
+        float* const pe = PT + r0 * PSS + BF + n;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float h = relu(acc[0][r] * wi + bias);
-          pe[acc_drow(r) * PSS] = h;
-          hm = fmaxf(hm, h);
-        }
-        hm = wave_absmax(hm);
-        if (lane == 0) TMX[0][wave] = hm;   // h's tile maximum (phase F's scale); TMX[0] (u1's)
-      }                                     // was last read in phase D, two barriers ago
+        for (int r = 0; r < 16; ++r)
+          pe[acc_drow(r) * PSS] = relu(acc[0][r] * (RSI[r0 + acc_drow(r)] * wi) + bias);
+      }
+      __syncthreads();                    // h complete; E's reads of x_out's scales done
+      split_pass(BF);                     // h -> its fp16 planes, a scale per row
       __syncthreads();
       if (wave < 4) {
-        float m = 0.f, inv;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) m = fmaxf(m, TMX[0][w]);
-        const float sc = h3_scale(m, 14, &inv);
         zero(acc[0]);
-        h3_mfma<1, 4, ABL>(acc, split_rows(BF, sc), bw);
+        h3_mfma<1, 4, ABL>(acc, plane_frag(mb, BF), bw);
         load_w<4, ABL>(bw, wr, wl, wA);
         const float bias = BS[4 * BF + n];
-        const float wi = inv * W.winv[WI_OT2 + n];
-        float* const pf = PT + opaque((32 * mb + acc_row(0, lane)) * PSS + n);
+        const float wi = W.winv[WI_OT2 + n];
+        const int r0 = opaque(32 * mb + acc_row(0, lane));
+        float* const pf = PT + r0 * PSS + n;
 #pragma unroll
         for (int r = 0; r < 16; ++r)      // y over x_out's rows in PT (read by E, before F)
-          pf[acc_drow(r) * PSS] = acc[0][r] * wi + bias;
+          pf[acc_drow(r) * PSS] = acc[0][r] * (RSI[r0 + acc_drow(r)] * wi) + bias;
       }
     }
     if constexpr (OT) __syncthreads();    // F's y rows in PT complete

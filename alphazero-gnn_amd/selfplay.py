@@ -452,6 +452,15 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
         lane.start()
     streams = _lane_streams(nnet, use_gnn, lanes)
     inflight = [None] * lanes
+    # diagnostics (tools/sp_pipeline_probe.py): stats["timeline"] = [] asks for one record per
+    # lock-step round -- host times and the batch's GPU span from timing events on its stream
+    tl_on = stats is not None and isinstance(stats.get("timeline"), list) and \
+        streams[0] is not None
+    if tl_on:
+        import torch
+        ref_ev = torch.cuda.Event(enable_timing=True)
+        ref_ev.record()
+        gpu_ev = []
     t0 = time.perf_counter()
     t_wait = t_launch = 0.0
     idle = 0
@@ -459,19 +468,30 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
     try:
         while any(lane.live() for lane in L) or any(x is not None for x in inflight):
             lane = L[i]
+            rec = {"lane": i, "t_start": time.perf_counter() - t0} if tl_on else None
             if inflight[i] is not None:
                 tw = time.perf_counter()
                 p, inflight[i] = inflight[i], None
                 if hasattr(p, "event"):
                     p.event.synchronize()
                 t_wait += time.perf_counter() - tw
+                if tl_on:
+                    rec["wait"] = time.perf_counter() - tw
                 lane.deliver(p)
                 idle = 0
             if lane.live():
                 boards = lane.gather()
                 if boards is not None:
                     tl = time.perf_counter()
+                    if tl_on:
+                        e0, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(2))
+                        e0.record(streams[i])
                     inflight[i] = _launch(nnet, boards, use_gnn, streams[i])
+                    if tl_on:
+                        e1.record(streams[i])
+                        gpu_ev.append((len(stats["timeline"]), e0, e1))
+                        rec.update(n=len(boards), t_launch=tl - t0,
+                                   launch=time.perf_counter() - tl)
                     t_launch += time.perf_counter() - tl
                     idle = 0
                 else:
@@ -480,6 +500,8 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
                     if idle > 4 * lanes + 4 and not any(x is not None for x in inflight) and \
                             any(ln.live() for ln in L):
                         raise RuntimeError("native self-play made no progress (engine/driver bug)")
+            if tl_on:
+                stats["timeline"].append(rec)
             i = (i + 1) % lanes
         tf = time.perf_counter()
         for lane in L:
@@ -488,6 +510,11 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
     finally:
         if pool is not None:
             pool.shutdown(wait=True)
+    if tl_on:
+        torch.cuda.synchronize()
+        for k, e0, e1 in gpu_ev:     # GPU span of each batch, ms from the reference event
+            stats["timeline"][k].update(gpu_start=ref_ev.elapsed_time(e0) * 1e-3,
+                                        gpu_end=ref_ev.elapsed_time(e1) * 1e-3)
     if stats is not None:
         stats["assemble_drain_s"] = drain_s
         stats.update(rounds=sum(ln.rounds for ln in L), rows=sum(ln.rows for ln in L),
