@@ -153,6 +153,8 @@ SIGNATURES = {
     "az_adam_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_double, c_double,
                             c_double, c_double, c_int, c_void_p]),
     "az_weights_changed": (c_int, []),
+    "az_weights_register": (c_int, [c_void_p, c_size_t]),
+    "az_weights_unregister": (c_int, [c_void_p]),
     "az_gemm_form": (c_int, [c_int, c_int, c_int, c_size_t]),
 }
 

@@ -18,6 +18,21 @@ def weights_changed():
     _lib.check(_lib.load().az_weights_changed(), "az_weights_changed")
 
 
+def _register(owner, flat):
+    """Declare `flat` parameter storage to libaz_hip.so (az_weights_register: its weights' fp16
+    GEMM scales / planes may be cached between az_weights_changed calls) for as long as `owner`
+    lives."""
+    if flat.device.type != "cuda" or flat.numel() == 0:
+        return
+    import weakref
+    from . import _lib
+    L = _lib.load()
+    ptr = flat.data_ptr()
+    _lib.check(L.az_weights_register(ptr, flat.numel() * 4), "az_weights_register")
+    # the buffer outlives the owner only through views; unregistering early only disables caching
+    weakref.finalize(owner, L.az_weights_unregister, ptr)
+
+
 def _align4(n):
     return (n + 3) & ~3
 
@@ -34,6 +49,7 @@ class FlatParams:
             off = _align4(off + n)
         self.numel = off
         self.flat = torch.zeros(off, dtype=torch.float32, device=self.device)
+        _register(self, self.flat)
         self.views = self._views(self.flat)
         self._grad = None
         self.m = None

@@ -1453,8 +1453,17 @@ __host__ __device__ __forceinline__ int csk_block_of(int u, int b, int W) {
   return ((u + 1) * b - 1) / W;
 }
 
-template <bool MASK, bool H3>
+// gemm_p3_body (below): the tile on operands already split into planes, LDS-DMA only
+template <int BM, int BN, int WGM, int WGN, bool H3 = false, bool FLEX = false>
+__device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int mt, int nt,
+                                             int sp, int kbeg, int kend, int bma = BM);
+
+// P2: the fp16 form on pre-split planes (p.apl: A's two planes from h3_split_rows_kernel, p.bpl:
+// W's, cached per weight generation), every stage global -> LDS by LDS-DMA; same products in the
+// same order as the in-tile split, so the same bits.
+template <bool MASK, bool H3, bool P2 = false>
 __global__ __launch_bounds__(512) void gemm_x3_csk(GemmArgs p, CskPlan q) {
+  static_assert(!P2 || (H3 && !MASK), "P2: the fp16 form on whole 32-k tiles");
   __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<256, 128, 4, 2, 32, H3 ? 2 : 3>()];
   const int L = xcd_swizzle(blockIdx.x, q.B);
   int r, b, am, an, mt0, nt0, bma;
@@ -1495,8 +1504,12 @@ __global__ __launch_bounds__(512) void gemm_x3_csk(GemmArgs p, CskPlan q) {
     const int fn = f / am;
     int mt_i = mt0 + (f - fn * am), bma_i = bma;   // opaque per segment: keeps the body's
     asm volatile("" : "+s"(mt_i), "+s"(bma_i));    // address setup in the loop (hoisted, it spills)
-    gemm_x3_body<256, 128, 4, 2, MASK, 0, false, 32, true, H3>(g, smem, mt_i, nt0 + fn, sp,
-                                                              32 * k0, min(p.K, 32 * k1), bma_i);
+    if constexpr (P2)
+      gemm_p3_body<256, 128, 4, 2, true, true>(g, smem, mt_i, nt0 + fn, sp, 32 * k0,
+                                               min(p.K, 32 * k1), bma_i);
+    else
+      gemm_x3_body<256, 128, 4, 2, MASK, 0, false, 32, true, H3>(g, smem, mt_i, nt0 + fn, sp,
+                                                                32 * k0, min(p.K, 32 * k1), bma_i);
     i0 += k1 - k0;
     if (i0 < i1) __syncthreads();         // the next segment's prologue reuses the LDS
   }
@@ -1655,9 +1668,11 @@ constexpr int p3_smem_bytes() {
   return 2 * BUF > STAGE ? 2 * BUF : STAGE;
 }
 
-template <int BM, int BN, int WGM, int WGN, bool H3 = false>
+// FLEX (the cycled stream-K tail): bma = 256 (256 x 128 tile) or 128 (128 x 256), as gemm_x3_body.
+template <int BM, int BN, int WGM, int WGN, bool H3, bool FLEX>
 __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int mt, int nt,
-                                             int sp, int kbeg, int kend) {
+                                             int sp, int kbeg, int kend, int bma) {
+  static_assert(!FLEX || (BM == 256 && BN == 128 && WGM == 4 && WGN == 2), "FLEX: 256 x 128");
   constexpr int PL = H3 ? 2 : 3;
   constexpr int BK = 32;
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
@@ -1668,9 +1683,11 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
   constexpr int PIECES = PL * ROWS / 16;           // 1-KB DMA pieces per stage
   static_assert(ROWS % 16 == 0 && PIECES % NW == 0 && TI >= 1 && TJ >= 1, "bad p3 tile");
   constexpr int PPW = PIECES / NW;
-  const int m0 = mt * BM, n0 = nt * BN;
+  const int tbm = FLEX ? bma : BM, tbn = FLEX ? BM + BN - bma : BN;
+  const int wgn = FLEX ? tbn / WN : WGN;
+  const int m0 = mt * tbm, n0 = nt * tbn;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave / WGN, wn = wave % WGN;
+  const int wm = wave / wgn, wn = wave % wgn;
 
   // piece q * NW + wave covers image rows 16 piece .. + 15 (plane-major [3][ROWS]); lane l lands
   // at byte 16 l of it: row 16 piece + (l >> 2), chunk slot l & 3 = logical chunk (l & 3) ^ key
@@ -1680,11 +1697,11 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
     const int R = (q * NW + wave) * 16 + (lane >> 2);
     const int pl = R / ROWS, r = R % ROWS;
     const int c = (lane & 3) ^ ((r >> 2) & 3);
-    if (r < BM) {
+    if (r < tbm) {
       const int gr = min(m0 + r, p.M - 1);
       src[q] = p.apl + pl * p.apl_plane + (size_t)gr * p.K + 8 * c;
     } else {
-      const int gr = min(n0 + r - BM, p.N - 1);
+      const int gr = min(n0 + r - tbm, p.N - 1);
       src[q] = p.bpl + pl * p.bpl_plane + (size_t)gr * p.K + 8 * c;
     }
   }
@@ -1713,7 +1730,7 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
   }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    const int row = BM + wn * WN + j * 32 + (lane & 31);
+    const int row = tbm + wn * WN + j * 32 + (lane & 31);
     boff[j] = row * 64;
     bkey[j] = (row >> 2) & 3;
   }
@@ -1797,7 +1814,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3(GemmArgs p) {
   const int bid = xcd_swizzle(blockIdx.x, nwg);
   const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
   const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
-  gemm_p3_body<BM, BN, WGM, WGN, H3>(p, smem, mt, nt, sp, kbeg, kend);
+  gemm_p3_body<BM, BN, WGM, WGN, H3, false>(p, smem, mt, nt, sp, kbeg, kend, BM);
 }
 
 // gemm_p3 in stream-K form (see gemm_x3_sk), pieces summed by streamk_fixup4_kernel
@@ -1820,7 +1837,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3_sk(GemmArgs p, SkPlan 
       q.splits = 2;
       sp = b - sk_block(sq, t, 0);
     }
-    gemm_p3_body<BM, BN, WGM, WGN>(q, smem, t % mt_n, t / mt_n, sp, 32 * k0, min(p.K, 32 * k1));
+    gemm_p3_body<BM, BN, WGM, WGN, false, false>(q, smem, t % mt_n, t / mt_n, sp, 32 * k0,
+                                                  min(p.K, 32 * k1), BM);
     i0 += k1 - k0;
     if (i0 < i1) __syncthreads();
   }
@@ -3310,6 +3328,66 @@ __global__ __launch_bounds__(256) void row_scale_kernel(const float* __restrict_
   }
 }
 
+// A row's power-of-two scale (as row_scale_kernel: sc[r] = s, sc[rows + r] = 1 / s) AND its two fp16
+// planes (split2s of x s: plane 0 at out + r * cols, plane 1 at out + plane + r * cols), one
+// 256-thread block per row, the row read once when cols <= 4096 (8-float chunks in registers):
+// the P2 GEMM's operands.  cols % 8 == 0 and 16-B aligned rows (the caller checks).
+__global__ __launch_bounds__(256) void h3_split_rows_kernel(const float* __restrict__ X, int rows,
+                                                            int cols, int ld, int T,
+                                                            unsigned short* __restrict__ out,
+                                                            size_t plane, float* __restrict__ sc) {
+  __shared__ float wm[4];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  if (r >= rows) return;
+  const float* x = X + (size_t)r * ld;
+  const int nch = cols >> 3;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  f32x4 v[2][2];
+  float m = 0.f;
+  auto amax = [](const f32x4& a, const f32x4& b) {
+    return fmaxf(fmaxf(fmaxf(fabsf(a[0]), fabsf(a[1])), fmaxf(fabsf(a[2]), fabsf(a[3]))),
+                 fmaxf(fmaxf(fabsf(b[0]), fabsf(b[1])), fmaxf(fabsf(b[2]), fabsf(b[3]))));
+  };
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int ch = tid + 256 * u;
+    v[u][0] = ch < nch ? *reinterpret_cast<const f32x4*>(x + 8 * ch) : z;
+    v[u][1] = ch < nch ? *reinterpret_cast<const f32x4*>(x + 8 * ch + 4) : z;
+    m = fmaxf(m, amax(v[u][0], v[u][1]));
+  }
+  for (int ch = tid + 512; ch < nch; ch += 256)      // rows longer than 4096
+    m = fmaxf(m, amax(*reinterpret_cast<const f32x4*>(x + 8 * ch),
+                      *reinterpret_cast<const f32x4*>(x + 8 * ch + 4)));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (lane == 0) wm[tid >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+  int e = 0;
+  if (m > 0.f && m <= 3.4e38f) {
+    int ex;
+    (void)frexpf(m, &ex);
+    e = min(120, max(-120, T - ex));
+  }
+  const float s = ldexpf(1.f, e);
+  if (tid == 0) {
+    sc[r] = s;
+    sc[rows + r] = ldexpf(1.f, -e);
+  }
+  unsigned short* d = out + (size_t)r * cols;
+  auto put = [&](int ch, const f32x4& a, const f32x4& b) {
+    u32x4 o[2];
+    split2s(a, b, s, o);
+    *reinterpret_cast<u32x4*>(d + 8 * ch) = o[0];
+    *reinterpret_cast<u32x4*>(d + plane + 8 * ch) = o[1];
+  };
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (tid + 256 * u < nch) put(tid + 256 * u, v[u][0], v[u][1]);
+  for (int ch = tid + 512; ch < nch; ch += 256)
+    put(ch, *reinterpret_cast<const f32x4*>(x + 8 * ch), *reinterpret_cast<const f32x4*>(x + 8 * ch + 4));
+}
+
 // A's rows are scaled into [2^13, 2^14) (fp16 max 65504); W's into [2^9, 2^10): its scales are
 // cached between weight updates (below) and stay safe while the weights grow up to 64x.
 constexpr int H3_TA = 14, H3_TW = 10;
@@ -3327,18 +3405,56 @@ struct WScaleEntry {
   long gen;
   float* buf[2];
   int cur;
+  unsigned short* planes[2];   // the P2 GEMM's W planes [2][n][k] (nullptr until first asked)
+  long pgen;                   // generation the current planes (buf[cur] too) were split at
 };
 static std::mutex g_wmu;
 static std::vector<WScaleEntry> g_wcache;
+
+// Parameter storage the caller registered (az_weights_register): only weights inside it are
+// cached -- anywhere else a pointer says nothing about the values behind it (a freed tensor's
+// memory can hold the next one), so their scales are computed per call and the pre-split planes
+// are not used.
+static std::mutex g_regmu;
+static std::vector<std::pair<uintptr_t, uintptr_t>> g_regs;
+
+static bool weights_registered(const float* w, int n, int k, int ld) {
+  const uintptr_t b = reinterpret_cast<uintptr_t>(w);
+  const uintptr_t e = b + ((size_t)(n - 1) * ld + k) * sizeof(float);
+  std::lock_guard<std::mutex> lk(g_regmu);
+  for (const auto& r : g_regs)
+    if (b >= r.first && e <= r.second) return true;
+  return false;
+}
 
 }  // namespace az
 extern "C" int az_weights_changed(void) {
   az::g_wgen.fetch_add(1);
   return AZ_OK;
 }
+extern "C" int az_weights_register(const void* base, size_t bytes) {
+  AZ_REQUIRE(base && bytes > 0, AZ_EINVAL, "az_weights_register: null / empty range");
+  {
+    std::lock_guard<std::mutex> lk(az::g_regmu);
+    const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+    az::g_regs.emplace_back(b, b + bytes);
+  }
+  return az_weights_changed();           // a reused range must not meet old cache entries
+}
+extern "C" int az_weights_unregister(const void* base) {
+  {
+    std::lock_guard<std::mutex> lk(az::g_regmu);
+    const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+    for (size_t i = 0; i < az::g_regs.size();)
+      if (az::g_regs[i].first == b) az::g_regs.erase(az::g_regs.begin() + i);
+      else ++i;
+  }
+  return az_weights_changed();
+}
 namespace az {
 
 static const float* w_row_scales(const float* w, int n, int k, int ld, hipStream_t s) {
+  if (!weights_registered(w, n, k, ld)) return nullptr;   // the caller computes them per call
   const long gen = g_wgen.load();
   std::lock_guard<std::mutex> lk(g_wmu);
   WScaleEntry* e = nullptr;
@@ -3346,7 +3462,7 @@ static const float* w_row_scales(const float* w, int n, int k, int ld, hipStream
     if (x.w == w && x.n == n && x.k == k && x.ld == ld) e = &x;
   if (e && e->gen == gen) return e->buf[e->cur];
   if (!e) {
-    WScaleEntry x{w, n, k, ld, 0, {nullptr, nullptr}, 0};
+    WScaleEntry x{w, n, k, ld, 0, {nullptr, nullptr}, 0, {nullptr, nullptr}, 0};
     if (hipMalloc(&x.buf[0], (size_t)4 * n * sizeof(float)) != hipSuccess) return nullptr;
     x.buf[1] = x.buf[0] + 2 * n;
     x.cur = 1;
@@ -3362,6 +3478,47 @@ static const float* w_row_scales(const float* w, int n, int k, int ld, hipStream
   return e->buf[nxt];
 }
 
+// W's fp16 planes and scales for the P2 GEMM, cached like the scales above (two buffers, the
+// recompute synchronises its stream before publishing); nullptr when memory is short.
+static const unsigned short* w_planes(const float* w, int n, int k, int ld, hipStream_t s,
+                                      const float** scales) {
+  if (!weights_registered(w, n, k, ld)) return nullptr;
+  const long gen = g_wgen.load();
+  std::lock_guard<std::mutex> lk(g_wmu);
+  WScaleEntry* e = nullptr;
+  for (auto& x : g_wcache)
+    if (x.w == w && x.n == n && x.k == k && x.ld == ld) e = &x;
+  if (!e) {
+    WScaleEntry x{w, n, k, ld, 0, {nullptr, nullptr}, 0, {nullptr, nullptr}, 0};
+    if (hipMalloc(&x.buf[0], (size_t)4 * n * sizeof(float)) != hipSuccess) return nullptr;
+    x.buf[1] = x.buf[0] + 2 * n;
+    x.cur = 1;
+    g_wcache.push_back(x);
+    e = &g_wcache.back();
+  }
+  if (!e->planes[0]) {
+    const size_t one = (size_t)2 * n * k;
+    if (hipMalloc(&e->planes[0], 2 * one * sizeof(unsigned short)) != hipSuccess) {
+      e->planes[0] = nullptr;
+      return nullptr;
+    }
+    e->planes[1] = e->planes[0] + one;
+    e->pgen = 0;
+  }
+  if (e->pgen == gen && e->gen == gen) {
+    *scales = e->buf[e->cur];
+    return e->planes[e->cur];
+  }
+  const int nxt = e->cur ^ 1;
+  hipLaunchKernelGGL(h3_split_rows_kernel, dim3(n), dim3(256), 0, s, w, n, k, ld, H3_TW,
+                     e->planes[nxt], (size_t)n * k, e->buf[nxt]);
+  if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+  e->cur = nxt;
+  e->gen = e->pgen = gen;
+  *scales = e->buf[nxt];
+  return e->planes[nxt];
+}
+
 // gemm_x3 launch for a K-major A and W (no A2 / gathered rows), M > 64: 256x128 (8 waves) above
 // M = 256, else 128x128 (4 waves); split-K so the grid nears one block per CU (measured on
 // MI355X, tools/gemm_sweep.py x3: M = 512 75 us vs 103 us for the fp32 MFMA tile, M = 800 147 vs
@@ -3373,15 +3530,50 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   // the fp16 form (H3) for the product tiles when the workspace can hold A's row scales (taken
   // from its end, after every split-K slab); tuning build: AZ_GEMM_PREC=x3 keeps the bf16 form
   static const char* env_prec = tuning_env("AZ_GEMM_PREC");
-  const size_t sa_bytes = ((size_t)2 * a.M * sizeof(float) + 255) / 256 * 256;
+  // A's scales [2][M] and, for weights outside registered parameter storage, W's [2][N]
+  const size_t sa_bytes = ((size_t)2 * (a.M + a.N) * sizeof(float) + 255) / 256 * 256;
   bool h3 = !(env_prec && strcmp(env_prec, "x3") == 0) && a.slab && ws_bytes >= sa_bytes + 256;
   if (h3) ws_bytes = (ws_bytes - sa_bytes) / 256 * 256;
   float* const sa_buf = h3 ? reinterpret_cast<float*>(reinterpret_cast<char*>(a.slab) + ws_bytes)
                            : nullptr;
+  float* const sw_buf = h3 ? sa_buf + 2 * a.M : nullptr;
+  // P2 (product dispatch, whole 32-k tiles): A split once per call into its two fp16 planes
+  // (h3_split_rows_kernel, also its row scales) in the workspace before the scales, W's planes
+  // cached per weight generation (w_planes); the tile then moves both by LDS-DMA with no VALU --
+  // 8-12 % faster tiles than splitting in the tile, bit-identical (tools/p2h_probe.py)
+  const bool whole_k = a.K % 32 == 0;
+  const size_t p2a_bytes = ((size_t)4 * a.M * a.K + 255) / 256 * 256;
+  bool p2 = h3 && !tuning_env("AZ_GEMM_X3") && !tuning_env("AZ_GEMM_SPLITS") &&
+            !tuning_env("AZ_GEMM_NOP2") && whole_k && a.lda % 4 == 0 && a.ldb % 4 == 0 &&
+            aligned16(a.A) && aligned16(a.B) && ws_bytes >= p2a_bytes + 256 &&
+            weights_registered(a.B, a.N, a.K, a.ldb);
+  unsigned short* apl_buf = nullptr;
+  if (p2) {
+    ws_bytes = (ws_bytes - p2a_bytes) / 256 * 256;
+    apl_buf = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(a.slab) + ws_bytes);
+  }
+  auto p2_prep = [&]() {
+    const float* sw = nullptr;
+    const unsigned short* wpl = w_planes(a.B, a.N, a.K, a.ldb, s, &sw);
+    if (!wpl) return false;
+    hipLaunchKernelGGL(h3_split_rows_kernel, dim3(a.M), dim3(256), 0, s, a.A, a.M, a.K, a.lda,
+                       H3_TA, apl_buf, (size_t)a.M * a.K, sa_buf);
+    a.apl = apl_buf;
+    a.apl_plane = (size_t)a.M * a.K;
+    a.bpl = wpl;
+    a.bpl_plane = (size_t)a.N * a.K;
+    a.sa = sa_buf;
+    a.sw = sw;
+    return true;
+  };
   // A's row scales and W's (cached) just before the launch that uses them
   auto h3_scales = [&]() {
     const float* sw = w_row_scales(a.B, a.N, a.K, a.ldb, s);
-    if (!sw) return false;
+    if (!sw) {                          // not cacheable: this call's own W scales
+      hipLaunchKernelGGL(row_scale_kernel, dim3(a.N), dim3(256), 0, s, a.B, a.N, a.K, a.ldb,
+                         H3_TW, sw_buf);
+      sw = sw_buf;
+    }
     hipLaunchKernelGGL(row_scale_kernel, dim3(a.M), dim3(256), 0, s, a.A, a.M, a.K,
                        a.lda, H3_TA, sa_buf);
     a.sa = sa_buf;
@@ -3454,8 +3646,10 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
       ok = csk_plan(a.M, a.N, a.K, cus, CSK_MISS_COST, cq);
 #endif
       if (use_csk && ok && (size_t)csk_max_pieces(cq) * a.M * a.N * 4 <= ws_bytes) {
-        if (h3) h3 = h3_scales();
-        if (h3 && whole) hipLaunchKernelGGL((gemm_x3_csk<false, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        if (p2) p2 = p2_prep();
+        if (!p2 && h3) h3 = h3_scales();
+        if (p2) hipLaunchKernelGGL((gemm_x3_csk<false, true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        else if (h3 && whole) hipLaunchKernelGGL((gemm_x3_csk<false, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
         else if (h3) hipLaunchKernelGGL((gemm_x3_csk<true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
         else if (whole) hipLaunchKernelGGL((gemm_x3_csk<false, false>), dim3(cq.B), dim3(512), 0, s, a, cq);
         else hipLaunchKernelGGL((gemm_x3_csk<true, false>), dim3(cq.B), dim3(512), 0, s, a, cq);
@@ -3599,6 +3793,11 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
                                 dim3(64 * WM_ * WN_), 0, s, a);                                \
   else hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, true, 0, false, 32, true>), grid,         \
                           dim3(64 * WM_ * WN_), 0, s, a);
+  if (p2 && (tile == 1 || tile == 2) && p2_prep()) {
+    if (tile == 1) hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true>), grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((gemm_p3<128, 128, 2, 2, true>), grid, dim3(256), 0, s, a);
+    return true;
+  }
   if (h3 && (tile == 1 || tile == 2) && h3_scales()) {
     if (tile == 1) { AZ_H3(256, 128, 4, 2) }
     else { AZ_H3(128, 128, 2, 2) }

@@ -868,8 +868,11 @@ extern "C" int az_c4_trunk_heads_fwd(const int8_t* boards, int B, const float* c
 static size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
 extern "C" size_t az_transform_heads_ws_bytes(int B, int F, int A) {
-  // the heads' chunk partials, then room for 8 split-K slabs of the [B][F] GEMM outputs
-  return align256(az_heads_ws_bytes(B, F, A)) + (size_t)8 * B * F * 4;
+  // the heads' chunk partials, then room for 8 split-K slabs of the [B][F] GEMM outputs, the
+  // GEMM's A operand as two fp16 planes (the fp16 form on pre-split planes, az_gemm.hip) and
+  // A's row scales
+  return align256(az_heads_ws_bytes(B, F, A)) + (size_t)8 * B * F * 4 +
+         align256((size_t)4 * B * F) + align256((size_t)8 * B) + 256;
 }
 
 template <int S>

@@ -368,6 +368,16 @@ int az_adam_f32(float* p, const float* g, float* m, float* v, int64_t n,
  * A stale scale cannot overflow (64x headroom) but costs precision as the weights move. */
 int az_weights_changed(void);
 
+/* Parameter storage: [base, base + bytes) holds weights whose values change only where
+ * az_weights_changed() says so.  Only weights inside a registered range have their fp16-form
+ * row scales and pre-split planes cached (az_gemm_f32's large K-major GEMMs: W split once per
+ * weight update instead of in every tile); any other weight pointer gets its scales computed per
+ * call, since a pointer alone says nothing about the values behind it.  Registering or
+ * unregistering also invalidates every cache entry.  The Python parameter store (azhip/params.py
+ * FlatParams) registers its flat buffer. */
+int az_weights_register(const void* base, size_t bytes);
+int az_weights_unregister(const void* base);
+
 #ifdef __cplusplus
 }
 #endif

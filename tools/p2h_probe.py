@@ -19,6 +19,9 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 N = K = 3136
 g = torch.Generator(device="cuda").manual_seed(0)
 w = (torch.rand((N, K), device="cuda", generator=g) * 2 - 1) / K ** 0.5
+if os.environ.get("AZ_PROBE_REGISTER", "1") == "1":      # as parameter storage: W's planes cached
+    from azhip import _lib
+    _lib.check(_lib.load().az_weights_register(w.data_ptr(), w.numel() * 4), "az_weights_register")
 b = torch.rand((N,), device="cuda", generator=g)
 for M in Ms:
     x = torch.rand((M, K), device="cuda", generator=g) * 2 - 1
