@@ -215,6 +215,27 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
   return xcd * base + min(xcd, rem) + local;
 }
 
+// (m tile, n tile, split) of swizzled id `bid`.  Up to 8 m tiles: m fastest (the tiles of one W
+// panel adjacent).  More (large M, no split): groups of 4 m tiles, m fastest inside a group and
+// the group's n tiles in turn, so an XCD's ~32 resident blocks are 4 m x 8 n tiles -- W panels
+// re-read per group of 4 m tiles instead of A panels per n tile (M = 65,536 x 3136: the m-fastest
+// order re-fetched every 3.2 MB A panel for each of the 25 n tiles, 22 GB per call; L2 hit 0.33)
+__device__ __forceinline__ void tile_of(int bid, int mt_n, int nt_n, int& mt, int& nt, int& sp) {
+  const int tiles = mt_n * nt_n;
+  sp = bid / tiles;
+  const int t = bid - sp * tiles;
+  if (mt_n <= 8) {
+    mt = t % mt_n;
+    nt = t / mt_n;
+    return;
+  }
+  constexpr int GM = 4;
+  const int per = GM * nt_n, g = t / per, r = t - g * per;
+  const int gm = min(GM, mt_n - g * GM);     // the last group may be ragged
+  mt = g * GM + r % gm;
+  nt = r / gm;
+}
+
 // Tile epilogue shared by the tile kernels.  A wave owns the TI x TJ MF x MF accumulators of
 // its sub-tile at (r0, c0).  No split: the fused epilogue straight from the accumulators.
 // Split-K: the raw partial goes to slab[sp] and splitk_reduce_kernel sums the slabs in s order.
@@ -1288,8 +1309,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<BM, BN, WGM, WGN, MF, H3 ? 2 : 3>()];
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
   const int nwg = mt_n * nt_n * p.splits;
-  const int bid = xcd_swizzle(blockIdx.x, nwg);
-  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  int mt, nt, sp;
+  tile_of(xcd_swizzle(blockIdx.x, nwg), mt_n, nt_n, mt, nt, sp);
   const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
   gemm_x3_body<BM, BN, WGM, WGN, MASK, ABL, APL, MF, false, H3>(p, smem, mt, nt, sp, kbeg, kend);
 }
@@ -1454,7 +1475,7 @@ __host__ __device__ __forceinline__ int csk_block_of(int u, int b, int W) {
 }
 
 // gemm_p3_body (below): the tile on operands already split into planes, LDS-DMA only
-template <int BM, int BN, int WGM, int WGN, bool H3 = false, bool FLEX = false>
+template <int BM, int BN, int WGM, int WGN, bool H3 = false, bool FLEX = false, int NBUF = 2>
 __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int mt, int nt,
                                              int sp, int kbeg, int kend, int bma = BM);
 
@@ -1661,17 +1682,20 @@ static bool csk_plan(int M, int N, int K, int cus, double miss_cost, CskPlan& ou
 // H3 (tile 16 of the tuning build): the fp16 form on pre-split planes -- two fp16 planes of the
 // row-scaled operands (h3_split_kernel), three products per step, accumulators unscaled by
 // 1 / (sa sw) before the epilogue.
-template <int BM, int BN, int WGM, int WGN, bool H3 = false>
+template <int BM, int BN, int WGM, int WGN, bool H3 = false, int NBUF = 2>
 constexpr int p3_smem_bytes() {
   constexpr int NW = WGM * WGN, WM = BM / WGM;
   constexpr int BUF = (H3 ? 2 : 3) * (BM + BN) * 64, STAGE = NW * WM * 36 * 4;
-  return 2 * BUF > STAGE ? 2 * BUF : STAGE;
+  return NBUF * BUF > STAGE ? NBUF * BUF : STAGE;
 }
 
 // FLEX (the cycled stream-K tail): bma = 256 (256 x 128 tile) or 128 (128 x 256), as gemm_x3_body.
-template <int BM, int BN, int WGM, int WGN, bool H3, bool FLEX>
+// NBUF = 3: a three-stage ring (stage kt + 2 issued while stage kt computes), one barrier per
+// stage as with two; the fp16 256 x 128 ring is 3 x 48 KB.
+template <int BM, int BN, int WGM, int WGN, bool H3, bool FLEX, int NBUF>
 __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int mt, int nt,
                                              int sp, int kbeg, int kend, int bma) {
+  static_assert(NBUF == 2 || NBUF == 3, "p3 ring: 2 or 3 stages");
   static_assert(!FLEX || (BM == 256 && BN == 128 && WGM == 4 && WGN == 2), "FLEX: 256 x 128");
   constexpr int PL = H3 ? 2 : 3;
   constexpr int BK = 32;
@@ -1768,11 +1792,18 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
   constexpr int NG = TI * TJ;
   const int nk = (kend - kbeg) / BK;
   if (nk > 0) issue(0, kbeg);
+  if (NBUF == 3 && nk > 1) issue(1, kbeg + BK);
+  int cur = 0;             // kt % NBUF
   for (int kt = 0; kt < nk; ++kt) {
-    wait_vm<0>();          // this wave's pieces of stage kt have landed
+    if (NBUF == 3 && kt + 1 < nk) wait_vm<PPW>();   // stage kt + 1's pieces may still fly
+    else wait_vm<0>();     // this wave's pieces of stage kt have landed
     lds_barrier();         // ... everyone's; and every wave is done reading stage kt - 1
-    if (kt + 1 < nk) issue((kt + 1) & 1, kbeg + (kt + 1) * BK);
-    const char* S = smem + (kt & 1) * BUF;
+    if (kt + NBUF - 1 < nk) {
+      const int nb = cur == 0 ? NBUF - 1 : cur - 1;  // (kt + NBUF - 1) % NBUF: stage kt - 1's
+      issue(nb, kbeg + (kt + NBUF - 1) * BK);
+    }
+    const char* S = smem + cur * BUF;
+    cur = cur + 1 == NBUF ? 0 : cur + 1;
     Frags f0, f1;
     read(f0, S, 0);
 #pragma unroll
@@ -1806,15 +1837,15 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
 }
 
-template <int BM, int BN, int WGM, int WGN, bool H3 = false>
+template <int BM, int BN, int WGM, int WGN, bool H3 = false, int NBUF = 2>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3(GemmArgs p) {
-  __shared__ __attribute__((aligned(1024))) char smem[p3_smem_bytes<BM, BN, WGM, WGN, H3>()];
+  __shared__ __attribute__((aligned(1024))) char smem[p3_smem_bytes<BM, BN, WGM, WGN, H3, NBUF>()];
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
   const int nwg = mt_n * nt_n * p.splits;
-  const int bid = xcd_swizzle(blockIdx.x, nwg);
-  const int mt = bid % mt_n, nt = (bid / mt_n) % nt_n, sp = bid / (mt_n * nt_n);
+  int mt, nt, sp;
+  tile_of(xcd_swizzle(blockIdx.x, nwg), mt_n, nt_n, mt, nt, sp);
   const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
-  gemm_p3_body<BM, BN, WGM, WGN, H3, false>(p, smem, mt, nt, sp, kbeg, kend, BM);
+  gemm_p3_body<BM, BN, WGM, WGN, H3, false, NBUF>(p, smem, mt, nt, sp, kbeg, kend, BM);
 }
 
 // gemm_p3 in stream-K form (see gemm_x3_sk), pieces summed by streamk_fixup4_kernel
@@ -3794,7 +3825,11 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   else hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, true, 0, false, 32, true>), grid,         \
                           dim3(64 * WM_ * WN_), 0, s, a);
   if (p2 && (tile == 1 || tile == 2) && p2_prep()) {
-    if (tile == 1) hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true>), grid, dim3(512), 0, s, a);
+    static const char* env_ring = tuning_env("AZ_P3_RING");
+    const int ring = env_ring ? atoi(env_ring) : 2;
+    if (tile == 1 && ring == 3)
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3>), grid, dim3(512), 0, s, a);
+    else if (tile == 1) hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true>), grid, dim3(512), 0, s, a);
     else hipLaunchKernelGGL((gemm_p3<128, 128, 2, 2, true>), grid, dim3(256), 0, s, a);
     return true;
   }
