@@ -422,6 +422,39 @@ def transform_heads(x, w0, b0, w2, b2, wp, bp, wv, bv, hidden=None, y=None, logp
     return logp, pi, v, y, hidden
 
 
+def c4_gnn_eval(boards, W, G, feat=None, hidden=None, y=None, logp=None, pi=None, v=None):
+    """predict_with_gnn over a batch of 7x7 Connect4 boards (Connect4GNN.py:86-120 per row) as
+    ONE az_c4_eval_fwd call: trunk -> output_transform -> heads.  The trunk also writes
+    output_transform.0's A in the GEMM's split form and that GEMM's split-K reduce writes
+    output_transform.2's, so neither GEMM launches a split of its own; bit-identical to
+    c4_trunk + transform_heads.  W / G: the Connect4Net / PolicyValueGNN parameter dicts (their
+    storage registered, e.g. FlatParams).  Returns (logp, pi, v)."""
+    B = boards.shape[0]
+    F = 3136
+    A = W["fc_policy.weight"].shape[0]
+    dev = boards.device
+    assert boards.dtype == torch.int8 and boards.is_contiguous() and tuple(boards.shape[1:]) == (7, 7)
+    feat = torch.empty((B, F), device=dev) if feat is None else feat
+    hidden = torch.empty((B, F), device=dev) if hidden is None else hidden
+    y = torch.empty((B, F), device=dev) if y is None else y
+    logp = torch.empty((B, A), device=dev) if logp is None else logp
+    pi = torch.empty((B, A), device=dev) if pi is None else pi
+    v = torch.empty((B,), device=dev) if v is None else v
+    L = _lib.lib()
+    ws = workspace(dev, max(int(L.az_transform_heads_ws_bytes(B, F, A)), 96 << 20))
+    P = lambda t: t.data_ptr()  # noqa: E731
+    desc = _lib.C4Eval(
+        P(W["conv1.weight"]), P(W["conv1.bias"]), P(W["conv2.weight"]), P(W["conv2.bias"]),
+        P(W["fc_policy.weight"]), P(W["fc_policy.bias"]), P(W["fc_value.weight"]),
+        P(W["fc_value.bias"]), A, P(G["output_transform.0.weight"]),
+        P(G["output_transform.0.bias"]), P(G["output_transform.2.weight"]),
+        P(G["output_transform.2.bias"]), B, P(feat), P(hidden), P(y), P(logp), P(logp), P(ws),
+        ws.numel())
+    _lib.check(L.az_c4_eval_fwd(ctypes.byref(desc), _p(boards), B, None, None, _p(pi), _p(v),
+                                _stream()), "az_c4_eval_fwd")
+    return logp, pi, v
+
+
 def linear_heads(x, w, b, wp, bp, wv, bv, y=None, logp=None, pi=None, v=None, want_pi=True):
     """y = x w^T + b then the heads of y, with the GEMM's split-K reduction fused into the
     heads' first pass (the second half of transform_heads).  Returns (logp, pi, v, y)."""

@@ -3419,9 +3419,84 @@ __global__ __launch_bounds__(256) void h3_split_rows_kernel(const float* __restr
     put(ch, *reinterpret_cast<const f32x4*>(x + 8 * ch), *reinterpret_cast<const f32x4*>(x + 8 * ch + 4));
 }
 
-// A's rows are scaled into [2^13, 2^14) (fp16 max 65504); W's into [2^9, 2^10): its scales are
-// cached between weight updates (below) and stay safe while the weights grow up to 64x.
-constexpr int H3_TA = 14, H3_TW = 10;
+// The split-K reduce of a GEMM whose C is the next GEMM's A, fused with that GEMM's A split (the
+// output_transform.0 -> .2 hand-off, gnn_utils.py:115): one 256-thread block per row; each lane's
+// 8-column chunks are summed over the S slabs in slab order from 0.f, then bias and activation
+// -- splitk_reduce4_kernel's arithmetic, so C's bits are unchanged -- and stored; the row's max
+// |C| (one block reduction) gives the scale, and the chunks, still in registers, leave as the two
+// fp16 planes + scales h3_split_rows_kernel would make of C (out [2][M][N], sc [2][M]).  N % 8
+// == 0, N <= 4096, bias / activation epilogue only, 16-B aligned rows (splitk_reduce_split).
+template <int S>
+__global__ __launch_bounds__(256) void splitk_reduce_split_kernel(GemmArgs p,
+                                                                  unsigned short* __restrict__ out,
+                                                                  float* __restrict__ sc) {
+  __shared__ float wm[4];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int nch = p.N >> 3;
+  const size_t plane = (size_t)p.M * p.N;
+  const float* sl = p.slab + (size_t)r * p.N;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  f32x4 x[2][S][2], bb[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {               // every load issued before the first add
+    const int c = 8 * min(tid + 256 * u, nch - 1);
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      x[u][q][0] = *reinterpret_cast<const f32x4*>(sl + q * plane + c);
+      x[u][q][1] = *reinterpret_cast<const f32x4*>(sl + q * plane + c + 4);
+    }
+    bb[u][0] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + c) : z;
+    bb[u][1] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + c + 4) : z;
+  }
+  f32x4 v[2][2];
+  float m = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < S; ++q) t += x[u][q][h][e];
+        if (p.bias) t += bb[u][h][e];
+        v[u][h][e] = apply_act(t, p.act);
+      }
+    const int ch = tid + 256 * u;
+    if (ch < nch) {
+      float* dst = p.C + (size_t)r * p.ldc + 8 * ch;
+      *reinterpret_cast<f32x4*>(dst) = v[u][0];
+      *reinterpret_cast<f32x4*>(dst + 4) = v[u][1];
+      m = fmaxf(m, fmaxf(fmaxf(fmaxf(fabsf(v[u][0][0]), fabsf(v[u][0][1])),
+                               fmaxf(fabsf(v[u][0][2]), fabsf(v[u][0][3]))),
+                         fmaxf(fmaxf(fabsf(v[u][1][0]), fabsf(v[u][1][1])),
+                               fmaxf(fabsf(v[u][1][2]), fabsf(v[u][1][3])))));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (lane == 0) wm[tid >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+  float inv;
+  const float s = h3_scale(m, H3_TA, &inv);
+  if (tid == 0) {
+    sc[r] = s;
+    sc[p.M + r] = inv;
+  }
+  unsigned short* d = out + (size_t)r * p.N;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int ch = tid + 256 * u;
+    if (ch < nch) {
+      u32x4 o[2];
+      split2s(v[u][0], v[u][1], s, o);
+      *reinterpret_cast<u32x4*>(d + 8 * ch) = o[0];
+      *reinterpret_cast<u32x4*>(d + plane + 8 * ch) = o[1];
+    }
+  }
+}
+
 
 // W row-scale cache: weights change only between calls that say so (az_weights_changed, which
 // az_adam_f32 also calls; the Python parameter store calls it on every load / copy), so a
@@ -3555,7 +3630,7 @@ static const unsigned short* w_planes(const float* w, int n, int k, int ld, hipS
 // MI355X, tools/gemm_sweep.py x3: M = 512 75 us vs 103 us for the fp32 MFMA tile, M = 800 147 vs
 // 185, M = 4096 516 vs 767).  Tuning build: AZ_GEMM_X3=0 keeps the fp32 MFMA tiles, 1..4 forces
 // a tile, AZ_GEMM_SPLITS the split.  Sets a.splits / a.kc; false = not launched.
-static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
+static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSplitA* pre) {
   static const char* env = tuning_env("AZ_GEMM_X3");
   static const char* env_split = tuning_env("AZ_GEMM_SPLITS");
   // the fp16 form (H3) for the product tiles when the workspace can hold A's row scales (taken
@@ -3573,13 +3648,16 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
   // cached per weight generation (w_planes); the tile then moves both by LDS-DMA with no VALU --
   // 8-12 % faster tiles than splitting in the tile, bit-identical (tools/p2h_probe.py)
   const bool whole_k = a.K % 32 == 0;
-  const size_t p2a_bytes = ((size_t)4 * a.M * a.K + 255) / 256 * 256;
+  // a caller that already holds A's planes and scales (PreSplitA: the trunk / the fused split-K
+  // reduce of the layer before) needs no room for them here
+  const bool have_pre = pre && pre->planes && pre->sc && aligned16(pre->planes);
+  const size_t p2a_bytes = have_pre ? 0 : ((size_t)4 * a.M * a.K + 255) / 256 * 256;
   bool p2 = h3 && !tuning_env("AZ_GEMM_X3") && !tuning_env("AZ_GEMM_SPLITS") &&
             !tuning_env("AZ_GEMM_NOP2") && whole_k && a.lda % 4 == 0 && a.ldb % 4 == 0 &&
             aligned16(a.A) && aligned16(a.B) && ws_bytes >= p2a_bytes + 256 &&
             weights_registered(a.B, a.N, a.K, a.ldb);
   unsigned short* apl_buf = nullptr;
-  if (p2) {
+  if (p2 && !have_pre) {
     ws_bytes = (ws_bytes - p2a_bytes) / 256 * 256;
     apl_buf = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(a.slab) + ws_bytes);
   }
@@ -3587,13 +3665,18 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s) {
     const float* sw = nullptr;
     const unsigned short* wpl = w_planes(a.B, a.N, a.K, a.ldb, s, &sw);
     if (!wpl) return false;
-    hipLaunchKernelGGL(h3_split_rows_kernel, dim3(a.M), dim3(256), 0, s, a.A, a.M, a.K, a.lda,
-                       H3_TA, apl_buf, (size_t)a.M * a.K, sa_buf);
-    a.apl = apl_buf;
+    if (have_pre) {
+      a.apl = pre->planes;
+      a.sa = pre->sc;
+    } else {
+      hipLaunchKernelGGL(h3_split_rows_kernel, dim3(a.M), dim3(256), 0, s, a.A, a.M, a.K, a.lda,
+                         H3_TA, apl_buf, (size_t)a.M * a.K, sa_buf);
+      a.apl = apl_buf;
+      a.sa = sa_buf;
+    }
     a.apl_plane = (size_t)a.M * a.K;
     a.bpl = wpl;
     a.bpl_plane = (size_t)a.N * a.K;
-    a.sa = sa_buf;
     a.sw = sw;
     return true;
   };
@@ -3884,7 +3967,7 @@ static bool full_waves_256x128(int M, int N) {
 // The GEMM without its split-K reduction: when the plan splits K, the raw partial sums are left
 // in d->ws as slabs [*splits_out][M][N] and C is NOT written (the caller reduces them, e.g.
 // fused with its consumer: az_transform_heads_fwd); otherwise C is written and *splits_out = 1.
-int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
+int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out, const PreSplitA* pre) {
   *splits_out = 1;
   AZ_REQUIRE(d != nullptr, AZ_EINVAL, "az_gemm_f32: null descriptor");
   AZ_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, AZ_EINVAL, "az_gemm_f32: negative size");
@@ -3946,7 +4029,7 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out) {
     }
   }
   const bool glds_ok = akm && bkm && !d->A2 && !d->a_rows;
-  if (glds_ok && d->M > 8 && d->K >= 1024 && d->N >= 256 && launch_x3(a, d->ws_bytes, s)) {
+  if (glds_ok && d->M > 8 && d->K >= 1024 && d->N >= 256 && launch_x3(a, d->ws_bytes, s, pre)) {
     *splits_out = a.splits;
     return check_launch("gemm_x3");
   }
@@ -4031,6 +4114,39 @@ int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s) {
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, a);
   return check_launch("splitk_reduce_kernel");
+}
+
+// splitk_reduce, and C's rows split for a P2 GEMM that takes C as its A (PreSplitA{planes, sc}:
+// planes [2][M][N] fp16, sc [2][M]); C's bits are splitk_reduce's.  Returns 1 when launched, 0 when
+// the shapes / epilogue do not qualify (nothing launched: the caller reduces the usual way), or a
+// negative AZ_E* code.
+int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* planes, float* sc,
+                        hipStream_t s) {
+  if (!(splits >= 2 && splits <= 8 && d->N % 8 == 0 && d->N <= 4096 && d->M > 0 && !d->C2 &&
+        !d->R && !d->G && !d->c_rows && d->beta == 0.f &&
+        (d->act == AZ_ACT_NONE || d->act == AZ_ACT_RELU) && d->ldc % 4 == 0 && aligned16(d->C) &&
+        (!d->bias || aligned16(d->bias)) && aligned16(d->ws) && planes && sc &&
+        aligned16(planes)))
+    return 0;
+  GemmArgs a = {};
+  a.M = d->M; a.N = d->N;
+  a.bias = d->bias; a.act = d->act; a.C = d->C; a.ldc = d->ldc;
+  a.slab = static_cast<float*>(d->ws);
+  a.splits = splits;
+  switch (splits) {
+#define AZ_RS(SS) case SS: hipLaunchKernelGGL(splitk_reduce_split_kernel<SS>, dim3(a.M), dim3(256), \
+                                             0, s, a, planes, sc); break;
+    AZ_RS(2) AZ_RS(3) AZ_RS(4) AZ_RS(5) AZ_RS(6) AZ_RS(7) default: AZ_RS(8)
+#undef AZ_RS
+  }
+  const int rc = check_launch("splitk_reduce_split_kernel");
+  return rc == AZ_OK ? 1 : rc;
+}
+
+// Whether a GEMM with weight w (n x k, row stride ld) takes the P2 path's cached weight planes,
+// i.e. whether splitting its A ahead of the call (PreSplitA) can pay off.
+bool gemm_p2_weights(const float* w, int n, int k, int ld) {
+  return k % 32 == 0 && weights_registered(w, n, k, ld);
 }
 
 // gemv_side_heads for the batch-1 leaf and small speculative batches: d must be M <= 8 (the
@@ -4138,7 +4254,7 @@ extern "C" int az_tuning_leaf_trace(unsigned long long* out) {
 
 int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
   int splits = 1;
-  int rc = gemm_f32_partial(d, s, &splits);
+  int rc = gemm_f32_partial(d, s, &splits, nullptr);
   if (rc || splits <= 1) return rc;
   return splitk_reduce(d, splits, s);
 }

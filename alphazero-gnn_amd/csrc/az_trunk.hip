@@ -17,6 +17,7 @@
 #include "az_common.h"
 #include "az_heads.h"
 #include "az_trunk_split.h"
+#include "az_x3.h"
 
 namespace az {
 
@@ -33,13 +34,18 @@ constexpr int trunk_union_floats() {
 // (each lane then reads its 72 fragments from LDS -- one pass over the 74 KB per block instead of
 // 72 scattered 4-byte loads per lane in all 8 waves), and with NB <= 4 the feature rows are then
 // assembled in it (still there on return).
+// apl / asc (NB <= 4 only; may be null): the feature rows also leave as the P2 GEMM's A operand
+// for output_transform.0 (PreSplitA: two fp16 planes [2][B][3136] and scales [2][B], the bits
+// h3_split_rows_kernel would make of feat), so that GEMM needs no split launch of its own.
 template <int NB>
 __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards, int B,
                                               const float* __restrict__ w1,
                                               const float* __restrict__ b1,
                                               const float* __restrict__ w2,
                                               const float* __restrict__ b2,
-                                              float* __restrict__ feat, float* un) {
+                                              float* __restrict__ feat, float* un,
+                                              unsigned short* __restrict__ apl = nullptr,
+                                              float* __restrict__ asc = nullptr) {
   float* const ob = un;
   constexpr int P = 49, PP = 81, CI = 32;
   constexpr int ROWS = NB * P;
@@ -168,7 +174,50 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
     __syncthreads();
     f32x4v* dst = reinterpret_cast<f32x4v*>(feat + (size_t)b0 * 3136);
     const f32x4v* src = reinterpret_cast<const f32x4v*>(ob);
-    for (int i = tid; i < nb * 784; i += 512) dst[i] = src[i];
+    if (!apl) {
+      for (int i = tid; i < nb * 784; i += 512) dst[i] = src[i];
+      return;
+    }
+    // each board's max |feature| (max is exact: any order gives h3_split_rows_kernel's value)
+    __shared__ float wmax[NB][8];
+    float m[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) m[b] = 0.f;
+    for (int i = tid; i < nb * 784; i += 512) {
+      const f32x4v q = src[i];
+      const float a = fmaxf(fmaxf(fabsf(q[0]), fabsf(q[1])), fmaxf(fabsf(q[2]), fabsf(q[3])));
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (i / 784 == b) m[b] = fmaxf(m[b], a);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m[b] = fmaxf(m[b], __shfl_xor(m[b], o));
+      if (lane == 0) wmax[b][wave] = m[b];
+    }
+    __syncthreads();
+    const size_t plane = (size_t)B * 3136;
+    for (int ch = tid; ch < nb * 392; ch += 512) {     // 8-float chunks: fp32 row + two planes
+      const int b = ch / 392, c = ch - b * 392;
+      float mx = wmax[b][0];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) mx = fmaxf(mx, wmax[b][w]);
+      float inv;
+      const float sc = h3_scale(mx, H3_TA, &inv);
+      const f32x4v lo = src[2 * ch], hi = src[2 * ch + 1];
+      dst[2 * ch] = lo;
+      dst[2 * ch + 1] = hi;
+      u32x4 o[2];
+      split2s(__builtin_bit_cast(f32x4, lo), __builtin_bit_cast(f32x4, hi), sc, o);
+      unsigned short* d = apl + (size_t)(b0 + b) * 3136 + 8 * c;
+      *reinterpret_cast<u32x4*>(d) = o[0];
+      *reinterpret_cast<u32x4*>(d + plane) = o[1];
+      if (c == 0) {
+        asc[b0 + b] = sc;
+        asc[B + b0 + b] = inv;
+      }
+    }
   }
 }
 
@@ -181,6 +230,17 @@ __global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict_
                                                       float* __restrict__ feat) {
   __shared__ __attribute__((aligned(16))) float un[trunk_union_floats<NB>()];
   c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, un);
+}
+
+// c4_trunk_kernel that also writes feat's rows as output_transform.0's pre-split A (NB <= 4)
+template <int NB>
+__global__ __launch_bounds__(512) void c4_trunk_split_a_kernel(
+    const int8_t* __restrict__ boards, int B, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    float* __restrict__ feat, unsigned short* __restrict__ apl, float* __restrict__ asc) {
+  static_assert(NB <= 4, "the A split reads the LDS staging tile");
+  __shared__ __attribute__((aligned(16))) float un[trunk_union_floats<NB>()];
+  c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, un, apl, asc);
 }
 
 // Generic 3x3 conv + ReLU, one thread per output (TicTacToe trunks: tiny, latency-bound).
@@ -654,14 +714,14 @@ __global__ __launch_bounds__(512) void c4_trunk_heads_kernel(
 
 using namespace az;
 
-extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w,
-                               const float* conv1_b, const float* conv2_w, const float* conv2_b,
-                               float* feat, void* stream) {
-  AZ_REQUIRE(B >= 0, AZ_EINVAL, "az_c4_trunk_fwd: B=%d", B);
-  if (B == 0) return AZ_OK;
-  AZ_REQUIRE(boards && conv1_w && conv1_b && conv2_w && conv2_b && feat, AZ_EINVAL,
-             "az_c4_trunk_fwd: null pointer");
-  hipStream_t s = as_stream(stream);
+namespace az {
+// The Connect4 trunk launch (az_c4_trunk_fwd); apl / asc non-null: when the chosen NB stages its
+// output in LDS (NB <= 4: B <= 1,024 on 256 CUs) the rows also leave as output_transform.0's
+// pre-split A (c4_trunk_split_a_kernel) and *split is set; otherwise *split stays false.
+static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
+                           const float* conv1_b, const float* conv2_w, const float* conv2_b,
+                           float* feat, unsigned short* apl, float* asc, bool* split,
+                           hipStream_t s) {
   static const char* env = tuning_env("AZ_TRUNK_NB");   // tuning experiments only
   // boards per block: the time is whole rounds of blocks over the CUs, each round t(NB) (one
   // block per CU at a time in effect; measured on MI355X, profiles/r03w_trunk_nb_sweep.jsonl:
@@ -686,6 +746,13 @@ extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w
     }
   }
   if (env) nbk = atoi(env);
+  const bool sa = apl && asc && nbk >= 1 && nbk <= 4;
+  if (split) *split = sa;
+#define AZ_TRUNK(NB_)                                                                            \
+  if (sa) hipLaunchKernelGGL(c4_trunk_split_a_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), \
+                             0, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, apl, asc); \
+  else hipLaunchKernelGGL(c4_trunk_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), 0, s,       \
+                          boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat);
   switch (nbk) {
     case 8:
       hipLaunchKernelGGL(c4_trunk_kernel<8>, dim3((B + 7) / 8), dim3(512), 0, s, boards, B,
@@ -703,27 +770,29 @@ extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w
       hipLaunchKernelGGL(c4_trunk_kernel<5>, dim3((B + 4) / 5), dim3(512), 0, s, boards, B,
                          conv1_w, conv1_b, conv2_w, conv2_b, feat);
       break;
-    case 4:
-      hipLaunchKernelGGL(c4_trunk_kernel<4>, dim3((B + 3) / 4), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
-      break;
-    case 3:
-      hipLaunchKernelGGL(c4_trunk_kernel<3>, dim3((B + 2) / 3), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
-      break;
-    case 2:
-      hipLaunchKernelGGL(c4_trunk_kernel<2>, dim3((B + 1) / 2), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
-      break;
+    case 4: AZ_TRUNK(4) break;
+    case 3: AZ_TRUNK(3) break;
+    case 2: AZ_TRUNK(2) break;
     case 0:   // latency form: 4 blocks per board (bit-identical)
       hipLaunchKernelGGL(c4_trunk_split_kernel, dim3(B, 4), dim3(256), 0, s, boards, conv1_w,
                          conv1_b, conv2_w, conv2_b, feat);
       break;
-    default:
-      hipLaunchKernelGGL(c4_trunk_kernel<1>, dim3(B), dim3(512), 0, s, boards, B, conv1_w,
-                         conv1_b, conv2_w, conv2_b, feat);
+    default: AZ_TRUNK(1)
   }
+#undef AZ_TRUNK
   return check_launch("c4_trunk_kernel");
+}
+}  // namespace az
+
+extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w,
+                               const float* conv1_b, const float* conv2_w, const float* conv2_b,
+                               float* feat, void* stream) {
+  AZ_REQUIRE(B >= 0, AZ_EINVAL, "az_c4_trunk_fwd: B=%d", B);
+  if (B == 0) return AZ_OK;
+  AZ_REQUIRE(boards && conv1_w && conv1_b && conv2_w && conv2_b && feat, AZ_EINVAL,
+             "az_c4_trunk_fwd: null pointer");
+  return c4_trunk_launch(boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, nullptr, nullptr,
+                         nullptr, as_stream(stream));
 }
 
 extern "C" int az_conv3x3_relu_fwd(const void* in, int in_int8, int B, int Cin, int H, int W,
@@ -752,8 +821,32 @@ int gemv1_with_side_heads(const az_gemm_desc* d, const SideHeads* h, hipStream_t
 int c4_leaf_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, float* v, float* gpi,
                 float* gv, hipStream_t s);
 int gemm_f32(const az_gemm_desc* d, hipStream_t s);
-int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out);
+int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out, const PreSplitA* pre);
 int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s);
+int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* planes, float* sc,
+                        hipStream_t s);
+bool gemm_p2_weights(const float* w, int n, int k, int ld);
+
+static size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
+// The B x F pre-split-A region at the END of a transform_heads / c4_eval workspace: two fp16
+// planes [2][B][F] and scales [2][B] (PreSplitA), written by the trunk for output_transform.0 and
+// then by output_transform.0's fused reduce for output_transform.2.
+struct PreRegion {
+  unsigned short* planes;
+  float* sc;
+  size_t bytes;   // taken from the end of the workspace (0: no region)
+};
+static size_t pre_region_bytes(int B, int F) {
+  return align256((size_t)4 * B * F) + align256((size_t)8 * B) + 256;
+}
+static PreRegion pre_region(void* ws, size_t ws_bytes, int B, int F, size_t reserved) {
+  const size_t need = pre_region_bytes(B, F);
+  if (!ws || ws_bytes < reserved + need) return {nullptr, nullptr, 0};
+  char* base = static_cast<char*>(ws) + (ws_bytes - need + 255) / 256 * 256;
+  return {reinterpret_cast<unsigned short*>(base),
+          reinterpret_cast<float*>(base + align256((size_t)4 * B * F)), need};
+}
 }  // namespace az
 
 extern "C" size_t az_heads_ws_bytes(int B, int K, int A) {
@@ -865,14 +958,14 @@ extern "C" int az_c4_trunk_heads_fwd(const int8_t* boards, int B, const float* c
                       ws_bytes, stream);
 }
 
-static size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
 extern "C" size_t az_transform_heads_ws_bytes(int B, int F, int A) {
   // the heads' chunk partials, then room for 8 split-K slabs of the [B][F] GEMM outputs, the
   // GEMM's A operand as two fp16 planes (the fp16 form on pre-split planes, az_gemm.hip) and
-  // A's row scales
+  // A's row scales, and the pre-split-A region (pre_region) at the end
   return align256(az_heads_ws_bytes(B, F, A)) + (size_t)8 * B * F * 4 +
-         align256((size_t)4 * B * F) + align256((size_t)8 * B) + 256;
+         align256((size_t)4 * B * F) + align256((size_t)8 * B) + 256 +
+         az::pre_region_bytes(B, F);
 }
 
 template <int S>
@@ -899,10 +992,12 @@ static void launch_splitk_heads(const float* slab, int B, int K, const float* bi
                      wp, A, wv, part);
 }
 
-extern "C" int az_linear_heads_fwd(const float* x, int B, int F, const float* w, const float* b,
-                                   const float* wp, const float* bp, int A, const float* wv,
-                                   const float* bv, float* y, float* logp, float* pi, float* v,
-                                   void* ws, size_t ws_bytes, void* stream) {
+namespace az {
+// az_linear_heads_fwd with x optionally already in the P2 GEMM's form (pre, may be null)
+static int linear_heads_impl(const float* x, int B, int F, const float* w, const float* b,
+                             const float* wp, const float* bp, int A, const float* wv,
+                             const float* bv, float* y, float* logp, float* pi, float* v,
+                             void* ws, size_t ws_bytes, void* stream, const PreSplitA* pre) {
   AZ_REQUIRE(B >= 0 && F > 0 && F % 4 == 0 && A > 0 && A <= 32, AZ_EINVAL,
              "az_linear_heads_fwd: bad shape B=%d F=%d A=%d", B, F, A);
   if (B == 0) return AZ_OK;
@@ -925,7 +1020,7 @@ extern "C" int az_linear_heads_fwd(const float* x, int B, int F, const float* w,
   d.C = y; d.ldc = F;
   d.ws = slabs; d.ws_bytes = ws_bytes - part_bytes;
   int S = 1;
-  if ((rc = gemm_f32_partial(&d, s, &S))) return rc;
+  if ((rc = gemm_f32_partial(&d, s, &S, pre))) return rc;
   const float* sl = static_cast<const float*>(slabs);
   // one launch: splitk_heads_rowsw_kernel (AZ_SPLITK_HEADS_MODE = rows / chunks select the
   // one-row-per-block kernel / chunk partials + finalize for A/B runs)
@@ -980,6 +1075,58 @@ extern "C" int az_linear_heads_fwd(const float* x, int B, int F, const float* w,
   return az_heads_fwd(y, F, y, F, B, F, wp, bp, A, wv, bv, logp, pi, v, part, part_bytes, stream);
 }
 
+// az_transform_heads_fwd with x optionally pre-split (pre_x: the trunk wrote it into the
+// workspace's pre_region).  When output_transform.0 leaves split-K slabs and output_transform.2
+// takes the P2 path, the slabs' reduce also writes hidden's planes into pre_region
+// (splitk_reduce_split), so neither GEMM launches a split of its own; every output is bit-identical
+// to the unfused sequence (same planes, same products, same reduce arithmetic).
+static int transform_heads_impl(const float* x, int B, int F, const float* w0, const float* b0,
+                                const float* w2, const float* b2, const float* wp,
+                                const float* bp, int A, const float* wv, const float* bv,
+                                float* hidden, float* y, float* logp, float* pi, float* v,
+                                void* ws, size_t ws_bytes, void* stream, const PreSplitA* pre_x) {
+  const size_t part_bytes = align256(az_heads_ws_bytes(B, F, A > 0 ? A : 1));
+  AZ_REQUIRE(ws_bytes >= part_bytes, AZ_EINVAL, "az_transform_heads_fwd: workspace too small");
+  hipStream_t s = as_stream(stream);
+  static const bool no_fuse = tuning_env("AZ_NO_PRESPLIT") != nullptr;   // A/B experiments
+  // the region is reserved whenever the caller's pre_x lives in it (the same address: pre_region
+  // depends only on ws, ws_bytes, B, F)
+  const PreRegion R = pre_x || (!no_fuse && gemm_p2_weights(w2, F, F, F))
+                          ? pre_region(ws, ws_bytes, B, F, part_bytes + (size_t)B * F * 8)
+                          : PreRegion{nullptr, nullptr, 0};
+  AZ_REQUIRE(!pre_x || pre_x->planes == R.planes, AZ_EINVAL,
+             "az_transform_heads_fwd: pre-split A outside the workspace's region");
+  // hidden = relu(x W0^T + b0)   (output_transform.0 + ReLU); slabs after the heads' partials
+  az_gemm_desc d = {};
+  d.M = B; d.N = F; d.K = F;
+  d.A = x; d.lda = F; d.a_kmajor = 1;
+  d.B = w0; d.ldb = F; d.b_kmajor = 1; d.bias = b0; d.act = AZ_ACT_RELU;
+  d.C = hidden; d.ldc = F;
+  d.ws = static_cast<char*>(ws) + part_bytes;
+  d.ws_bytes = ws_bytes - part_bytes - R.bytes;
+  int S = 1, rc;
+  if ((rc = gemm_f32_partial(&d, s, &S, pre_x))) return rc;
+  PreSplitA pre_h{nullptr, nullptr};
+  if (S > 1) {
+    rc = R.planes ? splitk_reduce_split(&d, S, R.planes, R.sc, s) : 0;
+    if (rc < 0) return rc;
+    if (rc == 1) pre_h = {R.planes, R.sc};
+    else if ((rc = splitk_reduce(&d, S, s))) return rc;
+  }
+  // y = hidden W2^T + b2 (output_transform.2) and the heads
+  return linear_heads_impl(hidden, B, F, w2, b2, wp, bp, A, wv, bv, y, logp, pi, v, ws,
+                           ws_bytes - R.bytes, stream, pre_h.planes ? &pre_h : nullptr);
+}
+}  // namespace az
+
+extern "C" int az_linear_heads_fwd(const float* x, int B, int F, const float* w, const float* b,
+                                   const float* wp, const float* bp, int A, const float* wv,
+                                   const float* bv, float* y, float* logp, float* pi, float* v,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  return az::linear_heads_impl(x, B, F, w, b, wp, bp, A, wv, bv, y, logp, pi, v, ws, ws_bytes,
+                               stream, nullptr);
+}
+
 extern "C" int az_transform_heads_fwd(const float* x, int B, int F, const float* w0,
                                       const float* b0, const float* w2, const float* b2,
                                       const float* wp, const float* bp, int A, const float* wv,
@@ -992,20 +1139,8 @@ extern "C" int az_transform_heads_fwd(const float* x, int B, int F, const float*
   AZ_REQUIRE(x && w0 && b0 && hidden && ws, AZ_EINVAL, "az_transform_heads_fwd: null pointer");
   AZ_REQUIRE(aligned16(x) && aligned16(hidden) && aligned16(ws), AZ_EINVAL,
              "az_transform_heads_fwd: operands need 16B alignment");
-  const size_t part_bytes = align256(az_heads_ws_bytes(B, F, A > 0 ? A : 1));
-  AZ_REQUIRE(ws_bytes >= part_bytes, AZ_EINVAL, "az_transform_heads_fwd: workspace too small");
-  // hidden = relu(x W0^T + b0)   (output_transform.0 + ReLU); slabs after the heads' partials
-  az_gemm_desc d = {};
-  d.M = B; d.N = F; d.K = F;
-  d.A = x; d.lda = F; d.a_kmajor = 1;
-  d.B = w0; d.ldb = F; d.b_kmajor = 1; d.bias = b0; d.act = AZ_ACT_RELU;
-  d.C = hidden; d.ldc = F;
-  d.ws = static_cast<char*>(ws) + part_bytes; d.ws_bytes = ws_bytes - part_bytes;
-  int rc = gemm_f32(&d, as_stream(stream));
-  if (rc) return rc;
-  // y = hidden W2^T + b2 (output_transform.2) and the heads
-  return az_linear_heads_fwd(hidden, B, F, w2, b2, wp, bp, A, wv, bv, y, logp, pi, v, ws,
-                             ws_bytes, stream);
+  return transform_heads_impl(x, B, F, w0, b0, w2, b2, wp, bp, A, wv, bv, hidden, y, logp, pi, v,
+                              ws, ws_bytes, stream, nullptr);
 }
 
 extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi,
@@ -1042,19 +1177,31 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
                                  e->glogp, gpi, gv, e->ws, e->ws_bytes, stream);
     // shapes not covered: the general sequence below (re-runs the trunk, harmless)
   }
+  // GNN tail only (predict_with_gnn batches): the trunk also writes feat's rows as
+  // output_transform.0's pre-split A into the workspace's pre_region when that GEMM takes the
+  // P2 path (c4_trunk_launch decides by its NB)
+  PreRegion R{nullptr, nullptr, 0};
+  bool split = false;
+  static const bool no_fuse = tuning_env("AZ_NO_PRESPLIT") != nullptr;   // A/B experiments
+  if (!v && gv && !no_fuse && e->ot0_w && aligned16(e->ws) && gemm_p2_weights(e->ot0_w, 3136, 3136, 3136))
+    R = pre_region(e->ws, e->ws_bytes, B, 3136,
+                   align256(az_heads_ws_bytes(B, 3136, e->A)) + (size_t)B * 3136 * 8);
   if (v) {
     rc = az_c4_trunk_heads_fwd(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b,
                                e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,
                                e->feat, e->logp, pi, v, e->ws, e->ws_bytes, stream);
   } else {
-    rc = az_c4_trunk_fwd(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b, e->feat,
-                         stream);
+    rc = c4_trunk_launch(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b, e->feat,
+                         R.planes, R.sc, &split, as_stream(stream));
   }
   if (rc || !gv) return rc;
   AZ_REQUIRE(e->ot0_w && e->ot0_b && e->ot2_w && e->ot2_b && e->hidden && e->y && e->glogp,
              AZ_EINVAL, "az_c4_eval_fwd: GNN tail requested without its weights / scratch");
-  return az_transform_heads_fwd(e->feat, B, 3136, e->ot0_w, e->ot0_b, e->ot2_w, e->ot2_b,
-                                e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w,
-                                e->fc_value_b, e->hidden, e->y, e->glogp, gpi, gv, e->ws,
-                                e->ws_bytes, stream);
+  AZ_REQUIRE(aligned16(e->feat) && aligned16(e->hidden) && aligned16(e->ws), AZ_EINVAL,
+             "az_c4_eval_fwd: scratch needs 16B alignment");
+  const PreSplitA pre{R.planes, R.sc};
+  return transform_heads_impl(e->feat, B, 3136, e->ot0_w, e->ot0_b, e->ot2_w, e->ot2_b,
+                              e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,
+                              e->hidden, e->y, e->glogp, gpi, gv, e->ws, e->ws_bytes, stream,
+                              split ? &pre : nullptr);
 }

@@ -132,4 +132,17 @@ __device__ __forceinline__ f32x16 mfma6_32x32x16(const bf16x8 (&a)[3], const bf1
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], t, 0, 0, 0);
 }
 
+// A's rows are scaled into [2^13, 2^14) (fp16 max 65504); W's into [2^9, 2^10): W's scales are
+// cached between weight updates (az_gemm.hip) and stay safe while the weights grow up to 64x.
+constexpr int H3_TA = 14, H3_TW = 10;
+
+// An A operand already in the P2 GEMM's form, made by whoever produced A (the Connect4 trunk,
+// the fused split-K reduce of the GEMM before): planes = two fp16 planes [2][M][K] (split2s of
+// x * s), sc = [2][M] (s, then 1 / s) with s = h3_scale(max_k |x|, H3_TA) -- exactly what
+// h3_split_rows_kernel would write, so the GEMM's bits do not depend on who split A.
+struct PreSplitA {
+  const unsigned short* planes;
+  const float* sc;
+};
+
 }  // namespace az

@@ -1,0 +1,67 @@
+"""The pre-split A hand-offs of the batched predict_with_gnn (Connect4GNN.py:86-120 per row,
+output_transform = gnn_utils.py:115): the trunk writing output_transform.0's A as the fp16-form
+GEMM's planes + row scales, and output_transform.0's split-K reduce writing output_transform.2's
+(ops.c4_gnn_eval, one az_c4_eval_fwd call), give the same bits as the unfused calls -- trunk,
+then each GEMM splitting its own A -- at every batch size (trunk NB 1..8, split-K and stream-K
+GEMMs), and the same bits with unregistered weights (no hand-off: the plain path)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ev():
+    from azhip.nets import C4Evaluator
+    from azhip.weights import connect4_net_spec, gnn_spec, synthetic_state_dict
+    W = synthetic_state_dict(connect4_net_spec(7), 1)
+    G = synthetic_state_dict(gnn_spec(3136, 2), 2)
+    return C4Evaluator(W, G, device=torch.device("cuda"))
+
+
+def _unfused(ops, boards, Wn, Gn):
+    feat = ops.c4_trunk(boards, Wn)
+    h = ops.linear(feat, Gn["output_transform.0.weight"], Gn["output_transform.0.bias"],
+                   act=ops.ACT_RELU)
+    logp, pi, v, _ = ops.linear_heads(h, Gn["output_transform.2.weight"],
+                                      Gn["output_transform.2.bias"], Wn["fc_policy.weight"],
+                                      Wn["fc_policy.bias"], Wn["fc_value.weight"],
+                                      Wn["fc_value.bias"])
+    return feat, h, logp, pi, v
+
+
+@pytest.mark.parametrize("B", [1, 9, 300, 512, 1024, 1576, 3150])
+def test_c4_gnn_eval_equals_unfused_calls(ev, B):
+    from azhip import ops
+    Wn, Gn = ev.nnet.params, ev.gnn.params
+    rng = np.random.default_rng(B)
+    boards = torch.from_numpy(rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int8)).cuda()
+    feat = torch.empty((B, 3136), device="cuda")
+    hidden = torch.empty((B, 3136), device="cuda")
+    logp, pi, v = ops.c4_gnn_eval(boards, Wn, Gn, feat=feat, hidden=hidden)
+    feat_u, h_u, logp_u, pi_u, v_u = _unfused(ops, boards, Wn, Gn)
+    _, pi_e, v_e = ev.evaluate(boards, gnn=True)
+    torch.cuda.synchronize()
+    assert torch.equal(feat, feat_u)
+    assert torch.equal(hidden, h_u)
+    assert torch.equal(logp, logp_u) and torch.equal(pi, pi_u) and torch.equal(v, v_u)
+    assert torch.equal(pi, pi_e) and torch.equal(v, v_e)
+
+
+def test_c4_gnn_eval_unregistered_weights(ev):
+    """Weights outside registered parameter storage: no cached planes, so no hand-off; the call
+    still computes the same network (bit-identical to the unfused calls on the same copies)."""
+    from azhip import ops
+    Wn = {k: ev.nnet.params[k].clone() for k in ev.nnet.params.keys()}
+    Gn = {k: ev.gnn.params[k].clone() for k in ev.gnn.params.keys()}
+    B = 512
+    rng = np.random.default_rng(7)
+    boards = torch.from_numpy(rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int8)).cuda()
+    logp, pi, v = ops.c4_gnn_eval(boards, Wn, Gn)
+    _, _, logp_u, pi_u, v_u = _unfused(ops, boards, Wn, Gn)
+    _, pi_r, v_r = ev.evaluate(boards, gnn=True)
+    torch.cuda.synchronize()
+    assert torch.equal(logp, logp_u) and torch.equal(pi, pi_u) and torch.equal(v, v_u)
+    # registered vs unregistered storage of the same values: the same bits (same planes)
+    assert torch.equal(pi, pi_r) and torch.equal(v, v_r)
