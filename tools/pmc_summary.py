@@ -54,15 +54,19 @@ def main(d, tag):
             prv = rows[i - 1][1] if i > 0 else ""
             # output_transform.0 = the tile kernel followed by its splitk_reduce_kernel (the
             # second GEMM's slabs go to splitk_heads_partial_kernel instead)
-            if tile_pred(name) and "splitk_reduce" in nxt:
+            # (the standalone call; the bench step's output_transform.0 hands its slabs to
+            # splitk_reduce_split_kernel, which also splits the next GEMM's A: not matched)
+            if tile_pred(name) and ("splitk_reduce4_kernel" in nxt or
+                                    "splitk_reduce_kernel" in nxt):
                 tile.append(kb)
                 red.append(rows[i + 1][2])
-                scl.append(rows[i - 1][2] if "row_scale_kernel" in prv else 0.0)
+                scl.append(rows[i - 1][2] if ("row_scale_kernel" in prv or
+                                              "h3_split_rows_kernel" in prv) else 0.0)
         n = max(1, len(tile))
         return sum(tile) / n, sum(red) / n, len(tile), sum(scl) / n
 
     # the forward Linear path of the bench GEMMs (gemm_x3 from r02m on)
-    is_fwd_gemm = lambda n: "gemm_f32_glds" in n or "gemm_x3" in n
+    is_fwd_gemm = lambda n: "gemm_f32_glds" in n or "gemm_x3" in n or "gemm_p3" in n
     ft, fr, nf, fs = call_bytes(fetch, is_fwd_gemm)
     wt, wr, _, ws = call_bytes(write, is_fwd_gemm)
     gemm_tile = int((2 * ft + wt) * 1024)
@@ -82,7 +86,9 @@ def main(d, tag):
                   f"half of wide reads, MI355X_MICROARCH.md HBM section)",
         "gemm": {"kernel": "az_gemm_f32 output_transform.0 call (%s%s tile kernel + "
                            "splitk_reduce4_kernel)" % (
-                               "row_scale_kernel + " if gemm_scale else "",
+                               ("h3_split_rows_kernel + " if any("gemm_p3" in r[1] for r in fetch)
+                                else "row_scale_kernel + ") if gemm_scale else "",
+                               "gemm_p3" if any("gemm_p3" in r[1] for r in fetch) else
                                "gemm_x3" if any("gemm_x3" in r[1] for r in fetch)
                                else "gemm_f32_glds2"),
                  "dispatches": nf,
