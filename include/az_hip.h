@@ -167,7 +167,11 @@ typedef struct az_c4_eval {
   int* sync; int* err;
 } az_c4_eval;
 /* v != NULL: standard heads into pi [B][A] (may be NULL) and v [B];  gv != NULL: the GNN tail
- * into gpi / gv.  boards, pi, v, gpi, gv may be az_host_alloc memory. */
+ * into gpi / gv.  boards, pi, v, gpi, gv may be az_host_alloc memory.  With v == NULL (the
+ * batched predict_with_gnn alone) and registered output_transform weights, the trunk writes
+ * output_transform.0's operand already split for the fp16-form GEMM and that GEMM's split-K
+ * reduce writes output_transform.2's, both into the last az_transform_heads_ws_bytes-sized
+ * region of e->ws; the outputs are bit-identical to az_c4_trunk_fwd + az_transform_heads_fwd. */
 int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, float* v,
                    float* gpi, float* gv, void* stream);
 
