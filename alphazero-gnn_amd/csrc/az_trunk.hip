@@ -1029,17 +1029,19 @@ static int linear_heads_impl(const float* x, int B, int F, const float* w, const
   const bool rows_mode = mode != 'c' && F <= SPLITK_ROWS_MAXK &&
                          (F + HEADS_KC - 1) / HEADS_KC <= HEADS_ROWS_MAXC;
   const int nch = (F + HEADS_KC - 1) / HEADS_KC;
+  // rows per block: 1 (512 blocks at B = 512, 1.2-2 us faster per call than 2 rows at B = 256 ..
+  // 4,096 in the fused step: profiles/r04x/heads_rows_ab.jsonl; the same bits for any R)
   static const char* env_r = tuning_env("AZ_SPLITK_HEADS_R");   // rows per block, A/B runs
-  const int R = env_r ? atoi(env_r) : 2;
+  const int R = env_r ? atoi(env_r) : 1;
   if (S > 1 && A <= 8 && S <= 8 && rows_mode && mode == 'w' && nch <= 16 &&
       (R == 1 || R == 2 || R == 4)) {
     const dim3 g((B + R - 1) / R), blk(64 * nch);
     switch (S * 8 + R) {
 #define AZ_SKW(SS, RR) case SS * 8 + RR: hipLaunchKernelGGL((splitk_heads_rowsw_kernel<8, SS, RR>), g, \
                            blk, 0, s, sl, B, F, b, y, wp, A, wv, bp, bv, logp, pi, v); break;
-      AZ_SKW(2, 2) AZ_SKW(3, 2) AZ_SKW(4, 2) AZ_SKW(5, 2) AZ_SKW(6, 2) AZ_SKW(7, 2) AZ_SKW(8, 2)
-#ifdef AZ_TUNING   // 1 and 4 rows per block: measured slower than 2 (AZ_SPLITK_HEADS_R)
       AZ_SKW(2, 1) AZ_SKW(3, 1) AZ_SKW(4, 1) AZ_SKW(5, 1) AZ_SKW(6, 1) AZ_SKW(7, 1) AZ_SKW(8, 1)
+#ifdef AZ_TUNING   // 2 and 4 rows per block (AZ_SPLITK_HEADS_R): 2 measured equal or slower
+      AZ_SKW(2, 2) AZ_SKW(3, 2) AZ_SKW(4, 2) AZ_SKW(5, 2) AZ_SKW(6, 2) AZ_SKW(7, 2) AZ_SKW(8, 2)
       AZ_SKW(2, 4) AZ_SKW(3, 4) AZ_SKW(4, 4) AZ_SKW(5, 4) AZ_SKW(6, 4) AZ_SKW(7, 4) AZ_SKW(8, 4)
 #endif
 #undef AZ_SKW

@@ -7,6 +7,10 @@ its own on the same inputs, and the product library's default run is compared to
   - the GNN tail's split-K heads: rowsw (default) vs one row per block
     (AZ_SPLITK_HEADS_MODE=rows) vs chunk partials + finalize (=chunks) -- gnn_utils.py:115;
   - the split-K reduce: float4 (default) vs scalar (AZ_GEMM_NOVEC=1);
+  - the split-K heads' rows per block: 1 (default) vs 2 / 4 (AZ_SPLITK_HEADS_R);
+  - the fp16-form GEMM on pre-split planes (default for registered weights) vs splitting in the
+    tile (AZ_GEMM_NOP2=1, and weights outside registered storage), and output_transform.0's
+    fused reduce + split of .2's operand vs the plain reduce (AZ_NO_PRESPLIT=1);
   - the fp32 MFMA 256x128 GEMM tile (AZ_GEMM_X3=0, the path before gemm_x3 took these shapes):
     2-buffer vs 3-buffer ring and its stagger (AZ_GEMM_RING=3 / 4): the same k order, so the same
     sums (compared with the fp32 tile's own default, since gemm_x3 sums differently)."""
@@ -26,8 +30,11 @@ import sys
 import numpy as np
 import torch
 sys.path.insert(0, sys.argv[1] + "/alphazero-gnn_amd")
-from azhip import ops
+import os
+from azhip import ops, _lib
 out = {}
+reg = os.environ.get("AZ_TEST_REGISTER", "1") == "1"   # weights as registered parameter storage
+keep = []   # registered weights stay allocated: a freed one's address must not come back as new
 F, A = 3136, 8
 for B in (33, 100, 512):
     g = torch.Generator().manual_seed(B)
@@ -40,6 +47,10 @@ for B in (33, 100, 512):
     wv = (torch.rand((1, F), generator=g) * 2 - 1) / F ** 0.5
     bp, bv = torch.rand((A,), generator=g) - 0.5, torch.rand((1,), generator=g) - 0.5
     c = [t.cuda() for t in (x, w0, b0, w2, b2, wp, bp, wv, bv)]
+    keep.append(c)
+    if reg:
+        for t in (c[1], c[3]):
+            _lib.check(_lib.load().az_weights_register(t.data_ptr(), t.numel() * 4), "register")
     logp, pi, v, y, hid = ops.transform_heads(*c)
     hl, hp_, hv_ = ops.heads(c[0], c[5], c[6], c[7], c[8])
     for k, t in (("logp", logp), ("pi", pi), ("v", v), ("y", y), ("hid", hid),
@@ -54,6 +65,11 @@ VARIANTS = {
     "twopass_chunks": {"AZ_HEADS_TWOPASS": "1", "AZ_SPLITK_HEADS_MODE": "chunks"},
     "rows": {"AZ_SPLITK_HEADS_MODE": "rows"},
     "novec": {"AZ_GEMM_NOVEC": "1"},
+    "heads_r2": {"AZ_SPLITK_HEADS_R": "2"},
+    "heads_r4": {"AZ_SPLITK_HEADS_R": "4"},
+    "nop2": {"AZ_GEMM_NOP2": "1"},
+    "no_presplit": {"AZ_NO_PRESPLIT": "1"},
+    "unregistered": {"AZ_TEST_REGISTER": "0"},
 }
 FP32_VARIANTS = {
     "fp32": {"AZ_GEMM_X3": "0"},
@@ -69,7 +85,8 @@ def _run(tmp_path, name, env_extra, tuning=True):
     if tuning:
         env["AZ_TUNING_LIB"] = "1"
     for k in ("AZ_HEADS_TWOPASS", "AZ_SPLITK_HEADS_MODE", "AZ_GEMM_NOVEC", "AZ_GEMM_RING",
-              "AZ_GEMM_X3"):
+              "AZ_GEMM_X3", "AZ_SPLITK_HEADS_R", "AZ_GEMM_NOP2", "AZ_NO_PRESPLIT",
+              "AZ_TEST_REGISTER"):
         env.pop(k, None)
     env.update(env_extra)
     path = str(tmp_path / f"{name}.npz")
