@@ -136,6 +136,10 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
     }
     return c1 + base + 8 * h;
   };
+  // bm: each board's max feature (>= 0 after the ReLU) over this lane's stores, for the A split
+  float bm[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) bm[b] = 0.f;
   auto store_tile = [&](int mt, const f32x4v& acc) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -143,8 +147,15 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
       if (row < nb * P) {
         const int b = row / P, p = row % P;
         const float v = acc[r] + bias;
-        if constexpr (STAGE) ob[b * 3136 + co * P + p] = v > 0.f ? v : 0.f;
-        else feat[(size_t)(b0 + b) * 3136 + co * P + p] = v > 0.f ? v : 0.f;
+        const float o = v > 0.f ? v : 0.f;
+        if constexpr (STAGE) {
+          ob[b * 3136 + co * P + p] = o;
+#pragma unroll
+          for (int q = 0; q < NB; ++q)
+            if (q == b) bm[q] = fmaxf(bm[q], o);
+        } else {
+          feat[(size_t)(b0 + b) * 3136 + co * P + p] = o;
+        }
       }
     }
   };
@@ -171,6 +182,17 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
     if (mt + 2 < MT) store_tile(mt + 2, acc1);
   }
   if constexpr (STAGE) {
+    // each board's max feature, one per wave (max is exact: any order gives the value
+    // h3_split_rows_kernel computes from feat)
+    __shared__ float wmax[NB][8];
+    if (apl) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) bm[b] = fmaxf(bm[b], __shfl_xor(bm[b], o));
+        if (lane == 0) wmax[b][wave] = bm[b];
+      }
+    }
     __syncthreads();
     f32x4v* dst = reinterpret_cast<f32x4v*>(feat + (size_t)b0 * 3136);
     const f32x4v* src = reinterpret_cast<const f32x4v*>(ob);
@@ -178,25 +200,6 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
       for (int i = tid; i < nb * 784; i += 512) dst[i] = src[i];
       return;
     }
-    // each board's max |feature| (max is exact: any order gives h3_split_rows_kernel's value)
-    __shared__ float wmax[NB][8];
-    float m[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) m[b] = 0.f;
-    for (int i = tid; i < nb * 784; i += 512) {
-      const f32x4v q = src[i];
-      const float a = fmaxf(fmaxf(fabsf(q[0]), fabsf(q[1])), fmaxf(fabsf(q[2]), fabsf(q[3])));
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-        if (i / 784 == b) m[b] = fmaxf(m[b], a);
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) m[b] = fmaxf(m[b], __shfl_xor(m[b], o));
-      if (lane == 0) wmax[b][wave] = m[b];
-    }
-    __syncthreads();
     const size_t plane = (size_t)B * 3136;
     for (int ch = tid; ch < nb * 392; ch += 512) {     // 8-float chunks: fp32 row + two planes
       const int b = ch / 392, c = ch - b * 392;
