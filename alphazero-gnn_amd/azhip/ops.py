@@ -113,10 +113,20 @@ def pinned_workspace(device, t):
             _WS_PINNED[key] = prev
 
 
+def _p2_bytes(d):
+    """Workspace the fp16-form GEMM on pre-split planes (az_gemm.hip, P2) needs beyond the
+    default for a large K-major GEMM: A's two fp16 planes [2][M][K] + row scales (0 otherwise)."""
+    if (d.K >= 1024 and d.N >= 256 and d.K % 32 == 0 and d.a_kmajor and d.b_kmajor
+            and not d.A2 and not d.a_rows):
+        return 4 * d.M * d.K + 8 * (d.M + d.N) + (1 << 20)
+    return 0
+
+
 def gemm(desc, device=None):
     L = _lib.lib()
     if device is not None and not desc.ws:
-        ws = workspace(device)
+        # large M (65,536 x 3136: 0.8 GB of A planes) gets room for the pre-split operands
+        ws = workspace(device, max(256 << 20, _p2_bytes(desc)))
         desc.ws, desc.ws_bytes = ws.data_ptr(), ws.numel()
     _lib.check(L.az_gemm_f32(ctypes.byref(desc), _stream()), "az_gemm_f32")
 
@@ -125,9 +135,10 @@ def linear(x, w, b=None, act=ACT_NONE, out=None, x2=None, a_rows=None, R=None, G
            c_rows=None, beta=0.0, M=None, C2=None):
     """out = act(cat(x, x2) @ w.T + b) (optionally gated residual R + G*(...)), nn.Linear layout.
     x: [M, K1] (row stride taken from the tensor), x2: [M, K2] or None, w: [N, K1+K2].
-    Large GEMMs cache w's per-row fp16-form scales by pointer and shape: after writing new
-    values into w -- or passing a different tensor that reuses a freed w's memory -- call
-    params.weights_changed() (include/az_hip.h az_weights_changed)."""
+    Large GEMMs cache w's per-row fp16-form scales and planes when w lies in registered
+    parameter storage (FlatParams registers its buffer; az_weights_register): after writing new
+    values into it, call params.weights_changed() (include/az_hip.h az_weights_changed).  Other
+    weights get per-call scales."""
     _need(x, name="x")
     _need(w, name="w")
     K1 = x.shape[1]
