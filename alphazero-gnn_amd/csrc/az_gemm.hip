@@ -248,10 +248,17 @@ __device__ __forceinline__ void tile_of(int bid, int mt_n, int nt_n, int& mt, in
 template <int MF, int TI, int TJ, bool WAVE_LOCAL = false, class Acc>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][TJ], int r0,
                                               int c0, int sp, float* stage = nullptr) {
-  auto sync = [] {
+  // Each wave stages through its own LDS region, so only the first wait needs the block (the k
+  // loop's last LDS reads, other waves' included, must be done before the region is written);
+  // the per-chunk waits are wave-local: a __syncthreads there is also a release fence that drains
+  // every outstanding global store (s_waitcnt vmcnt(0)) -- twice per 32-column chunk, with every
+  // block of a one-round grid storing at once (MI355X, tools/gpu_p3_abl.sh: 15 of 41 us at
+  // M = 512, 158 of 594 at M = 8,192 were this epilogue)
+  auto sync_first = [] {
     if constexpr (WAVE_LOCAL) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     else __syncthreads();
   };
+  auto sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
   constexpr int NACC = MF == 32 ? 16 : 4;
   constexpr int WM = TI * MF, WN = TJ * MF;
   const int lane = threadIdx.x & 63;
@@ -267,7 +274,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][
     // stores over 2-4 rows per instruction): each 32-column chunk of the wave tile is written
     // to LDS [WM][36] and read back as float4 rows, 8 lanes per 128-B row segment.
     constexpr int LD = 36, CH = 32 / MF;   // MFMA column tiles per 32-column chunk
-    sync();                                 // the k loop's last LDS reads are done everywhere
+    sync_first();                           // the k loop's last LDS reads are done everywhere
 #pragma unroll
     for (int cc = 0; cc < WN / 32; ++cc) {
 #pragma unroll
@@ -1475,7 +1482,8 @@ __host__ __device__ __forceinline__ int csk_block_of(int u, int b, int W) {
 }
 
 // gemm_p3_body (below): the tile on operands already split into planes, LDS-DMA only
-template <int BM, int BN, int WGM, int WGN, bool H3 = false, bool FLEX = false, int NBUF = 2>
+template <int BM, int BN, int WGM, int WGN, bool H3 = false, bool FLEX = false, int NBUF = 2,
+          int ABL = 0>
 __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int mt, int nt,
                                              int sp, int kbeg, int kend, int bma = BM);
 
@@ -1692,7 +1700,9 @@ constexpr int p3_smem_bytes() {
 // FLEX (the cycled stream-K tail): bma = 256 (256 x 128 tile) or 128 (128 x 256), as gemm_x3_body.
 // NBUF = 3: a three-stage ring (stage kt + 2 issued while stage kt computes), one barrier per
 // stage as with two; the fp16 256 x 128 ring is 3 x 48 KB.
-template <int BM, int BN, int WGM, int WGN, bool H3, bool FLEX, int NBUF>
+// ABL (tuning-build timing ablations, results wrong by design): 1 = no epilogue stores,
+// 2 = no MFMAs, 4 = no DMA (stale LDS)
+template <int BM, int BN, int WGM, int WGN, bool H3, bool FLEX, int NBUF, int ABL>
 __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int mt, int nt,
                                              int sp, int kbeg, int kend, int bma) {
   static_assert(NBUF == 2 || NBUF == 3, "p3 ring: 2 or 3 stages");
@@ -1730,6 +1740,7 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
     }
   }
   auto issue = [&](int buf, int k0) {
+    if constexpr ((ABL & 4) != 0) return;
 #pragma unroll
     for (int q = 0; q < PPW; ++q)
       __builtin_amdgcn_global_load_lds(
@@ -1774,6 +1785,13 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
   };
   auto mfma6 = [&](const Frags& f, int i, int j) {
     f32x16 t = acc[i][j];
+    if constexpr ((ABL & 2) != 0) {       // keep the fragment reads live, no MFMA
+      acc[i][j][0] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, f.a[0][i])[0]) +
+                      __builtin_bit_cast(float, __builtin_bit_cast(u32x4, f.b[0][j])[0]) +
+                      __builtin_bit_cast(float, __builtin_bit_cast(u32x4, f.a[PL - 1][i])[1]) +
+                      __builtin_bit_cast(float, __builtin_bit_cast(u32x4, f.b[PL - 1][j])[1]);
+      return;
+    }
     if constexpr (H3) {
       const f16x8 ah = __builtin_bit_cast(f16x8, f.a[0][i]), al = __builtin_bit_cast(f16x8, f.a[PL - 1][i]);
       const f16x8 bh = __builtin_bit_cast(f16x8, f.b[0][j]), bl = __builtin_bit_cast(f16x8, f.b[PL - 1][j]);
@@ -1833,11 +1851,22 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
       }
     __syncthreads();           // the epilogue's staging reuses the stage buffers
   }
+  if constexpr ((ABL & 1) != 0) {        // no stores unless a sentinel appears (every
+    float t = 0.f;                         // accumulator stays live: no MFMA is dead code)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+    if (t == 12345.f) p.C[0] = t;
+    return;
+  }
   tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
 }
 
-template <int BM, int BN, int WGM, int WGN, bool H3 = false, int NBUF = 2>
+template <int BM, int BN, int WGM, int WGN, bool H3 = false, int NBUF = 2, int ABL = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[p3_smem_bytes<BM, BN, WGM, WGN, H3, NBUF>()];
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
@@ -1845,7 +1874,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3(GemmArgs p) {
   int mt, nt, sp;
   tile_of(xcd_swizzle(blockIdx.x, nwg), mt_n, nt_n, mt, nt, sp);
   const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
-  gemm_p3_body<BM, BN, WGM, WGN, H3, false, NBUF>(p, smem, mt, nt, sp, kbeg, kend, BM);
+  gemm_p3_body<BM, BN, WGM, WGN, H3, false, NBUF, ABL>(p, smem, mt, nt, sp, kbeg, kend, BM);
 }
 
 // gemm_p3 in stream-K form (see gemm_x3_sk), pieces summed by streamk_fixup4_kernel
@@ -3910,8 +3939,27 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
   if (p2 && (tile == 1 || tile == 2) && p2_prep()) {
     static const char* env_ring = tuning_env("AZ_P3_RING");
     const int ring = env_ring ? atoi(env_ring) : 2;
+    static const char* env_abl = tuning_env("AZ_P3_ABL");
+    const int abl = env_abl ? atoi(env_abl) : 0;
     if (tile == 1 && ring == 3)
       hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3>), grid, dim3(512), 0, s, a);
+#ifdef AZ_TUNING
+    else if (tile == 1 && abl == 1)
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 1>), grid, dim3(512), 0, s, a);
+    else if (tile == 1 && abl == 2)
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 2>), grid, dim3(512), 0, s, a);
+    else if (tile == 1 && abl == 4)
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 4>), grid, dim3(512), 0, s, a);
+    else if (tile == 1 && abl == 5)
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 5>), grid, dim3(512), 0, s, a);
+    else if (tile == 1 && abl == 6)
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 6>), grid, dim3(512), 0, s, a);
+    else if (tile == 1 && a.splits == 1 && tuning_env("AZ_P3_WIDE")) {
+      // 256 x 256 tiles (waves 4 x 2 of 64 x 128): half the L2 misses per flop of 256 x 128
+      const dim3 gw((unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256)));
+      hipLaunchKernelGGL((gemm_p3<256, 256, 4, 2, true>), gw, dim3(512), 0, s, a);
+    }
+#endif
     else if (tile == 1) hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true>), grid, dim3(512), 0, s, a);
     else hipLaunchKernelGGL((gemm_p3<128, 128, 2, 2, true>), grid, dim3(256), 0, s, a);
     return true;
