@@ -14,6 +14,9 @@ Ms = [int(m) for m in sys.argv[1].split(",")]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 N = K = 3136
 w = (torch.rand((N, K), device="cuda") * 2 - 1) / K ** 0.5
+if os.environ.get("AZ_PROBE_REGISTER", "1") == "1":      # as parameter storage (the product path)
+    from azhip import _lib
+    _lib.check(_lib.load().az_weights_register(w.data_ptr(), w.numel() * 4), "az_weights_register")
 b = torch.rand((N,), device="cuda")
 for M in Ms:
     x = torch.rand((M, K), device="cuda") * 2 - 1
