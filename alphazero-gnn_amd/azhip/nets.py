@@ -80,6 +80,7 @@ class Connect4Net(_Net):
     def features(self, b):
         """b: int8 [B,n,n] on HBM -> [B, 64*n*n] (Connect4Net.py:42-49)."""
         W = self.params
+        W.sync()
         if self.n == 7:
             return ops.c4_trunk(b, W)
         s = ops.conv3x3_relu(b, W["conv1.weight"], W["conv1.bias"], 1)
@@ -92,11 +93,13 @@ class Connect4Net(_Net):
         if self.n != 7:
             f = self.features(b)
             return (f,) + self.heads(f, pi=pi, v=v)
+        self.params.sync()
         return ops.c4_trunk_heads(b, self.params, pi=pi, v=v)
 
     def heads(self, feat, want_pi=True, pi=None, v=None):
         """Connect4GNN.py:48-57 (pi / v: optional output buffers, e.g. HostBuffer views)."""
         W = self.params
+        W.sync()
         return ops.heads(feat, W["fc_policy.weight"], W["fc_policy.bias"], W["fc_value.weight"],
                          W["fc_value.bias"], want_pi=want_pi, pi=pi, v=v)
 
@@ -121,6 +124,7 @@ class TicTacToeNet(_Net):
 
     def features(self, b):
         W = self.params
+        W.sync()
         s = ops.conv3x3_relu(b, W["conv1.weight"], W["conv1.bias"], 1)
         s = ops.conv3x3_relu(s, W["conv2.weight"], W["conv2.bias"], 1)
         s = ops.conv3x3_relu(s, W["conv3.weight"], W["conv3.bias"], 0)
@@ -128,6 +132,7 @@ class TicTacToeNet(_Net):
 
     def hidden(self, feat):
         W = self.params
+        W.sync()
         h1 = ops.linear(feat, W["fc1.weight"], W["fc1.bias"], act=ops.ACT_RELU)
         h2 = ops.linear(feat, W["fc2.weight"], W["fc2.bias"], act=ops.ACT_RELU)
         return h1, h2
@@ -178,6 +183,7 @@ class PolicyValueGNN(_Net):
 
     def output_transform(self, x):
         W = self.params
+        W.sync()
         y, _ = ops.mlp2(x, W["output_transform.0.weight"], W["output_transform.0.bias"],
                         W["output_transform.2.weight"], W["output_transform.2.bias"])
         return y
@@ -185,6 +191,7 @@ class PolicyValueGNN(_Net):
     def run_layers(self, x, graph):
         """The layer stack; in eval mode nothing is kept for a backward pass
         (az_gnn_layer_infer: one fused kernel per layer on grid-shaped graphs)."""
+        self.params.sync()
         for layer in self.layers:
             x, self._ws = ops.gnn_layer(graph, x, layer.weights(), ws=self._ws,
                                         save=self.training)
@@ -208,6 +215,7 @@ class PolicyValueGNN(_Net):
         graphs one launch, the layer's output never reaches HBM)."""
         if self.training or not self.layers:
             return self.output_transform(self.run_layers(x, graph))
+        self.params.sync()
         for layer in self.layers[:-1]:
             x, self._ws = ops.gnn_layer(graph, x, layer.weights(), ws=self._ws, save=False)
         W = self.params
@@ -226,6 +234,8 @@ def gnn_per_row_heads(nnet, gnn, feat, want_pi=True, pi=None, v=None):
     az_transform_heads_fwd call; TicTacToe's heads go through fc1/fc2 first."""
     if isinstance(nnet, Connect4Net):
         G, W = gnn.params, nnet.params
+        G.sync()
+        W.sync()
         logp, pi, v, _, _ = ops.transform_heads(
             feat, G["output_transform.0.weight"], G["output_transform.0.bias"],
             G["output_transform.2.weight"], G["output_transform.2.bias"], W["fc_policy.weight"],

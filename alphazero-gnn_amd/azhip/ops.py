@@ -445,6 +445,9 @@ def c4_gnn_eval(boards, W, G, feat=None, hidden=None, y=None, logp=None, pi=None
     A = W["fc_policy.weight"].shape[0]
     dev = boards.device
     assert boards.dtype == torch.int8 and boards.is_contiguous() and tuple(boards.shape[1:]) == (7, 7)
+    for P_ in (W, G):
+        if hasattr(P_, "sync"):
+            P_.sync()       # FlatParams: announce torch-side weight writes (params.py)
     feat = torch.empty((B, F), device=dev) if feat is None else feat
     hidden = torch.empty((B, F), device=dev) if hidden is None else hidden
     y = torch.empty((B, F), device=dev) if y is None else y

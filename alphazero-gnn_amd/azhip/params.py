@@ -29,8 +29,10 @@ def _register(owner, flat):
     L = _lib.load()
     ptr = flat.data_ptr()
     _lib.check(L.az_weights_register(ptr, flat.numel() * 4), "az_weights_register")
-    # the buffer outlives the owner only through views; unregistering early only disables caching
-    weakref.finalize(owner, L.az_weights_unregister, ptr)
+    # the buffer outlives the owner only through views; unregistering early only disables caching.
+    # Not at interpreter exit: the library frees its cache entries then, and the HIP runtime may
+    # already be going down.
+    weakref.finalize(owner, L.az_weights_unregister, ptr).atexit = False
 
 
 def _align4(n):
@@ -54,8 +56,23 @@ class FlatParams:
         self._grad = None
         self.m = None
         self.v = None
+        self._seen = self.flat._version
         if init is not None:
             self.load_state_dict(init)
+
+    def sync(self):
+        """Announce torch-side writes to libaz_hip.so before the weights are read again.  The
+        library caches fp16 planes of registered weights (az_weights_register) until
+        az_weights_changed(); a write through a state_dict() / parameters() / params[k] view
+        (an optimizer step, an in-place edit) would otherwise be served the OLD weights' planes.
+        Every such write bumps the flat buffer's version counter (views share it), so comparing
+        it with the one seen at the last sync finds them; every forward entry point calls this
+        (one attribute read when nothing changed).  Writes by the library's own kernels
+        (az_adam_f32) announce themselves."""
+        v = self.flat._version
+        if v != self._seen:
+            weights_changed()
+            self._seen = v
 
     def _views(self, buf):
         return OrderedDict((k, buf[o:o + n].view(s)) for k, (o, n, s) in self.offsets.items())
@@ -102,11 +119,13 @@ class FlatParams:
                                    f"{tuple(dst.shape)}")
             dst.copy_(src.to(torch.float32), non_blocking=False)
         weights_changed()
+        self._seen = self.flat._version
 
     def copy_flat_(self, src):
         """Overwrite the whole parameter buffer (a snapshot restore) and say so to the library."""
         self.flat.copy_(src)
         weights_changed()
+        self._seen = self.flat._version
 
     # -- training buffers -------------------------------------------------------------------
     @property

@@ -423,8 +423,16 @@ class NetWrapper:
         self.train_seed = 0
 
     # -- evaluation ------------------------------------------------------------------------
+    def _sync_params(self):
+        """FlatParams.sync for both nets: the batch-1 and lock-step paths read the weights by
+        pointer, so torch-side writes are announced here before they run."""
+        self.nnet.params.sync()
+        if self.has_gnn:
+            self.gnn.params.sync()
+
     def _graph1(self, kind):
         """The batch-1 graph of `kind`, captured on first use (None when disabled)."""
+        self._sync_params()
         if not _graphs_enabled():
             return None
         g = getattr(self, "_g1", None)
@@ -478,6 +486,7 @@ class NetWrapper:
         stream: run it on that HIP stream with its own device scratch (the lock-step lanes give
         each lane a stream, so one lane's batch can overlap the other's on the GPU); the caller
         orders the stream after any parameter update (play_episodes_engine does)."""
+        self._sync_params()
         if self.has_gnn and _direct_ok(self) and len(boards) > 0:
             directs = self.__dict__.setdefault("_directs", {})
             key = None if stream is None else stream.cuda_stream
@@ -557,6 +566,7 @@ class NetWrapper:
         """Connect4GNN.py:122-197: fresh Adam per call, `epochs` x (CNN step on a batch sampled
         with replacement by np.random.randint; GNN step on a second sample)."""
         lr = self.args.lr
+        self._sync_params()
         self.nnet.params.reset_adam()
         if self.has_gnn:
             self.gnn.params.reset_adam()

@@ -3537,14 +3537,31 @@ static std::atomic<long> g_wgen{1};
 struct WScaleEntry {
   const float* w;
   int n, k, ld;
-  long gen;
+  long gen;                    // generation buf[cur] (the in-tile GEMM's row scales) is from
   float* buf[2];
   int cur;
   unsigned short* planes[2];   // the P2 GEMM's W planes [2][n][k] (nullptr until first asked)
-  long pgen;                   // generation the current planes (buf[cur] too) were split at
+  float* pbuf[2];              // their row scales: a double buffer of its own, so a recompute
+  int pcur;                    // of one kind never overwrites the other kind's live buffer
+  long pgen;                   // generation planes[pcur] / pbuf[pcur] were split at
 };
+
 static std::mutex g_wmu;
 static std::vector<WScaleEntry> g_wcache;
+
+// the entry of (w, n, k, ld), created on first use (caller holds g_wmu); nullptr when out of memory
+static WScaleEntry* wcache_entry(const float* w, int n, int k, int ld) {
+  for (auto& x : g_wcache)
+    if (x.w == w && x.n == n && x.k == k && x.ld == ld) return &x;
+  WScaleEntry x{w, n, k, ld, 0, {nullptr, nullptr}, 1, {nullptr, nullptr}, {nullptr, nullptr},
+                1, 0};
+  if (hipMalloc(&x.buf[0], (size_t)8 * n * sizeof(float)) != hipSuccess) return nullptr;
+  x.buf[1] = x.buf[0] + 2 * n;
+  x.pbuf[0] = x.buf[0] + 4 * n;
+  x.pbuf[1] = x.buf[0] + 6 * n;
+  g_wcache.push_back(x);
+  return &g_wcache.back();
+}
 
 // Parameter storage the caller registered (az_weights_register): only weights inside it are
 // cached -- anywhere else a pointer says nothing about the values behind it (a freed tensor's
@@ -3577,12 +3594,40 @@ extern "C" int az_weights_register(const void* base, size_t bytes) {
   return az_weights_changed();           // a reused range must not meet old cache entries
 }
 extern "C" int az_weights_unregister(const void* base) {
+  std::vector<std::pair<uintptr_t, uintptr_t>> gone;
   {
     std::lock_guard<std::mutex> lk(az::g_regmu);
     const uintptr_t b = reinterpret_cast<uintptr_t>(base);
     for (size_t i = 0; i < az::g_regs.size();)
-      if (az::g_regs[i].first == b) az::g_regs.erase(az::g_regs.begin() + i);
-      else ++i;
+      if (az::g_regs[i].first == b) {
+        gone.push_back(az::g_regs[i]);
+        az::g_regs.erase(az::g_regs.begin() + i);
+      } else {
+        ++i;
+      }
+  }
+  // free the cache entries (row scales + fp16 planes: 8 N K bytes per weight, 79 MB for a
+  // 3136 x 3136 one) of weights inside the range, once no launched GEMM can still read them
+  if (!gone.empty()) {
+    std::lock_guard<std::mutex> lk(az::g_wmu);
+    bool synced = false;
+    for (size_t i = 0; i < az::g_wcache.size();) {
+      const uintptr_t w = reinterpret_cast<uintptr_t>(az::g_wcache[i].w);
+      bool inside = false;
+      for (const auto& r : gone) inside |= w >= r.first && w < r.second;
+      if (!inside) {
+        ++i;
+        continue;
+      }
+      if (!synced) {
+        AZ_REQUIRE(hipDeviceSynchronize() == hipSuccess, AZ_EDEVICE,
+                   "az_weights_unregister: hipDeviceSynchronize failed");
+        synced = true;
+      }
+      (void)hipFree(az::g_wcache[i].buf[0]);
+      if (az::g_wcache[i].planes[0]) (void)hipFree(az::g_wcache[i].planes[0]);
+      az::g_wcache.erase(az::g_wcache.begin() + i);
+    }
   }
   return az_weights_changed();
 }
@@ -3592,18 +3637,9 @@ static const float* w_row_scales(const float* w, int n, int k, int ld, hipStream
   if (!weights_registered(w, n, k, ld)) return nullptr;   // the caller computes them per call
   const long gen = g_wgen.load();
   std::lock_guard<std::mutex> lk(g_wmu);
-  WScaleEntry* e = nullptr;
-  for (auto& x : g_wcache)
-    if (x.w == w && x.n == n && x.k == k && x.ld == ld) e = &x;
-  if (e && e->gen == gen) return e->buf[e->cur];
-  if (!e) {
-    WScaleEntry x{w, n, k, ld, 0, {nullptr, nullptr}, 0, {nullptr, nullptr}, 0};
-    if (hipMalloc(&x.buf[0], (size_t)4 * n * sizeof(float)) != hipSuccess) return nullptr;
-    x.buf[1] = x.buf[0] + 2 * n;
-    x.cur = 1;
-    g_wcache.push_back(x);
-    e = &g_wcache.back();
-  }
+  WScaleEntry* e = wcache_entry(w, n, k, ld);
+  if (!e) return nullptr;
+  if (e->gen == gen) return e->buf[e->cur];
   const int nxt = e->cur ^ 1;
   hipLaunchKernelGGL(row_scale_kernel, dim3(n), dim3(256), 0, s, w, n, k, ld, H3_TW,
                      e->buf[nxt]);
@@ -3620,17 +3656,8 @@ static const unsigned short* w_planes(const float* w, int n, int k, int ld, hipS
   if (!weights_registered(w, n, k, ld)) return nullptr;
   const long gen = g_wgen.load();
   std::lock_guard<std::mutex> lk(g_wmu);
-  WScaleEntry* e = nullptr;
-  for (auto& x : g_wcache)
-    if (x.w == w && x.n == n && x.k == k && x.ld == ld) e = &x;
-  if (!e) {
-    WScaleEntry x{w, n, k, ld, 0, {nullptr, nullptr}, 0, {nullptr, nullptr}, 0};
-    if (hipMalloc(&x.buf[0], (size_t)4 * n * sizeof(float)) != hipSuccess) return nullptr;
-    x.buf[1] = x.buf[0] + 2 * n;
-    x.cur = 1;
-    g_wcache.push_back(x);
-    e = &g_wcache.back();
-  }
+  WScaleEntry* e = wcache_entry(w, n, k, ld);
+  if (!e) return nullptr;
   if (!e->planes[0]) {
     const size_t one = (size_t)2 * n * k;
     if (hipMalloc(&e->planes[0], 2 * one * sizeof(unsigned short)) != hipSuccess) {
@@ -3640,17 +3667,17 @@ static const unsigned short* w_planes(const float* w, int n, int k, int ld, hipS
     e->planes[1] = e->planes[0] + one;
     e->pgen = 0;
   }
-  if (e->pgen == gen && e->gen == gen) {
-    *scales = e->buf[e->cur];
-    return e->planes[e->cur];
+  if (e->pgen == gen) {
+    *scales = e->pbuf[e->pcur];
+    return e->planes[e->pcur];
   }
-  const int nxt = e->cur ^ 1;
+  const int nxt = e->pcur ^ 1;
   hipLaunchKernelGGL(h3_split_rows_kernel, dim3(n), dim3(256), 0, s, w, n, k, ld, H3_TW,
-                     e->planes[nxt], (size_t)n * k, e->buf[nxt]);
+                     e->planes[nxt], (size_t)n * k, e->pbuf[nxt]);
   if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
-  e->cur = nxt;
-  e->gen = e->pgen = gen;
-  *scales = e->buf[nxt];
+  e->pcur = nxt;
+  e->pgen = gen;
+  *scales = e->pbuf[nxt];
   return e->planes[nxt];
 }
 

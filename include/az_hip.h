@@ -364,12 +364,14 @@ int az_mlp2_bwd(const float* x, int M, int F, const float* w0, const float* w2,
 int az_adam_f32(float* p, const float* g, float* m, float* v, int64_t n,
                 double lr, double beta1, double beta2, double eps, int step, void* stream);
 
-/* Parameters changed: every cached per-row weight scale of the fp16 GEMM form (az_gemm_f32's
- * large K-major GEMMs, az_gemm.hip row_scale_kernel) is recomputed before its next use.  The
- * cache is keyed by the weight pointer and shape, so a caller that writes weights any other way
- * (loading a checkpoint, copying buffers, or freeing a weight buffer and passing new weights at
- * the same address) must call it before the next GEMM on those weights; az_adam_f32 calls it.
- * A stale scale cannot overflow (64x headroom) but costs precision as the weights move. */
+/* Parameters changed: every cached per-row weight scale and fp16 weight plane of the fp16 GEMM
+ * form (az_gemm_f32's large K-major GEMMs on registered weights, below) is recomputed before its
+ * next use.  The cache is keyed by the weight pointer and shape, so a caller that writes
+ * registered weights any way other than az_adam_f32 (which calls it) -- an optimizer step of its
+ * own, loading a checkpoint, copying buffers -- must call it before the next GEMM on them.
+ * A missed call is NOT a precision loss: above 64 rows the GEMM multiplies by the cached planes,
+ * i.e. it returns the PREVIOUS weights' result.  (azhip/params.py FlatParams calls it for every
+ * torch-side write, found through the buffer's version counter.) */
 int az_weights_changed(void);
 
 /* Parameter storage: [base, base + bytes) holds weights whose values change only where
@@ -377,8 +379,9 @@ int az_weights_changed(void);
  * row scales and pre-split planes cached (az_gemm_f32's large K-major GEMMs: W split once per
  * weight update instead of in every tile); any other weight pointer gets its scales computed per
  * call, since a pointer alone says nothing about the values behind it.  Registering or
- * unregistering also invalidates every cache entry.  The Python parameter store (azhip/params.py
- * FlatParams) registers its flat buffer. */
+ * unregistering also invalidates every cache entry; unregistering waits for the device and frees
+ * the entries of weights inside the range (8 N K bytes each).  The Python parameter store
+ * (azhip/params.py FlatParams) registers its flat buffer. */
 int az_weights_register(const void* base, size_t bytes);
 int az_weights_unregister(const void* base);
 

@@ -47,6 +47,32 @@ def c4_gnn_weights():
     return synthetic_state_dict(gnn_spec(3136, 2), seed)
 
 
+def report(name, **fields):
+    """Append one JSON line to $AZ_REPORT_DIR/margins.jsonl (no-op without the variable)."""
+    d = os.environ.get("AZ_REPORT_DIR")
+    if d:
+        import json
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "margins.jsonl"), "a") as f:
+            f.write(json.dumps({"check": name, **fields}) + "\n")
+
+
+def assert_close(name, got, ref, tol=1e-5, rel_floor=None):
+    """max |got - ref| <= tol (or, with rel_floor, max |got - ref| / max(rel_floor, |ref|) <=
+    tol: used for log-probabilities, whose magnitude reaches hundreds on trained weights, where
+    one fp32 ulp is already > 1e-5).  Records the error and the margin tol / error."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(got - ref)
+    if rel_floor is not None:
+        err = err / np.maximum(np.abs(ref), rel_floor)
+    worst = float(err.max()) if err.size else 0.0
+    report(name, max_err=worst, tol=tol, margin=(tol / worst if worst > 0 else float("inf")),
+           n=int(err.size), relative=rel_floor is not None)
+    assert worst <= tol, (name, worst, tol)
+    return worst
+
+
 def gpu_available():
     try:
         import torch

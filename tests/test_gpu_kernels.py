@@ -3,7 +3,7 @@ float64 restatement of the reference) or, for plain GEMM shapes, a torch fp32 re
 import numpy as np
 import pytest
 
-from conftest import golden, split_weights
+from conftest import assert_close, golden, split_weights
 
 import os
 
@@ -268,11 +268,21 @@ def test_h3_gemm_wide_dynamic_range(ops):
     _x3_check(ops, x, w, b, report={"operands": "rows spanning 2^-30 .. 2^30, W ~ 2^20"})
 
 
+def _registered(t):
+    """Register a device tensor's storage like FlatParams does (az_weights_register), so its
+    GEMMs take the cached fp16 planes; returns an unregister callable."""
+    from azhip import _lib
+    L = _lib.load()
+    _lib.check(L.az_weights_register(t.data_ptr(), t.numel() * 4), "az_weights_register")
+    return lambda: _lib.check(L.az_weights_unregister(t.data_ptr()), "az_weights_unregister")
+
+
 def test_h3_weight_scales_follow_weight_updates(ops):
-    """The fp16 form caches each weight matrix's row scales between weight updates
-    (az_weights_changed; az_adam_f32 and the parameter store call it).  Growing W 4096x in place
-    -- far past the scales' 64x headroom -- and announcing it gives the right result again; the
-    same GEMM before the update is right too."""
+    """The fp16 form caches each REGISTERED weight matrix's row scales and fp16 planes between
+    weight updates (az_weights_changed; az_adam_f32 and the parameter store call it).  Growing W
+    4096x in place -- far past the scales' 64x headroom -- and announcing it gives the right
+    result again; the same GEMM before the update is right too; unregistered storage is right
+    without any announcement."""
     from azhip import params as P
     M, N, K = 512, 3136, 3136
     g = torch.Generator().manual_seed(9)
@@ -280,10 +290,109 @@ def test_h3_weight_scales_follow_weight_updates(ops):
     w = ((torch.rand((N, K), generator=g) * 2 - 1) / K ** 0.5)
     b = torch.rand((N,), generator=g) - 0.5
     wd = w.cuda()
-    _x3_check_dev(ops, x, wd, w, b)
-    wd.mul_(4096.0)
-    P.weights_changed()
-    _x3_check_dev(ops, x, wd, w * 4096.0, b)
+    unreg = _registered(wd)
+    try:
+        _x3_check_dev(ops, x, wd, w, b)
+        wd.mul_(4096.0)
+        P.weights_changed()
+        _x3_check_dev(ops, x, wd, w * 4096.0, b)
+    finally:
+        unreg()
+    wd.mul_(1.0 / 1024.0)                          # unregistered: per-call scales, no cache
+    _x3_check_dev(ops, x, wd, w * 4.0, b)
+
+
+def test_missed_weights_changed_serves_previous_weights(ops):
+    """What INTEGRATION.md says a missed az_weights_changed() does on registered storage: above
+    64 rows the GEMM multiplies by the cached planes, so it returns the PREVIOUS weights' result
+    bit for bit (not a slightly less precise one); after the call it is the new weights'."""
+    from azhip import params as P
+    M, N, K = 300, 1024, 2048
+    g = torch.Generator().manual_seed(10)
+    x = (torch.rand((M, K), generator=g) * 2 - 1).cuda()
+    w = ((torch.rand((N, K), generator=g) * 2 - 1) / K ** 0.5).cuda()
+    b = torch.zeros((N,)).cuda()
+    unreg = _registered(w)
+    try:
+        y0 = ops.linear(x, w, b)
+        w.add_(0.01)
+        y_stale = ops.linear(x, w, b)
+        assert torch.equal(y_stale, y0)
+        P.weights_changed()
+        y1 = ops.linear(x, w, b)
+        assert not torch.equal(y1, y0)
+        _x3_check_dev(ops, x.cpu(), w, w.cpu(), b.cpu())
+    finally:
+        unreg()
+
+
+def test_reference_side_adam_recipe_on_registered_weights(ops):
+    """INTEGRATION.md §2's recipe for a reference-side integration that keeps torch.optim.Adam
+    (Connect4GNN.py:132-135): register output_transform's weight storage, optimizer.step(),
+    az_weights_changed(), predict -> the new weights' result (vs float64), at M = 512."""
+    from azhip import _lib
+    M, N, K = 512, 3136, 3136
+    g = torch.Generator().manual_seed(11)
+    x = (torch.rand((M, K), generator=g) * 2 - 1).cuda()
+    lin = torch.nn.Linear(K, N).cuda()
+    unreg = _registered(lin.weight.data)
+    try:
+        y0 = ops.linear(x, lin.weight.data, lin.bias.data)
+        opt = torch.optim.Adam(lin.parameters(), lr=0.01)
+        loss = (lin(x) ** 2).mean()
+        loss.backward()
+        opt.step()
+        _lib.check(_lib.load().az_weights_changed(), "az_weights_changed")
+        w1, b1 = lin.weight.data.cpu(), lin.bias.data.cpu()
+        y1 = ops.linear(x, lin.weight.data, lin.bias.data)
+        assert not torch.equal(y1, y0)
+        _x3_check_dev(ops, x.cpu(), lin.weight.data, w1, b1)
+    finally:
+        unreg()
+
+
+def test_flatparams_views_cannot_serve_stale_planes(ops):
+    """FlatParams (the package's registered storage) finds torch-side writes itself: an
+    in-place edit through a state_dict() view, a parameters() view or a torch optimizer-style
+    update, with NO az_weights_changed call by the user, and the next c4_gnn_eval (B = 512: the
+    cached-plane GEMMs) gives the new weights' result against float64; an az_adam_f32 step
+    (the library's own write) likewise."""
+    import oracle.nets as O
+    from azhip.nets import Connect4Net, PolicyValueGNN
+    from azhip.weights import connect4_net_spec, gnn_spec, synthetic_state_dict
+    from types import SimpleNamespace
+    W0 = synthetic_state_dict(connect4_net_spec(7), 5)
+    game = SimpleNamespace(getBoardSize=lambda: (7, 7), getActionSize=lambda: 8)
+    net = Connect4Net(game, {"dropout": 0.0}, init=W0).eval()
+    G0 = {k: v for k, v in synthetic_state_dict(gnn_spec(3136, 2), 6).items()}
+    gnn = PolicyValueGNN(3136, 2, init=G0).eval()
+    boards = np.random.default_rng(12).integers(-1, 2, size=(512, 7, 7)).astype(np.int8)
+    bd = cu(boards)
+
+    def check(tag):
+        lp, pi, v = ops.c4_gnn_eval(bd, net.params, gnn.params)
+        W = {k: v.numpy() for k, v in net.params.cpu_state_dict().items()}
+        G = {k: gnn.params[k].cpu().numpy() for k in (
+            "output_transform.0.weight", "output_transform.0.bias",
+            "output_transform.2.weight", "output_transform.2.bias")}
+        lp64, v64 = O.c4_heads(O.output_transform(O.c4_features(boards, W), G), W)
+        assert_close(f"stale_planes/{tag}/pi", pi.cpu().numpy(), np.exp(lp64), 1e-5)
+        assert_close(f"stale_planes/{tag}/v", v.cpu().numpy(), v64, 1e-5)
+
+    check("initial")
+    gnn.state_dict()["output_transform.0.weight"].mul_(1.5)           # state_dict view
+    check("state_dict_view")
+    for p in gnn.parameters():                                         # parameters() views
+        if p.shape == (3136, 3136):
+            p.add_(torch.sign(p) * 1e-3)                               # an Adam-like step
+    check("parameters_views")
+    P = gnn.params
+    P.zero_grad()
+    P.grad_flat.normal_(generator=torch.Generator(device="cuda").manual_seed(3))
+    P.reset_adam()
+    P.step = 1
+    ops.adam(P.flat, P.grad_flat, P.m, P.v, 0.01, P.step)              # az_adam_f32
+    check("az_adam_f32")
 
 
 def _x3_check_dev(ops, x, wd, w, b):
@@ -661,6 +770,56 @@ def test_band_layer_equals_training_path(ops, V, maxdeg, R):
     if V <= 4099:
         ref = O.gnn_layer_csr(x0.astype(np.float64), rowptr, col, G, 1)
         np.testing.assert_allclose(b, ref, atol=1e-5)
+
+
+def _grid_shard(graphs, h=32, w=32):
+    """`graphs` disjoint 4-neighbour h x w grids, node-ordered (bench.py's config-5 shard)."""
+    z = golden("synth_gnn.npz")
+    rp, cl = z["rowptr"].astype(np.int64), z["col"].astype(np.int64)
+    V1, E1 = h * w, len(cl)
+    gi = np.arange(graphs, dtype=np.int64)
+    rowptr = np.concatenate([(rp[:-1][None, :] + (gi * E1)[:, None]).ravel(), [graphs * E1]])
+    col = (cl[None, :] + (gi * V1)[:, None]).ravel()
+    return rowptr, col, rp, cl
+
+
+def test_band_layer_and_forward_at_shard_size(ops):
+    """Config 5 at the per-GPU shard the bench times (VERDICT r04 'do this' #2): 512 grids,
+    V = 524,288, E = 2,031,616 -- 32 64-row tiles per block of the band kernel, so its LDS ring
+    runs its long steady state.  Every row of the band layer against the training path's
+    unfused kernels (2e-6), the eval forward (band layer 0, then layer 1 + output_transform in
+    one launch) against the training-path layers + az_mlp2_fwd (4e-6), and grids 0, 255 and
+    511 of both against the float64 oracle (gnn_utils.py:30-117) at 1e-5."""
+    from azhip.nets import PolicyValueGNN
+    from oracle import nets as O
+    _, G, _ = _synth()
+    rowptr, col, rp1, cl1 = _grid_shard(512)
+    g = ops.DeviceGraph(rowptr, col)
+    assert g.V == 524288 and g.E == 2031616 and 0 < g.band <= 32
+    x0 = (np.random.default_rng(512).random((g.V, 64), dtype=np.float32) * 2 - 1)
+    Gd = {k: cu(v) for k, v in G.items()}
+    x = cu(x0)
+    Wl = [{k[len(f"layers.{i}."):]: v for k, v in Gd.items() if k.startswith(f"layers.{i}.")}
+          for i in range(2)]
+    a1, _ = ops.gnn_layer(g, x, Wl[0], save=True)
+    b1, _ = ops.gnn_layer(g, x, Wl[0], save=False)
+    assert_close("config5_shard/band_layer_vs_training_path", b1.cpu().numpy(), a1.cpu().numpy(),
+                 2e-6)
+    a2, _ = ops.gnn_layer(g, a1, Wl[1], save=True)
+    ref_y, _ = ops.mlp2(a2, Gd["output_transform.0.weight"], Gd["output_transform.0.bias"],
+                        Gd["output_transform.2.weight"], Gd["output_transform.2.bias"])
+    net = PolicyValueGNN(64, 2, init=G).eval()
+    y = net.forward_graph(x, g)
+    torch.cuda.synchronize()
+    y, ref_y, b1 = y.cpu().numpy(), ref_y.cpu().numpy(), b1.cpu().numpy()
+    assert_close("config5_shard/forward_vs_training_path", y, ref_y, 4e-6)
+    for gi in (0, 255, 511):
+        rows = slice(gi * 1024, (gi + 1) * 1024)
+        xg = x0[rows].astype(np.float64)
+        l1 = O.gnn_layer_csr(xg, rp1, cl1, G, 0)
+        assert_close(f"config5_shard/band_layer_vs_oracle_grid{gi}", b1[rows], l1, 1e-5)
+        yo = O.policy_value_gnn_csr(xg, rp1, cl1, G)
+        assert_close(f"config5_shard/forward_vs_oracle_grid{gi}", y[rows], yo, 1e-5)
 
 
 @pytest.mark.parametrize("kind", ["grid", "band", "random"])

@@ -26,7 +26,7 @@ from types import SimpleNamespace
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden, split_weights
+from conftest import assert_close, GOLDEN, golden, split_weights
 from test_mcts_golden import Args, _tag
 from test_selfplay import _norm_gnn, _norm_std
 
@@ -64,11 +64,11 @@ def test_hip_outputs_on_every_visited_board(c4):
     """Every (board -> pi, v) the reference's search requested, standard and GNN, batched."""
     z = golden(CASE + ".npz")
     pi, v, _, _ = c4.predict_both(z["std_boards"].astype(np.int64))
-    np.testing.assert_allclose(pi, z["std_pi"], atol=TOL)
-    np.testing.assert_allclose(v, z["std_v"], atol=TOL)
+    assert_close("G6b/predict_both/std_pi", pi, z["std_pi"], TOL)
+    assert_close("G6b/predict_both/std_v", v, z["std_v"], TOL)
     _, _, gpi, gv = c4.predict_both(z["gnn_boards"].astype(np.int64))
-    np.testing.assert_allclose(gpi, z["gnn_pi"], atol=TOL)
-    np.testing.assert_allclose(gv, z["gnn_v"], atol=TOL)
+    assert_close("G6b/predict_both/gnn_pi", gpi, z["gnn_pi"], TOL)
+    assert_close("G6b/predict_both/gnn_v", gv, z["gnn_v"], TOL)
 
 
 class _Recorded:
