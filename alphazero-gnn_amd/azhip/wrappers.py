@@ -567,6 +567,12 @@ class NetWrapper:
         with replacement by np.random.randint; GNN step on a second sample)."""
         lr = self.args.lr
         self._sync_params()
+        if (nets._args_get(self.args, "train_parallel", "replicas") == "auto"
+                and getattr(self, "_tp_auto", None) is None):
+            from . import dist as D
+            if D.world_rank()[0] > 1:
+                self._tp_auto, self.train_parallel_probe = self._probe_train_parallel(
+                    examples, gnn_examples)
         self.nnet.params.reset_adam()
         if self.has_gnn:
             self.gnn.params.reset_adam()
@@ -595,11 +601,81 @@ class NetWrapper:
     def _dp_world(self):
         """>1 when the train steps are data-parallel over ranks (args.train_parallel ==
         "allreduce" under torch.distributed: CNN rows split + gradient all_reduce, the GNN step
-        as train.gnn_step_dp); "replicas" (default) runs them whole everywhere."""
+        as train.gnn_step_dp); "replicas" (default) runs them whole everywhere; "auto" is
+        whichever _probe_train_parallel measured faster on this process group."""
         from . import dist as D
-        if nets._args_get(self.args, "train_parallel", "replicas") != "allreduce":
+        mode = nets._args_get(self.args, "train_parallel", "replicas")
+        if mode == "auto":
+            mode = getattr(self, "_tp_auto", None) or "replicas"
+        if mode != "allreduce":
             return 1
         return D.world_rank()[0]
+
+    def _probe_train_parallel(self, examples, gnn_examples):
+        """train_parallel="auto" ('choose by measurement'): before the first
+        train() under a process group of P > 1 ranks, time one gradient computation each way on
+        this node -- the whole batch on every rank (replicas) against the data-parallel form
+        with its collectives (the CNN rows sharded + the 188 KB all_reduce; the GNN step's
+        sharded trunk, gathered features and the 78.7 MB output_transform all_reduce, or the
+        478.6 MB one for gnn_grad_sync="flat") -- and keep the faster.  The Adam step is the same
+        in both modes, so it is not timed.  The probe uses the first batch_size examples (no
+        np.random draw: the training batches stay the reference's) and only writes gradient
+        buffers, which every step overwrites.  Times are max over ranks, so every rank makes the
+        same choice.  Returns (choice, {timings in ms})."""
+        import time
+        import torch.distributed as dist
+        from . import dist as D
+        world, rank = D.world_rank()
+        sync = nets._args_get(self.args, "gnn_grad_sync", "row0")
+        n = self.args.batch_size
+        jobs = {}
+        if examples:
+            sel = examples[:n]
+            b = _dev_array([e[0] for e in sel], np.int8, self.device)
+            p = _dev_array([e[1] for e in sel], np.float32, self.device)
+            v = _dev_array(np.array([e[2] for e in sel]).astype(np.float64), np.float32,
+                           self.device)
+            Bg = b.shape[0]
+            r0, r1 = D.row_shard(Bg, world, rank)
+
+            def cnn_dp():
+                T.cnn_grads(self.nnet, b[r0:r1], p[r0:r1], v[r0:r1], seed=1, B_norm=Bg)
+                D.allreduce_sum_(self.nnet.params.grad_flat)
+
+            jobs["cnn"] = (lambda: T.cnn_grads(self.nnet, b, p, v, seed=1), cnn_dp)
+        if self.has_gnn and gnn_examples:
+            sel = gnn_examples[:n]
+            gb = _dev_array([e[0] for e in sel], np.int8, self.device)
+            gp = _dev_array([e[4] for e in sel], np.float32, self.device)
+            gv = _dev_array(np.array([e[5] for e in sel]).astype(np.float64), np.float32,
+                            self.device)
+            jobs["gnn"] = (lambda: T.gnn_grads(self.nnet, self.gnn, gb, gp, gv, seed=1),
+                           lambda: T.gnn_grads_dp(self.nnet, self.gnn, gb, gp, gv, seed=1,
+                                                  grad_sync=sync))
+
+        def timed(fn, reps=3):
+            fn()                                      # first call: allocations, workspaces
+            ts = []
+            for _ in range(reps):
+                dist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            return float(np.median(ts)) * 1e3
+
+        names, vals = [], []
+        for k, (rep, dp) in jobs.items():
+            names += [f"{k}_replicas_ms", f"{k}_allreduce_ms"]
+            vals += [timed(rep), timed(dp)]
+        t = torch.tensor(vals, dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        res = dict(zip(names, [round(float(x), 4) for x in t.tolist()]))
+        rep_ms = sum(res[k] for k in names if k.endswith("_replicas_ms"))
+        dp_ms = sum(res[k] for k in names if k.endswith("_allreduce_ms"))
+        res.update(world=world, gnn_grad_sync=sync)
+        return ("allreduce" if dp_ms < rep_ms else "replicas"), res
 
     def _cnn_step_allreduce(self, b, p, v, lr):
         """CNN step with the sampled rows split over ranks: each rank's loss is normalised by

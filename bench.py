@@ -715,6 +715,92 @@ def train_leg(W, G, device):
                               "frac": round(gbs / HBM_PEAK_GBS, 4)}}
 
 
+def train_dp_leg(W, G, device, world, rank):
+    """Coach.learn's train() across P ranks (Coach.py:131-135,
+    Connect4GNN.py:140-197) -- the leg that puts RCCL on a data path at N > 1: one full train()
+    call (20 epochs x (CNN step + 64-row star GNN step)) per mode, each rank on its own GPU:
+    * "replicas": the identical step on every rank, no collective;
+    * "allreduce" + gnn_grad_sync "row0": CNN rows sharded + a 188 KB all_reduce; the GNN step's
+      trunk sharded, features gathered, output_transform's 78.7 MB gradient all_reduced;
+    * "allreduce" + "flat": the literal one-bucket all_reduce of the 478.6 MB GNN gradient;
+    * "auto": the measured choice (wrappers._probe_train_parallel, timed on this node).
+    Per mode: ms per train() call (max over ranks) and params_in_sync (bit-identical parameters
+    on every rank).  Beside them, the collectives alone: one all_reduce of each payload (max over
+    ranks), with the ring's bus bandwidth 2(P-1)/P x bytes / time."""
+    import torch
+    import torch.distributed as dist
+    from azhip import dist as D
+    from connect4.Connect4GNN import Connect4GNNWrapper
+    from connect4.Connect4Game import Connect4Game
+    rng = np.random.default_rng(7)
+    boards = rng.integers(-1, 2, size=(256, 7, 7)).astype(np.int64)
+    pis = rng.dirichlet(np.ones(8), 256)
+    zs = rng.choice([-1, 1], 256)
+    ex = [(boards[i], pis[i], int(zs[i])) for i in range(256)]
+    gex = [(boards[i], 1, pis[i], np.float32(0.1), pis[i], np.float32(zs[i] * 0.5), int(zs[i]))
+           for i in range(128)]
+
+    def max_ms(x):
+        t = torch.tensor([x], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return round(float(t.item()), 3)
+
+    out = {"workload": "Connect4GNNWrapper.train (20 epochs x (CNN step + GNN star step), "
+                       "batch 64, fresh Adam, 256 std / 128 GNN synthetic examples) per rank",
+           "world": world, "backend": dist.get_backend(), "modes": {}}
+    for mode, sync in (("replicas", "row0"), ("allreduce", "row0"), ("allreduce", "flat"),
+                       ("auto", "row0")):
+        sa = selfplay_args(2)
+        sa.lr, sa.epochs, sa.batch_size = 0.001, 20, 64
+        sa.train_parallel, sa.gnn_grad_sync = mode, sync
+        net = Connect4GNNWrapper(Connect4Game(7), sa)
+        net.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()})
+        net.gnn.load_state_dict({k: torch.from_numpy(v) for k, v in G.items()})
+        np.random.seed(0)
+        net.train(ex, gex)                              # warm-up (allocations; auto: the probe)
+        reps = 2
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            net.train(ex, gex)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        rec = {"train_call_ms": max_ms(ms),
+               "params_in_sync": bool(D.params_in_sync(net.gnn.params.flat) and
+                                      D.params_in_sync(net.nnet.params.flat))}
+        if mode == "auto":
+            rec["choice"] = net._tp_auto
+            rec["probe"] = net.train_parallel_probe
+        out["modes"][mode if mode != "allreduce" else f"allreduce_{sync}"] = rec
+        if mode == "allreduce" and sync == "flat":
+            P = net.gnn.params
+            s, e = P.span("output_transform.")
+            payloads = {"cnn_grad": net.nnet.params.grad_flat,
+                        "output_transform_grad": P.grad_flat[s:e], "gnn_grad_flat": P.grad_flat}
+            coll = {}
+            for name, buf in payloads.items():
+                D.allreduce_sum_(buf)
+                ts = []
+                for _ in range(3):
+                    dist.barrier()
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    D.allreduce_sum_(buf)
+                    torch.cuda.synchronize()
+                    ts.append(time.perf_counter() - t0)
+                t_ms = max_ms(float(np.median(ts)) * 1e3)
+                nbytes = buf.numel() * 4
+                coll[name] = {"bytes": nbytes, "all_reduce_ms": t_ms,
+                              "algbw_GBs": round(nbytes / (t_ms * 1e-3) / 1e9, 2),
+                              "busbw_GBs": round(2 * (world - 1) / world * nbytes /
+                                                 (t_ms * 1e-3) / 1e9, 2)}
+            out["all_reduce"] = coll
+        del net
+        torch.cuda.empty_cache()
+    return out
+
+
 def selfplay_cpu_baseline(W, G, sims, seconds, threads):
     """The reference's sequential loop on the host: Coach.executeEpisode over this repo's Python
     MCTS (bit-exact with the reference's, tests/test_mcts_golden.py) with oracle/torch_ref.py as
@@ -978,6 +1064,8 @@ def main():
     tr = None
     if not args.no_train and rank == 0 and world == 1:
         tr = train_leg(W, G, device)
+    if not args.no_train and world > 1:
+        tr = train_dp_leg(W, G, device, world, rank)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
