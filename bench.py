@@ -542,8 +542,11 @@ def _pmc_selfplay_gemm(M):
     try:
         d = json.load(open(os.path.join(ROOT, "profiles", "pmc.json")))["gemm_selfplay"]
         r = d["by_M"][str(M)]["csk"]
-        return {"traffic": r["hbm_bytes_per_dispatch"], "traffic_algorithmic": r["algorithmic_bytes"],
-                "l2_hit": r.get("l2_hit"), "traffic_run": r.get("tag", d.get("tag"))}
+        # not measured by this run: a committed profile's counters, labelled with its tag
+        return {"committed_pmc": {"traffic": r["hbm_bytes_per_dispatch"],
+                                  "traffic_algorithmic": r["algorithmic_bytes"],
+                                  "l2_hit": r.get("l2_hit"), "tag": r.get("tag", d.get("tag")),
+                                  "source": "profiles/pmc.json gemm_selfplay"}}
     except (OSError, KeyError, ValueError):
         return None
 
