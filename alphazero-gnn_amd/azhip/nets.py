@@ -240,7 +240,7 @@ def gnn_per_row_heads(nnet, gnn, feat, want_pi=True, pi=None, v=None):
             feat, G["output_transform.0.weight"], G["output_transform.0.bias"],
             G["output_transform.2.weight"], G["output_transform.2.bias"], W["fc_policy.weight"],
             W["fc_policy.bias"], W["fc_value.weight"], W["fc_value.bias"], want_pi=want_pi,
-            pi=pi, v=v)
+            pi=pi, v=v, want_y=False)
         return logp, pi, v
     return nnet.heads(gnn.forward_per_row(feat), want_pi=want_pi, pi=pi, v=v)
 

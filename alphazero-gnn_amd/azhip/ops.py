@@ -412,15 +412,19 @@ def mlp2(x, w0, b0, w2, b2, hidden=None, out=None):
 
 
 def transform_heads(x, w0, b0, w2, b2, wp, bp, wv, bv, hidden=None, y=None, logp=None, pi=None,
-                    v=None, want_pi=True):
+                    v=None, want_pi=True, want_y=True):
     """Per-row output_transform + heads (gnn_utils.py:115, Connect4GNN.py:48-57) in one C call:
-    the second GEMM's split-K reduction is fused with the heads' first pass.
+    the second GEMM's split-K reduction is fused with the heads' first pass; with want_y=False
+    y is never formed (the heads come from the GEMM's tiles, include/az_hip.h) and None returned.
     Returns (logp, pi, v, y, hidden)."""
     B, F = x.shape
     A = wp.shape[0]
     dev = x.device
     hidden = torch.empty_like(x) if hidden is None else hidden
-    y = torch.empty_like(x) if y is None else y
+    if want_y:
+        y = torch.empty_like(x) if y is None else y
+    else:
+        y = None
     logp = torch.empty((B, A), device=dev) if logp is None else logp
     pi = (torch.empty((B, A), device=dev) if pi is None else pi) if want_pi else None
     v = torch.empty((B,), device=dev) if v is None else v
@@ -469,13 +473,18 @@ def c4_gnn_eval(boards, W, G, feat=None, hidden=None, y=None, logp=None, pi=None
     return logp, pi, v
 
 
-def linear_heads(x, w, b, wp, bp, wv, bv, y=None, logp=None, pi=None, v=None, want_pi=True):
+def linear_heads(x, w, b, wp, bp, wv, bv, y=None, logp=None, pi=None, v=None, want_pi=True,
+                 want_y=True):
     """y = x w^T + b then the heads of y, with the GEMM's split-K reduction fused into the
-    heads' first pass (the second half of transform_heads).  Returns (logp, pi, v, y)."""
+    heads' first pass (the second half of transform_heads); want_y=False: y never formed
+    (None returned).  Returns (logp, pi, v, y)."""
     B, F = x.shape
     A = wp.shape[0]
     dev = x.device
-    y = torch.empty_like(x) if y is None else y
+    if want_y:
+        y = torch.empty_like(x) if y is None else y
+    else:
+        y = None
     logp = torch.empty((B, A), device=dev) if logp is None else logp
     pi = (torch.empty((B, A), device=dev) if pi is None else pi) if want_pi else None
     v = torch.empty((B,), device=dev) if v is None else v

@@ -5,6 +5,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "../../include/az_hip.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -16,6 +18,16 @@ namespace az {
 // retrievable with az_last_error() (thread-local).
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+
+// f(std::integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time (for intrinsics
+// that need the index as a constant, e.g. a DPP control)
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
 
 enum Act { ACT_NONE = AZ_ACT_NONE, ACT_RELU = AZ_ACT_RELU, ACT_SIGMOID = AZ_ACT_SIGMOID,
            ACT_TANH = AZ_ACT_TANH };

@@ -60,6 +60,9 @@ struct GemmArgs {
   // W ([2][N]), row_scale_kernel
   const float* sa;
   const float* sw;
+  // gemm_p3 HEADS: the heads' dot products per tile row instead of C / slabs (az_x3.h HeadsEpi)
+  HeadsEpi he;
+  int heads_done;   // host side: launch_x3 ran the HEADS form (no C, no slabs written)
 };
 
 __device__ __forceinline__ void epilogue_store(const GemmArgs& p, int row, int col, float acc) {
@@ -322,6 +325,124 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, Acc (&acc)[TI][
         if (row < p.M && col < p.N && (!skip || acc[i][j][r] != acc[i][j][r]))
           slab[(size_t)row * p.N + col] = acc[i][j][r];
       }
+}
+
+// The heads' weights (and y's bias) a HEADS tile's wave needs, loaded before the k loop so their
+// latency hides under it: chunk cc (32 columns from c0 + 32 cc), slot a (policy rows a < A, slot
+// 8 the value row), half h: lane l holds column c0 + 32 cc + 16 h + (l & 15).  The epilogue gives
+// every lane the weight of column c with a DPP row_share:(c & 15) operand -- no LDS, no scalar
+// loads in the epilogue.
+template <int TJ>
+struct HeadsRegs {
+  float w[TJ][HEADS_TILE_SLOTS][2];
+  float b[TJ][2];
+};
+template <int TJ>
+__device__ __forceinline__ void heads_preload(const GemmArgs& p, int c0, HeadsRegs<TJ>& hr) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int cc = 0; cc < TJ; ++cc)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int col = c0 + cc * 32 + 16 * h + (lane & 15);
+      const bool in = c0 + cc * 32 < p.N;         // N % 32 == 0: whole chunks
+      const int cl = in ? col : 0;
+#pragma unroll
+      for (int a = 0; a < HEADS_TILE_SLOTS; ++a) {
+        const bool use = in && (a == 8 || a < p.he.A);
+        const float* src = a < 8 ? p.he.wp + (size_t)min(a, max(p.he.A - 1, 0)) * p.N : p.he.wv;
+        hr.w[cc][a][h] = use ? src[cl] : 0.f;
+      }
+      hr.b[cc][h] = in && p.bias ? p.bias[cl] : 0.f;
+    }
+}
+
+// acc + bcast(w) * x and x + bcast(b), bcast = lane C of each 16-lane row (DPP row_newbcast, the
+// gfx950 row_share) as the operand modifier of the VALU op itself: one instruction each.  The
+// first use of a weight register per chunk waits 2 cycles (s_nop 1): a VALU write of a VGPR that a
+// DPP operand reads needs 2 wait states, and the register may have been copied just before.
+template <int C>
+__device__ __forceinline__ float fma_share(float acc, float w, float x) {
+  if constexpr (C == 0)
+    asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(w), "v"(x), "i"(C));
+  else
+    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(w), "v"(x), "i"(C));
+  return acc;
+}
+template <int C>
+__device__ __forceinline__ float add_share(float x, float b) {
+  if constexpr (C == 0)
+    asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %0 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+        : "+v"(x) : "v"(b), "i"(C));
+  else
+    asm("v_add_f32_dpp %0, %1, %0 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+        : "+v"(x) : "v"(b), "i"(C));
+  return x;
+}
+
+// The HEADS epilogue of a 64-row wave tile (gemm_p3 / gemm_x3 HEADS; az_x3.h HeadsEpi): per row,
+// the dot products of the wave's WN columns of the tile (+ the bias in k split 0) with the 8 policy
+// rows and the value row, in column order; the WGN waves sharing the rows are added in wave order
+// through LDS and the block's row results leave as part[row][nt * splits + sp][0..8].  Every
+// wave reaches the block barrier.  stage: the wave's [64][36] region; comb: [WGM][64][9] floats.
+template <int TI, int TJ, int WGM, int WGN>
+__device__ __forceinline__ void heads_tile_epilogue(const GemmArgs& p, f32x16 (&acc)[TI][TJ],
+                                                    const HeadsRegs<TJ>& hr, int r0, int c0,
+                                                    int nt, int sp, int wm, int wn, float* stage,
+                                                    float* comb) {
+  constexpr int WM = TI * 32, LD = 36, HS = HEADS_TILE_SLOTS;
+  static_assert(WM == 64, "one row per lane");
+  const int lane = threadIdx.x & 63;
+  float part[HS];
+#pragma unroll
+  for (int a = 0; a < HS; ++a) part[a] = 0.f;
+#pragma unroll
+  for (int cc = 0; cc < TJ; ++cc) {
+    if (c0 + cc * 32 >= p.N) break;          // N % 32 == 0 (host-checked): whole chunks only
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        stage[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LD + (lane & 31)] =
+            acc[i][cc][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave-local: own region
+    f32x4 x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = *reinterpret_cast<const f32x4*>(stage + lane * LD + 4 * q);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the next chunk's stores
+    if (sp == 0) {
+      static_for<32>([&](auto C) {
+        constexpr int c = decltype(C)::value;
+        x[c >> 2][c & 3] = add_share<c & 15>(x[c >> 2][c & 3], hr.b[cc][c >> 4]);
+      });
+    }
+    static_for<32>([&](auto C) {
+      constexpr int c = decltype(C)::value;
+#pragma unroll
+      for (int a = 0; a < HS; ++a)
+        part[a] = fma_share<c & 15>(part[a], hr.w[cc][a][c >> 4], x[c >> 2][c & 3]);
+    });
+  }
+  // the WGN waves of this row group: wave order, through LDS
+  if (wn > 0) {
+#pragma unroll
+    for (int a = 0; a < HS; ++a) comb[((wn - 1) * WGM + wm) * 64 * HS + lane * HS + a] = part[a];
+  }
+  __syncthreads();
+  if (wn == 0) {
+    for (int w = 1; w < WGN; ++w)
+#pragma unroll
+      for (int a = 0; a < HS; ++a) part[a] += comb[((w - 1) * WGM + wm) * 64 * HS + lane * HS + a];
+    const int row = r0 + lane;
+    if (row < p.M) {
+      const int P = ((p.N + WGN * 64 - 1) / (WGN * 64)) * p.splits;
+      float* dst = p.he.part + ((size_t)row * P + nt * p.splits + sp) * HS;
+#pragma unroll
+      for (int a = 0; a < HS; ++a) dst[a] = part[a];
+    }
+  }
 }
 
 // Waves arranged WGM x WGN; each wave computes a (BM/WGM) x (BN/WGN) sub-tile as TI x TJ
@@ -1048,7 +1169,7 @@ constexpr int x3_smem_bytes() {
 // MFMAs), and the accumulators multiplied back by 1 / (sa[row] sw[col]) (exact) before the
 // epilogue.
 template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false, int MF = 32,
-          bool FLEX = false, bool H3 = false>
+          bool FLEX = false, bool H3 = false, bool HEADS = false>
 __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int mt, int nt,
                                              int sp, int kbeg, int kend, int bma = BM) {
   static_assert(!APL || !MASK, "pre-split A needs whole 32-k tiles");
@@ -1278,6 +1399,8 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
     body(std::integral_constant<bool, MASK>{}, kt, nxt, fut);
   };
 
+  HeadsRegs<TJ> hregs;                 // HEADS: the heads' weights, loaded before the loop
+  if constexpr (HEADS) heads_preload<TJ>(p, n0 + wn * WN, hregs);
   const int nk = (kend - kbeg + BK - 1) / BK;
   Regs r0, r1;
   gload(r0, kbeg);
@@ -1306,20 +1429,32 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
         for (int j = 0; j < TJ; ++j) acc[i][j][r] *= ia * iw[j];
       }
   }
+  if constexpr (HEADS) {     // the same epilogue as gemm_p3's: the same bits for the same planes
+    static_assert(H3 && !FLEX && MF == 32 && WN == 64 && TI == 2, "heads epilogue: fp16 tiles");
+    __syncthreads();         // the k loop's last LDS reads are done everywhere
+    float* f = reinterpret_cast<float*>(smem);
+    heads_tile_epilogue<TI, TJ, WGM, WGN>(p, acc, hregs, m0 + wm * WM, n0 + wn * WN, nt, sp, wm,
+                                          wn, f + wave * (WM * 36), f + WGM * WGN * WM * 36);
+    return;
+  }
   tile_epilogue<MF, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
 }
 
 template <int BM, int BN, int WGM, int WGN, bool MASK, int ABL = 0, bool APL = false, int MF = 32,
-          bool H3 = false>
+          bool H3 = false, bool HEADS = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_x3(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<BM, BN, WGM, WGN, MF, H3 ? 2 : 3>()];
+  static_assert(!HEADS || x3_smem_bytes<BM, BN, WGM, WGN, MF, H3 ? 2 : 3>() >=
+                              (WGM * WGN * 64 * 36 + WGM * (WGN - 1) * 64 * HEADS_TILE_SLOTS) * 4,
+                "heads epilogue: stage + comb must fit");
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
   const int nwg = mt_n * nt_n * p.splits;
   int mt, nt, sp;
   tile_of(xcd_swizzle(blockIdx.x, nwg), mt_n, nt_n, mt, nt, sp);
   const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
-  gemm_x3_body<BM, BN, WGM, WGN, MASK, ABL, APL, MF, false, H3>(p, smem, mt, nt, sp, kbeg, kend);
+  gemm_x3_body<BM, BN, WGM, WGN, MASK, ABL, APL, MF, false, H3, HEADS>(p, smem, mt, nt, sp, kbeg,
+                                                                       kend);
 }
 
 // Stream-K form of gemm_x3 for grids whose tile count does not fill the chip in whole rounds
@@ -1483,7 +1618,7 @@ __host__ __device__ __forceinline__ int csk_block_of(int u, int b, int W) {
 
 // gemm_p3_body (below): the tile on operands already split into planes, LDS-DMA only
 template <int BM, int BN, int WGM, int WGN, bool H3 = false, bool FLEX = false, int NBUF = 2,
-          int ABL = 0>
+          int ABL = 0, bool HEADS = false>
 __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int mt, int nt,
                                              int sp, int kbeg, int kend, int bma = BM);
 
@@ -1702,7 +1837,7 @@ constexpr int p3_smem_bytes() {
 // stage as with two; the fp16 256 x 128 ring is 3 x 48 KB.
 // ABL (tuning-build timing ablations, results wrong by design): 1 = no epilogue stores,
 // 2 = no MFMAs, 4 = no DMA (stale LDS)
-template <int BM, int BN, int WGM, int WGN, bool H3, bool FLEX, int NBUF, int ABL>
+template <int BM, int BN, int WGM, int WGN, bool H3, bool FLEX, int NBUF, int ABL, bool HEADS>
 __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int mt, int nt,
                                              int sp, int kbeg, int kend, int bma) {
   static_assert(NBUF == 2 || NBUF == 3, "p3 ring: 2 or 3 stages");
@@ -1808,6 +1943,8 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][i], f.b[0][j], t, 0, 0, 0);
   };
   constexpr int NG = TI * TJ;
+  HeadsRegs<TJ> hregs;                 // HEADS: the heads' weights, loaded before the loop
+  if constexpr (HEADS) heads_preload<TJ>(p, n0 + wn * WN, hregs);
   const int nk = (kend - kbeg) / BK;
   if (nk > 0) issue(0, kbeg);
   if (NBUF == 3 && nk > 1) issue(1, kbeg + BK);
@@ -1862,19 +1999,31 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
     if (t == 12345.f) p.C[0] = t;
     return;
   }
+  if constexpr (HEADS) {
+    static_assert(H3 && !FLEX && WN == 64 && TI == 2, "heads epilogue: the P2 split-K tiles");
+    float* f = reinterpret_cast<float*>(smem);
+    heads_tile_epilogue<TI, TJ, WGM, WGN>(p, acc, hregs, m0 + wm * WM, n0 + wn * WN, nt, sp, wm,
+                                          wn, f + wave * (WM * 36), f + NW * WM * 36);
+    return;
+  }
   tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
 }
 
-template <int BM, int BN, int WGM, int WGN, bool H3 = false, int NBUF = 2, int ABL = 0>
+template <int BM, int BN, int WGM, int WGN, bool H3 = false, int NBUF = 2, int ABL = 0,
+          bool HEADS = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[p3_smem_bytes<BM, BN, WGM, WGN, H3, NBUF>()];
+  static_assert(!HEADS || p3_smem_bytes<BM, BN, WGM, WGN, H3, NBUF>() >=
+                              (WGM * WGN * 64 * 36 + WGM * (WGN - 1) * 64 * HEADS_TILE_SLOTS) * 4,
+                "heads epilogue: stage + comb must fit the stage buffers");
   const int mt_n = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
   const int nwg = mt_n * nt_n * p.splits;
   int mt, nt, sp;
   tile_of(xcd_swizzle(blockIdx.x, nwg), mt_n, nt_n, mt, nt, sp);
   const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
-  gemm_p3_body<BM, BN, WGM, WGN, H3, false, NBUF, ABL>(p, smem, mt, nt, sp, kbeg, kend, BM);
+  gemm_p3_body<BM, BN, WGM, WGN, H3, false, NBUF, ABL, HEADS>(p, smem, mt, nt, sp, kbeg, kend,
+                                                              BM);
 }
 
 // gemm_p3 in stream-K form (see gemm_x3_sk), pieces summed by streamk_fixup4_kernel
@@ -3987,11 +4136,28 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
       hipLaunchKernelGGL((gemm_p3<256, 256, 4, 2, true>), gw, dim3(512), 0, s, a);
     }
 #endif
+    else if (a.he.part && tile == 1) {
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 0, true>), grid, dim3(512), 0, s, a);
+      a.heads_done = 1;
+    } else if (a.he.part) {
+      hipLaunchKernelGGL((gemm_p3<128, 128, 2, 2, true, 2, 0, true>), grid, dim3(256), 0, s, a);
+      a.heads_done = 1;
+    }
     else if (tile == 1) hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true>), grid, dim3(512), 0, s, a);
     else hipLaunchKernelGGL((gemm_p3<128, 128, 2, 2, true>), grid, dim3(256), 0, s, a);
     return true;
   }
   if (h3 && (tile == 1 || tile == 2) && h3_scales()) {
+    if (a.he.part && whole) {     // the heads from the tiles, as on the P2 tiles (same bits)
+      if (tile == 1)
+        hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 0, false, 32, true, true>), grid,
+                           dim3(512), 0, s, a);
+      else
+        hipLaunchKernelGGL((gemm_x3<128, 128, 2, 2, false, 0, false, 32, true, true>), grid,
+                           dim3(256), 0, s, a);
+      a.heads_done = 1;
+      return true;
+    }
     if (tile == 1) { AZ_H3(256, 128, 4, 2) }
     else { AZ_H3(128, 128, 2, 2) }
     return true;
@@ -4042,8 +4208,10 @@ static bool full_waves_256x128(int M, int N) {
 // The GEMM without its split-K reduction: when the plan splits K, the raw partial sums are left
 // in d->ws as slabs [*splits_out][M][N] and C is NOT written (the caller reduces them, e.g.
 // fused with its consumer: az_transform_heads_fwd); otherwise C is written and *splits_out = 1.
-int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out, const PreSplitA* pre) {
+int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out, const PreSplitA* pre,
+                     const HeadsEpi* he, bool* heads_done) {
   *splits_out = 1;
+  if (heads_done) *heads_done = false;
   AZ_REQUIRE(d != nullptr, AZ_EINVAL, "az_gemm_f32: null descriptor");
   AZ_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, AZ_EINVAL, "az_gemm_f32: negative size");
   if (d->M == 0 || d->N == 0) return AZ_OK;
@@ -4104,10 +4272,17 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out, cons
     }
   }
   const bool glds_ok = akm && bkm && !d->A2 && !d->a_rows;
+  // the heads from the tiles (az_x3.h HeadsEpi): only a plain y = x W^T + b, whole 32-column
+  // chunks, A <= 8; launch_x3 takes it on its P2 split-K tiles and says so in a.heads_done
+  if (he && he->part && he->A <= 8 && d->N % 32 == 0 && d->act == AZ_ACT_NONE && !d->R &&
+      !d->G && !d->C2 && d->beta == 0.f && !d->c_rows && (!d->bias || aligned16(d->bias)))
+    a.he = *he;
   if (glds_ok && d->M > 8 && d->K >= 1024 && d->N >= 256 && launch_x3(a, d->ws_bytes, s, pre)) {
     *splits_out = a.splits;
+    if (heads_done) *heads_done = a.heads_done != 0;
     return check_launch("gemm_x3");
   }
+  a.he = HeadsEpi{};
   // tile choice (tuning override for experiments: AZ_GEMM_CFG=<index into kCfgs>)
   static const char* env_cfg = tuning_env("AZ_GEMM_CFG");
   int cfg = 0;
@@ -4329,7 +4504,7 @@ extern "C" int az_tuning_leaf_trace(unsigned long long* out) {
 
 int gemm_f32(const az_gemm_desc* d, hipStream_t s) {
   int splits = 1;
-  int rc = gemm_f32_partial(d, s, &splits, nullptr);
+  int rc = gemm_f32_partial(d, s, &splits, nullptr, nullptr, nullptr);
   if (rc || splits <= 1) return rc;
   return splitk_reduce(d, splits, s);
 }

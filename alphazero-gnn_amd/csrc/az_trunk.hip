@@ -471,6 +471,51 @@ __global__ __launch_bounds__(256) void heads_finalize_kernel(const float* __rest
   v[row] = tanhf(sm[r][A] + bv[0]);
 }
 
+// The heads from a P2 GEMM's tile partials (az_x3.h HeadsEpi; the GEMM added the bias b of y in
+// its first k split): one wave per row sums the P partials of every slot in tile order (lane t
+// takes t, t + 64, ... in turn, then a fixed butterfly, so the bits do not depend on the launch
+// shape), adds the heads' biases and applies log_softmax / exp / tanh as heads_finalize_kernel.
+__global__ __launch_bounds__(256) void heads_tiles_finalize_kernel(
+    const float* __restrict__ part, int P, int B, int A, const float* __restrict__ bp,
+    const float* __restrict__ bv, float* __restrict__ logp, float* __restrict__ pi,
+    float* __restrict__ v) {
+  constexpr int HS = HEADS_TILE_SLOTS;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float* src = part + (size_t)row * P * HS;
+  float s[HS];
+#pragma unroll
+  for (int a = 0; a < HS; ++a) s[a] = 0.f;
+  for (int t = lane; t < P; t += 64)
+#pragma unroll
+    for (int a = 0; a < HS; ++a) s[a] += src[(size_t)t * HS + a];
+#pragma unroll
+  for (int a = 0; a < HS; ++a) s[a] = wave_sum(s[a]);
+  if (lane != 0) return;
+  float l[8];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+    if (a < A) {
+      l[a] = s[a] + bp[a];
+      mx = fmaxf(mx, l[a]);
+    }
+  float se = 0.f;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+    if (a < A) se += expf(l[a] - mx);
+  const float lse = logf(se);
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+    if (a < A) {
+      const float o = (l[a] - mx) - lse;
+      logp[(size_t)row * A + a] = o;
+      if (pi) pi[(size_t)row * A + a] = expf(o);
+    }
+  v[row] = tanhf(s[8] + bv[0]);
+}
+
 // Small batches (B <= HEADS_ROWS_MAXB, the batch-1 MCTS leaf): both passes in ONE launch, one
 // 512-thread block per row.  Wave w forms the chunk partials of chunks w, w+8, ... with exactly
 // heads_partial_kernel's arithmetic (two chunks' loads issued together), parks them in LDS, and
@@ -824,7 +869,8 @@ int gemv1_with_side_heads(const az_gemm_desc* d, const SideHeads* h, hipStream_t
 int c4_leaf_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, float* v, float* gpi,
                 float* gv, hipStream_t s);
 int gemm_f32(const az_gemm_desc* d, hipStream_t s);
-int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out, const PreSplitA* pre);
+int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out, const PreSplitA* pre,
+                     const HeadsEpi* he = nullptr, bool* heads_done = nullptr);
 int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s);
 int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* planes, float* sc,
                         hipStream_t s);
@@ -966,9 +1012,11 @@ extern "C" size_t az_transform_heads_ws_bytes(int B, int F, int A) {
   // the heads' chunk partials, then room for 8 split-K slabs of the [B][F] GEMM outputs, the
   // GEMM's A operand as two fp16 planes (the fp16 form on pre-split planes, az_gemm.hip) and
   // A's row scales, and the pre-split-A region (pre_region) at the end
+  // (+ [B][F] scratch for y when the caller passes y = NULL and the GEMM's shape has no heads
+  // epilogue)
   return align256(az_heads_ws_bytes(B, F, A)) + (size_t)8 * B * F * 4 +
          align256((size_t)4 * B * F) + align256((size_t)8 * B) + 256 +
-         az::pre_region_bytes(B, F);
+         az::pre_region_bytes(B, F) + align256((size_t)4 * B * F);
 }
 
 template <int S>
@@ -1004,14 +1052,25 @@ static int linear_heads_impl(const float* x, int B, int F, const float* w, const
   AZ_REQUIRE(B >= 0 && F > 0 && F % 4 == 0 && A > 0 && A <= 32, AZ_EINVAL,
              "az_linear_heads_fwd: bad shape B=%d F=%d A=%d", B, F, A);
   if (B == 0) return AZ_OK;
-  AZ_REQUIRE(x && w && b && wp && bp && wv && bv && y && logp && v && ws, AZ_EINVAL,
+  AZ_REQUIRE(x && w && b && wp && bp && wv && bv && logp && v && ws, AZ_EINVAL,
              "az_linear_heads_fwd: null pointer");
   const size_t part_bytes = align256(az_heads_ws_bytes(B, F, A));
   AZ_REQUIRE(ws_bytes >= part_bytes, AZ_EINVAL, "az_linear_heads_fwd: workspace too small");
-  AZ_REQUIRE(aligned16(x) && aligned16(y) && aligned16(wp) && aligned16(wv) && aligned16(b) &&
-                 aligned16(ws),
+  AZ_REQUIRE(aligned16(x) && (!y || aligned16(y)) && aligned16(wp) && aligned16(wv) &&
+                 aligned16(b) && aligned16(ws),
              AZ_EINVAL, "az_linear_heads_fwd: operands need 16B alignment");
   hipStream_t s = as_stream(stream);
+  // y == NULL: the caller wants only the heads.  The GEMM then hands its tiles' head dot
+  // products to heads_tiles_finalize_kernel when it can (az_x3.h HeadsEpi); the other shapes
+  // form y in a [B][F] scratch at the workspace's end
+  const bool want_y = y != nullptr;
+  if (!want_y) {
+    const size_t yb = align256((size_t)4 * B * F);
+    AZ_REQUIRE(ws_bytes >= part_bytes + yb + 256, AZ_EINVAL,
+               "az_linear_heads_fwd: workspace too small for y = NULL");
+    ws_bytes = (ws_bytes - yb) / 256 * 256;
+    y = reinterpret_cast<float*>(static_cast<char*>(ws) + ws_bytes);
+  }
   float* part = static_cast<float*>(ws);
   void* slabs = static_cast<char*>(ws) + part_bytes;
   int rc;
@@ -1023,7 +1082,19 @@ static int linear_heads_impl(const float* x, int B, int F, const float* w, const
   d.C = y; d.ldc = F;
   d.ws = slabs; d.ws_bytes = ws_bytes - part_bytes;
   int S = 1;
-  if ((rc = gemm_f32_partial(&d, s, &S, pre))) return rc;
+  // the tile partials [B][P][9] (P <= ceil(F / 128) * 8) at the start of the slab region
+  const size_t tiles_bytes = (size_t)B * ((F + 127) / 128) * 8 * HEADS_TILE_SLOTS * 4;
+  const HeadsEpi he{wp, wv, A, static_cast<float*>(slabs)};
+  bool heads_done = false;
+  static const bool no_tiles = tuning_env("AZ_NO_HEADS_TILES") != nullptr;   // A/B experiments
+  const bool try_tiles = !want_y && !no_tiles && A <= 8 && 2 * tiles_bytes <= d.ws_bytes;
+  if ((rc = gemm_f32_partial(&d, s, &S, pre, try_tiles ? &he : nullptr, &heads_done))) return rc;
+  if (heads_done) {
+    const int P = (F + 127) / 128 * S;
+    hipLaunchKernelGGL(heads_tiles_finalize_kernel, dim3((B + 3) / 4), dim3(256), 0, s, he.part,
+                       P, B, A, bp, bv, logp, pi, v);
+    return check_launch("heads_tiles_finalize_kernel");
+  }
   const float* sl = static_cast<const float*>(slabs);
   // one launch: splitk_heads_rowsw_kernel (AZ_SPLITK_HEADS_MODE = rows / chunks select the
   // one-row-per-block kernel / chunk partials + finalize for A/B runs)
@@ -1205,8 +1276,10 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
   AZ_REQUIRE(aligned16(e->feat) && aligned16(e->hidden) && aligned16(e->ws), AZ_EINVAL,
              "az_c4_eval_fwd: scratch needs 16B alignment");
   const PreSplitA pre{R.planes, R.sc};
+  // y (the transform's output) is not an output of the evaluator: the heads come from the
+  // GEMM's tiles (az_x3.h HeadsEpi) wherever its shape allows
   return transform_heads_impl(e->feat, B, 3136, e->ot0_w, e->ot0_b, e->ot2_w, e->ot2_b,
                               e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,
-                              e->hidden, e->y, e->glogp, gpi, gv, e->ws, e->ws_bytes, stream,
+                              e->hidden, nullptr, e->glogp, gpi, gv, e->ws, e->ws_bytes, stream,
                               split ? &pre : nullptr);
 }

@@ -145,4 +145,20 @@ struct PreSplitA {
   const float* sc;
 };
 
+// The policy / value heads taken straight from a P2 GEMM's tiles (az_linear_heads_fwd /
+// az_transform_heads_fwd without y, az_c4_eval_fwd).  The heads are linear in
+// y = x W^T + b (Connect4GNN.py:48-57: fc_policy / fc_value read y itself), so instead of storing
+// its part of y, each block leaves the dot products of its tile's columns (+ b in the first k
+// split) with the heads' weight rows: part[row][t][9], t = n_tile * splits + split, slot a < A the
+// policy row a, slot 8 the value row.  heads_tiles_finalize_kernel sums the t in order, adds the
+// heads' biases and runs log_softmax / exp / tanh.  y is never written: 12.8 MB less traffic per
+// B = 512 call than the split-K slabs and the heads pass that re-read them.
+constexpr int HEADS_TILE_SLOTS = 9;
+struct HeadsEpi {
+  const float* wp;   // fc_policy.weight [A][N]
+  const float* wv;   // fc_value.weight [N]
+  int A;             // <= 8
+  float* part;       // [M][P][HEADS_TILE_SLOTS], P = n tiles x k splits
+};
+
 }  // namespace az

@@ -941,8 +941,9 @@ def main():
     def step():
         # the product's batched predict_with_gnn, one az_c4_eval_fwd call: trunk (also writing
         # output_transform.0's A in the GEMM's split form) -> output_transform.0 (+ReLU; its
-        # split-K reduce also splitting output_transform.2's A) -> output_transform.2 with its
-        # reduce fused into the heads' first pass
+        # split-K reduce also splitting output_transform.2's A) -> output_transform.2, every
+        # tile folding its part of y (+ bias) into the heads' dot products (y is not an output
+        # of predict_with_gnn and is never stored; az_x3.h HeadsEpi) -> the heads' finalize
         ops.c4_gnn_eval(boards, Wn, Gn, feat=featbuf, hidden=h, y=y, logp=logp, pi=pi, v=v)
 
     def step_unfused():
@@ -952,7 +953,7 @@ def main():
                    act=ops.ACT_RELU, out=h)
         return ops.linear_heads(h, Gn["output_transform.2.weight"], Gn["output_transform.2.bias"],
                                 Wn["fc_policy.weight"], Wn["fc_policy.bias"],
-                                Wn["fc_value.weight"], Wn["fc_value.bias"])
+                                Wn["fc_value.weight"], Wn["fc_value.bias"], want_y=False)
 
     # correctness guard: the bench path is bit-identical to the unfused calls and to the
     # evaluator's predict_with_gnn path

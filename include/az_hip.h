@@ -171,7 +171,9 @@ typedef struct az_c4_eval {
  * batched predict_with_gnn alone) and registered output_transform weights, the trunk writes
  * output_transform.0's operand already split for the fp16-form GEMM and that GEMM's split-K
  * reduce writes output_transform.2's, both into the last az_transform_heads_ws_bytes-sized
- * region of e->ws; the outputs are bit-identical to az_c4_trunk_fwd + az_transform_heads_fwd. */
+ * region of e->ws; the GNN tail runs as az_transform_heads_fwd with y = NULL (e->y is not
+ * written for B > 8), so the outputs are bit-identical to az_c4_trunk_fwd +
+ * az_transform_heads_fwd(y = NULL). */
 int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, float* v,
                    float* gpi, float* gv, void* stream);
 
@@ -184,7 +186,13 @@ int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, 
  * When the second GEMM is split over K, its slab reduction, bias, the store of y and the heads'
  * dot products run in one pass (y is not re-read); results equal az_gemm_f32 + az_heads_fwd
  * bit for bit.  ws: >= az_heads_ws_bytes(B, F, A) rounded up to 256 B; az_transform_heads_ws_bytes
- * leaves room for the split-K slabs (a smaller workspace only limits the K split). */
+ * leaves room for the split-K slabs (a smaller workspace only limits the K split).
+ * y may be NULL when only the heads are wanted (the evaluators): y is then never written -- on
+ * the fp16-form split-K tiles (A <= 8, F % 32 == 0) every block folds its tile of y (+ b in its
+ * first k split) into per-row dot products with wp / wv, heads_tiles_finalize_kernel sums them in
+ * tile order (the heads are linear in y); other shapes form y in workspace scratch
+ * (az_transform_heads_ws_bytes includes it).  Those results are the same function to fp32
+ * rounding, not bit-identical to the y != NULL path (tests/test_gpu_kernels.py bounds it). */
 size_t az_transform_heads_ws_bytes(int B, int F, int A);
 /* Its second half alone: y = x W^T + b, then the heads of y (same fusion, same workspace). */
 int az_linear_heads_fwd(const float* x, int B, int F, const float* w, const float* b,

@@ -53,8 +53,10 @@ for B in (33, 100, 512):
             _lib.check(_lib.load().az_weights_register(t.data_ptr(), t.numel() * 4), "register")
     logp, pi, v, y, hid = ops.transform_heads(*c)
     hl, hp_, hv_ = ops.heads(c[0], c[5], c[6], c[7], c[8])
+    tl, tp, tv, _, th = ops.transform_heads(*c, want_y=False)   # heads from the GEMM tiles
     for k, t in (("logp", logp), ("pi", pi), ("v", v), ("y", y), ("hid", hid),
-                 ("h_logp", hl), ("h_pi", hp_), ("h_v", hv_)):
+                 ("h_logp", hl), ("h_pi", hp_), ("h_v", hv_), ("t_logp", tl), ("t_pi", tp),
+                 ("t_v", tv), ("t_hid", th)):
         out["%s_%d" % (k, B)] = t.cpu().numpy()
 np.savez(sys.argv[2], **out)
 print("ok")

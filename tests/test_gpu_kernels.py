@@ -1034,6 +1034,55 @@ def test_transform_heads_fused_equals_unfused(ops, B):
     assert np.abs(v.cpu().numpy() - ov).max() < 1e-5
 
 
+@pytest.mark.parametrize("B", [1, 9, 65, 300, 512, 1024, 1576, 4096])
+@pytest.mark.parametrize("registered", [True, False])
+def test_transform_heads_without_y(ops, B, registered):
+    """az_transform_heads_fwd with y = NULL (what every evaluator calls): y is never formed --
+    on the fp16 split-K tiles each block folds its tile of y into the heads' dot products
+    (az_x3.h HeadsEpi) and heads_tiles_finalize_kernel sums them in tile order; other shapes
+    (B <= 64, stream-K batches) form y in scratch.  The heads are linear in y
+    (Connect4GNN.py:48-57), so this is the same function: within 1e-5 of the oracle
+    (gnn_utils.py:115, per row), within 2e-6 of the y path, hidden bit-identical to it, and the
+    same bits on registered (cached W planes) and unregistered (in-tile split) weights."""
+    from oracle import nets as O
+    F, A = 3136, 8
+    g = torch.Generator().manual_seed(B + 77)
+    x = torch.rand((B, F), generator=g) * 2 - 1
+    w0 = (torch.rand((F, F), generator=g) * 2 - 1) / F ** 0.5
+    w2 = (torch.rand((F, F), generator=g) * 2 - 1) / F ** 0.5
+    b0, b2 = (torch.rand((F,), generator=g) - 0.5) * 0.1, (torch.rand((F,), generator=g) - 0.5) * 0.1
+    wp = (torch.rand((A, F), generator=g) * 2 - 1) / F ** 0.5
+    wv = (torch.rand((1, F), generator=g) * 2 - 1) / F ** 0.5
+    bp, bv = torch.rand((A,), generator=g) - 0.5, torch.rand((1,), generator=g) - 0.5
+    c = [t.cuda() for t in (x, w0, b0, w2, b2, wp, bp, wv, bv)]
+    unreg = []
+    if registered:
+        unreg = [_registered(c[1]), _registered(c[3])]
+    try:
+        logp, pi, v, y, hid = ops.transform_heads(*c)
+        tl, tp, tv, ty, th = ops.transform_heads(*c, want_y=False)
+        if registered:
+            cu_ = [t.clone() for t in c]              # the same values, unregistered storage
+            ul, up, uv, _, _ = ops.transform_heads(*cu_, want_y=False)
+            torch.cuda.synchronize()
+            assert torch.equal(ul, tl) and torch.equal(up, tp) and torch.equal(uv, tv)
+    finally:
+        for u in unreg:
+            u()
+    torch.cuda.synchronize()
+    assert ty is None and torch.equal(th, hid)
+    assert_close(f"heads_without_y/B{B}/logp_vs_y_path", tl.cpu().numpy(), logp.cpu().numpy(), 2e-6)
+    assert_close(f"heads_without_y/B{B}/v_vs_y_path", tv.cpu().numpy(), v.cpu().numpy(), 2e-6)
+    G = {"output_transform.0.weight": w0.numpy(), "output_transform.0.bias": b0.numpy(),
+         "output_transform.2.weight": w2.numpy(), "output_transform.2.bias": b2.numpy()}
+    W = {"fc_policy.weight": wp.numpy(), "fc_policy.bias": bp.numpy(),
+         "fc_value.weight": wv.numpy(), "fc_value.bias": bv.numpy()}
+    olp, ov = O.c4_heads(O.policy_value_gnn_per_row(x.numpy(), G), W)
+    assert_close(f"heads_without_y/B{B}/logp_vs_oracle", tl.cpu().numpy(), olp, 1e-5)
+    assert_close(f"heads_without_y/B{B}/pi_vs_oracle", tp.cpu().numpy(), np.exp(olp), 1e-5)
+    assert_close(f"heads_without_y/B{B}/v_vs_oracle", tv.cpu().numpy(), ov, 1e-5)
+
+
 @pytest.mark.parametrize("A,K", [(8, 3136), (9, 512), (7, 256), (20, 1000)])
 def test_heads_small_batch_bit_identical(ops, A, K):
     """B <= 32 runs the one-launch heads_rows_kernel; every row equals the two-launch path's

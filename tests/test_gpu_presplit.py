@@ -3,7 +3,8 @@ output_transform = gnn_utils.py:115): the trunk writing output_transform.0's A a
 GEMM's planes + row scales, and output_transform.0's split-K reduce writing output_transform.2's
 (ops.c4_gnn_eval, one az_c4_eval_fwd call), give the same bits as the unfused calls -- trunk,
 then each GEMM splitting its own A -- at every batch size (trunk NB 1..8, split-K and stream-K
-GEMMs), and the same bits with unregistered weights (no hand-off: the plain path)."""
+GEMMs), and the same bits with unregistered weights (no hand-off: the plain path).  The unfused
+calls ask for the heads without y too (linear_heads(want_y=False)), as the evaluator does."""
 import numpy as np
 import pytest
 import torch
@@ -27,7 +28,7 @@ def _unfused(ops, boards, Wn, Gn):
     logp, pi, v, _ = ops.linear_heads(h, Gn["output_transform.2.weight"],
                                       Gn["output_transform.2.bias"], Wn["fc_policy.weight"],
                                       Wn["fc_policy.bias"], Wn["fc_value.weight"],
-                                      Wn["fc_value.bias"])
+                                      Wn["fc_value.bias"], want_y=False)
     return feat, h, logp, pi, v
 
 
