@@ -382,11 +382,14 @@ __device__ __forceinline__ float add_share(float x, float b) {
   return x;
 }
 
-// The HEADS epilogue of a 64-row wave tile (gemm_p3 / gemm_x3 HEADS; az_x3.h HeadsEpi): per row,
-// the dot products of the wave's WN columns of the tile (+ the bias in k split 0) with the 8 policy
-// rows and the value row, in column order; the WGN waves sharing the rows are added in wave order
-// through LDS and the block's row results leave as part[row][nt * splits + sp][0..8].  Every
-// wave reaches the block barrier.  stage: the wave's [64][36] region; comb: [WGM][64][9] floats.
+// The HEADS epilogue of a 64-row wave tile (gemm_p3 / gemm_x3 / gemm_x3_csk HEADS; az_x3.h
+// HeadsEpi): per row, the dot products of the wave's WN columns of the tile (+ the bias in k split
+// / piece 0) with the 8 policy rows and the value row, in column order.
+//   split-K form (p.he.mp == 0): the WGN waves sharing the rows are added in wave order through
+//     LDS and the block's row results leave as part[row][nt * splits + sp][0..8] -- every wave
+//     reaches the block barrier; comb: [WGM][64][9] floats;
+//   stream-K form (p.he.mp > 0): each wave writes its own slot part[row][(c0 / 64) mp + sp].
+// stage: the wave's [64][36] region.
 template <int TI, int TJ, int WGM, int WGN>
 __device__ __forceinline__ void heads_tile_epilogue(const GemmArgs& p, f32x16 (&acc)[TI][TJ],
                                                     const HeadsRegs<TJ>& hr, int r0, int c0,
@@ -425,6 +428,16 @@ __device__ __forceinline__ void heads_tile_epilogue(const GemmArgs& p, f32x16 (&
         part[a] = fma_share<c & 15>(part[a], hr.w[cc][a][c >> 4], x[c >> 2][c & 3]);
     });
   }
+  const int row = r0 + lane;
+  if (p.he.mp > 0) {                         // stream-K: one slot per wave
+    if (row < p.M && c0 < p.N) {
+      const int P = (p.N >> 6) * p.he.mp;
+      float* dst = p.he.part + ((size_t)row * P + (c0 >> 6) * p.he.mp + sp) * HS;
+#pragma unroll
+      for (int a = 0; a < HS; ++a) dst[a] = part[a];
+    }
+    return;
+  }
   // the WGN waves of this row group: wave order, through LDS
   if (wn > 0) {
 #pragma unroll
@@ -435,7 +448,6 @@ __device__ __forceinline__ void heads_tile_epilogue(const GemmArgs& p, f32x16 (&
     for (int w = 1; w < WGN; ++w)
 #pragma unroll
       for (int a = 0; a < HS; ++a) part[a] += comb[((w - 1) * WGM + wm) * 64 * HS + lane * HS + a];
-    const int row = r0 + lane;
     if (row < p.M) {
       const int P = ((p.N + WGN * 64 - 1) / (WGN * 64)) * p.splits;
       float* dst = p.he.part + ((size_t)row * P + nt * p.splits + sp) * HS;
@@ -1430,7 +1442,7 @@ __device__ __forceinline__ void gemm_x3_body(const GemmArgs& p, char* smem, int 
       }
   }
   if constexpr (HEADS) {     // the same epilogue as gemm_p3's: the same bits for the same planes
-    static_assert(H3 && !FLEX && MF == 32 && WN == 64 && TI == 2, "heads epilogue: fp16 tiles");
+    static_assert(H3 && MF == 32 && WN == 64 && TI == 2, "heads epilogue: fp16 tiles");
     __syncthreads();         // the k loop's last LDS reads are done everywhere
     float* f = reinterpret_cast<float*>(smem);
     heads_tile_epilogue<TI, TJ, WGM, WGN>(p, acc, hregs, m0 + wm * WM, n0 + wn * WN, nt, sp, wm,
@@ -1625,9 +1637,10 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
 // P2: the fp16 form on pre-split planes (p.apl: A's two planes from h3_split_rows_kernel, p.bpl:
 // W's, cached per weight generation), every stage global -> LDS by LDS-DMA; same products in the
 // same order as the in-tile split, so the same bits.
-template <bool MASK, bool H3, bool P2 = false>
+template <bool MASK, bool H3, bool P2 = false, bool HEADS = false>
 __global__ __launch_bounds__(512) void gemm_x3_csk(GemmArgs p, CskPlan q) {
   static_assert(!P2 || (H3 && !MASK), "P2: the fp16 form on whole 32-k tiles");
+  static_assert(!HEADS || (H3 && !MASK), "HEADS: the fp16 form on whole 32-k tiles");
   __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<256, 128, 4, 2, 32, H3 ? 2 : 3>()];
   const int L = xcd_swizzle(blockIdx.x, q.B);
   int r, b, am, an, mt0, nt0, bma;
@@ -1665,15 +1678,16 @@ __global__ __launch_bounds__(512) void gemm_x3_csk(GemmArgs p, CskPlan q) {
       g.splits = 2;                       // a piece: raw partials into slab[piece]
       sp = r - csk_block_of(f * q.KT, b, W);
     }
+    // HEADS: every piece leaves its heads' dot products in slot (column block, piece sp)
     const int fn = f / am;
     int mt_i = mt0 + (f - fn * am), bma_i = bma;   // opaque per segment: keeps the body's
     asm volatile("" : "+s"(mt_i), "+s"(bma_i));    // address setup in the loop (hoisted, it spills)
     if constexpr (P2)
-      gemm_p3_body<256, 128, 4, 2, true, true>(g, smem, mt_i, nt0 + fn, sp, 32 * k0,
-                                               min(p.K, 32 * k1), bma_i);
+      gemm_p3_body<256, 128, 4, 2, true, true, 2, 0, HEADS>(g, smem, mt_i, nt0 + fn, sp, 32 * k0,
+                                                           min(p.K, 32 * k1), bma_i);
     else
-      gemm_x3_body<256, 128, 4, 2, MASK, 0, false, 32, true, H3>(g, smem, mt_i, nt0 + fn, sp,
-                                                                32 * k0, min(p.K, 32 * k1), bma_i);
+      gemm_x3_body<256, 128, 4, 2, MASK, 0, false, 32, true, H3, HEADS>(
+          g, smem, mt_i, nt0 + fn, sp, 32 * k0, min(p.K, 32 * k1), bma_i);
     i0 += k1 - k0;
     if (i0 < i1) __syncthreads();         // the next segment's prologue reuses the LDS
   }
@@ -2000,7 +2014,7 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
     return;
   }
   if constexpr (HEADS) {
-    static_assert(H3 && !FLEX && WN == 64 && TI == 2, "heads epilogue: the P2 split-K tiles");
+    static_assert(H3 && WN == 64 && TI == 2, "heads epilogue: the P2 tiles");
     float* f = reinterpret_cast<float*>(smem);
     heads_tile_epilogue<TI, TJ, WGM, WGN>(p, acc, hregs, m0 + wm * WM, n0 + wn * WN, nt, sp, wm,
                                           wn, f + wave * (WM * 36), f + NW * WM * 36);
@@ -3693,6 +3707,9 @@ struct WScaleEntry {
   float* pbuf[2];              // their row scales: a double buffer of its own, so a recompute
   int pcur;                    // of one kind never overwrites the other kind's live buffer
   long pgen;                   // generation planes[pcur] / pbuf[pcur] were split at
+  float* frags[2];             // conv2's weights in the trunk's MFMA fragment order (conv2_frags)
+  int fcur;
+  long fgen;
 };
 
 static std::mutex g_wmu;
@@ -3703,7 +3720,7 @@ static WScaleEntry* wcache_entry(const float* w, int n, int k, int ld) {
   for (auto& x : g_wcache)
     if (x.w == w && x.n == n && x.k == k && x.ld == ld) return &x;
   WScaleEntry x{w, n, k, ld, 0, {nullptr, nullptr}, 1, {nullptr, nullptr}, {nullptr, nullptr},
-                1, 0};
+                1, 0, {nullptr, nullptr}, 1, 0};
   if (hipMalloc(&x.buf[0], (size_t)8 * n * sizeof(float)) != hipSuccess) return nullptr;
   x.buf[1] = x.buf[0] + 2 * n;
   x.pbuf[0] = x.buf[0] + 4 * n;
@@ -3775,6 +3792,7 @@ extern "C" int az_weights_unregister(const void* base) {
       }
       (void)hipFree(az::g_wcache[i].buf[0]);
       if (az::g_wcache[i].planes[0]) (void)hipFree(az::g_wcache[i].planes[0]);
+      if (az::g_wcache[i].frags[0]) (void)hipFree(az::g_wcache[i].frags[0]);
       az::g_wcache.erase(az::g_wcache.begin() + i);
     }
   }
@@ -3828,6 +3846,154 @@ static const unsigned short* w_planes(const float* w, int n, int k, int ld, hipS
   e->pgen = gen;
   *scales = e->pbuf[nxt];
   return e->planes[nxt];
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xF, 0xF, false));
+}
+
+// The heads from a GEMM's tile partials (az_x3.h HeadsEpi; the GEMM added the bias b of y in its
+// first k split / piece): one wave per row sums the row's slots in a fixed order -- split-K form:
+// lane t takes slots t, t + 64, ... in turn; stream-K form (CSK): lane t takes 64-column block t
+// and its pieces in k order (their count from the plan, as csk_fixup4_kernel) -- then one
+// butterfly over the lanes for all 9 values at once, so the bits do not depend on the launch
+// shape; then the heads' biases and log_softmax / exp / tanh as heads_finalize_kernel.
+template <bool CSK>
+__global__ __launch_bounds__(256) void heads_tiles_finalize_kernel(HeadsEpi he, int M, int N,
+                                                                   int P, CskPlan q) {
+  constexpr int HS = HEADS_TILE_SLOTS;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* src = he.part + (size_t)row * P * HS;
+  float s[16];
+#pragma unroll
+  for (int a = 0; a < 16; ++a) s[a] = 0.f;
+  if constexpr (CSK) {
+    const int cb = lane, col = 64 * cb;
+    if (col < N) {
+      const int mt = row >> 8;
+      int f, b, W;
+      if (q.tail && mt == q.mt_n - 1) {
+        f = (col >> 8) % q.at;
+        b = q.bt;
+        W = q.at * q.KT;
+      } else {
+        f = mt % q.am + q.am * ((col >> 7) % q.an);
+        b = q.bf;
+        W = q.am * q.an * q.KT;
+      }
+      const int np = csk_block_of((f + 1) * q.KT - 1, b, W) - csk_block_of(f * q.KT, b, W) + 1;
+      // every piece's loads issued before the first add (pieces in k order; <= 8 of them in
+      // the plans csk_plan makes -- a longer tail, if any, is summed after, in order)
+      float v[8][HS];
+#pragma unroll
+      for (int pc = 0; pc < 8; ++pc)
+#pragma unroll
+        for (int a = 0; a < HS; ++a)
+          v[pc][a] = pc < np ? src[(size_t)(cb * he.mp + pc) * HS + a] : 0.f;
+#pragma unroll
+      for (int pc = 0; pc < 8; ++pc)
+#pragma unroll
+        for (int a = 0; a < HS; ++a)
+          if (pc < np) s[a] += v[pc][a];
+      for (int pc = 8; pc < np; ++pc)
+#pragma unroll
+        for (int a = 0; a < HS; ++a) s[a] += src[(size_t)(cb * he.mp + pc) * HS + a];
+    }
+  } else {
+    for (int t = lane; t < P; t += 64)
+#pragma unroll
+      for (int a = 0; a < HS; ++a) s[a] += src[(size_t)t * HS + a];
+  }
+  // the lane sums: DPP adds within each 16-lane row (quad_perm [1,0,3,2], [2,3,0,1],
+  // row_half_mirror, row_mirror: no LDS), then the four row sums in row order (readlane)
+#pragma unroll
+  for (int a = 0; a < HS; ++a) {
+    float v = s[a];
+    v += dpp_mov<0xB1>(v);
+    v += dpp_mov<0x4E>(v);
+    v += dpp_mov<0x141>(v);
+    v += dpp_mov<0x140>(v);
+    s[a] = (__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0)) +
+            __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16)) +
+            __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32)) +
+            __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48)));
+  }
+  if (lane != 0) return;
+  const int A = he.A;
+  float l[8];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+    if (a < A) {
+      l[a] = s[a] + he.bp[a];
+      mx = fmaxf(mx, l[a]);
+    }
+  float se = 0.f;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+    if (a < A) se += expf(l[a] - mx);
+  const float lse = logf(se);
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+    if (a < A) {
+      const float o = (l[a] - mx) - lse;
+      he.logp[(size_t)row * A + a] = o;
+      if (he.pi) he.pi[(size_t)row * A + a] = expf(o);
+    }
+  he.v[row] = tanhf(s[8] + he.bv[0]);
+}
+
+// The Connect4 trunk's conv2 weights ([64][32][3][3]) in the order its MFMA fragments use them
+// (az_trunk.hip c4_trunk_tile): frag[nt][q][lane][e] = w2[co][ci][tap] for step s = 4q + e
+// = tap * 8 + j, co = 16 nt + (lane & 15), ci = 8 (lane >> 4) + j.  A wave then loads its 72
+// weights as 18 coalesced 1-KB float4 loads instead of staging the 74 KB through LDS.
+__global__ __launch_bounds__(256) void c4_w2_frag_kernel(const float* __restrict__ w2,
+                                                         float* __restrict__ frag) {
+  const int i = blockIdx.x * 256 + threadIdx.x;       // 4 * 18 * 64 * 4 = 18,432 values
+  if (i >= 18432) return;
+  const int e = i & 3, lane = (i >> 2) & 63, q = (i >> 8) % 18, nt = i / (18 * 256);
+  const int st = 4 * q + e, tap = st >> 3, j = st & 7;
+  const int co = 16 * nt + (lane & 15), ci = 8 * (lane >> 4) + j;
+  frag[i] = w2[co * 288 + ci * 9 + tap];
+}
+
+// conv2_frags: the fragment-ordered copy of registered conv2 weights, cached per weight
+// generation like w_planes (double buffer, the recompute synchronises its stream before
+// publishing); nullptr for unregistered weights or when memory is short (the trunk then stages
+// the weights through LDS itself: the same values, the same bits).
+const float* conv2_frags(const float* w2, hipStream_t s) {
+  if (!weights_registered(w2, 64, 288, 288)) return nullptr;
+  const long gen = g_wgen.load();
+  std::lock_guard<std::mutex> lk(g_wmu);
+  WScaleEntry* e = wcache_entry(w2, 64, 288, 288);
+  if (!e) return nullptr;
+  if (!e->frags[0]) {
+    if (hipMalloc(&e->frags[0], (size_t)2 * 18432 * sizeof(float)) != hipSuccess) {
+      e->frags[0] = nullptr;
+      return nullptr;
+    }
+    e->frags[1] = e->frags[0] + 18432;
+    e->fgen = 0;
+  }
+  if (e->fgen == gen) return e->frags[e->fcur];
+  const int nxt = e->fcur ^ 1;
+  hipLaunchKernelGGL(c4_w2_frag_kernel, dim3(72), dim3(256), 0, s, w2, e->frags[nxt]);
+  if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+  e->fcur = nxt;
+  e->fgen = gen;
+  return e->frags[nxt];
+}
+
+// the split-K HEADS tiles' finalize (P = 128-column tiles x k splits)
+static void launch_heads_finalize(GemmArgs& a, hipStream_t s) {
+  const int P = (a.N + 127) / 128 * a.splits;
+  hipLaunchKernelGGL(heads_tiles_finalize_kernel<false>, dim3((a.M + 3) / 4), dim3(256), 0, s,
+                     a.he, a.M, a.N, P, CskPlan{});
+  a.heads_done = 1;
 }
 
 // gemm_x3 launch for a K-major A and W (no A2 / gathered rows), M > 64: 256x128 (8 waves) above
@@ -3964,7 +4130,23 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
 #else
       ok = csk_plan(a.M, a.N, a.K, cus, CSK_MISS_COST, cq);
 #endif
-      if (use_csk && ok && (size_t)csk_max_pieces(cq) * a.M * a.N * 4 <= ws_bytes) {
+      const int mp = use_csk && ok ? csk_max_pieces(cq) : 0;
+      if (use_csk && ok && a.he.part && whole && (p2 || h3) &&
+          (size_t)a.M * (a.N / 64) * mp * HEADS_TILE_SLOTS * 4 * 2 <= ws_bytes) {
+        // the heads from the pieces (az_x3.h HeadsEpi, stream-K slots): no fix-up, no C
+        if (p2) p2 = p2_prep();
+        if (!p2) h3 = h3_scales();
+        a.he.mp = mp;
+        if (p2) hipLaunchKernelGGL((gemm_x3_csk<false, true, true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        else hipLaunchKernelGGL((gemm_x3_csk<false, true, false, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        const int P = (a.N / 64) * mp;
+        hipLaunchKernelGGL(heads_tiles_finalize_kernel<true>, dim3((a.M + 3) / 4), dim3(256), 0, s,
+                           a.he, a.M, a.N, P, cq);
+        a.splits = 1;
+        a.heads_done = 1;
+        return true;
+      }
+      if (use_csk && ok && mp * (size_t)a.M * a.N * 4 <= ws_bytes) {
         if (p2) p2 = p2_prep();
         if (!p2 && h3) h3 = h3_scales();
         if (p2) hipLaunchKernelGGL((gemm_x3_csk<false, true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
@@ -4136,12 +4318,12 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
       hipLaunchKernelGGL((gemm_p3<256, 256, 4, 2, true>), gw, dim3(512), 0, s, a);
     }
 #endif
-    else if (a.he.part && tile == 1) {
-      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 0, true>), grid, dim3(512), 0, s, a);
-      a.heads_done = 1;
-    } else if (a.he.part) {
-      hipLaunchKernelGGL((gemm_p3<128, 128, 2, 2, true, 2, 0, true>), grid, dim3(256), 0, s, a);
-      a.heads_done = 1;
+    else if (a.he.part) {
+      if (tile == 1)
+        hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 0, true>), grid, dim3(512), 0, s, a);
+      else
+        hipLaunchKernelGGL((gemm_p3<128, 128, 2, 2, true, 2, 0, true>), grid, dim3(256), 0, s, a);
+      launch_heads_finalize(a, s);
     }
     else if (tile == 1) hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true>), grid, dim3(512), 0, s, a);
     else hipLaunchKernelGGL((gemm_p3<128, 128, 2, 2, true>), grid, dim3(256), 0, s, a);
@@ -4155,7 +4337,7 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
       else
         hipLaunchKernelGGL((gemm_x3<128, 128, 2, 2, false, 0, false, 32, true, true>), grid,
                            dim3(256), 0, s, a);
-      a.heads_done = 1;
+      launch_heads_finalize(a, s);
       return true;
     }
     if (tile == 1) { AZ_H3(256, 128, 4, 2) }

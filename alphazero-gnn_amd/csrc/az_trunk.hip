@@ -37,6 +37,10 @@ constexpr int trunk_union_floats() {
 // apl / asc (NB <= 4 only; may be null): the feature rows also leave as the P2 GEMM's A operand
 // for output_transform.0 (PreSplitA: two fp16 planes [2][B][3136] and scales [2][B], the bits
 // h3_split_rows_kernel would make of feat), so that GEMM needs no split launch of its own.
+// w2f (may be null): conv2's weights already in fragment order (az_gemm.hip conv2_frags, cached
+// per weight generation): each lane loads its 72 weights as 18 coalesced float4 loads, issued
+// first, and the LDS staging of w2 (its bank-conflicted scalar stores and reads, a barrier) is
+// skipped; the registers hold the same values, so the bits are the same.
 template <int NB>
 __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards, int B,
                                               const float* __restrict__ w1,
@@ -45,7 +49,8 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
                                               const float* __restrict__ b2,
                                               float* __restrict__ feat, float* un,
                                               unsigned short* __restrict__ apl = nullptr,
-                                              float* __restrict__ asc = nullptr) {
+                                              float* __restrict__ asc = nullptr,
+                                              const float* __restrict__ w2f = nullptr) {
   float* const ob = un;
   constexpr int P = 49, PP = 81, CI = 32;
   constexpr int ROWS = NB * P;
@@ -70,11 +75,22 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   // Every global load of the prologue is issued before the first one is waited for (conv2's
   // 9 float4 per thread, the boards, conv1's weights, the bias), then the LDS stores: as a
   // load -> store loop each iteration waited for its own round trip (11 in a row).
-  // conv2's weights -> LDS (row co = 288 floats = 72 float4, so no float4 crosses a row)
+  // conv2's weights -> LDS (row co = 288 floats = 72 float4, so no float4 crosses a row), or
+  // straight into the fragment registers from the fragment-ordered copy
   constexpr int NW2 = 64 * 72 / 512;
   f32x4v wst[NW2];
+  float breg[72];   // step s = tap * 8 + j takes channel ci = 8h + j of tap (lane group h)
+  if (w2f) {
 #pragma unroll
-  for (int j = 0; j < NW2; ++j) wst[j] = reinterpret_cast<const f32x4v*>(w2)[tid + 512 * j];
+    for (int q = 0; q < 18; ++q) {
+      const f32x4v v = reinterpret_cast<const f32x4v*>(w2f)[(nt * 18 + q) * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) breg[4 * q + e] = v[e];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NW2; ++j) wst[j] = reinterpret_cast<const f32x4v*>(w2)[tid + 512 * j];
+  }
   constexpr int NBD = (NB * PP + 511) / 512;
   int8_t bdv[NBD];
   bool bdin[NBD];
@@ -88,22 +104,25 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   const float w1v = tid < CI * 9 ? w1[tid] : b1[min(tid - CI * 9, CI - 1)];
   const float bias = b2[co];
   __builtin_amdgcn_sched_barrier(0);   // no load sinks into the guarded stores below
+  if (!w2f) {
 #pragma unroll
-  for (int j = 0; j < NW2; ++j) {
-    const int i = tid + 512 * j;
-    float* d = un + (i / 72) * W2S_STRIDE + (i % 72) * 4;
-    d[0] = wst[j][0]; d[1] = wst[j][1]; d[2] = wst[j][2]; d[3] = wst[j][3];
+    for (int j = 0; j < NW2; ++j) {
+      const int i = tid + 512 * j;
+      float* d = un + (i / 72) * W2S_STRIDE + (i % 72) * 4;
+      d[0] = wst[j][0]; d[1] = wst[j][1]; d[2] = wst[j][2]; d[3] = wst[j][3];
+    }
   }
 #pragma unroll
   for (int j = 0; j < NBD; ++j)   // unguarded (past-the-end lanes hit bd's pad slot): a guarded
     bd[min(tid + 512 * j, NB * PP)] = bdin[j] ? (float)bdv[j] : 0.f;   // use sinks the load
   w1s[min(tid, CI * 9 + CI)] = w1v;     // unguarded: lanes past the 320 weights hit the pad
   __syncthreads();
-  float breg[72];   // step s = tap * 8 + j takes channel ci = 8h + j of tap (lane group h)
+  if (!w2f) {
 #pragma unroll
-  for (int s = 0; s < 72; ++s) {
-    const int tap = s >> 3, ci = 8 * h + (s & 7);
-    breg[s] = un[co * W2S_STRIDE + ci * 9 + (tap / 3) * 3 + (tap % 3)];
+    for (int s = 0; s < 72; ++s) {
+      const int tap = s >> 3, ci = 8 * h + (s & 7);
+      breg[s] = un[co * W2S_STRIDE + ci * 9 + (tap / 3) * 3 + (tap % 3)];
+    }
   }
   if constexpr (!STAGE) __syncthreads();   // conv1's output overwrites the weights in `un`
   for (int i = tid; i < NB * PP * CI; i += 512) {
@@ -230,9 +249,10 @@ __global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict_
                                                       const float* __restrict__ b1,
                                                       const float* __restrict__ w2,
                                                       const float* __restrict__ b2,
-                                                      float* __restrict__ feat) {
+                                                      float* __restrict__ feat,
+                                                      const float* __restrict__ w2f = nullptr) {
   __shared__ __attribute__((aligned(16))) float un[trunk_union_floats<NB>()];
-  c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, un);
+  c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, un, nullptr, nullptr, w2f);
 }
 
 // c4_trunk_kernel that also writes feat's rows as output_transform.0's pre-split A (NB <= 4)
@@ -240,10 +260,11 @@ template <int NB>
 __global__ __launch_bounds__(512) void c4_trunk_split_a_kernel(
     const int8_t* __restrict__ boards, int B, const float* __restrict__ w1,
     const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
-    float* __restrict__ feat, unsigned short* __restrict__ apl, float* __restrict__ asc) {
+    float* __restrict__ feat, unsigned short* __restrict__ apl, float* __restrict__ asc,
+    const float* __restrict__ w2f = nullptr) {
   static_assert(NB <= 4, "the A split reads the LDS staging tile");
   __shared__ __attribute__((aligned(16))) float un[trunk_union_floats<NB>()];
-  c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, un, apl, asc);
+  c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, un, apl, asc, w2f);
 }
 
 // Generic 3x3 conv + ReLU, one thread per output (TicTacToe trunks: tiny, latency-bound).
@@ -469,51 +490,6 @@ __global__ __launch_bounds__(256) void heads_finalize_kernel(const float* __rest
       if (pi) pi[(size_t)row * A + a] = expf(o);
     }
   v[row] = tanhf(sm[r][A] + bv[0]);
-}
-
-// The heads from a P2 GEMM's tile partials (az_x3.h HeadsEpi; the GEMM added the bias b of y in
-// its first k split): one wave per row sums the P partials of every slot in tile order (lane t
-// takes t, t + 64, ... in turn, then a fixed butterfly, so the bits do not depend on the launch
-// shape), adds the heads' biases and applies log_softmax / exp / tanh as heads_finalize_kernel.
-__global__ __launch_bounds__(256) void heads_tiles_finalize_kernel(
-    const float* __restrict__ part, int P, int B, int A, const float* __restrict__ bp,
-    const float* __restrict__ bv, float* __restrict__ logp, float* __restrict__ pi,
-    float* __restrict__ v) {
-  constexpr int HS = HEADS_TILE_SLOTS;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= B) return;
-  const float* src = part + (size_t)row * P * HS;
-  float s[HS];
-#pragma unroll
-  for (int a = 0; a < HS; ++a) s[a] = 0.f;
-  for (int t = lane; t < P; t += 64)
-#pragma unroll
-    for (int a = 0; a < HS; ++a) s[a] += src[(size_t)t * HS + a];
-#pragma unroll
-  for (int a = 0; a < HS; ++a) s[a] = wave_sum(s[a]);
-  if (lane != 0) return;
-  float l[8];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-    if (a < A) {
-      l[a] = s[a] + bp[a];
-      mx = fmaxf(mx, l[a]);
-    }
-  float se = 0.f;
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-    if (a < A) se += expf(l[a] - mx);
-  const float lse = logf(se);
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-    if (a < A) {
-      const float o = (l[a] - mx) - lse;
-      logp[(size_t)row * A + a] = o;
-      if (pi) pi[(size_t)row * A + a] = expf(o);
-    }
-  v[row] = tanhf(s[8] + bv[0]);
 }
 
 // Small batches (B <= HEADS_ROWS_MAXB, the batch-1 MCTS leaf): both passes in ONE launch, one
@@ -763,6 +739,8 @@ __global__ __launch_bounds__(512) void c4_trunk_heads_kernel(
 using namespace az;
 
 namespace az {
+const float* conv2_frags(const float* w2, hipStream_t s);   // az_gemm.hip
+
 // The Connect4 trunk launch (az_c4_trunk_fwd); apl / asc non-null: when the chosen NB stages its
 // output in LDS (NB <= 4: B <= 1,024 on 256 CUs) the rows also leave as output_transform.0's
 // pre-split A (c4_trunk_split_a_kernel) and *split is set; otherwise *split stays false.
@@ -796,27 +774,31 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
   if (env) nbk = atoi(env);
   const bool sa = apl && asc && nbk >= 1 && nbk <= 4;
   if (split) *split = sa;
+  // conv2's weights in fragment order when they are registered (cached per weight generation)
+  static const bool no_frag = tuning_env("AZ_TRUNK_NO_W2F") != nullptr;   // A/B experiments
+  const float* w2f = nbk >= 1 && !no_frag ? conv2_frags(conv2_w, s) : nullptr;
 #define AZ_TRUNK(NB_)                                                                            \
   if (sa) hipLaunchKernelGGL(c4_trunk_split_a_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), \
-                             0, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, apl, asc); \
+                             0, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, apl, asc, \
+                             w2f);                                                               \
   else hipLaunchKernelGGL(c4_trunk_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), 0, s,       \
-                          boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat);
+                          boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
   switch (nbk) {
     case 8:
       hipLaunchKernelGGL(c4_trunk_kernel<8>, dim3((B + 7) / 8), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
       break;
     case 7:
       hipLaunchKernelGGL(c4_trunk_kernel<7>, dim3((B + 6) / 7), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
       break;
     case 6:
       hipLaunchKernelGGL(c4_trunk_kernel<6>, dim3((B + 5) / 6), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
       break;
     case 5:
       hipLaunchKernelGGL(c4_trunk_kernel<5>, dim3((B + 4) / 5), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat);
+                         conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
       break;
     case 4: AZ_TRUNK(4) break;
     case 3: AZ_TRUNK(3) break;
@@ -875,6 +857,7 @@ int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s);
 int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* planes, float* sc,
                         hipStream_t s);
 bool gemm_p2_weights(const float* w, int n, int k, int ld);
+const float* conv2_frags(const float* w2, hipStream_t s);
 
 static size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
@@ -1084,17 +1067,13 @@ static int linear_heads_impl(const float* x, int B, int F, const float* w, const
   int S = 1;
   // the tile partials [B][P][9] (P <= ceil(F / 128) * 8) at the start of the slab region
   const size_t tiles_bytes = (size_t)B * ((F + 127) / 128) * 8 * HEADS_TILE_SLOTS * 4;
-  const HeadsEpi he{wp, wv, A, static_cast<float*>(slabs)};
+  // (the stream-K form's slots: 49 column blocks x its max pieces, <= 8 for these shapes)
+  const HeadsEpi he{wp, wv, A, static_cast<float*>(slabs), 0, bp, bv, logp, pi, v};
   bool heads_done = false;
   static const bool no_tiles = tuning_env("AZ_NO_HEADS_TILES") != nullptr;   // A/B experiments
   const bool try_tiles = !want_y && !no_tiles && A <= 8 && 2 * tiles_bytes <= d.ws_bytes;
   if ((rc = gemm_f32_partial(&d, s, &S, pre, try_tiles ? &he : nullptr, &heads_done))) return rc;
-  if (heads_done) {
-    const int P = (F + 127) / 128 * S;
-    hipLaunchKernelGGL(heads_tiles_finalize_kernel, dim3((B + 3) / 4), dim3(256), 0, s, he.part,
-                       P, B, A, bp, bv, logp, pi, v);
-    return check_launch("heads_tiles_finalize_kernel");
-  }
+  if (heads_done) return AZ_OK;   // the GEMM's dispatch also ran the heads' finalize
   const float* sl = static_cast<const float*>(slabs);
   // one launch: splitk_heads_rowsw_kernel (AZ_SPLITK_HEADS_MODE = rows / chunks select the
   // one-row-per-block kernel / chunk partials + finalize for A/B runs)

@@ -153,12 +153,21 @@ struct PreSplitA {
 // policy row a, slot 8 the value row.  heads_tiles_finalize_kernel sums the t in order, adds the
 // heads' biases and runs log_softmax / exp / tanh.  y is never written: 12.8 MB less traffic per
 // B = 512 call than the split-K slabs and the heads pass that re-read them.
+// The stream-K form (gemm_x3_csk) writes one slot per wave instead: t = (64-column block) x
+// max_pieces + piece, and its finalize reads each tile's piece count from the plan.
 constexpr int HEADS_TILE_SLOTS = 9;
 struct HeadsEpi {
   const float* wp;   // fc_policy.weight [A][N]
   const float* wv;   // fc_value.weight [N]
   int A;             // <= 8
-  float* part;       // [M][P][HEADS_TILE_SLOTS], P = n tiles x k splits
+  float* part;       // [M][P][HEADS_TILE_SLOTS]
+  int mp;            // stream-K: slots per 64-column block (max pieces); 0: split-K form
+  // the finalize's operands (launched by the GEMM's dispatch, which knows P)
+  const float* bp;   // fc_policy.bias [A]
+  const float* bv;   // fc_value.bias [1]
+  float* logp;       // [M][A]
+  float* pi;         // [M][A] (may be null)
+  float* v;          // [M]
 };
 
 }  // namespace az
