@@ -232,12 +232,24 @@ __device__ __forceinline__ int acc_row(int r, int lane) {
 }
 
 // ring row `slot`, plane pl, 16-B chunk c (8 features) -> fp16 offset; the row's 16 chunk
-// positions (both planes) are XOR-swizzled by slot & 15, so the 16 rows a 16-lane group of an
-// MFMA fragment read touches (one plane, one chunk) land on 16 distinct 16-B bank positions of
-// the 256-B row stride
-__device__ __forceinline__ int xr_off(int slot, int pl, int c) {
-  return slot * XRS + ((((pl << 3) | c) ^ (slot & 15)) << 3);
+// positions (both planes) are XOR-swizzled by the low 4 bits of slot with its bit pairs swapped
+// (s1 s0 s3 s2), a bijection of slot mod 16:
+//  * the 16 rows a 16-lane group of an MFMA fragment read touches (one plane, one chunk) land on
+//    16 distinct 16-B bank positions of the 256-B row stride;
+//  * the edge phase's source reads -- 4 destinations per 16-lane group, each reading 4 chunks of
+//    its source, the sources of consecutive destinations in consecutive slots -- are conflict-free
+//    too once each destination's lanes take their chunks in the order ej ^ x_chunk_flip(ei) (the
+//    plain slot & 15 swizzle put two destinations of a group on the same 4 positions: 2-way
+//    conflicts on every x read, 4.2e6 of the layer's 4.7e6 conflict cycles per launch, PMC r05i)
+__device__ __forceinline__ int xr_swz(int slot) {
+  return ((slot & 3) << 2) | ((slot >> 2) & 3);
 }
+__device__ __forceinline__ int xr_off(int slot, int pl, int c) {
+  return slot * XRS + ((((pl << 3) | c) ^ xr_swz(slot)) << 3);
+}
+// the chunk order of destination ei's 8 lanes in the edge phase (searched with the swizzle above:
+// flip the chunk's bit 2 for destinations 1 and 2 of every 4)
+__device__ __forceinline__ int x_chunk_flip(int ei) { return ((ei + 1) & 2) << 1; }
 
 // the accumulator rows of register r relative to the lane's first (acc_row(r, lane) - acc_row(0,
 // lane)), and an opaque copy of a lane's base offset: the per-register stores then use base +
@@ -558,12 +570,15 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
           }
           return sigmoid_fast(sum8(acc) + b2);
         };
+        // this lane's feature chunk of the aggregation (ej in a destination-dependent order, so
+        // the x reads of a 16-lane group hit 16 distinct bank positions: xr_off)
+        const int ec = ej ^ x_chunk_flip(ei);
         auto x_of = [&](int s, f32x4 (&v)[2]) {
           if (FAST || (unsigned)(s - lo) < (unsigned)RING) {
-            x_ring(s & (RING - 1), ej, v);
+            x_ring(s & (RING - 1), ec, v);
           } else {
-            v[0] = *reinterpret_cast<const f32x4*>(x + (size_t)s * BF + 8 * ej);
-            v[1] = *reinterpret_cast<const f32x4*>(x + (size_t)s * BF + 8 * ej + 4);
+            v[0] = *reinterpret_cast<const f32x4*>(x + (size_t)s * BF + 8 * ec);
+            v[1] = *reinterpret_cast<const f32x4*>(x + (size_t)s * BF + 8 * ec + 4);
           }
         };
         int src[4];
@@ -633,7 +648,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
           for (int q = 0; q < 4; ++q) {
 #pragma unroll
             for (int pl = 0; pl < 2; ++pl)
-              xp[q][pl] = *reinterpret_cast<const u32x4*>(XR + xr_off(src[q] & (RING - 1), pl, ej));
+              xp[q][pl] = *reinterpret_cast<const u32x4*>(XR + xr_off(src[q] & (RING - 1), pl, ec));
             xi[q] = XSI[src[q] & (RING - 1)];
           }
 #pragma unroll
@@ -676,14 +691,14 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
         }
         // the group's 8 lanes read their Pt row above (same wave, in order): the row now takes
         // agg's two fp16 planes (scaled by the row's power of two), plane pl at byte 128 pl,
-        // 16-B chunk ej
+        // 16-B chunk ec
         float ainv;
         const float asc = h3_scale(max8(absmax8(g)), 14, &ainv);
         u32x4 o[2];
         split2s(g[0], g[1], asc, o);
         unsigned short* arow = reinterpret_cast<unsigned short*>(PT + ei * PSS);
 #pragma unroll
-        for (int pl = 0; pl < 2; ++pl) *reinterpret_cast<u32x4*>(arow + pl * BF + 8 * ej) = o[pl];
+        for (int pl = 0; pl < 2; ++pl) *reinterpret_cast<u32x4*>(arow + pl * BF + 8 * ec) = o[pl];
         if (ej == 0) AGSI[ei] = ainv;
       };
       bool ok = deg <= 4 && ne <= BNT;
