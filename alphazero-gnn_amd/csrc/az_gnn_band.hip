@@ -251,6 +251,25 @@ __device__ __forceinline__ int xr_off(int slot, int pl, int c) {
 // flip the chunk's bit 2 for destinations 1 and 2 of every 4)
 __device__ __forceinline__ int x_chunk_flip(int ei) { return ((ei + 1) & 2) << 1; }
 
+// The edge phase's Pt / Ps / w2 reads (16-B chunks of 128 hidden units, 4 per lane, 16-lane
+// read groups of 4 destinations x 4 lanes).  Ps rows (stride 128 floats) put chunk h on bank
+// position h mod 16, Pt rows (stride PSS = 33 chunks) on (row + h) mod 16.  With the Pt of
+// destination i in row i, no assignment of chunks to lanes is conflict-free for both (the 16
+// positions of a group sum to 8 mod 16 in Ps, to 8 + 4 (4 e + 6) = 0 mod 16 in Pt for rows e ..
+// e + 3).  So phase A stores destination i's Pt in row pt_row(i) (i's low 3 bits (b2 b1 b0) ->
+// (b1 b0 b2): the group's 4 rows are 0, 2, 4, 6 apart), and lane (i, j) takes at step c the
+// chunk h_chunk: the 4 destinations of a group use 4 different residues mod 4 at every step
+// ((i + c) & 3; shifted by 2 (i & 3) in Pt still 4 different ones) and their lanes the 4
+// multiples of 4 -- conflict-free in both (a row's agg planes go to row i: every Pt row of the
+// wave is read before any agg write, so the permutation stays inside the wave's 8 rows).
+__device__ __forceinline__ int pt_row(int i) { return (i & ~7) | ((i & 3) << 1) | ((i >> 2) & 1); }
+__device__ __forceinline__ int h_chunk(int ei, int ej, int c) { return ((ei + c) & 3) + 4 * ej; }
+// the row passes (split_pass, the residual, the y copy-out: 8 threads per row, 2 float4 reads
+// each at PT stride 33 chunks): thread c of row i takes 8-float group row_chunk(i, c), rotated
+// by one for rows 2, 3 (mod 4) -- plain c put rows i and i + 2 of a 16-lane group on the same
+// bank positions (2-way conflicts on every read)
+__device__ __forceinline__ int row_chunk(int i, int c) { return (c - ((i >> 1) & 1)) & 7; }
+
 // the accumulator rows of register r relative to the lane's first (acc_row(r, lane) - acc_row(0,
 // lane)), and an opaque copy of a lane's base offset: the per-register stores then use base +
 // constant (the DS immediate offset) instead of 16 loop-invariant addresses hoisted out of the
@@ -376,7 +395,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
   // their own precision.  Thread = (row tid >> 3, chunk tid & 7): a row's 8 threads sit in one
   // wave and read their chunks before any of them writes (the row maximum needs all of them).
   auto split_pass = [&](int col0) {
-    const int i = tid >> 3, c = tid & 7;
+    const int i = tid >> 3, c = row_chunk(i, tid & 7);
     float* const rowp = PT + i * PSS + col0;
     f32x4 v[2];
     v[0] = *reinterpret_cast<const f32x4*>(rowp + 8 * c);
@@ -501,7 +520,8 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = 32 * mb + acc_row(r, lane);
-          PT[row * PSS + 32 * wave + lr] = acc[mb][r] * (XSI[(d0 + row) & (RING - 1)] * wi) + b1n;
+          const int prow = 32 * mb + 8 * (r >> 2) + ((r & 3) << 1) + hc;   // pt_row(row)
+          PT[prow * PSS + 32 * wave + lr] = acc[mb][r] * (XSI[(d0 + row) & (RING - 1)] * wi) + b1n;
         }
     }
     BSTAMP(1);
@@ -529,25 +549,28 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
       // its destination registers with the LDS path and makes the compiler wait vmcnt there too)
       auto edges = [&](auto col_of, auto fast) {
         constexpr bool FAST = decltype(fast)::value;
-        // lane: hidden units 4 ej + 32 cc (+0..3), cc = c ^ (ei & 1) -- the two destinations
-        // of a 16-lane LDS read group read opposite 128-B halves of their rows
-        const int par = ei & 1;
+        // lane: hidden units 4 h_chunk(ei, ej, c) (+0..3), c = 0..3 (conflict-free with Pt in
+        // row pt_row(ei): see h_chunk)
+        int hk[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) hk[c] = 4 * h_chunk(ei, ej, c);
+        const float* const ptrow = PT + pt_row(ei) * PSS;
         f32x4 pt[4], ww[4];                 // Pt + b1, w2
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          pt[c] = *reinterpret_cast<const f32x4*>(PT + ei * PSS + 4 * ej + 32 * (c ^ par));
-          ww[c] = *reinterpret_cast<const f32x4*>(B1W2 + BH + 4 * ej + 32 * (c ^ par));
+          pt[c] = *reinterpret_cast<const f32x4*>(ptrow + hk[c]);
+          ww[c] = *reinterpret_cast<const f32x4*>(B1W2 + BH + hk[c]);
         }
         auto alpha_of = [&](int s) {
           float acc = 0.f;
           if (FAST || (unsigned)(s - lo) < (unsigned)RING) {
             // two interleaved partial sums (even / odd hidden unit): the adds and FMAs go out
             // as packed v_pk_add_f32 / v_pk_fma_f32, half the instructions of the scalar chain
-            const float* ps = PSR + (s & (RING - 1)) * PSRS + 4 * ej;
+            const float* ps = PSR + (s & (RING - 1)) * PSRS;
             f32x2 acc2 = {0.f, 0.f};
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-              const f32x4 p = *reinterpret_cast<const f32x4*>(ps + 32 * (c ^ par));
+              const f32x4 p = *reinterpret_cast<const f32x4*>(ps + hk[c]);
 #pragma unroll
               for (int u = 0; u < 4; u += 2) {
                 f32x2 t = f32x2{pt[c][u], pt[c][u + 1]} + f32x2{p[u], p[u + 1]};
@@ -560,12 +583,12 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
             const float* xs = x + (size_t)s * BF;
 #pragma unroll 1
             for (int q = 0; q < 16; ++q) {
-              const int c = q >> 2, u = q & 3, h = 4 * ej + 32 * (c ^ par) + u;
+              const int u = q & 3, h = 4 * h_chunk(ei, ej, q >> 2) + u;
               const float* wr = W.w1 + (size_t)h * (2 * BF) + BF;
               float p = 0.f;
 #pragma unroll 4
               for (int k = 0; k < BF; ++k) p = fmaf(wr[k], xs[k], p);
-              acc = fmaf(relu(PT[ei * PSS + h] + p), B1W2[BH + h], acc);
+              acc = fmaf(relu(ptrow[h] + p), B1W2[BH + h], acc);
             }
           }
           return sigmoid_fast(sum8(acc) + b2);
@@ -597,7 +620,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
 #pragma unroll
             for (int c = 0; c < 4; ++c)
               p[q][c] = *reinterpret_cast<const f32x4*>(PSR + (src[q] & (RING - 1)) * PSRS +
-                                                        4 * ej + 32 * (c ^ par));
+                                                        hk[c]);
           float z[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -794,7 +817,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     //      waves 4-7 compute the next tile's Ps rows into the ring's dead slots.
     // the residual's x rows, requested now (L2: they entered the ring a tile ago) and used after
     // the u2 barrier: x_out is x + gate * u2 with x itself, not its fp16 planes
-    const int ri = tid >> 3, rc = tid & 7;     // row, features 8 rc .. 8 rc + 7
+    const int ri = tid >> 3, rc = row_chunk(ri, tid & 7);   // row, features 8 rc .. 8 rc + 7
     f32x4 xres[2];
     {
       const size_t xo = (size_t)min(d0 + ri, V - 1) * BF + 8 * rc;
@@ -902,7 +925,7 @@ __global__ __launch_bounds__(BNT, 1) void gnn_layer_band_kernel(
     }
     if constexpr (OT) __syncthreads();    // F's y rows in PT complete
     if constexpr (OT) {                   // y leaves row by row, two float4 per thread
-      const int i = tid >> 3, c = tid & 7, d = d0 + i;
+      const int i = tid >> 3, c = row_chunk(i, tid & 7), d = d0 + i;
       if (d < V) {
         const float* src = PT + i * PSS + 8 * c;
         *reinterpret_cast<f32x4*>(x_out + (size_t)d * BF + 8 * c) = *reinterpret_cast<const f32x4*>(src);
