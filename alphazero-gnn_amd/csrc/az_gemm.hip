@@ -18,6 +18,7 @@
 #include <mutex>
 #include <type_traits>
 #include <utility>
+#include <unordered_map>
 #include <vector>
 
 #include "az_common.h"
@@ -1824,6 +1825,43 @@ static bool csk_plan(int M, int N, int K, int cus, double miss_cost, CskPlan& ou
     }
   }
   return found;
+}
+
+// csk_plan memoised per shape: the search walks up to ~10^4 (am, an, bf, at) candidates, tens of
+// microseconds of host time per call -- every lock-step self-play batch (a new M each round, from
+// a few hundred distinct values) launched two such GEMMs
+static bool csk_plan_cached(int M, int N, int K, int cus, double miss_cost, CskPlan& out) {
+  struct Key {
+    int M, N, K, cus;
+    double miss;
+    bool operator==(const Key& o) const {
+      return M == o.M && N == o.N && K == o.K && cus == o.cus && miss == o.miss;
+    }
+  };
+  struct Hash {
+    size_t operator()(const Key& k) const {
+      return std::hash<long long>()(((long long)k.M << 40) ^ ((long long)k.N << 20) ^ k.K ^
+                                    ((long long)k.cus << 52));
+    }
+  };
+  static std::mutex mu;
+  static std::unordered_map<Key, std::pair<bool, CskPlan>, Hash> memo;
+  const Key key{M, N, K, cus, miss_cost};
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    const auto it = memo.find(key);
+    if (it != memo.end()) {
+      out = it->second.second;
+      return it->second.first;
+    }
+  }
+  CskPlan q{};
+  const bool ok = csk_plan(M, N, K, cus, miss_cost, q);
+  std::lock_guard<std::mutex> lk(mu);
+  if (memo.size() > 65536) memo.clear();
+  memo.emplace(key, std::make_pair(ok, q));
+  out = q;
+  return ok;
 }
 
 // gemm_x3 on operands that are ALREADY split ("p3"): A as three bf16 planes [3][M][K] (p.apl,
@@ -3866,12 +3904,32 @@ __global__ __launch_bounds__(256) void heads_tiles_finalize_kernel(HeadsEpi he, 
   constexpr int HS = HEADS_TILE_SLOTS;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  const float* src = he.part + (size_t)row * P * HS;
+  const float* src = he.part + (size_t)min(row, M - 1) * P * HS;
   float s[16];
 #pragma unroll
   for (int a = 0; a < 16; ++a) s[a] = 0.f;
   if constexpr (CSK) {
+    // the row's P * HS slot values (contiguous) staged in LDS by coalesced loads first: read in
+    // place, lane cb's pieces sit P * HS / 49 floats from its neighbour's, so every load
+    // instruction touched ~49 cache lines (41 us per M = 3,150 launch, PMC-free trace r05m)
+    extern __shared__ float hstage[];
+    float* const st = hstage + (threadIdx.x >> 6) * P * HS;
+    const int n = P * HS;
+    for (int i0 = 0; i0 < n; i0 += 8 * 64) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 64 * u + lane;
+        t[u] = i < n ? src[i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 64 * u + lane;
+        if (i < n) st[i] = t[u];
+      }
+    }
+    __syncthreads();
+    if (row >= M) return;
     const int cb = lane, col = 64 * cb;
     if (col < N) {
       const int mt = row >> 8;
@@ -3886,24 +3944,13 @@ __global__ __launch_bounds__(256) void heads_tiles_finalize_kernel(HeadsEpi he, 
         W = q.am * q.an * q.KT;
       }
       const int np = csk_block_of((f + 1) * q.KT - 1, b, W) - csk_block_of(f * q.KT, b, W) + 1;
-      // every piece's loads issued before the first add (pieces in k order; <= 8 of them in
-      // the plans csk_plan makes -- a longer tail, if any, is summed after, in order)
-      float v[8][HS];
+      // the pieces in k order
+      for (int pc = 0; pc < np; ++pc)
 #pragma unroll
-      for (int pc = 0; pc < 8; ++pc)
-#pragma unroll
-        for (int a = 0; a < HS; ++a)
-          v[pc][a] = pc < np ? src[(size_t)(cb * he.mp + pc) * HS + a] : 0.f;
-#pragma unroll
-      for (int pc = 0; pc < 8; ++pc)
-#pragma unroll
-        for (int a = 0; a < HS; ++a)
-          if (pc < np) s[a] += v[pc][a];
-      for (int pc = 8; pc < np; ++pc)
-#pragma unroll
-        for (int a = 0; a < HS; ++a) s[a] += src[(size_t)(cb * he.mp + pc) * HS + a];
+        for (int a = 0; a < HS; ++a) s[a] += st[(cb * he.mp + pc) * HS + a];
     }
   } else {
+    if (row >= M) return;
     for (int t = lane; t < P; t += 64)
 #pragma unroll
       for (int a = 0; a < HS; ++a) s[a] += src[(size_t)t * HS + a];
@@ -4123,16 +4170,17 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
         ok = csk_make(a.M, a.N, a.K, cus, am, an, bf, at, bt, cq);
       }
       if (use_csk && !forced)
-        ok = csk_plan(a.M, a.N, a.K, cus, env_miss ? atof(env_miss) : CSK_MISS_COST, cq);
+        ok = csk_plan_cached(a.M, a.N, a.K, cus, env_miss ? atof(env_miss) : CSK_MISS_COST, cq);
       if (ok && tuning_env("AZ_CSK_PRINT"))
         fprintf(stderr, "csk M=%d: am=%d an=%d cycles=%d bf=%d tail=%d at=%d ct=%d bt=%d B=%d pieces=%d\n",
                 a.M, cq.am, cq.an, cq.Cf, cq.bf, cq.tail, cq.at, cq.ct, cq.bt, cq.B, csk_max_pieces(cq));
 #else
-      ok = csk_plan(a.M, a.N, a.K, cus, CSK_MISS_COST, cq);
+      ok = csk_plan_cached(a.M, a.N, a.K, cus, CSK_MISS_COST, cq);
 #endif
       const int mp = use_csk && ok ? csk_max_pieces(cq) : 0;
       if (use_csk && ok && a.he.part && whole && (p2 || h3) &&
-          (size_t)a.M * (a.N / 64) * mp * HEADS_TILE_SLOTS * 4 * 2 <= ws_bytes) {
+          (size_t)a.M * (a.N / 64) * mp * HEADS_TILE_SLOTS * 4 * 2 <= ws_bytes &&
+          (size_t)4 * (a.N / 64) * mp * HEADS_TILE_SLOTS * 4 <= 65536) {   // finalize's LDS
         // the heads from the pieces (az_x3.h HeadsEpi, stream-K slots): no fix-up, no C
         if (p2) p2 = p2_prep();
         if (!p2) h3 = h3_scales();
@@ -4140,8 +4188,9 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
         if (p2) hipLaunchKernelGGL((gemm_x3_csk<false, true, true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
         else hipLaunchKernelGGL((gemm_x3_csk<false, true, false, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
         const int P = (a.N / 64) * mp;
-        hipLaunchKernelGGL(heads_tiles_finalize_kernel<true>, dim3((a.M + 3) / 4), dim3(256), 0, s,
-                           a.he, a.M, a.N, P, cq);
+        hipLaunchKernelGGL(heads_tiles_finalize_kernel<true>, dim3((a.M + 3) / 4), dim3(256),
+                           (size_t)4 * P * HEADS_TILE_SLOTS * sizeof(float), s, a.he, a.M, a.N,
+                           P, cq);
         a.splits = 1;
         a.heads_done = 1;
         return true;
