@@ -402,6 +402,21 @@ struct Tree {
     root_id = -1;
   }
 
+  // capacity for `hint` nodes up front (an episode's tree: az_mcts_episode_begin): growing the
+  // node and edge pools by doubling copied them ~3 times per episode and returned the old blocks
+  // to the OS (page faults, TLB shootdowns across the engine's threads); reserved pages are not
+  // touched until used.  The table starts at the size `hint` nodes fill to load 1/2 or less.
+  void reserve(int32_t hint, int A) {
+    nodes.reserve((size_t)hint);
+    EP.reserve((size_t)hint * A);
+    size_t tsz = 1024;
+    while (tsz * 2 <= (size_t)hint * 2) tsz *= 2;
+    if (tsz > table.size()) {
+      table.assign(tsz, HSlot{{0, 0}, -1, 0});
+      mask = tsz - 1;
+    }
+  }
+
   int32_t find(const Key& k) const {
     if (table.empty()) return -1;
     for (uint64_t h = khash(k) & mask;; h = (h + 1) & mask) {
@@ -411,7 +426,7 @@ struct Tree {
     }
   }
 
-  // the slot a lookup of k starts at (advance_group prefetches it a step ahead)
+  // the slot a lookup of k starts at (run_window prefetches it a step ahead)
   const HSlot* home(const Key& k) const { return table.empty() ? nullptr : &table[khash(k) & mask]; }
 
   void grow() {
@@ -444,6 +459,10 @@ struct Tree {
     nd.has_ns = nd.expanded = 0;
     int32_t id = (int32_t)nodes.size();
     nodes.push_back(nd);
+    // the node's edge block is block `id` of the pool, reserved now (alloc_edges fills it): a
+    // descent knows where a child's edges live as soon as it knows the child, so it requests
+    // the node and its edge lines together (one dependent miss per tree level, not two)
+    EP.resize((size_t)(id + 1) * R.A, Edge{0.0, 0.0, 0, -1, T_NONE, 0});
     table[h] = HSlot{k, id, 0};
     if ((uint64_t)nodes.size() * 2 > table.size()) grow();
     return id;
@@ -452,9 +471,9 @@ struct Tree {
   void alloc_edges(int32_t id, const Rules& R) {
     Node& nd = nodes[id];
     if (nd.edge >= 0) return;
-    nd.edge = edges++;
+    nd.edge = id;                                // the block find_or_add reserved
+    edges += 1;
     size_t A = R.A;
-    EP.resize(EP.size() + A, Edge{0.0, 0.0, 0, -1, T_NONE, 0});
     uint8_t v[kMaxA];
     R.valids(nd.key, v);
     Edge* e = &EP[(size_t)nd.edge * A];
@@ -578,58 +597,88 @@ void backup(az_mcts* m, Tree& t, Val v) {
 void expand(az_mcts* m, Tree& t, const float* pi, float v_std, const float* gpi, float gv,
             bool failed);
 
-// Searches of several slots, interleaved one tree level at a time (the slots' trees are
-// independent, so each tree sees exactly the sequence of searches advance() would run).  A
-// descent is a chain of dependent cache misses -- a node, then its edge block, then the child --
-// so one slot at a time leaves the core waiting on DRAM; here the node and edge lines of every
-// slot's next step are prefetched and the other slots' steps run while they arrive.  Each slot
-// runs until it waits on a new leaf or has no searches left; a new leaf with a cached row
-// (az_mcts_cache_put / az_mcts_feed_spec) is expanded on the spot.
-constexpr int kGroup = 8;
+// Searches of many slots, interleaved one tree level at a time over a window of kWin slots (the
+// slots' trees are independent, so each tree sees exactly the sequence of searches and episode
+// steps it would see alone).  A descent is a chain of dependent cache misses -- a node and its
+// edge block, then the child -- so one slot at a time leaves the core waiting on DRAM; here every
+// window slot's next node and edge lines are requested a pass ahead and the other slots' steps
+// run while they arrive.  A slot leaves the window when it waits on a new leaf (or the network,
+// or has nothing left) and the next slot of the source takes its place at once: the window
+// stays full (with fixed groups of 8, descents of unequal depth left ~2.6 slots live per pass
+// on average).  A new leaf with a cached row (az_mcts_cache_put / az_mcts_feed_spec) is
+// expanded on the spot.
+constexpr int kWin = 8;
 
 inline bool searching(const Tree& t) { return t.remaining > 0 && t.pending_leaf < 0; }
 
 inline void prefetch_node(const Tree& t, int32_t id) { __builtin_prefetch(&t.nodes[id]); }
 
-inline void prefetch_edges(const Tree& t, int32_t edge, int A) {
-  const char* p = reinterpret_cast<const char*>(&t.EP[(size_t)edge * A]);
+// a node's line and its edge block's lines (block id: find_or_add), requested together
+inline void prefetch_node_edges(const Tree& t, int32_t id, int A) {
+  __builtin_prefetch(&t.nodes[id]);
+  const char* p = reinterpret_cast<const char*>(&t.EP[(size_t)id * A]);
   const size_t bytes = sizeof(Edge) * (size_t)A;
   for (size_t o = 0; o < bytes; o += 64) __builtin_prefetch(p + o);
 }
 
-void advance_group(az_mcts* m, Tree* const* ts, int n) {
-  enum : uint8_t { START, NODE, SELECT, LOOKUP, DONE };
+int drive_episode(az_mcts* m, Tree& t);
+
+// does slot t have a descent to run now?  drive: episode-mode slots first advance their episode
+// (drive_episode: move bookkeeping, the next move's searches) until they need a descent, wait on
+// the network or are done
+inline bool has_descent(az_mcts* m, Tree& t, bool drive) {
+  if (!drive) return searching(t);
+  if (t.pending_leaf >= 0 || t.pending_std) return false;
+  return (t.ep.phase != E_IDLE ? drive_episode(m, t) : (searching(t) ? 2 : 0)) == 2;
+}
+
+// next(): the source's next slot (nullptr when exhausted)
+template <class Next>
+void run_window(az_mcts* m, Next next, bool drive) {
+  enum : uint8_t { START, NODE, SELECT, LOOKUP };
   const int A = m->R.A;
-  int32_t id[kGroup];
-  Key nkey[kGroup];        // LOOKUP: the child state whose table slot was prefetched
-  int32_t eidx[kGroup];    // ... and the edge that will point at it
-  uint8_t ph[kGroup];
-  int live = 0;
-  for (int i = 0; i < n; ++i) {
-    ph[i] = searching(*ts[i]) ? START : DONE;
-    live += ph[i] != DONE;
-  }
-  auto finish = [&](int i, Tree& t, Val v) {   // a search ended at a terminal / stuck node
-    backup(m, t, v);
-    t.remaining -= 1;
-    ph[i] = searching(t) ? START : DONE;
+  Tree* ts[kWin];
+  int32_t id[kWin];
+  Key nkey[kWin];          // LOOKUP: the child state whose table slot was prefetched
+  int32_t eidx[kWin];      // ... and the edge that will point at it
+  uint8_t ph[kWin];
+  auto admit = [&](int i) {                     // window place i <- the source's next slot
+    while (Tree* t = next())
+      if (has_descent(m, *t, drive)) {
+        ts[i] = t;
+        ph[i] = START;
+        return true;
+      }
+    return false;
   };
-  while (live > 0) {
-    for (int i = 0; i < n; ++i) {
-      if (ph[i] == DONE) continue;
+  int n = 0;
+  while (n < kWin && admit(n)) ++n;
+  // slot i has no descent in progress: its next one, else the next slot (false: none left)
+  auto retire = [&](int i) {
+    if (has_descent(m, *ts[i], drive)) {
+      ph[i] = START;
+      return true;
+    }
+    return admit(i);
+  };
+  while (n > 0) {
+    for (int i = 0; i < n;) {
       Tree& t = *ts[i];
+      bool keep = true;
       switch (ph[i]) {
         case START:
           t.path.clear();
           if (t.root_id < 0) t.root_id = t.find_or_add(t.root, m->R);
           id[i] = t.root_id;
-          prefetch_node(t, id[i]);
+          prefetch_node_edges(t, id[i], A);
           ph[i] = NODE;
           break;
         case NODE: {
           const Node& nd = t.nodes[id[i]];
           if (nd.es.x != 0.0) {                  // terminal (MCTS.py:152-157)
-            finish(i, t, nd.es);
+            backup(m, t, nd.es);
+            t.remaining -= 1;
+            keep = retire(i);
           } else if (!nd.expanded) {             // new leaf: Vs, then the network
             t.alloc_edges(id[i], m->R);
             t.pending_leaf = id[i];
@@ -639,21 +688,22 @@ void advance_group(az_mcts* m, Tree* const* ts, int n) {
               expand(m, t, row, row[A], m->use_gnn ? row + A + 1 : nullptr,
                      m->use_gnn ? row[2 * A + 1] : 0.f, false);
               t.cache_hits += 1;
-              ph[i] = searching(t) ? START : DONE;
-            } else {
-              ph[i] = DONE;
             }
-          } else {
-            prefetch_edges(t, nd.edge, A);
-            ph[i] = SELECT;
+            keep = retire(i);
+          } else {                               // its edges were requested with it:
+            ph[i] = SELECT;                      // select in this same pass
+            goto select;
           }
           break;
         }
-        case SELECT: {
+        case SELECT:
+        select: {
           const Node& nd = t.nodes[id[i]];
           const int a = select_action(m, t, nd);
           if (a < 0) {                           // MCTS.py:220-221
-            finish(i, t, vint(0));
+            backup(m, t, vint(0));
+            t.remaining -= 1;
+            keep = retire(i);
             break;
           }
           const size_t e = (size_t)nd.edge * A + a;
@@ -667,7 +717,7 @@ void advance_group(az_mcts* m, Tree* const* ts, int n) {
             break;
           }
           id[i] = child;
-          prefetch_node(t, child);
+          prefetch_node_edges(t, child, A);
           ph[i] = NODE;
           break;
         }
@@ -675,12 +725,21 @@ void advance_group(az_mcts* m, Tree* const* ts, int n) {
           const int32_t child = t.find_or_add(nkey[i], m->R);   // may grow t.nodes
           t.EP[(size_t)eidx[i]].C = child;
           id[i] = child;
-          prefetch_node(t, child);
+          prefetch_node_edges(t, child, A);
           ph[i] = NODE;
           break;
         }
       }
-      live -= ph[i] == DONE;
+      if (keep) {
+        ++i;
+      } else {                                   // the window shrinks: the last place moves here
+        --n;
+        ts[i] = ts[n];
+        id[i] = id[n];
+        nkey[i] = nkey[n];
+        eidx[i] = eidx[n];
+        ph[i] = ph[n];
+      }
     }
   }
 }
@@ -688,12 +747,12 @@ void advance_group(az_mcts* m, Tree* const* ts, int n) {
 // Run searches of one slot until it waits on a leaf (returns 1) or has none left (0).
 int advance(az_mcts* m, Tree& t) {
   Tree* one = &t;
-  advance_group(m, &one, 1);
+  run_window(m, [&]() { Tree* r = one; one = nullptr; return r; }, false);
   return t.pending_leaf >= 0 ? 1 : 0;
 }
 
 // drive_episode's view of a slot's queued searches: 1 = waiting on a leaf, 2 = descents to run
-// (advance_group), 0 = none left
+// (run_window), 0 = none left
 inline int search_state(const Tree& t) {
   if (t.pending_leaf >= 0) return 1;
   return t.remaining > 0 ? 2 : 0;
@@ -925,6 +984,9 @@ int az_mcts_episode_begin(az_mcts* m, int slot, uint32_t seed, int sims, int exp
     return fail(AZM_EINVAL, "az_mcts_episode_begin: bad args");
   Tree& t = m->trees[slot];
   t.clear();
+  // an episode's tree holds ~sims x (moves ~ cells) / 1.4 nodes (Connect4 7x7 at 100 sims: 3,408
+  // on average, 4,155 at most, tools/native/mcts_prof.cpp): room for sims x cells
+  t.reserve((int32_t)std::min<int64_t>((int64_t)std::max(sims, 1) * m->R.cells, 32768), m->R.A);
   Episode& E = t.ep;
   E.reset();
   E.rng.seed(seed);
@@ -1173,40 +1235,34 @@ int collect_impl(az_mcts* m, int8_t* boards, int32_t* slots, int cap, int thread
   std::vector<uint8_t> has(S, 0);
   if (threads < 1) threads = 1;
   m->threads = threads;
-  // groups of kGroup consecutive slots: the episode state machines of a group run until every
-  // slot waits on the network or is idle, their descents interleaved by advance_group
-  const int ngroups = (S + kGroup - 1) / kGroup;
+  // chunks of kChunk consecutive slots per thread (dynamic): each chunk's episode state machines
+  // run, kWin at a time (run_window), until every slot waits on the network or is idle
+  constexpr int kChunk = 32;
+  const int ngroups = (S + kChunk - 1) / kChunk;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
   for (int gi = 0; gi < ngroups; ++gi) {
-    const int s0 = gi * kGroup, s1 = std::min(S, s0 + kGroup);
+    const int s0 = gi * kChunk, s1 = std::min(S, s0 + kChunk);
     if (fr) {
-      // the group's backups touch every node and edge on each fed slot's path, last written a
-      // round ago (often by another thread): their lines are requested for all slots first
-      for (int s = s0; s < s1; ++s)
-        if (fr->row_of[s] >= 0) {
-          const Tree& t = m->trees[s];
-          if (t.pending_leaf >= 0) prefetch_node(t, t.pending_leaf);
-          for (const auto& pe : t.path) {
-            prefetch_node(t, pe.first);
-            __builtin_prefetch(&t.EP[(size_t)pe.second]);
-          }
+      // the backups touch every node and edge on each fed slot's path, last written a round ago
+      // (often by another thread): their lines are requested kWin slots ahead of the feed
+      auto request = [&](int s) {
+        if (s >= s1 || fr->row_of[s] < 0) return;
+        const Tree& t = m->trees[s];
+        if (t.pending_leaf >= 0) prefetch_node_edges(t, t.pending_leaf, m->R.A);
+        for (const auto& pe : t.path) {
+          prefetch_node(t, pe.first);
+          __builtin_prefetch(&t.EP[(size_t)pe.second]);
         }
-      for (int s = s0; s < s1; ++s)
+      };
+      for (int s = s0; s < s0 + kWin; ++s) request(s);
+      for (int s = s0; s < s1; ++s) {
+        request(s + kWin);
         if (fr->row_of[s] >= 0)
           feed_row(m, m->trees[s], fr->row_of[s], fr->pi, fr->v, fr->gpi, fr->gv, false);
-    }
-    for (;;) {
-      Tree* need[kGroup];
-      int nn = 0;
-      for (int s = s0; s < s1; ++s) {
-        Tree& t = m->trees[s];
-        if (t.pending_leaf >= 0 || t.pending_std) continue;
-        const int r = t.ep.phase != E_IDLE ? drive_episode(m, t) : (searching(t) ? 2 : 0);
-        if (r == 2) need[nn++] = &t;
       }
-      if (nn == 0) break;
-      advance_group(m, need, nn);
     }
+    int nx = s0;
+    run_window(m, [&]() { return nx < s1 ? &m->trees[nx++] : nullptr; }, true);
     for (int s = s0; s < s1; ++s) {
       const Tree& t = m->trees[s];
       if (t.pending_leaf >= 0) {
