@@ -23,6 +23,12 @@ namespace az {
 
 // LDS the kernel hands to c4_trunk_tile: conv2's weights while they are read into registers,
 // then (NB <= 4) the NB*3136-float output staging tile, or (NB = 8, no staging) conv1's output
+// `un` always has room for conv2's staged weights, even when the fragment-ordered copy makes the
+// staging unnecessary: that keeps one trunk block per CU.  Smaller blocks (two per CU for NB <= 3,
+// round 5) ran 1.4x faster at self-play sizes but gave WRONG rows, nondeterministically, in
+// blocks that shared a CU with another block (tools/trunk_cmp_probe.py; correct with the same code
+// when extra dynamic LDS forced one block per CU, AZ_TRUNK_DYN_LDS in the tuning build); the
+// cause was not found, so the layout that rules it out stays.
 template <int NB>
 constexpr int trunk_union_floats() {
   constexpr int after = NB <= 4 ? NB * 3136 : NB * C1_FLOATS_PER_BOARD;
@@ -53,18 +59,19 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
                                               const float* __restrict__ w2f = nullptr) {
   float* const ob = un;
   constexpr int P = 49, PP = 81, CI = 32;
-  constexpr int ROWS = NB * P;
-  constexpr int MT = (ROWS + 15) / 16;
+  constexpr int NT = TTILES[NB];          // 16-row tiles (az_trunk_rows.h order)
   // STAGE: the output tile is assembled in LDS in NCHW-flatten order and written as whole
   // float4 rows (the MFMA layout puts 16 channels 49 floats apart on consecutive lanes, so
   // direct stores scatter 4-byte writes); NB = 8 lacks the LDS for it
   constexpr bool STAGE = NB <= 4;
   __shared__ float bd[NB * PP + 1];
-  // conv1's output: its own LDS when the output is staged (NB <= 4), else in `un` once conv2's
-  // weights have moved to registers
+  // conv1's output planes (az_trunk_split.h): own LDS when the output is staged (NB <= 4), else
+  // in `un` once conv2's weights have moved to registers
   __shared__ __attribute__((aligned(16))) float c1s[STAGE ? NB * C1_FLOATS_PER_BOARD : 4];
   float* const c1 = STAGE ? c1s : un;
   __shared__ float w1s[CI * 9 + CI + 1];   // conv1 weights, bias, pad: one round trip, then LDS
+  __shared__ float c1wmax[NB][8];          // each board's largest conv1 value, per wave
+  __shared__ float c1inv[NB];              // ... its planes' 1 / scale
   const int tid = threadIdx.x;
   const int b0 = blockIdx.x * NB;
   const int nb = min(NB, B - b0);
@@ -72,6 +79,7 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   const int nt = wave & 3, mh = wave >> 2;
   const int h = lane >> 4, c16 = lane & 15;
   const int co = nt * 16 + c16;
+  const uint16_t* const rows = trunk_rows<NB>();
   // Every global load of the prologue is issued before the first one is waited for (conv2's
   // 9 float4 per thread, the boards, conv1's weights, the bias), then the LDS stores: as a
   // load -> store loop each iteration waited for its own round trip (11 in a row).
@@ -124,37 +132,56 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
       breg[s] = un[co * W2S_STRIDE + ci * 9 + (tap / 3) * 3 + (tap % 3)];
     }
   }
+  bf16x8 bh[9], bl[9];
+  const float iw = w2_planes(breg, bh, bl);
   if constexpr (!STAGE) __syncthreads();   // conv1's output overwrites the weights in `un`
-  for (int i = tid; i < NB * PP * CI; i += 512) {
-    const int b = i / (PP * CI), rem = i % (PP * CI), pp = rem / CI, ci = rem % CI;
-    const int px = pp / 9, py = pp % 9;
-    float v = 0.f;
-    if (px >= 1 && px <= 7 && py >= 1 && py <= 7) {
-      float s = 0.f;
+  // conv1: (board, padded position, channel octet) items, kept in registers until each board's
+  // maximum (its plane scale) is known
+  constexpr int NI = NB * PP * 4, NIT = (NI + 511) / 512;
+  float cv[NIT][8];
+  float cm[NB];                            // this lane's maximum per board, then the wave's
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh)
+  for (int b = 0; b < NB; ++b) cm[b] = 0.f;
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw)
-          s = fmaf(w1s[ci * 9 + kh * 3 + kw], bd[b * PP + (px - 1 + kh) * 9 + (py - 1 + kw)], s);
-      s += w1s[CI * 9 + ci];
-      v = s > 0.f ? s : 0.f;
+  for (int it = 0; it < NIT; ++it) {
+    const int i = tid + 512 * it;
+    if (i < NI) {
+      const int b = i / (PP * 4), r = i - b * (PP * 4);
+      conv1_octet(w1s, bd + b * PP, r >> 2, r & 3, cv[it]);
+      const float m = octet_max(cv[it]);
+#pragma unroll
+      for (int q = 0; q < NB; ++q)
+        if (q == b) cm[q] = fmaxf(cm[q], m);
     }
-    c1[b * C1_FLOATS_PER_BOARD + pp * C1S + ci] = v;
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cm[b] = fmaxf(cm[b], __shfl_xor(cm[b], o));
+    if (lane == 0) c1wmax[b][wave] = cm[b];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = tid + 512 * it;
+    if (i < NI) {
+      const int b = i / (PP * 4), r = i - b * (PP * 4);
+      float mx = c1wmax[b][0];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) mx = fmaxf(mx, c1wmax[b][w]);
+      float inv;
+      const float sa = h3_scale(mx, H3_TA, &inv);
+      c1_store(c1 + b * C1_FLOATS_PER_BOARD, r >> 2, r & 3, cv[it], sa);
+      if (r == 0) c1inv[b] = inv;
+    }
   }
   __syncthreads();
 
-  // the wave's m-tiles go in pairs (mt, mt + 2) with their two MFMA chains interleaved: each
+  // the wave's row tiles go in pairs (mt, mt + 2) with their two MFMA chains interleaved: each
   // chain keeps its own k order (same sums as one tile at a time), but the pipeline now has two
   // independent accumulators to alternate between instead of stalling on one
-  auto a_base = [&](int mt) {
-    const int i = mt * 16 + c16;
-    int base = 0;
-    if (mt < MT && i < ROWS) {
-      const int b = i / P, p = i % P;
-      base = b * C1_FLOATS_PER_BOARD + ((p / 7) * 9 + (p % 7)) * C1S;
-    }
-    return c1 + base + 8 * h;
-  };
+  const u32x4* const c1u = reinterpret_cast<const u32x4*>(c1);
+  auto a_unit = [&](int mt) { return mt < NT ? c1_row_unit(rows[16 * mt + c16] & 0x7fff, h) : h; };
   // bm: each board's max feature (>= 0 after the ReLU) over this lane's stores, for the A split
   float bm[NB];
 #pragma unroll
@@ -162,10 +189,10 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   auto store_tile = [&](int mt, const f32x4v& acc) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = mt * 16 + h * 4 + r;
-      if (row < nb * P) {
-        const int b = row / P, p = row % P;
-        const float v = acc[r] + bias;
+      const int e = rows[16 * mt + h * 4 + r];
+      const int b = (e & 0x7fff) / P, p = (e & 0x7fff) - P * ((e & 0x7fff) / P);
+      if (!(e & 0x8000) && b < nb) {
+        const float v = acc[r] * (c1inv[b] * iw) + bias;
         const float o = v > 0.f ? v : 0.f;
         if constexpr (STAGE) {
           ob[b * 3136 + co * P + p] = o;
@@ -178,27 +205,19 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
       }
     }
   };
-  for (int mt = mh; mt < MT; mt += 4) {
-    const float* a0 = a_base(mt);
-    const float* a1 = a_base(mt + 2);
+  for (int mt = mh; mt < NT; mt += 4) {
+    const int u0 = a_unit(mt), u1 = a_unit(mt + 2);
     f32x4v acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      const int off = ((tap / 3) * 9 + (tap % 3)) * C1S;
-      const f32x4v x0 = *reinterpret_cast<const f32x4v*>(a0 + off);
-      const f32x4v y0 = *reinterpret_cast<const f32x4v*>(a0 + off + 4);
-      const f32x4v x1 = *reinterpret_cast<const f32x4v*>(a1 + off);
-      const f32x4v y1 = *reinterpret_cast<const f32x4v*>(a1 + off + 4);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(j < 4 ? x0[j] : y0[j - 4], breg[tap * 8 + j],
-                                                    acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(j < 4 ? x1[j] : y1[j - 4], breg[tap * 8 + j],
-                                                    acc1, 0, 0, 0);
-      }
+      const int off = c1_tap_units(tap);
+      const u32x4 ah0 = c1u[u0 + off], al0 = c1u[u0 + off + 4];
+      const u32x4 ah1 = c1u[u1 + off], al1 = c1u[u1 + off + 4];
+      acc0 = conv2_step(ah0, al0, bh[tap], bl[tap], acc0);
+      acc1 = conv2_step(ah1, al1, bh[tap], bl[tap], acc1);
     }
     store_tile(mt, acc0);
-    if (mt + 2 < MT) store_tile(mt + 2, acc1);
+    if (mt + 2 < NT) store_tile(mt + 2, acc1);
   }
   if constexpr (STAGE) {
     // each board's max feature, one per wave (max is exact: any order gives the value
@@ -749,11 +768,12 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
                            float* feat, unsigned short* apl, float* asc, bool* split,
                            hipStream_t s) {
   static const char* env = tuning_env("AZ_TRUNK_NB");   // tuning experiments only
-  // boards per block: the time is whole rounds of blocks over the CUs, each round t(NB) (one
-  // block per CU at a time in effect; measured on MI355X, profiles/r03w_trunk_nb_sweep.jsonl:
-  // t = 9, 16, 22, 25, 28.5, 33, 42, 47 us for NB = 1..8, every NB bit-identical), so pick the
-  // NB with the fewest rounds x t(NB): B = 512 -> 2, 1,024 -> 4, 1,576 -> 7, 2,048 -> 8,
-  // 2,560 -> 5 (56 vs 89 us for 8), 3,150 -> 7 (85 vs 90), 4,096 -> 8
+  // boards per block from a fitted time model, t(NB, B) = a(NB) + b(NB) x ceil(blocks / CUs)
+  // (one block per CU; blocks = ceil(B / NB)), fitted to the sweep of every NB at B = 256 ..
+  // 4,096 on MI355X (profiles/r05/trunk_nb_sweep.txt, every NB bit-identical); when the caller
+  // wants output_transform.0's A pre-split (apl), NB > 4 pays the separate split pass (~3.8 ns
+  // per board).  B = 512 -> 2 (13.4 us), 768 -> 3, 1,024 -> 4, 1,576 -> 4, 3,150 -> 3 (63 us;
+  // the round-4 kernel took 85 at NB = 7), 4,096 -> 8
   static int cus = 0;
   if (cus <= 0) {
     int dev = 0, n = 0;
@@ -763,11 +783,12 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
   }
   int nbk = 0;
   if (B > 8) {
-    static const float t_nb[9] = {0.f, 9.f, 16.f, 22.f, 25.f, 28.5f, 33.f, 42.f, 47.f};
+    static const float ta[9] = {0.f, 2.f, 2.6f, 3.7f, 3.5f, 3.f, 0.f, 0.f, 0.f};
+    static const float tb[9] = {0.f, 7.6f, 10.8f, 11.8f, 15.5f, 22.f, 26.f, 30.5f, 33.f};
     float best = 0.f;
     for (int nb = 1; nb <= 8; ++nb) {
       const long rounds = ((long)(B + nb - 1) / nb + cus - 1) / cus;
-      const float t = (float)rounds * t_nb[nb];
+      const float t = ta[nb] + (float)rounds * tb[nb] + (apl && nb > 4 ? 0.0038f * B : 0.f);
       if (nb == 1 || t < best) best = t, nbk = nb;
     }
   }
@@ -777,29 +798,26 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
   // conv2's weights in fragment order when they are registered (cached per weight generation)
   static const bool no_frag = tuning_env("AZ_TRUNK_NO_W2F") != nullptr;   // A/B experiments
   const float* w2f = nbk >= 1 && !no_frag ? conv2_frags(conv2_w, s) : nullptr;
+#ifdef AZ_TUNING   // AZ_TRUNK_DYN_LDS=<bytes>: extra (unused) LDS per block, to limit residency
+  static const char* env_dyn = tuning_env("AZ_TRUNK_DYN_LDS");
+  const size_t dyn = env_dyn ? (size_t)atol(env_dyn) : 0;
+#else
+  constexpr size_t dyn = 0;
+#endif
 #define AZ_TRUNK(NB_)                                                                            \
   if (sa) hipLaunchKernelGGL(c4_trunk_split_a_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), \
-                             0, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, apl, asc, \
-                             w2f);                                                               \
-  else hipLaunchKernelGGL(c4_trunk_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), 0, s,       \
+                             dyn, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, apl,   \
+                             asc, w2f);                                                          \
+  else hipLaunchKernelGGL(c4_trunk_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), dyn, s,     \
                           boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
+#define AZ_TRUNK_BIG(NB_)                                                                      \
+  hipLaunchKernelGGL(c4_trunk_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), dyn, s, boards, \
+                     B, conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
   switch (nbk) {
-    case 8:
-      hipLaunchKernelGGL(c4_trunk_kernel<8>, dim3((B + 7) / 8), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
-      break;
-    case 7:
-      hipLaunchKernelGGL(c4_trunk_kernel<7>, dim3((B + 6) / 7), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
-      break;
-    case 6:
-      hipLaunchKernelGGL(c4_trunk_kernel<6>, dim3((B + 5) / 6), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
-      break;
-    case 5:
-      hipLaunchKernelGGL(c4_trunk_kernel<5>, dim3((B + 4) / 5), dim3(512), 0, s, boards, B,
-                         conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
-      break;
+    case 8: AZ_TRUNK_BIG(8) break;
+    case 7: AZ_TRUNK_BIG(7) break;
+    case 6: AZ_TRUNK_BIG(6) break;
+    case 5: AZ_TRUNK_BIG(5) break;
     case 4: AZ_TRUNK(4) break;
     case 3: AZ_TRUNK(3) break;
     case 2: AZ_TRUNK(2) break;
@@ -810,6 +828,7 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
     default: AZ_TRUNK(1)
   }
 #undef AZ_TRUNK
+#undef AZ_TRUNK_BIG
   return check_launch("c4_trunk_kernel");
 }
 }  // namespace az

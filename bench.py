@@ -71,7 +71,7 @@ def parse():
     return ap.parse_args()
 
 
-CALIBRATION = "profiles/r04_cpu_calibration.json"   # tools/cpu_calibration.py, build container
+CALIBRATION = "profiles/r05/cpu_calibration.json"   # tools/cpu_calibration.py, build container
 CPU_CHILD = "--cpu-baselines-child"
 
 
@@ -151,7 +151,7 @@ def cpu_baselines_child(spec):
     out["cnn_b512"] = cpu_baseline(W, G, min(sec, 5.0), B, threads, gnn=False)
     if spec.get("selfplay"):
         # the batch-1 loop is latency-bound: timed on every visible core AND on one torch thread
-        # (the faster of the two is the baseline; profiles/r04_cpu_calibration.json
+        # (the faster of the two is the baseline; profiles/r05/cpu_calibration.json
         # selfplay_by_threads: one thread is as fast or faster for the reference too)
         sps = max(sec, 20.0)              # room for one whole episode (~8-11 s on one core)
         out["selfplay"] = {str(t): selfplay_cpu_baseline(W, G, spec["sims"], sps, t)
@@ -810,7 +810,7 @@ def selfplay_cpu_baseline(W, G, sims, seconds, threads):
     the network behind the reference's batch-1 predict plumbing (Connect4GNN.py:59-120), torch
     on `threads` threads: moves finished in `seconds`.
     tools/cpu_calibration.py measured this loop against the imported reference's loop on the
-    same episode (profiles/r02_cpu_calibration.json: selfplay)."""
+    same whole episode (profiles/r05/cpu_calibration.json: selfplay)."""
     import torch
     import Coach as C
     import MCTS as M

@@ -3,7 +3,7 @@ container, time the imported reference and this repo's CPU restatements on ident
 thread counts, and record the ratios.  bench.py's cpu_baseline (run on the GPU box, where the
 reference does not exist) uses the restatement whose ratio is recorded here.
 
-    PYTHONDONTWRITEBYTECODE=1 python tools/cpu_calibration.py > profiles/r04_cpu_calibration.json
+    PYTHONDONTWRITEBYTECODE=1 python tools/cpu_calibration.py > profiles/r05/cpu_calibration.json
 
 Legs (8 torch threads, fp32, eval mode, torch.no_grad, median of >= 10 after 3 warm-ups):
   gnn_b512  predict_with_gnn per-row semantics at B = 512 (Connect4GNN.py:31-57 +
@@ -131,10 +131,10 @@ def main():
     import importlib
     ref_coach = importlib.import_module("Coach")
     ref_mcts = importlib.import_module("MCTS")
-    moves_cap = 12
+    moves_cap = 10 ** 6          # whole episodes, as bench.py's self-play baseline samples them
 
     def episode_rate(coach_mod, mcts_mod, net, generator=False):
-        """moves/s of the first moves_cap moves of episode seed 0 (the reference's MCTS has
+        """moves/s over the whole of episode seed 0 (moves_cap is not reached; the reference's MCTS has
         getActionProb; this repo's Coach drives the generator form getActionProb_g)."""
         coach = coach_mod.Coach.__new__(coach_mod.Coach)
         coach.game, coach.args, coach.nnet = game, args, net
@@ -212,7 +212,7 @@ def main():
     port_rate = port_rates[THREADS]
     torch.set_num_threads(THREADS)
     out["selfplay"] = {"config": "Connect4 7x7, use_gnn, numMCTSSims 100, expand_by 5, episode "
-                                 f"seed 0, first {moves_cap} moves",
+                                 "seed 0, the whole episode",
                        "reference_moves_per_s": round(ref_rate, 3),
                        "port_moves_per_s": round(port_rate, 3),
                        "ratio_port_over_reference_time": round(ref_rate / port_rate, 3)}
