@@ -1121,10 +1121,11 @@ def main():
                              "note": "untimed full steps before the warmup (GPU clock ramp)"},
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32 (output_transform GEMMs: each fp32 operand row power-of-two scaled and "
-                     "split into 2 fp16 terms, 3 fp16 MFMA products, fp32 accumulate; ~22-bit "
-                     "operands: tests/test_gpu_trained.py holds pi / v / log pi to 1e-5 of the "
-                     "reference on its trained weights)",
+            "dtype": "f32 (fp16x2 row-scaled split, 3 products: output_transform GEMMs and the "
+                     "trunk's conv2 split each fp32 operand row, power-of-two scaled, into 2 fp16 "
+                     "terms, 3 fp16 MFMA products, fp32 accumulate; ~22-bit operands: "
+                     "tests/test_gpu_trained.py holds pi / v / log pi to 1e-5 of float64 and of "
+                     "the reference on its trained weights, margins reported)",
             "data": "synthetic (uniform random {-1,0,1} 7x7 boards; PCG64 random-init weights "
                     "of the reference shapes)",
             "config": {"workload": "Connect4 (reference 7x7+pass board) Connect4GNN "
