@@ -1251,22 +1251,32 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
                                  e->glogp, gpi, gv, e->ws, e->ws_bytes, stream);
     // shapes not covered: the general sequence below (re-runs the trunk, harmless)
   }
-  // GNN tail only (predict_with_gnn batches): the trunk also writes feat's rows as
-  // output_transform.0's pre-split A into the workspace's pre_region when that GEMM takes the
-  // P2 path (c4_trunk_launch decides by its NB)
+  // the GNN tail (predict_with_gnn batches, and predict_both above the one-launch trunk + heads
+  // size): the trunk also writes feat's rows as output_transform.0's pre-split A into the
+  // workspace's pre_region when that GEMM takes the P2 path (c4_trunk_launch decides by its
+  // NB), so the GEMM launches no split of its own; the standard heads (predict_both) then read
+  // feat as before -- the same kernels, the same bits
+  constexpr int TRUNK_HEADS_ONE_LAUNCH = 320;   // az_c4_trunk_heads_fwd's one-launch limit
   PreRegion R{nullptr, nullptr, 0};
   bool split = false;
   static const bool no_fuse = tuning_env("AZ_NO_PRESPLIT") != nullptr;   // A/B experiments
-  if (!v && gv && !no_fuse && e->ot0_w && aligned16(e->ws) && gemm_p2_weights(e->ot0_w, 3136, 3136, 3136))
+  static const bool no_both = tuning_env("AZ_NO_PRESPLIT_BOTH") != nullptr;
+  if (gv && (!v || (B > TRUNK_HEADS_ONE_LAUNCH && !no_both)) && !no_fuse && e->ot0_w &&
+      aligned16(e->ws) &&
+      gemm_p2_weights(e->ot0_w, 3136, 3136, 3136))
     R = pre_region(e->ws, e->ws_bytes, B, 3136,
                    align256(az_heads_ws_bytes(B, 3136, e->A)) + (size_t)B * 3136 * 8);
-  if (v) {
+  if (v && !R.planes) {
     rc = az_c4_trunk_heads_fwd(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b,
                                e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,
                                e->feat, e->logp, pi, v, e->ws, e->ws_bytes, stream);
   } else {
     rc = c4_trunk_launch(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b, e->feat,
                          R.planes, R.sc, &split, as_stream(stream));
+    if (!rc && v)             // what az_c4_trunk_heads_fwd runs after the trunk above 320 rows
+      rc = az_heads_fwd(e->feat, 3136, e->feat, 3136, B, 3136, e->fc_policy_w, e->fc_policy_b,
+                        e->A, e->fc_value_w, e->fc_value_b, e->logp, pi, v, e->ws, e->ws_bytes,
+                        stream);
   }
   if (rc || !gv) return rc;
   AZ_REQUIRE(e->ot0_w && e->ot0_b && e->ot2_w && e->ot2_b && e->hidden && e->y && e->glogp,
