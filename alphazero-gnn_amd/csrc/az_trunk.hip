@@ -27,12 +27,21 @@ namespace az {
 // staging unnecessary: that keeps one trunk block per CU.  Smaller blocks (two per CU for NB <= 3,
 // round 5) ran 1.4x faster at self-play sizes but gave WRONG rows, nondeterministically, in
 // blocks that shared a CU with another block (tools/trunk_cmp_probe.py; correct with the same code
-// when extra dynamic LDS forced one block per CU, AZ_TRUNK_DYN_LDS in the tuning build); the
-// cause was not found, so the layout that rules it out stays.
+// when extra dynamic LDS forced one block per CU, AZ_TRUNK_DYN_LDS in the tuning build).  Ruled
+// out (tools/trunk_residency_probe.py, tools/probes/lds_alloc_probe.hip, profiles/r05/
+// trunk_residency/): overlapping LDS allocations (HW_REG_LDS_ALLOC: disjoint, no word of a block
+// overwritten by its neighbour, 4- and 16-byte accesses), writes past the static LDS (4-32 KB of
+// extra dynamic LDS with two blocks per CU stay wrong), scratch (none), and the MFMA chain's wait
+// states alone (24 s_nop cycles after every tap: still wrong).  The cause is open, so the layout
+// that rules it out stays.
 template <int NB>
 constexpr int trunk_union_floats() {
   constexpr int after = NB <= 4 ? NB * 3136 : NB * C1_FLOATS_PER_BOARD;
+#ifdef AZ_TRUNK_SMALL_UNION   // residency experiment (tuning build): fragment-ordered weights only
+  return after;
+#else
   return W2S_FLOATS > after ? W2S_FLOATS : after;
+#endif
 }
 
 // The trunk of one 512-thread block (boards blockIdx.x*NB ...).  `un` is LDS of
@@ -262,8 +271,13 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   }
 }
 
+#ifdef AZ_TRUNK_SMALL_UNION
+#define AZ_TRUNK_LB __launch_bounds__(512, 4)
+#else
+#define AZ_TRUNK_LB __launch_bounds__(512)
+#endif
 template <int NB>
-__global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict__ boards, int B,
+__global__ AZ_TRUNK_LB void c4_trunk_kernel(const int8_t* __restrict__ boards, int B,
                                                       const float* __restrict__ w1,
                                                       const float* __restrict__ b1,
                                                       const float* __restrict__ w2,
@@ -276,7 +290,7 @@ __global__ __launch_bounds__(512) void c4_trunk_kernel(const int8_t* __restrict_
 
 // c4_trunk_kernel that also writes feat's rows as output_transform.0's pre-split A (NB <= 4)
 template <int NB>
-__global__ __launch_bounds__(512) void c4_trunk_split_a_kernel(
+__global__ AZ_TRUNK_LB void c4_trunk_split_a_kernel(
     const int8_t* __restrict__ boards, int B, const float* __restrict__ w1,
     const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
     float* __restrict__ feat, unsigned short* __restrict__ apl, float* __restrict__ asc,
@@ -798,6 +812,9 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
   // conv2's weights in fragment order when they are registered (cached per weight generation)
   static const bool no_frag = tuning_env("AZ_TRUNK_NO_W2F") != nullptr;   // A/B experiments
   const float* w2f = nbk >= 1 && !no_frag ? conv2_frags(conv2_w, s) : nullptr;
+#ifdef AZ_TRUNK_SMALL_UNION
+  if (nbk >= 1 && nbk <= 4 && !w2f) return AZ_EINVAL;   // `un` has no room for staged weights
+#endif
 #ifdef AZ_TUNING   // AZ_TRUNK_DYN_LDS=<bytes>: extra (unused) LDS per block, to limit residency
   static const char* env_dyn = tuning_env("AZ_TRUNK_DYN_LDS");
   const size_t dyn = env_dyn ? (size_t)atol(env_dyn) : 0;
