@@ -44,6 +44,90 @@ constexpr int trunk_union_floats() {
 #endif
 }
 
+// The standard heads (Connect4Net.py:48-57: log_softmax(feat wp^T + bp), tanh(feat wv^T + bv)) of
+// the block's feature rows, for predict_both batches whose trunk stages its rows in LDS.
+struct TrunkHeads {
+  const float* wp; const float* bp; int A; const float* wv; const float* bv;
+  float* logp; float* pi; float* v;
+};
+
+// heads_rowsw_kernel's arithmetic on rows already in LDS (ob: nb rows of 3136 floats): wave w takes
+// chunks w, w + 8, ... (256 columns each, the chunk's head weights loaded once for all nb rows),
+// the same per-(row, chunk) fma chains and wave reductions, the chunk partials summed in chunk
+// order from 0, then the same log_softmax / exp / tanh -- so the outputs are az_heads_fwd's bits.
+template <int NB>
+__device__ __forceinline__ void trunk_rows_heads(const float* ob, int nb, int b0,
+                                                 const TrunkHeads& hd) {
+  constexpr int AMAX = 8, PW = AMAX + 1, K = 3136, NCH = (K + HEADS_KC - 1) / HEADS_KC;
+  __shared__ float part[NB][NCH][PW];
+  __shared__ float hsm[NB][PW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int A = hd.A;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  for (int c = wave; c < NCH; c += 8) {
+    const int k = c * HEADS_KC + lane * 4;
+    const bool kin = k < K;
+    const int kc = kin ? k : 0;
+    f32x4 w[AMAX + 1];
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a)
+      w[a] = *reinterpret_cast<const f32x4*>(hd.wp + (size_t)min(a, A - 1) * K + kc);
+    w[AMAX] = *reinterpret_cast<const f32x4*>(hd.wv + kc);
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) w[a] = (a < A && kin) ? w[a] : z;
+    w[AMAX] = kin ? w[AMAX] : z;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (b >= nb) break;
+      const f32x4 x = kin ? *reinterpret_cast<const f32x4*>(ob + b * K + kc) : z;
+      float pv[AMAX];
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a)
+        pv[a] = fmaf(x[3], w[a][3], fmaf(x[2], w[a][2], fmaf(x[1], w[a][1], x[0] * w[a][0])));
+      const float ps = wave_multi_sum<AMAX>(pv);
+      const float vs = wave_sum(
+          fmaf(x[3], w[AMAX][3], fmaf(x[2], w[AMAX][2], fmaf(x[1], w[AMAX][1], x[0] * w[AMAX][0]))));
+      const int a = lane >> 3;
+      if ((lane & 7) == 0 && a < A) part[b][c][a] = ps;
+      if (lane == 0) part[b][c][A] = vs;
+    }
+  }
+  __syncthreads();
+  if (tid < NB * PW) {
+    const int b = tid / PW, a = tid % PW;
+    if (b < nb && a <= A) {
+      float s = 0.f;
+      for (int c = 0; c < NCH; ++c) s += part[b][c][a];
+      hsm[b][a] = s;
+    }
+  }
+  __syncthreads();
+  if (tid < nb) {
+    const int row = b0 + tid;
+    float l[AMAX];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a)
+      if (a < A) {
+        l[a] = hsm[tid][a] + hd.bp[a];
+        mx = fmaxf(mx, l[a]);
+      }
+    float se = 0.f;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a)
+      if (a < A) se += expf(l[a] - mx);
+    const float lse = logf(se);
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a)
+      if (a < A) {
+        const float o = (l[a] - mx) - lse;
+        hd.logp[(size_t)row * A + a] = o;
+        if (hd.pi) hd.pi[(size_t)row * A + a] = expf(o);
+      }
+    hd.v[row] = tanhf(hsm[tid][A] + hd.bv[0]);
+  }
+}
+
 // The trunk of one 512-thread block (boards blockIdx.x*NB ...).  `un` is LDS of
 // trunk_union_floats<NB>() floats: conv2's weights are staged there with coalesced float4 loads
 // (each lane then reads its 72 fragments from LDS -- one pass over the 74 KB per block instead of
@@ -56,7 +140,7 @@ constexpr int trunk_union_floats() {
 // per weight generation): each lane loads its 72 weights as 18 coalesced float4 loads, issued
 // first, and the LDS staging of w2 (its bank-conflicted scalar stores and reads, a barrier) is
 // skipped; the registers hold the same values, so the bits are the same.
-template <int NB>
+template <int NB, bool HEADS = false>
 __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards, int B,
                                               const float* __restrict__ w1,
                                               const float* __restrict__ b1,
@@ -65,7 +149,9 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
                                               float* __restrict__ feat, float* un,
                                               unsigned short* __restrict__ apl = nullptr,
                                               float* __restrict__ asc = nullptr,
-                                              const float* __restrict__ w2f = nullptr) {
+                                              const float* __restrict__ w2f = nullptr,
+                                              const TrunkHeads* hd = nullptr) {
+  static_assert(!HEADS || NB <= 4, "HEADS: the rows staged in LDS");
   float* const ob = un;
   constexpr int P = 49, PP = 81, CI = 32;
   constexpr int NT = TTILES[NB];          // 16-row tiles (az_trunk_rows.h order)
@@ -268,6 +354,7 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
         asc[B + b0 + b] = inv;
       }
     }
+    if constexpr (HEADS) trunk_rows_heads<NB>(ob, nb, b0, *hd);   // ob is final since the barrier
   }
 }
 
@@ -289,15 +376,16 @@ __global__ AZ_TRUNK_LB void c4_trunk_kernel(const int8_t* __restrict__ boards, i
 }
 
 // c4_trunk_kernel that also writes feat's rows as output_transform.0's pre-split A (NB <= 4)
-template <int NB>
+// HEADS: also the standard heads of the rows (predict_both above the one-launch trunk + heads size)
+template <int NB, bool HEADS = false>
 __global__ AZ_TRUNK_LB void c4_trunk_split_a_kernel(
     const int8_t* __restrict__ boards, int B, const float* __restrict__ w1,
     const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
     float* __restrict__ feat, unsigned short* __restrict__ apl, float* __restrict__ asc,
-    const float* __restrict__ w2f = nullptr) {
+    const float* __restrict__ w2f = nullptr, TrunkHeads hd = {}) {
   static_assert(NB <= 4, "the A split reads the LDS staging tile");
   __shared__ __attribute__((aligned(16))) float un[trunk_union_floats<NB>()];
-  c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, un, apl, asc, w2f);
+  c4_trunk_tile<NB, HEADS>(boards, B, w1, b1, w2, b2, feat, un, apl, asc, w2f, &hd);
 }
 
 // Generic 3x3 conv + ReLU, one thread per output (TicTacToe trunks: tiny, latency-bound).
@@ -780,7 +868,8 @@ const float* conv2_frags(const float* w2, hipStream_t s);   // az_gemm.hip
 static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
                            const float* conv1_b, const float* conv2_w, const float* conv2_b,
                            float* feat, unsigned short* apl, float* asc, bool* split,
-                           hipStream_t s) {
+                           hipStream_t s, const TrunkHeads* heads = nullptr,
+                           bool* heads_done = nullptr) {
   static const char* env = tuning_env("AZ_TRUNK_NB");   // tuning experiments only
   // boards per block from a fitted time model, t(NB, B) = a(NB) + b(NB) x ceil(blocks / CUs)
   // (one block per CU; blocks = ceil(B / NB)), fitted to the sweep of every NB at B = 256 ..
@@ -809,6 +898,9 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
   if (env) nbk = atoi(env);
   const bool sa = apl && asc && nbk >= 1 && nbk <= 4;
   if (split) *split = sa;
+  // the standard heads ride along when the rows are staged in LDS (the split-A kernel)
+  const bool hk = sa && heads && heads->A >= 1 && heads->A <= 8;
+  if (heads_done) *heads_done = hk;
   // conv2's weights in fragment order when they are registered (cached per weight generation)
   static const bool no_frag = tuning_env("AZ_TRUNK_NO_W2F") != nullptr;   // A/B experiments
   const float* w2f = nbk >= 1 && !no_frag ? conv2_frags(conv2_w, s) : nullptr;
@@ -822,9 +914,12 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
   constexpr size_t dyn = 0;
 #endif
 #define AZ_TRUNK(NB_)                                                                            \
-  if (sa) hipLaunchKernelGGL(c4_trunk_split_a_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), \
-                             dyn, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, apl,   \
-                             asc, w2f);                                                          \
+  if (hk) hipLaunchKernelGGL((c4_trunk_split_a_kernel<NB_, true>), dim3((B + NB_ - 1) / NB_),   \
+                             dim3(512), dyn, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b,   \
+                             feat, apl, asc, w2f, *heads);                                       \
+  else if (sa) hipLaunchKernelGGL(c4_trunk_split_a_kernel<NB_>, dim3((B + NB_ - 1) / NB_),      \
+                                  dim3(512), dyn, s, boards, B, conv1_w, conv1_b, conv2_w,       \
+                                  conv2_b, feat, apl, asc, w2f, TrunkHeads{});                   \
   else hipLaunchKernelGGL(c4_trunk_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), dyn, s,     \
                           boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
 #define AZ_TRUNK_BIG(NB_)                                                                      \
@@ -1288,9 +1383,19 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
                                e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,
                                e->feat, e->logp, pi, v, e->ws, e->ws_bytes, stream);
   } else {
+    // predict_both: the split-A trunk computes the standard heads from its LDS rows
+    // (trunk_rows_heads: az_heads_fwd's bits), else they run after it as az_c4_trunk_heads_fwd
+    // does above 320 rows
+    static const bool no_th = tuning_env("AZ_NO_TRUNK_HEADS") != nullptr;   // A/B experiments
+    const TrunkHeads th{e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,
+                        e->logp, pi, v};
+    bool heads_done = false;
     rc = c4_trunk_launch(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b, e->feat,
-                         R.planes, R.sc, &split, as_stream(stream));
-    if (!rc && v)             // what az_c4_trunk_heads_fwd runs after the trunk above 320 rows
+                         R.planes, R.sc, &split, as_stream(stream),
+                         v && !no_th && aligned16(e->fc_policy_w) && aligned16(e->fc_value_w)
+                             ? &th : nullptr,
+                         &heads_done);
+    if (!rc && v && !heads_done)
       rc = az_heads_fwd(e->feat, 3136, e->feat, 3136, B, 3136, e->fc_policy_w, e->fc_policy_b,
                         e->A, e->fc_value_w, e->fc_value_b, e->logp, pi, v, e->ws, e->ws_bytes,
                         stream);

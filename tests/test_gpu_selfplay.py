@@ -282,6 +282,22 @@ def test_lockstep_engine_parity_at_production_batches(c4, meta, G):
         assert max(st["batch_rows"]) > 64       # really ran the large-batch (x3 GEMM) path
 
 
+@pytest.mark.parametrize("B", [400, 1576, 3150])
+def test_predict_both_standard_heads_from_the_trunk(c4, B):
+    """predict_both above 320 rows: the split-A trunk computes the standard heads from its LDS
+    rows (trunk_rows_heads) -- the same bits as predict_batch, whose heads run as their own
+    launch on feat (az_heads_fwd), and the GNN heads as predict_batch_with_gnn."""
+    rng = np.random.default_rng(B)
+    boards = rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int64)
+    pi, v, gpi, gv = [np.array(x) for x in c4.predict_both_async(boards).result()]   # fused
+    pi1, v1 = [np.array(x) for x in c4.predict_batch_async(boards).result()[:2]]     # separate
+    assert np.array_equal(pi, pi1) and np.array_equal(v.ravel(), v1.ravel())
+    # and within the 1e-5 the evaluator is held to of the torch-op path (own launches)
+    pi2, v2, gpi2, gv2 = c4.predict_both(boards)
+    assert_close(f"predict_both_async/std_pi/B{B}", pi, pi2, 1e-5)
+    assert_close(f"predict_both_async/gnn_v/B{B}", gv.ravel(), np.asarray(gv2).ravel(), 1e-5)
+
+
 def test_batch_row_bit_identity_report(c4):
     """Which batch sizes give a row the batch-1 bits (the premise of exact lock-step parity):
     rows always agree within 1e-5; bit identity is reported."""
