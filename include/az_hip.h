@@ -173,7 +173,9 @@ typedef struct az_c4_eval {
  * reduce writes output_transform.2's, both into the last az_transform_heads_ws_bytes-sized
  * region of e->ws; the GNN tail runs as az_transform_heads_fwd with y = NULL (e->y is not
  * written for B > 8), so the outputs are bit-identical to az_c4_trunk_fwd +
- * az_transform_heads_fwd(y = NULL). */
+ * az_transform_heads_fwd(y = NULL).  Both v and gv above 320 rows (predict_both): the same
+ * hand-off, and the trunk kernel that writes the split operand also forms the standard heads from
+ * the rows in its LDS tile -- bit-identical to az_heads_fwd on feat. */
 int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, float* v,
                    float* gpi, float* gv, void* stream);
 
