@@ -13,3 +13,6 @@ timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $R/bench.log 
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/kt -o step -- python3 bench.py --steps 200 --warmup 20 --no-cpu --no-selfplay --no-grid --no-train --no-b1 --no-aggregate --large-batch 0 > $R/kt.log 2>&1 || exit $?
 echo done > $R/done
+# the self-play leg's kernels (two lanes; durations include the lanes' overlap)
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/sp -o sp -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-grid --no-train --no-b1 --no-aggregate --large-batch 0 --sp-check 0 > $R/sp.log 2>&1 || exit $?
+echo done > $R/done_sp
