@@ -68,6 +68,9 @@ def parse():
                          "sequential reference loop (rank 0; 'agreement')")
     ap.add_argument("--sp-lanes", type=int, default=2,
                     help="engines taking turns so host search overlaps the GPU batch")
+    ap.add_argument("--sp-parallel", type=int, default=0,
+                    help="games in flight at once (a finished game's slot takes the next one); "
+                         "0: all sp-games at once")
     return ap.parse_args()
 
 
@@ -580,7 +583,8 @@ def selfplay_leg(W, G, args, device, rank):
     st = {}
     cg0 = hostcpu.cgroup_cpu_stat()
     t0 = time.perf_counter()
-    out = play_episodes_engine(Connect4Game(7), net, sa, eps, seeds, args.sp_games,
+    par = args.sp_parallel if getattr(args, "sp_parallel", 0) > 0 else args.sp_games
+    out = play_episodes_engine(Connect4Game(7), net, sa, eps, seeds, par,
                                threads=args.sp_threads, stats=st, lanes=lanes)
     dt = time.perf_counter() - t0
     cg1 = hostcpu.cgroup_cpu_stat()
