@@ -1827,9 +1827,12 @@ static bool csk_plan(int M, int N, int K, int cus, double miss_cost, CskPlan& ou
   return found;
 }
 
-// csk_plan memoised per shape: the search walks up to ~10^4 (am, an, bf, at) candidates, tens of
-// microseconds of host time per call -- every lock-step self-play batch (a new M each round, from
-// a few hundred distinct values) launched two such GEMMs
+// csk_plan memoised per shape: the search walks up to ~10^4 (am, an, bf, at) candidates, up to
+// ~1 ms of host time per call.  A plan depends on M only through its 256-row tile count and
+// whether the last tile row has <= 128 rows (csk_plan / csk_make keep no M), so that pair is the
+// key: the lock-step self-play's shrinking batches (a new M nearly every round once games end)
+// then hit the memo instead of re-running the search for every M (~1 ms of host time per round,
+// measured in tools/sp_pipeline_probe.py's timeline)
 static bool csk_plan_cached(int M, int N, int K, int cus, double miss_cost, CskPlan& out) {
   struct Key {
     int M, N, K, cus;
@@ -1846,7 +1849,9 @@ static bool csk_plan_cached(int M, int N, int K, int cus, double miss_cost, CskP
   };
   static std::mutex mu;
   static std::unordered_map<Key, std::pair<bool, CskPlan>, Hash> memo;
-  const Key key{M, N, K, cus, miss_cost};
+  const int mt_n = (M + 255) / 256, rows_last = M - (mt_n - 1) * 256;
+  const int mkey = 2 * mt_n + (mt_n > 1 && rows_last <= 128 ? 1 : 0);   // the plan's M classes
+  const Key key{mkey, N, K, cus, miss_cost};
   {
     std::lock_guard<std::mutex> lk(mu);
     const auto it = memo.find(key);

@@ -461,6 +461,24 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
         ref_ev = torch.cuda.Event(enable_timing=True)
         ref_ev.record()
         gpu_ev = []
+    # The assembler thread runs Python while games finish; with the interpreter's default 5 ms
+    # switch interval the lane loop's next launch waited for the GIL behind it (~1 ms per round
+    # in the phase where most games end: tools/sp_pipeline_probe.py's timeline).  A short
+    # interval hands the GIL back within ~0.2 ms.  AZ_SP_SWITCH_INTERVAL (seconds; 0 keeps the
+    # interpreter's own) for A/B runs.
+    import os
+    import sys
+    sw_old = sys.getswitchinterval()
+    sw = float(os.environ.get("AZ_SP_SWITCH_INTERVAL", "0.0002"))
+    if sw > 0:
+        sys.setswitchinterval(sw)
+    # the cyclic collector paused for the loop: finished games allocate example lists by the
+    # thousand, and a full collection in the middle of a round stalled the next launch
+    # (AZ_SP_GC=1 keeps it running, for A/B runs); reference cycles are collected after the loop
+    import gc
+    gc_was = gc.isenabled()
+    if os.environ.get("AZ_SP_GC") != "1":
+        gc.disable()
     t0 = time.perf_counter()
     t_wait = t_launch = 0.0
     idle = 0
@@ -510,6 +528,9 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
     finally:
         if pool is not None:
             pool.shutdown(wait=True)
+        sys.setswitchinterval(sw_old)
+        if gc_was and not gc.isenabled():
+            gc.enable()
     if tl_on:
         torch.cuda.synchronize()
         for k, e0, e1 in gpu_ev:     # GPU span of each batch, ms from the reference event
