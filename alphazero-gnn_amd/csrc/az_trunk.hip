@@ -1392,7 +1392,9 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
     bool heads_done = false;
     rc = c4_trunk_launch(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b, e->feat,
                          R.planes, R.sc, &split, as_stream(stream),
-                         v && !no_th && aligned16(e->fc_policy_w) && aligned16(e->fc_value_w)
+                         v && e->logp && e->fc_policy_w && e->fc_policy_b && e->fc_value_w &&
+                                 e->fc_value_b && !no_th && aligned16(e->fc_policy_w) &&
+                                 aligned16(e->fc_value_w)
                              ? &th : nullptr,
                          &heads_done);
     if (!rc && v && !heads_done)
