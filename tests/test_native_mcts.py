@@ -240,8 +240,13 @@ def test_native_engine_errors_and_failed_batches():
     # with the GNN path, expand_tree's root predict is unguarded (MCTS.py:108-113): the
     # engine aborts the episode and the driver re-raises the network's exception
     gargs = Args(numMCTSSims=4, cpuct=1.0, tempThreshold=15, use_gnn=True, expand_by=2)
+    import gc
+    import sys
+    sw = sys.getswitchinterval()
     with pytest.raises(RuntimeError, match="device lost"):
         play_episodes_engine(Connect4Game(7), Broken(), gargs, [0], {0: 0}, 1, threads=1)
+    # the lane loop's GIL switch interval and paused collector are restored on the way out
+    assert gc.isenabled() and sys.getswitchinterval() == sw
 
 
 def test_rng_emulation_matches_numpy_randomstate(host_lib):
