@@ -324,6 +324,11 @@ def play_episodes_native(game, nnet, args, episodes, seeds, parallel_games=256, 
     return results
 
 
+# live games per engine thread below which a lane's round uses fewer threads (0, the default:
+# always all; AZ_SP_TAIL_SLOTS_PER_THREAD=16 for the A/B of tools/gpu_sp_tail.sh, unmeasured)
+_TAIL_SLOTS_PER_THREAD = int(os.environ.get("AZ_SP_TAIL_SLOTS_PER_THREAD", "0"))
+
+
 class _EpisodeLane:
     """One native engine running whole episodes in its slots (engine episode mode)."""
 
@@ -380,12 +385,17 @@ class _EpisodeLane:
     def gather(self):
         import time
         t = time.perf_counter()
+        # threads for this round's native pass: fewer once few games are left (each parallel
+        # region wakes every sleeping worker; at the end of the run the work is a few descents)
+        thr = self.threads
+        if _TAIL_SLOTS_PER_THREAD > 0:
+            thr = max(1, min(thr, len(self.running) // _TAIL_SLOTS_PER_THREAD))
         if self.fed is not None:        # last round's rows are fed inside this collect
             pi, v, gpi, gv = self.fed
             self.fed = None
-            self.k = self.eng.feed_collect(self.k, pi, v, gpi, gv, self.threads)
+            self.k = self.eng.feed_collect(self.k, pi, v, gpi, gv, thr)
         else:
-            self.k = self.eng.collect(self.threads)
+            self.k = self.eng.collect(thr)
         self.collect_s += time.perf_counter() - t
         if not self.k:
             return None
