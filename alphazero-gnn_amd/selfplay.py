@@ -325,7 +325,7 @@ def play_episodes_native(game, nnet, args, episodes, seeds, parallel_games=256, 
 
 
 # live games per engine thread below which a lane's round uses fewer threads (0, the default:
-# always all; AZ_SP_TAIL_SLOTS_PER_THREAD=16 for the A/B of tools/gpu_sp_tail.sh, unmeasured)
+# always all; AZ_SP_TAIL_SLOTS_PER_THREAD=16 measured equal in tools/gpu_sp_tail.sh's A/B)
 _TAIL_SLOTS_PER_THREAD = int(os.environ.get("AZ_SP_TAIL_SLOTS_PER_THREAD", "0"))
 
 
