@@ -31,8 +31,14 @@ HOST_FLAGS = ["-O3", "-fPIC", "-shared", "-std=c++17", "-fopenmp", "-ffp-contrac
 OBJ = os.path.join(CSRC, "build")
 SOURCES = ["az_runtime.hip", "az_gemm.hip", "az_trunk.hip", "az_gnn.hip", "az_gnn_fused.hip",
            "az_gnn_band.hip", "az_optim.hip", "az_backward.hip"]
+# No packed-FP32 VALU code (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32): on MI355X a packed op
+# gave wrong low-element results in lanes 48-63 when another workgroup shared the CU (round 6:
+# tools/trunk_selfcheck_probe.py, profiles/r06/trunk_packed_fp32/).  The feature is
+# a device target feature; the host compile ignores it with a one-line note.
+# tests/test_lib_abi.py::test_device_code_has_no_packed_fp32 disassembles both libraries.
+NO_PK_F32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wall",
-         "-Wno-unused-function", "-fno-gpu-rdc"]
+         "-Wno-unused-function", "-fno-gpu-rdc"] + NO_PK_F32
 
 
 def hipcc():
@@ -41,13 +47,24 @@ def hipcc():
             return c
 
 
+def _flags_current(odir):
+    """True when the objects in odir were compiled with today's FLAGS (a flag change rebuilds)."""
+    stamp = os.path.join(odir, "FLAGS")
+    return os.path.exists(stamp) and open(stamp).read() == " ".join(FLAGS)
+
+
+def _stamp_flags(odir):
+    with open(os.path.join(odir, "FLAGS"), "w") as f:
+        f.write(" ".join(FLAGS))
+
+
 def _compile(src, force=False, tuning=False):
     odir = os.path.join(OBJ, "tuning") if tuning else OBJ
     obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
     s = os.path.join(CSRC, src)
     deps = [s, os.path.join(os.path.dirname(PKG), "include", "az_hip.h")] + \
         [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
-    if not force and os.path.exists(obj) and \
+    if not force and os.path.exists(obj) and _flags_current(odir) and \
             all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj
     cmd = [hipcc()] + FLAGS + (["-DAZ_TUNING"] if tuning else []) + ["-c", s, "-o", obj]
@@ -96,6 +113,9 @@ def build(verbose=True, force=False, tuning=True):
     jobs = [(s, False) for s in srcs] + ([(s, True) for s in srcs] if tuning else [])
     with cf.ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
         objs = list(ex.map(lambda j: _compile(j[0], force, j[1]), jobs))
+    _stamp_flags(OBJ)
+    if tuning:
+        _stamp_flags(os.path.join(OBJ, "tuning"))
     changed = _link(objs[:len(srcs)], OUT, force)
     if tuning:
         changed |= _link(objs[len(srcs):], TUNING_OUT, force)

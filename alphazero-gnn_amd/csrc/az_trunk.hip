@@ -21,28 +21,36 @@
 
 namespace az {
 
-// LDS the kernel hands to c4_trunk_tile: conv2's weights while they are read into registers,
-// then (NB <= 4) the NB*3136-float output staging tile, or (NB = 8, no staging) conv1's output
-// `un` always has room for conv2's staged weights, even when the fragment-ordered copy makes the
-// staging unnecessary: that keeps one trunk block per CU.  Smaller blocks (two per CU for NB <= 3,
-// round 5) ran 1.4x faster at self-play sizes but gave WRONG rows, nondeterministically, in
-// blocks that shared a CU with another block (tools/trunk_cmp_probe.py; correct with the same code
-// when extra dynamic LDS forced one block per CU, AZ_TRUNK_DYN_LDS in the tuning build).  Ruled
-// out (tools/trunk_residency_probe.py, tools/probes/lds_alloc_probe.hip, profiles/r05/
-// trunk_residency/): overlapping LDS allocations (HW_REG_LDS_ALLOC: disjoint, no word of a block
-// overwritten by its neighbour, 4- and 16-byte accesses), writes past the static LDS (4-32 KB of
-// extra dynamic LDS with two blocks per CU stay wrong), scratch (none), and the MFMA chain's wait
-// states alone (24 s_nop cycles after every tap: still wrong).  The cause is open, so the layout
-// that rules it out stays.
-template <int NB>
+// LDS the kernel hands to c4_trunk_tile: (unregistered weights only) conv2's weights while they
+// are read into registers, then (NB <= 4) the NB*3136-float output staging tile, or (NB > 4, no
+// staging) conv1's output.  REGW (registered weights: the fragment-ordered copy is loaded straight
+// into registers) drops the 74 KB staging room, so NB <= 3 fits two blocks per CU.
+//
+// Round 5 ran two blocks per CU and got WRONG rows, nondeterministically, in blocks sharing a CU.
+// Round 6 found the cause (tools/trunk_selfcheck_probe.py, profiles/r06/trunk_packed_fp32/):
+// conv1's packed-FP32 fma chain (v_pk_fma_f32, two channels per instruction, the low operand
+// register written by the VALU instruction just before) returned a wrong LOW element in lanes
+// 48-63 -- the wave's last quarter -- only while another workgroup's waves shared the SIMD.
+// The conv1 image was then stored from those values (each thread's re-derivation of its item
+// disagreed with itself in exactly that element).  Every kernel is now compiled without
+// packed-FP32 code (azhip/build.py NO_PK_F32; tests/test_lib_abi.py asserts none is left), and
+// with it the probe finds no mismatch in 12 runs at two blocks per CU.
+#ifdef AZ_TRUNK_SELFCHECK
+__device__ unsigned* g_trunk_chk;   // residency experiment log (az_debug_trunk_chk)
+#endif
+
+template <int NB, bool REGW>
 constexpr int trunk_union_floats() {
   constexpr int after = NB <= 4 ? NB * 3136 : NB * C1_FLOATS_PER_BOARD;
-#ifdef AZ_TRUNK_SMALL_UNION   // residency experiment (tuning build): fragment-ordered weights only
-  return after;
-#else
-  return W2S_FLOATS > after ? W2S_FLOATS : after;
-#endif
+  return REGW || after >= W2S_FLOATS ? after : W2S_FLOATS;
 }
+
+// occupancy asked of the compiler (waves per SIMD): two 8-wave blocks per CU where their LDS fits
+// (REGW, NB <= 3: <= 76 KB per block), else no constraint
+template <int NB, bool REGW>
+constexpr int trunk_waves_per_eu() { return REGW && NB <= 3 ? 4 : 1; }
+template <int NB, bool REGW>
+constexpr int trunk_blocks_per_cu() { return REGW && NB <= 3 ? 2 : 1; }
 
 // The standard heads (Connect4Net.py:48-57: log_softmax(feat wp^T + bp), tanh(feat wv^T + bv)) of
 // the block's feature rows, for predict_both batches whose trunk stages its rows in LDS.
@@ -129,18 +137,18 @@ __device__ __forceinline__ void trunk_rows_heads(const float* ob, int nb, int b0
 }
 
 // The trunk of one 512-thread block (boards blockIdx.x*NB ...).  `un` is LDS of
-// trunk_union_floats<NB>() floats: conv2's weights are staged there with coalesced float4 loads
+// trunk_union_floats<NB, REGW>() floats: conv2's weights are staged there with coalesced float4 loads
 // (each lane then reads its 72 fragments from LDS -- one pass over the 74 KB per block instead of
 // 72 scattered 4-byte loads per lane in all 8 waves), and with NB <= 4 the feature rows are then
 // assembled in it (still there on return).
 // apl / asc (NB <= 4 only; may be null): the feature rows also leave as the P2 GEMM's A operand
 // for output_transform.0 (PreSplitA: two fp16 planes [2][B][3136] and scales [2][B], the bits
 // h3_split_rows_kernel would make of feat), so that GEMM needs no split launch of its own.
-// w2f (may be null): conv2's weights already in fragment order (az_gemm.hip conv2_frags, cached
-// per weight generation): each lane loads its 72 weights as 18 coalesced float4 loads, issued
-// first, and the LDS staging of w2 (its bank-conflicted scalar stores and reads, a barrier) is
-// skipped; the registers hold the same values, so the bits are the same.
-template <int NB, bool HEADS = false>
+// REGW: w2f (non-null) is conv2's weights already in fragment order (az_gemm.hip conv2_frags,
+// cached per weight generation): each lane loads its 72 weights as 18 coalesced float4 loads,
+// issued first, and the LDS staging of w2 (its bank-conflicted scalar stores and reads, a barrier)
+// is skipped; the registers hold the same values, so the bits are the same.  !REGW: w2f unused.
+template <int NB, bool HEADS = false, bool REGW = false>
 __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards, int B,
                                               const float* __restrict__ w1,
                                               const float* __restrict__ b1,
@@ -183,7 +191,7 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   constexpr int NW2 = 64 * 72 / 512;
   f32x4v wst[NW2];
   float breg[72];   // step s = tap * 8 + j takes channel ci = 8h + j of tap (lane group h)
-  if (w2f) {
+  if constexpr (REGW) {
 #pragma unroll
     for (int q = 0; q < 18; ++q) {
       const f32x4v v = reinterpret_cast<const f32x4v*>(w2f)[(nt * 18 + q) * 64 + lane];
@@ -207,7 +215,7 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   const float w1v = tid < CI * 9 ? w1[tid] : b1[min(tid - CI * 9, CI - 1)];
   const float bias = b2[co];
   __builtin_amdgcn_sched_barrier(0);   // no load sinks into the guarded stores below
-  if (!w2f) {
+  if constexpr (!REGW) {
 #pragma unroll
     for (int j = 0; j < NW2; ++j) {
       const int i = tid + 512 * j;
@@ -220,7 +228,7 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
     bd[min(tid + 512 * j, NB * PP)] = bdin[j] ? (float)bdv[j] : 0.f;   // use sinks the load
   w1s[min(tid, CI * 9 + CI)] = w1v;     // unguarded: lanes past the 320 weights hit the pad
   __syncthreads();
-  if (!w2f) {
+  if constexpr (!REGW) {
 #pragma unroll
     for (int s = 0; s < 72; ++s) {
       const int tap = s >> 3, ci = 8 * h + (s & 7);
@@ -229,7 +237,7 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   }
   bf16x8 bh[9], bl[9];
   const float iw = w2_planes(breg, bh, bl);
-  if constexpr (!STAGE) __syncthreads();   // conv1's output overwrites the weights in `un`
+  if constexpr (!STAGE && !REGW) __syncthreads();   // conv1's output overwrites the weights in `un`
   // conv1: (board, padded position, channel octet) items, kept in registers until each board's
   // maximum (its plane scale) is known
   constexpr int NI = NB * PP * 4, NIT = (NI + 511) / 512;
@@ -271,6 +279,52 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
     }
   }
   __syncthreads();
+#ifdef AZ_TRUNK_SELFCHECK
+  // residency experiment: every thread re-derives conv1 item i (conv1_octet + the split, the
+  // same arithmetic) and compares the two 16-B units of the image in LDS; mismatches are logged
+  // to g_trunk_chk (vector atomics only): [0] = count, then 8 words per entry
+  auto c1_check = [&](int phase, int i) {
+    if (i >= NI || !g_trunk_chk) return;
+    const int b = i / (PP * 4), r = i - b * (PP * 4);
+    float v[8], v2[8];
+    conv1_octet(w1s, bd + b * PP, r >> 2, r & 3, v);
+    asm volatile("" ::: "memory");
+    conv1_octet(w1s, bd + b * PP, r >> 2, r & 3, v2);
+    float mx = c1wmax[b][0];
+    for (int w = 1; w < 8; ++w) mx = fmaxf(mx, c1wmax[b][w]);
+    float inv;
+    const float sa = h3_scale(mx, H3_TA, &inv);
+    u32x4 o[2];
+    split2s(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, sa, o);
+    const u32x4* u = reinterpret_cast<const u32x4*>(c1 + b * C1_FLOATS_PER_BOARD) +
+                     C1_UNITS_PER_POS * (r >> 2) + (r & 3);
+    const u32x4 x0 = u[0], x1 = u[4];
+    int nbad = 0, nconv = 0;
+    for (int e = 0; e < 4; ++e) nbad += (x0[e] != o[0][e]) + (x1[e] != o[1][e]);
+    for (int e = 0; e < 8; ++e) nconv += __float_as_uint(v[e]) != __float_as_uint(v2[e]);
+    if (nbad || nconv) {
+      const unsigned k = atomicAdd(g_trunk_chk, 1u);
+      if (k < 2048) {
+        unsigned* d = g_trunk_chk + 64 + 48 * k;
+        d[0] = blockIdx.x; d[1] = tid; d[2] = i; d[3] = phase;
+        d[4] = nbad; d[5] = nconv;
+        d[6] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));   // HW_ID
+        d[7] = __float_as_uint(sa);
+        for (int e = 0; e < 4; ++e) {
+          d[8 + e] = x0[e]; d[12 + e] = x1[e];
+          d[16 + e] = o[0][e]; d[20 + e] = o[1][e];
+        }
+        for (int e = 0; e < 8; ++e) {
+          d[24 + e] = __float_as_uint(v[e]);
+          d[32 + e] = __float_as_uint(v2[e]);
+        }
+      }
+    }
+  };
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) c1_check(0, tid + 512 * it);       // own item
+  c1_check(1, (tid + 192) % (NIT * 512));                           // another wave's item
+#endif
 
   // the wave's row tiles go in pairs (mt, mt + 2) with their two MFMA chains interleaved: each
   // chain keeps its own k order (same sums as one tile at a time), but the pipeline now has two
@@ -327,6 +381,10 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
       }
     }
     __syncthreads();
+#ifdef AZ_TRUNK_SELFCHECK
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) c1_check(2, tid + 512 * it);     // the image at the end
+#endif
     f32x4v* dst = reinterpret_cast<f32x4v*>(feat + (size_t)b0 * 3136);
     const f32x4v* src = reinterpret_cast<const f32x4v*>(ob);
     if (!apl) {
@@ -358,34 +416,33 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
   }
 }
 
-#ifdef AZ_TRUNK_SMALL_UNION
-#define AZ_TRUNK_LB __launch_bounds__(512, 4)
-#else
-#define AZ_TRUNK_LB __launch_bounds__(512)
-#endif
-template <int NB>
-__global__ AZ_TRUNK_LB void c4_trunk_kernel(const int8_t* __restrict__ boards, int B,
+// REGW selects the registered-weights form (w2f non-null; `un` without the weight staging room)
+#define AZ_TRUNK_LB(NB_, REGW_)                                                                  \
+  __attribute__((amdgpu_flat_work_group_size(1, 512),                                            \
+                 amdgpu_waves_per_eu(trunk_waves_per_eu<NB_, REGW_>())))
+template <int NB, bool REGW = false>
+__global__ AZ_TRUNK_LB(NB, REGW) void c4_trunk_kernel(const int8_t* __restrict__ boards, int B,
                                                       const float* __restrict__ w1,
                                                       const float* __restrict__ b1,
                                                       const float* __restrict__ w2,
                                                       const float* __restrict__ b2,
                                                       float* __restrict__ feat,
                                                       const float* __restrict__ w2f = nullptr) {
-  __shared__ __attribute__((aligned(16))) float un[trunk_union_floats<NB>()];
-  c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, un, nullptr, nullptr, w2f);
+  __shared__ __attribute__((aligned(16))) float un[trunk_union_floats<NB, REGW>()];
+  c4_trunk_tile<NB, false, REGW>(boards, B, w1, b1, w2, b2, feat, un, nullptr, nullptr, w2f);
 }
 
 // c4_trunk_kernel that also writes feat's rows as output_transform.0's pre-split A (NB <= 4)
 // HEADS: also the standard heads of the rows (predict_both above the one-launch trunk + heads size)
-template <int NB, bool HEADS = false>
-__global__ AZ_TRUNK_LB void c4_trunk_split_a_kernel(
+template <int NB, bool HEADS = false, bool REGW = false>
+__global__ AZ_TRUNK_LB(NB, REGW) void c4_trunk_split_a_kernel(
     const int8_t* __restrict__ boards, int B, const float* __restrict__ w1,
     const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
     float* __restrict__ feat, unsigned short* __restrict__ apl, float* __restrict__ asc,
     const float* __restrict__ w2f = nullptr, TrunkHeads hd = {}) {
   static_assert(NB <= 4, "the A split reads the LDS staging tile");
-  __shared__ __attribute__((aligned(16))) float un[trunk_union_floats<NB>()];
-  c4_trunk_tile<NB, HEADS>(boards, B, w1, b1, w2, b2, feat, un, apl, asc, w2f, &hd);
+  __shared__ __attribute__((aligned(16))) float un[trunk_union_floats<NB, REGW>()];
+  c4_trunk_tile<NB, HEADS, REGW>(boards, B, w1, b1, w2, b2, feat, un, apl, asc, w2f, &hd);
 }
 
 // Generic 3x3 conv + ReLU, one thread per output (TicTacToe trunks: tiny, latency-bound).
@@ -845,7 +902,7 @@ __global__ __launch_bounds__(512) void c4_trunk_heads_kernel(
     float* __restrict__ feat, const float* __restrict__ wp, const float* __restrict__ bp, int A,
     const float* __restrict__ wv, const float* __restrict__ bv, float* __restrict__ logp,
     float* __restrict__ pi, float* __restrict__ v) {
-  __shared__ __attribute__((aligned(16))) float ob[trunk_union_floats<NB>()];
+  __shared__ __attribute__((aligned(16))) float ob[trunk_union_floats<NB, false>()];
   __shared__ float part[HEADS_ROWS_MAXC * 9];
   __shared__ float sm[9];
   c4_trunk_tile<NB>(boards, B, w1, b1, w2, b2, feat, ob);
@@ -871,8 +928,8 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
                            hipStream_t s, const TrunkHeads* heads = nullptr,
                            bool* heads_done = nullptr) {
   static const char* env = tuning_env("AZ_TRUNK_NB");   // tuning experiments only
-  // boards per block from a fitted time model, t(NB, B) = a(NB) + b(NB) x ceil(blocks / CUs)
-  // (one block per CU; blocks = ceil(B / NB)), fitted to the sweep of every NB at B = 256 ..
+  // boards per block from a fitted time model, t(NB, B) = a(NB) + b(NB) x ceil(blocks / slots)
+  // (slots = CUs x blocks per CU; blocks = ceil(B / NB)), fitted to the sweep of every NB at B = 256 ..
   // 4,096 on MI355X (profiles/r05/trunk_nb_sweep.txt, every NB bit-identical); when the caller
   // wants output_transform.0's A pre-split (apl), NB > 4 pays the separate split pass (~3.8 ns
   // per board).  B = 512 -> 2 (13.4 us), 768 -> 3, 1,024 -> 4, 1,576 -> 4, 3,150 -> 3 (63 us;
@@ -884,14 +941,23 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
            n > 0) ? n : 256;
   }
+  // conv2's weights in fragment order when they are registered (cached per weight generation):
+  // the REGW kernels, whose smaller LDS puts two blocks on a CU for NB <= 3
+  static const bool no_frag = tuning_env("AZ_TRUNK_NO_W2F") != nullptr;   // A/B experiments
+  const float* w2f = B > 8 && !no_frag ? conv2_frags(conv2_w, s) : nullptr;
+  const bool regw = w2f != nullptr;
   int nbk = 0;
   if (B > 8) {
+    // a(NB) + b(NB) x rounds; b2: the per-round time when two blocks share each CU
     static const float ta[9] = {0.f, 2.f, 2.6f, 3.7f, 3.5f, 3.f, 0.f, 0.f, 0.f};
     static const float tb[9] = {0.f, 7.6f, 10.8f, 11.8f, 15.5f, 22.f, 26.f, 30.5f, 33.f};
+    static const float tb2[4] = {0.f, 9.6f, 14.f, 17.5f};
     float best = 0.f;
     for (int nb = 1; nb <= 8; ++nb) {
-      const long rounds = ((long)(B + nb - 1) / nb + cus - 1) / cus;
-      const float t = ta[nb] + (float)rounds * tb[nb] + (apl && nb > 4 ? 0.0038f * B : 0.f);
+      const int per_cu = regw && nb <= 3 ? 2 : 1;
+      const long rounds = ((long)(B + nb - 1) / nb + (long)cus * per_cu - 1) / ((long)cus * per_cu);
+      const float t = ta[nb] + (float)rounds * (per_cu == 2 ? tb2[nb] : tb[nb]) +
+                      (apl && nb > 4 ? 0.0038f * B : 0.f);
       if (nb == 1 || t < best) best = t, nbk = nb;
     }
   }
@@ -901,30 +967,30 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
   // the standard heads ride along when the rows are staged in LDS (the split-A kernel)
   const bool hk = sa && heads && heads->A >= 1 && heads->A <= 8;
   if (heads_done) *heads_done = hk;
-  // conv2's weights in fragment order when they are registered (cached per weight generation)
-  static const bool no_frag = tuning_env("AZ_TRUNK_NO_W2F") != nullptr;   // A/B experiments
-  const float* w2f = nbk >= 1 && !no_frag ? conv2_frags(conv2_w, s) : nullptr;
-#ifdef AZ_TRUNK_SMALL_UNION
-  if (nbk >= 1 && nbk <= 4 && !w2f) return AZ_EINVAL;   // `un` has no room for staged weights
-#endif
 #ifdef AZ_TUNING   // AZ_TRUNK_DYN_LDS=<bytes>: extra (unused) LDS per block, to limit residency
   static const char* env_dyn = tuning_env("AZ_TRUNK_DYN_LDS");
   const size_t dyn = env_dyn ? (size_t)atol(env_dyn) : 0;
 #else
   constexpr size_t dyn = 0;
 #endif
+#define AZ_TRUNK_RW(NB_, RW_)                                                                    \
+  if (hk) hipLaunchKernelGGL((c4_trunk_split_a_kernel<NB_, true, RW_>),                          \
+                             dim3((B + NB_ - 1) / NB_), dim3(512), dyn, s, boards, B, conv1_w,  \
+                             conv1_b, conv2_w, conv2_b, feat, apl, asc, w2f, *heads);            \
+  else if (sa) hipLaunchKernelGGL((c4_trunk_split_a_kernel<NB_, false, RW_>),                    \
+                                  dim3((B + NB_ - 1) / NB_), dim3(512), dyn, s, boards, B,      \
+                                  conv1_w, conv1_b, conv2_w, conv2_b, feat, apl, asc, w2f,      \
+                                  TrunkHeads{});                                                 \
+  else hipLaunchKernelGGL((c4_trunk_kernel<NB_, RW_>), dim3((B + NB_ - 1) / NB_), dim3(512),    \
+                          dyn, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
 #define AZ_TRUNK(NB_)                                                                            \
-  if (hk) hipLaunchKernelGGL((c4_trunk_split_a_kernel<NB_, true>), dim3((B + NB_ - 1) / NB_),   \
-                             dim3(512), dyn, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b,   \
-                             feat, apl, asc, w2f, *heads);                                       \
-  else if (sa) hipLaunchKernelGGL(c4_trunk_split_a_kernel<NB_>, dim3((B + NB_ - 1) / NB_),      \
-                                  dim3(512), dyn, s, boards, B, conv1_w, conv1_b, conv2_w,       \
-                                  conv2_b, feat, apl, asc, w2f, TrunkHeads{});                   \
-  else hipLaunchKernelGGL(c4_trunk_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), dyn, s,     \
-                          boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
-#define AZ_TRUNK_BIG(NB_)                                                                      \
-  hipLaunchKernelGGL(c4_trunk_kernel<NB_>, dim3((B + NB_ - 1) / NB_), dim3(512), dyn, s, boards, \
-                     B, conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
+  if (regw) { AZ_TRUNK_RW(NB_, true) } else { AZ_TRUNK_RW(NB_, false) }
+#define AZ_TRUNK_BIG(NB_)                                                                        \
+  if (regw) hipLaunchKernelGGL((c4_trunk_kernel<NB_, true>), dim3((B + NB_ - 1) / NB_),         \
+                               dim3(512), dyn, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b, \
+                               feat, w2f);                                                       \
+  else hipLaunchKernelGGL((c4_trunk_kernel<NB_, false>), dim3((B + NB_ - 1) / NB_), dim3(512),  \
+                          dyn, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, nullptr);
   switch (nbk) {
     case 8: AZ_TRUNK_BIG(8) break;
     case 7: AZ_TRUNK_BIG(7) break;
@@ -940,10 +1006,17 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
     default: AZ_TRUNK(1)
   }
 #undef AZ_TRUNK
+#undef AZ_TRUNK_RW
 #undef AZ_TRUNK_BIG
   return check_launch("c4_trunk_kernel");
 }
 }  // namespace az
+
+#ifdef AZ_TRUNK_SELFCHECK
+extern "C" int az_debug_trunk_chk(void* log) {   // residency experiment library only
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_trunk_chk), &log, sizeof(log)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int az_c4_trunk_fwd(const int8_t* boards, int B, const float* conv1_w,
                                const float* conv1_b, const float* conv2_w, const float* conv2_b,

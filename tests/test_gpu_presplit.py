@@ -66,3 +66,29 @@ def test_c4_gnn_eval_unregistered_weights(ev):
     assert torch.equal(logp, logp_u) and torch.equal(pi, pi_u) and torch.equal(v, v_u)
     # registered vs unregistered storage of the same values: the same bits (same planes)
     assert torch.equal(pi, pi_r) and torch.equal(v, v_r)
+
+
+@pytest.mark.parametrize("B", [200, 500, 600, 1000, 1200, 1576, 1700, 3150, 4100])
+def test_c4_trunk_two_blocks_per_cu_equals_one(ev, B):
+    """Registered weights take the REGW trunk kernels, whose LDS (no conv2 staging room) puts two
+    512-thread blocks on a CU for NB <= 3; unregistered copies take the one-block-per-CU form.
+    Round 5 saw wrong rows whenever two trunk blocks shared a CU; the cause was packed-FP32 VALU
+    code (no longer emitted).  Both forms must give the same bits at every NB the
+    rounds model picks, twice in a row (the failure was nondeterministic), and match the oracle."""
+    from azhip import ops
+    from oracle import nets as O
+    Wn = ev.nnet.params
+    Wc = {k: Wn[k].clone() for k in Wn.keys()}
+    rng = np.random.default_rng(B + 1)
+    bnp = rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int8)
+    boards = torch.from_numpy(bnp).cuda()
+    reg = [ops.c4_trunk(boards, Wn) for _ in range(2)]
+    unreg = ops.c4_trunk(boards, Wc)
+    torch.cuda.synchronize()
+    for f in reg:
+        bad = torch.nonzero((f != unreg).any(1)).flatten().tolist()
+        assert not bad, f"B={B}: {len(bad)} rows differ, first {bad[:8]}"
+    sel = np.r_[0:4, B // 2:B // 2 + 4, B - 4:B]
+    W64 = {k: Wn[k].double().cpu().numpy() for k in Wn.keys()}
+    np.testing.assert_allclose(reg[0][torch.from_numpy(sel).cuda()].cpu().numpy(),
+                               O.c4_features(bnp[sel], W64), atol=1e-5, rtol=1e-5)

@@ -114,3 +114,54 @@ def test_unsupported_action_size_rejected_up_front():
     from tictactoe.TicTacToeGame import TicTacToeGame
     with pytest.raises(ValueError, match="action size 37"):
         TicTacToeGNNWrapper(TicTacToeGame(6), {"use_gnn": True, "gnn_layers": 2})
+
+
+def _device_code_objects(so_path):
+    """The gfx950 code objects inside a HIP shared library: its .hip_fatbin section is one
+    clang offload bundle per translation unit (-fno-gpu-rdc), each a header of (offset, size,
+    target triple) entries."""
+    import struct
+    import subprocess
+    import tempfile
+    objcopy = "/opt/rocm/lib/llvm/bin/llvm-objcopy"
+    with tempfile.TemporaryDirectory() as td:
+        fat = os.path.join(td, "fat.bin")
+        subprocess.run([objcopy, "--dump-section", f".hip_fatbin={fat}", so_path, os.devnull],
+                       check=True, capture_output=True)
+        blob = open(fat, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    out, pos = [], blob.find(magic)
+    while pos >= 0:
+        n = struct.unpack_from("<Q", blob, pos + 24)[0]
+        p = pos + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", blob, p)
+            triple = blob[p + 24:p + 24 + tlen].decode()
+            p += 24 + tlen
+            if "gfx950" in triple:
+                out.append(blob[pos + off:pos + off + size])
+        pos = blob.find(magic, pos + 32)
+    return out
+
+
+@pytest.mark.parametrize("name", ["libaz_hip.so", "libaz_hip_tuning.so"])
+def test_device_code_has_no_packed_fp32(built, name, tmp_path):
+    """Regression guard for the round-6 finding (azhip/build.py NO_PK_F32): packed-FP32
+    VALU instructions (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32) returned wrong low elements in
+    lanes 48-63 on MI355X while another workgroup shared the CU, so no kernel may contain one."""
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("no ROCm llvm-objdump")
+    so = os.path.join(os.path.dirname(built), name)
+    cos = _device_code_objects(so)
+    assert len(cos) >= 7, f"{name}: {len(cos)} gfx950 code objects"   # every kernel source
+    total = 0
+    for i, co in enumerate(cos):
+        p = tmp_path / f"co{i}.o"
+        p.write_bytes(co)
+        dis = subprocess.run([objdump, "-d", str(p)], capture_output=True, text=True,
+                             check=True).stdout
+        assert "v_mfma" in dis or "s_endpgm" in dis
+        total += len(re.findall(r"\bv_pk_(?:fma|mul|add|mov)_f32\b", dis))
+    assert total == 0, f"{name}: {total} packed-FP32 instructions"
