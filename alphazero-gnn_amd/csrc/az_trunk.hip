@@ -928,12 +928,10 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
                            hipStream_t s, const TrunkHeads* heads = nullptr,
                            bool* heads_done = nullptr) {
   static const char* env = tuning_env("AZ_TRUNK_NB");   // tuning experiments only
-  // boards per block from a fitted time model, t(NB, B) = a(NB) + b(NB) x ceil(blocks / slots)
-  // (slots = CUs x blocks per CU; blocks = ceil(B / NB)), fitted to the sweep of every NB at B = 256 ..
-  // 4,096 on MI355X (profiles/r05/trunk_nb_sweep.txt, every NB bit-identical); when the caller
+  // boards per block from a fitted time model (below; every NB is bit-identical); when the caller
   // wants output_transform.0's A pre-split (apl), NB > 4 pays the separate split pass (~3.8 ns
-  // per board).  B = 512 -> 2 (13.4 us), 768 -> 3, 1,024 -> 4, 1,576 -> 4, 3,150 -> 3 (63 us;
-  // the round-4 kernel took 85 at NB = 7), 4,096 -> 8
+  // per board).  Registered weights: B = 512 -> 2 (12.2 us), 1,024 -> 2, 1,576 -> 2 (28.7 us;
+  // 33.2 at one block per CU in round 5), 3,150 -> 3 (44.3 us; 62.7), 4,096 -> 3 (51.7 us; 68.2)
   static int cus = 0;
   if (cus <= 0) {
     int dev = 0, n = 0;
@@ -948,16 +946,19 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
   const bool regw = w2f != nullptr;
   int nbk = 0;
   if (B > 8) {
-    // a(NB) + b(NB) x rounds; b2: the per-round time when two blocks share each CU
-    static const float ta[9] = {0.f, 2.f, 2.6f, 3.7f, 3.5f, 3.f, 0.f, 0.f, 0.f};
-    static const float tb[9] = {0.f, 7.6f, 10.8f, 11.8f, 15.5f, 22.f, 26.f, 30.5f, 33.f};
-    static const float tb2[4] = {0.f, 9.6f, 14.f, 17.5f};
+    // t = a(NB) + b(NB) x k, k = ceil(blocks / CUs) blocks per CU.  Registered weights (REGW,
+    // two blocks per CU for NB <= 3): refitted to profiles/r06/trunk_nb_sweep.txt; unregistered
+    // (one block per CU, conv2 staged through LDS): the round-5 fit
+    static const float ra[9] = {0.f, 4.3f, 5.f, 7.3f, 2.5f, 1.5f, 0.f, 0.f, 0.5f};
+    static const float rb[9] = {0.f, 4.1f, 5.95f, 7.3f, 14.3f, 22.f, 26.f, 29.7f, 32.5f};
+    static const float ua[9] = {0.f, 2.f, 2.6f, 3.7f, 3.5f, 3.f, 0.f, 0.f, 0.f};
+    static const float ub[9] = {0.f, 7.6f, 10.8f, 11.8f, 15.5f, 22.f, 26.f, 30.5f, 33.f};
+    const float* ta = regw ? ra : ua;
+    const float* tb = regw ? rb : ub;
     float best = 0.f;
     for (int nb = 1; nb <= 8; ++nb) {
-      const int per_cu = regw && nb <= 3 ? 2 : 1;
-      const long rounds = ((long)(B + nb - 1) / nb + (long)cus * per_cu - 1) / ((long)cus * per_cu);
-      const float t = ta[nb] + (float)rounds * (per_cu == 2 ? tb2[nb] : tb[nb]) +
-                      (apl && nb > 4 ? 0.0038f * B : 0.f);
+      const long k = ((long)(B + nb - 1) / nb + cus - 1) / cus;
+      const float t = ta[nb] + (float)k * tb[nb] + (apl && nb > 4 ? 0.0038f * B : 0.f);
       if (nb == 1 || t < best) best = t, nbk = nb;
     }
   }

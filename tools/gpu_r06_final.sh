@@ -1,8 +1,8 @@
-# GPU-box, round 5: the round-end evidence at HEAD -- the whole GPU suite (margins reported),
+# GPU-box, round 6: the evidence at HEAD -- the whole GPU suite (margins reported),
 # smoke(), the driver's bench command, and a kernel trace (--stats) of the B = 512 step.
-#   bash tools/gpu_r05_final.sh TAG
+#   bash tools/gpu_r06_final.sh TAG
 set -u
-TAG=${1:-r05final}
+TAG=${1:-r06final}
 cd "$GRAFT_REPO_ROOT"
 R=gpurun_out/$TAG
 mkdir -p $R
