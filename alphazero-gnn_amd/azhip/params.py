@@ -68,7 +68,9 @@ class FlatParams:
         Every such write bumps the flat buffer's version counter (views share it), so comparing
         it with the one seen at the last sync finds them; every forward entry point calls this
         (one attribute read when nothing changed).  Writes by the library's own kernels
-        (az_adam_f32) announce themselves."""
+        (az_adam_f32) announce themselves.  Not seen: writes through `.data` and collectives
+        that write parameter views in place (dist.broadcast / all_reduce) leave the version
+        counter alone -- such a path calls weights_changed() (or copy_flat_) itself."""
         v = self.flat._version
         if v != self._seen:
             weights_changed()

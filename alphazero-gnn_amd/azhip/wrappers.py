@@ -628,6 +628,16 @@ class NetWrapper:
         world, rank = D.world_rank()
         sync = nets._args_get(self.args, "gnn_grad_sync", "row0")
         n = self.args.batch_size
+        # every rank must probe the same jobs (each runs barriers and an all_reduce sized by
+        # the job list): keep the kinds of examples every rank holds
+        have = torch.tensor([1.0 if examples else 0.0,
+                             1.0 if (self.has_gnn and gnn_examples) else 0.0],
+                            dtype=torch.float64, device=self.device)
+        dist.all_reduce(have, op=dist.ReduceOp.MIN)
+        if have[0].item() == 0.0:
+            examples = []
+        if have[1].item() == 0.0:
+            gnn_examples = []
         jobs = {}
         if examples:
             sel = examples[:n]

@@ -4183,7 +4183,8 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
       ok = csk_plan_cached(a.M, a.N, a.K, cus, CSK_MISS_COST, cq);
 #endif
       const int mp = use_csk && ok ? csk_max_pieces(cq) : 0;
-      if (use_csk && ok && a.he.part && whole && (p2 || h3) &&
+      // the finalize gives each lane one whole 64-column block of a row: N % 64 == 0, N <= 4,096
+      if (use_csk && ok && a.he.part && whole && (p2 || h3) && a.N % 64 == 0 && a.N <= 64 * 64 &&
           (size_t)a.M * (a.N / 64) * mp * HEADS_TILE_SLOTS * 4 * 2 <= ws_bytes &&
           (size_t)4 * (a.N / 64) * mp * HEADS_TILE_SLOTS * 4 <= 65536) {   // finalize's LDS
         // the heads from the pieces (az_x3.h HeadsEpi, stream-K slots): no fix-up, no C

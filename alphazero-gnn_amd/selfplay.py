@@ -484,7 +484,10 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
         sys.setswitchinterval(sw)
     # the cyclic collector paused for the loop: finished games allocate example lists by the
     # thousand, and a full collection in the middle of a round stalled the next launch
-    # (AZ_SP_GC=1 keeps it running, for A/B runs); reference cycles are collected after the loop
+    # (AZ_SP_GC=1 keeps it running, for A/B runs); reference cycles are collected after the loop.
+    # The switch interval and the collector are process-wide: the lane loop owns them while it
+    # runs, so one play_episodes_engine call at a time per process (the Coach and the bench
+    # call it from one thread).
     import gc
     gc_was = gc.isenabled()
     if os.environ.get("AZ_SP_GC") != "1":
@@ -541,6 +544,7 @@ def play_episodes_engine(game, nnet, args, episodes, seeds, parallel_games=1024,
         sys.setswitchinterval(sw_old)
         if gc_was and not gc.isenabled():
             gc.enable()
+            gc.collect()      # the reference cycles the paused collector left behind
     if tl_on:
         torch.cuda.synchronize()
         for k, e0, e1 in gpu_ev:     # GPU span of each batch, ms from the reference event

@@ -380,8 +380,11 @@ int az_adam_f32(float* p, const float* g, float* m, float* v, int64_t n,
  * registered weights any way other than az_adam_f32 (which calls it) -- an optimizer step of its
  * own, loading a checkpoint, copying buffers -- must call it before the next GEMM on them.
  * A missed call is NOT a precision loss: above 64 rows the GEMM multiplies by the cached planes,
- * i.e. it returns the PREVIOUS weights' result.  (azhip/params.py FlatParams calls it for every
- * torch-side write, found through the buffer's version counter.) */
+ * i.e. it returns the PREVIOUS weights' result.  (azhip/params.py FlatParams calls it for the
+ * torch-side writes that bump the buffer's version counter -- in-place ops on the parameter
+ * tensors -- and from copy_flat_ / weights_changed().  Writes through `.data`, and collectives
+ * that write parameter views in place (dist.broadcast / all_reduce), do not bump it: such a
+ * path must call FlatParams.weights_changed() itself.) */
 int az_weights_changed(void);
 
 /* Parameter storage: [base, base + bytes) holds weights whose values change only where

@@ -1103,3 +1103,41 @@ def test_heads_small_batch_bit_identical(ops, A, K):
             assert torch.equal(a, r[:B])
         np.testing.assert_allclose(got[0].cpu().numpy(), lp64[:B].numpy(), atol=1e-5)
         np.testing.assert_allclose(got[2].cpu().numpy(), v64[:B].numpy(), atol=1e-5)
+
+
+@pytest.mark.parametrize("F", [288, 4160])
+@pytest.mark.parametrize("registered", [False, True])
+def test_linear_heads_without_y_any_width(ops, F, registered):
+    """az_linear_heads_fwd with y = NULL at a stream-K batch size (B = 1,576) and widths the
+    stream-K heads epilogue cannot take (its finalize gives each lane one whole 64-column block:
+    F = 288 leaves a half block, F = 4,160 is 65 blocks): the call falls back to a path that forms
+    y, so the heads equal the y path within 2e-6 and fp64 (Connect4GNN.py:48-57 on
+    gnn_utils.py:115's last Linear) within 1e-5."""
+    B, A = 1576, 8
+    g = torch.Generator().manual_seed(F + registered)
+    x = torch.rand((B, F), generator=g) * 2 - 1
+    w = (torch.rand((F, F), generator=g) * 2 - 1) / F ** 0.5
+    b = (torch.rand((F,), generator=g) - 0.5) * 0.1
+    wp = (torch.rand((A, F), generator=g) * 2 - 1) / F ** 0.5
+    wv = (torch.rand((1, F), generator=g) * 2 - 1) / F ** 0.5
+    bp, bv = torch.rand((A,), generator=g) - 0.5, torch.rand((1,), generator=g) - 0.5
+    c = [t.cuda() for t in (x, w, b, wp, bp, wv, bv)]
+    unreg = [_registered(c[1])] if registered else []
+    try:
+        logp, pi, v, y = ops.linear_heads(*c)
+        tl, tp, tv, ty = ops.linear_heads(*c, want_y=False)
+        torch.cuda.synchronize()
+    finally:
+        for u in unreg:
+            u()
+    assert ty is None
+    assert_close(f"heads_any_width/F{F}/r{int(registered)}/logp_vs_y_path", tl.cpu().numpy(),
+                 logp.cpu().numpy(), 2e-6)
+    assert_close(f"heads_any_width/F{F}/r{int(registered)}/v_vs_y_path", tv.cpu().numpy(),
+                 v.cpu().numpy(), 2e-6)
+    yd = x.double() @ w.double().T + b.double()
+    lg = yd @ wp.double().T + bp.double()
+    olp = (lg - torch.logsumexp(lg, 1, keepdim=True)).numpy()
+    ov = torch.tanh(yd @ wv.double().T + bv.double()).flatten().numpy()
+    assert_close(f"heads_any_width/F{F}/r{int(registered)}/logp_vs_fp64", tl.cpu().numpy(), olp, 1e-5)
+    assert_close(f"heads_any_width/F{F}/r{int(registered)}/v_vs_fp64", tv.cpu().numpy(), ov, 1e-5)
