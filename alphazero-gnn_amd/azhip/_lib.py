@@ -117,6 +117,17 @@ SIGNATURES = {
                                        ctypes.POINTER(LayerW), c_void_p, c_void_p]),
     "az_gnn_layer_fwd": (c_int, [ctypes.POINTER(Graph), c_void_p, c_int, c_int,
                                  ctypes.POINTER(LayerW), c_void_p, c_void_p, c_size_t, c_void_p]),
+    "az_gnn_node_update_ws_bytes": (c_size_t, [c_int, c_int]),
+    "az_gnn_node_update_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                       c_void_p]),
+    "az_gnn_node_update_bwd_ws_bytes": (c_size_t, [c_int, c_int]),
+    "az_gnn_node_update_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                       c_void_p]),
     "az_mlp2_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "az_transform_heads_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
@@ -152,6 +163,8 @@ SIGNATURES = {
                             c_size_t, c_void_p]),
     "az_adam_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_double, c_double,
                             c_double, c_double, c_int, c_void_p]),
+    "az_adam_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_double, c_double,
+                             c_double, c_double, c_int, c_void_p]),
     "az_weights_changed": (c_int, []),
     "az_weights_register": (c_int, [c_void_p, c_size_t]),
     "az_weights_unregister": (c_int, [c_void_p]),

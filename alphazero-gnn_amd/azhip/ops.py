@@ -361,6 +361,48 @@ def gnn_layer(g, x, Wl, out=None, ws=None, H=128, save=True):
     return out, ws
 
 
+def gnn_node_update(x, agg, Wl, dst_rows=None, out=None, save=None):
+    """GNNLayer's gated node update alone (az_gnn_node_update_fwd, gnn_utils.py:18-28,67-74):
+    out[d] = x[d] + sigmoid(Wg [x_d; agg_d] + bg) * (Wu2 relu(Wu1 [x_d; agg_d] + bu1) + bu2) on
+    the destination rows dst_rows (int32 device tensor; None = every row), out = x elsewhere.
+    Returns (out, save); save [3][D][F] feeds gnn_node_update_bwd."""
+    V, F = x.shape
+    D = V if dst_rows is None else int(dst_rows.numel())
+    out = torch.empty_like(x) if out is None else out
+    save = torch.empty((3, D, F), device=x.device) if save is None else save
+    L = _lib.lib()
+    ws = workspace(x.device, int(L.az_gnn_node_update_ws_bytes(D, F)))
+    _lib.check(L.az_gnn_node_update_fwd(
+        _p(x), _p(agg), V, F, D, None if dst_rows is None else _p(dst_rows),
+        _p(Wl["gate.0.weight"]), _p(Wl["gate.0.bias"]), _p(Wl["update_net.0.weight"]),
+        _p(Wl["update_net.0.bias"]), _p(Wl["update_net.2.weight"]), _p(Wl["update_net.2.bias"]),
+        _p(out), _p(save), _p(ws), ctypes.c_size_t(ws.numel()), _stream()),
+        "az_gnn_node_update_fwd")
+    return out, save
+
+
+NODE_UPDATE_KEYS = ("gate.0.weight", "gate.0.bias", "update_net.0.weight", "update_net.0.bias",
+                    "update_net.2.weight", "update_net.2.bias")
+
+
+def gnn_node_update_bwd(x, agg, Wl, save, dout, grads, dst_rows=None, dx=None, dagg=None):
+    """az_gnn_node_update_bwd: dx (dout + the update's x-gradient on destination rows), dagg
+    (destination rows; others zero here) and the six parameter gradients into grads (dict with
+    NODE_UPDATE_KEYS).  Returns (dx, dagg)."""
+    V, F = x.shape
+    D = V if dst_rows is None else int(dst_rows.numel())
+    dx = torch.empty_like(x) if dx is None else dx
+    dagg = torch.zeros_like(x) if dagg is None else dagg
+    L = _lib.lib()
+    ws = workspace(x.device, int(L.az_gnn_node_update_bwd_ws_bytes(D, F)))
+    _lib.check(L.az_gnn_node_update_bwd(
+        _p(x), _p(agg), V, F, D, None if dst_rows is None else _p(dst_rows),
+        _p(Wl["gate.0.weight"]), _p(Wl["update_net.0.weight"]), _p(Wl["update_net.2.weight"]),
+        _p(save), _p(dout), _p(dx), _p(dagg), *[_p(grads[k]) for k in NODE_UPDATE_KEYS],
+        _p(ws), ctypes.c_size_t(ws.numel()), _stream()), "az_gnn_node_update_bwd")
+    return dx, dagg
+
+
 def gnn_layer_ot(g, x, Wl, w0, b0, w2, b2, out=None, ws=None, H=128):
     """The network's last GNNLayer followed by output_transform, eval mode
     (az_gnn_layer_ot_infer: one band-kernel launch on band graphs).  Returns (y, ws)."""
@@ -499,8 +541,8 @@ def linear_heads(x, w, b, wp, bp, wv, bv, y=None, logp=None, pi=None, v=None, wa
 
 def adam(p, g, m, v, lr, step, beta1=0.9, beta2=0.999, eps=1e-8):
     L = _lib.lib()
-    _lib.check(L.az_adam_f32(_p(p), _p(g), _p(m), _p(v), p.numel(), lr, beta1, beta2, eps, step,
-                             _stream()), "az_adam_f32")
+    _lib.check(L.az_adam_step(_p(p), _p(g), _p(m), _p(v), p.numel(), lr, beta1, beta2, eps, step,
+                             _stream()), "az_adam_step")
 
 
 # ----------------------------------------------------------------------------- backward

@@ -606,6 +606,79 @@ static BwdWs carve_bwd(void* ws, int V, int E, int D, int F, int H) {
   return w;
 }
 
+// The node update's backward (az_gnn_node_update_bwd, and az_gnn_layer_bwd's first half):
+// from dout (rows of the D destinations) and the forward's gate / u1 / u, the six parameter
+// gradients and dc = d[x_d ; agg_d] ([D][2F], compact destination rows).  Scratch du, dg, du1
+// ([D][F] each), part (colsum partials), split (GEMM split-K room).
+static int node_update_bwd(const float* x, const float* agg, int D, int F, const int* rows,
+                           const float* gate_w, const float* upd_w1, const float* upd_w2,
+                           const float* gate, const float* u1, const float* u,
+                           const float* dout, float* d_gate_w, float* d_gate_b, float* d_upd_w1,
+                           float* d_upd_b1, float* d_upd_w2, float* d_upd_b2, float* du,
+                           float* dg, float* du1, float* dc, float* part, void* split,
+                           size_t split_bytes, hipStream_t s) {
+  int rc;
+  const long DF = (long)D * F;
+  hipLaunchKernelGGL(gnn_gate_bwd_kernel, dim3(grid_for(DF)), dim3(256), 0, s, dout, D, F, rows,
+                     gate, u, du, dg);
+  if ((rc = check_launch("gnn_gate_bwd_kernel"))) return rc;
+
+  az_gemm_desc d = {};
+  // du1pre = (du . Wu2) * (u1 > 0)
+  d.M = D; d.N = F; d.K = F;
+  d.A = du; d.lda = F; d.a_kmajor = 1;
+  d.B = upd_w2; d.ldb = F; d.b_kmajor = 0;
+  d.act = AZ_ACT_DRELU; d.G = u1; d.ldg = F;
+  d.C = du1; d.ldc = F; d.ws = split; d.ws_bytes = split_bytes;
+  if ((rc = gemm_f32(&d, s))) return rc;
+  // dWu2 = du^T u1 ; dbu2 = colsum(du)
+  d = {};
+  d.M = F; d.N = F; d.K = D;
+  d.A = du; d.lda = F; d.a_kmajor = 0;
+  d.B = u1; d.ldb = F; d.b_kmajor = 0;
+  d.C = d_upd_w2; d.ldc = F; d.ws = split; d.ws_bytes = split_bytes;
+  if ((rc = gemm_f32(&d, s))) return rc;
+  if ((rc = colsum(du, D, F, F, d_upd_b2, 0.f, part, s))) return rc;
+  // dW{u1,g} = d{u1,g}pre^T [x_dst | agg_dst] (two column halves) ; biases
+  const float* pre_in[2] = {du1, dg};
+  float* wout[2] = {d_upd_w1, d_gate_w};
+  float* bout[2] = {d_upd_b1, d_gate_b};
+  for (int t = 0; t < 2; ++t) {
+    for (int half = 0; half < 2; ++half) {
+      d = {};
+      d.M = F; d.N = F; d.K = D;
+      d.A = pre_in[t]; d.lda = F; d.a_kmajor = 0;
+      d.B = half == 0 ? x : agg; d.ldb = F; d.b_kmajor = 0; d.b_rows = rows;
+      d.C = wout[t] + half * F; d.ldc = 2 * F; d.ws = split; d.ws_bytes = split_bytes;
+      if ((rc = gemm_f32(&d, s))) return rc;
+    }
+    if ((rc = colsum(pre_in[t], D, F, F, bout[t], 0.f, part, s))) return rc;
+  }
+  // dc = du1pre . Wu1 + dgpre . Wg      [D][2F]
+  d = {};
+  d.M = D; d.N = 2 * F; d.K = F;
+  d.A = du1; d.lda = F; d.a_kmajor = 1;
+  d.B = upd_w1; d.ldb = 2 * F; d.b_kmajor = 0;
+  d.C = dc; d.ldc = 2 * F; d.ws = split; d.ws_bytes = split_bytes;
+  if ((rc = gemm_f32(&d, s))) return rc;
+  d.A = dg; d.B = gate_w; d.beta = 1.f;
+  return gemm_f32(&d, s);
+}
+
+// dagg[dst_r] = dc[r][F:2F] (the agg half of dc, onto the destination rows)
+__global__ __launch_bounds__(256) void gnn_dc_agg_scatter_kernel(const float* __restrict__ dc,
+                                                                int D, int F,
+                                                                const int* __restrict__ rows,
+                                                                float* __restrict__ dagg) {
+  const long total = (long)D * F;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int j = i % F;
+    const long r = i / F;
+    const long d = rows ? rows[r] : r;
+    dagg[d * F + j] = dc[r * 2 * F + F + j];
+  }
+}
+
 extern "C" size_t az_gnn_layer_bwd_ws_bytes(int V, int E, int D, int F, int H) {
   return align256((size_t)D * F * 4) * 3 + align256((size_t)D * 2 * F * 4) +
          align256((size_t)E * 4) * 3 + align256((size_t)V * 2 * H * 4) +
@@ -649,50 +722,11 @@ extern "C" int az_gnn_layer_bwd(const az_graph* g, const float* x, int F, int H,
     return check_launch("hipMemsetAsync");
   }
   const long DF = (long)D * F;
-  hipLaunchKernelGGL(gnn_gate_bwd_kernel, dim3(grid_for(DF)), dim3(256), 0, s, dout, D, F, rows,
-                     sv.gate, sv.u, L.du, L.dg);
-  if ((rc = check_launch("gnn_gate_bwd_kernel"))) return rc;
-
-  az_gemm_desc d = {};
-  // du1pre = (du . Wu2) * (u1 > 0)
-  d.M = D; d.N = F; d.K = F;
-  d.A = L.du; d.lda = F; d.a_kmajor = 1;
-  d.B = w->upd_w2; d.ldb = F; d.b_kmajor = 0;
-  d.act = AZ_ACT_DRELU; d.G = sv.u1; d.ldg = F;
-  d.C = L.du1; d.ldc = F; d.ws = L.split; d.ws_bytes = kBwdSplitBytes;
-  if ((rc = gemm_f32(&d, s))) return rc;
-  // dWu2 = du^T u1 ; dbu2 = colsum(du)
-  d = {};
-  d.M = F; d.N = F; d.K = D;
-  d.A = L.du; d.lda = F; d.a_kmajor = 0;
-  d.B = sv.u1; d.ldb = F; d.b_kmajor = 0;
-  d.C = gr->upd_w2; d.ldc = F; d.ws = L.split; d.ws_bytes = kBwdSplitBytes;
-  if ((rc = gemm_f32(&d, s))) return rc;
-  if ((rc = colsum(L.du, D, F, F, gr->upd_b2, 0.f, L.part, s))) return rc;
-  // dW{u1,g} = d{u1,g}pre^T [x_dst | agg_dst] (two column halves) ; biases
-  const float* pre_in[2] = {L.du1, L.dg};
-  float* wout[2] = {gr->upd_w1, gr->gate_w};
-  float* bout[2] = {gr->upd_b1, gr->gate_b};
-  for (int t = 0; t < 2; ++t) {
-    for (int half = 0; half < 2; ++half) {
-      d = {};
-      d.M = F; d.N = F; d.K = D;
-      d.A = pre_in[t]; d.lda = F; d.a_kmajor = 0;
-      d.B = half == 0 ? x : sv.agg; d.ldb = F; d.b_kmajor = 0; d.b_rows = rows;
-      d.C = wout[t] + half * F; d.ldc = 2 * F; d.ws = L.split; d.ws_bytes = kBwdSplitBytes;
-      if ((rc = gemm_f32(&d, s))) return rc;
-    }
-    if ((rc = colsum(pre_in[t], D, F, F, bout[t], 0.f, L.part, s))) return rc;
-  }
-  // dc = du1pre . Wu1 + dgpre . Wg      [D][2F]
-  d = {};
-  d.M = D; d.N = 2 * F; d.K = F;
-  d.A = L.du1; d.lda = F; d.a_kmajor = 1;
-  d.B = w->upd_w1; d.ldb = 2 * F; d.b_kmajor = 0;
-  d.C = L.dc; d.ldc = 2 * F; d.ws = L.split; d.ws_bytes = kBwdSplitBytes;
-  if ((rc = gemm_f32(&d, s))) return rc;
-  d.A = L.dg; d.B = w->gate_w; d.beta = 1.f;
-  if ((rc = gemm_f32(&d, s))) return rc;
+  if ((rc = node_update_bwd(x, sv.agg, D, F, rows, w->gate_w, w->upd_w1, w->upd_w2, sv.gate,
+                            sv.u1, sv.u, dout, gr->gate_w, gr->gate_b, gr->upd_w1, gr->upd_b1,
+                            gr->upd_w2, gr->upd_b2, L.du, L.dg, L.du1, L.dc, L.part, L.split,
+                            kBwdSplitBytes, s)))
+    return rc;
   hipLaunchKernelGGL(gnn_dc_scatter_kernel, dim3(grid_for(DF)), dim3(256), 0, s, L.dc, D, F, rows,
                      dx);
   if ((rc = check_launch("gnn_dc_scatter_kernel"))) return rc;
@@ -715,7 +749,7 @@ extern "C" int az_gnn_layer_bwd(const az_graph* g, const float* x, int F, int H,
                      sv.P, w->att_b1, w->att_w2, L.dsc, L.an, L.dc, F, L.dP, dx);
   if ((rc = check_launch("gnn_attn_bwd_nodes_kernel"))) return rc;
   // dW1' = dP^T x  (W1 [H][2F] viewed as [2H][F]) ; dx += dP . W1'
-  d = {};
+  az_gemm_desc d = {};
   d.M = 2 * H; d.N = F; d.K = V;
   d.A = L.dP; d.lda = 2 * H; d.a_kmajor = 0;
   d.B = x; d.ldb = F; d.b_kmajor = 0;
@@ -740,6 +774,67 @@ extern "C" int az_gnn_layer_bwd(const az_graph* g, const float* x, int F, int H,
   hipLaunchKernelGGL(colsum_final_kernel, dim3(1), dim3(256), 0, s, L.part + 2 * H, nch, 2 * H + 1,
                      1, 0.f, gr->att_b2);
   return check_launch("attn param grads");
+}
+
+// ------------------------------------------------------------------------------ node update bwd
+static size_t node_update_bwd_part_bytes(int D, int F) {
+  return align256((size_t)colsum_chunks(D) * (size_t)F * 4);
+}
+
+extern "C" size_t az_gnn_node_update_bwd_ws_bytes(int D, int F) {
+  return align256((size_t)D * F * 4) * 3 + align256((size_t)D * 2 * F * 4) +
+         node_update_bwd_part_bytes(D, F) + kBwdSplitBytes;
+}
+
+extern "C" int az_gnn_node_update_bwd(const float* x, const float* agg, int V, int F, int D,
+                                      const int* dst_rows, const float* gate_w,
+                                      const float* upd_w1, const float* upd_w2,
+                                      const float* save, const float* dout, float* dx,
+                                      float* dagg, float* d_gate_w, float* d_gate_b,
+                                      float* d_upd_w1, float* d_upd_b1, float* d_upd_w2,
+                                      float* d_upd_b2, void* ws, size_t ws_bytes, void* stream) {
+  AZ_REQUIRE(V >= 0 && D >= 0 && D <= V && F > 0 && F % 16 == 0, AZ_EINVAL,
+             "az_gnn_node_update_bwd: V=%d D=%d F=%d (D <= V, F %% 16)", V, D, F);
+  if (V == 0) return AZ_OK;
+  AZ_REQUIRE(x && agg && save && dout && dx && dagg && ws && (D == V || dst_rows), AZ_EINVAL,
+             "az_gnn_node_update_bwd: bad pointers");
+  AZ_REQUIRE(gate_w && upd_w1 && upd_w2 && d_gate_w && d_gate_b && d_upd_w1 && d_upd_b1 &&
+                 d_upd_w2 && d_upd_b2,
+             AZ_EINVAL, "az_gnn_node_update_bwd: null weight / gradient");
+  AZ_REQUIRE(ws_bytes >= az_gnn_node_update_bwd_ws_bytes(D, F), AZ_EINVAL,
+             "az_gnn_node_update_bwd: workspace too small");
+  hipStream_t s = as_stream(stream);
+  // identity path: every row passes dout straight through (x_out[v] = x[v] + ...)
+  if (hipMemcpyAsync(dx, dout, (size_t)V * F * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return check_launch("hipMemcpyAsync");
+  if (D == 0) {
+    hipMemsetAsync(d_upd_w1, 0, (size_t)F * 2 * F * 4, s);
+    hipMemsetAsync(d_upd_b1, 0, (size_t)F * 4, s);
+    hipMemsetAsync(d_upd_w2, 0, (size_t)F * F * 4, s);
+    hipMemsetAsync(d_upd_b2, 0, (size_t)F * 4, s);
+    hipMemsetAsync(d_gate_w, 0, (size_t)F * 2 * F * 4, s);
+    hipMemsetAsync(d_gate_b, 0, (size_t)F * 4, s);
+    return check_launch("hipMemsetAsync");
+  }
+  const int* rows = (D == V) ? nullptr : dst_rows;
+  const size_t DF = (size_t)D * F;
+  char* p = static_cast<char*>(ws);
+  float* du = reinterpret_cast<float*>(p); p += align256(DF * 4);
+  float* dg = reinterpret_cast<float*>(p); p += align256(DF * 4);
+  float* du1 = reinterpret_cast<float*>(p); p += align256(DF * 4);
+  float* dc = reinterpret_cast<float*>(p); p += align256(2 * DF * 4);
+  float* part = reinterpret_cast<float*>(p); p += node_update_bwd_part_bytes(D, F);
+  int rc;
+  if ((rc = node_update_bwd(x, agg, D, F, rows, gate_w, upd_w1, upd_w2, save, save + DF,
+                            save + 2 * DF, dout, d_gate_w, d_gate_b, d_upd_w1, d_upd_b1, d_upd_w2,
+                            d_upd_b2, du, dg, du1, dc, part, p, kBwdSplitBytes, s)))
+    return rc;
+  hipLaunchKernelGGL(gnn_dc_scatter_kernel, dim3(grid_for((long)DF)), dim3(256), 0, s, dc, D, F,
+                     rows, dx);
+  if ((rc = check_launch("gnn_dc_scatter_kernel"))) return rc;
+  hipLaunchKernelGGL(gnn_dc_agg_scatter_kernel, dim3(grid_for((long)DF)), dim3(256), 0, s, dc, D,
+                     F, rows, dagg);
+  return check_launch("gnn_dc_agg_scatter_kernel");
 }
 
 // ------------------------------------------------------------------------------ mlp2 bwd

@@ -504,6 +504,38 @@ FwdSaved fwd_saved(const void* ws, int V, int E, int D, int F, int H) {
   return FwdSaved{L.P, L.alpha, L.agg, L.gate, L.u1, L.u};
 }
 
+// GNNLayer's gated node update (gnn_utils.py:18-28 gate / update_net, :67-74) for the D
+// destinations (rows dst_rows, or every row when D == V): c = [x_d ; agg_d],
+// gate = sigmoid(Wg c + bg), u1 = relu(Wu1 c + bu1), u = Wu2 u1 + bu2 (kept, pre-gate, for the
+// backward pass), x_out[d] = x[d] + gate * u.  Rows of x_out outside the destinations are the
+// caller's (az_gnn_layer_fwd / az_gnn_node_update_fwd copy x there first).
+int node_update(const float* x, const float* agg, int V, int F, int D, const int* dst_rows,
+                const float* gate_w, const float* gate_b, const float* upd_w1,
+                const float* upd_b1, const float* upd_w2, const float* upd_b2, float* x_out,
+                float* gate, float* u1, float* u, void* split, size_t split_bytes,
+                hipStream_t s) {
+  int rc;
+  az_gemm_desc c = {};
+  c.M = D; c.N = F; c.K = 2 * F;
+  c.A = x; c.lda = F; c.a_kmajor = 1; c.A2 = agg; c.lda2 = F; c.K0 = F;
+  c.a_rows = (D == V) ? nullptr : dst_rows;
+  c.b_kmajor = 1; c.ldb = 2 * F; c.ldc = F;
+  c.ws = split; c.ws_bytes = split_bytes;
+  c.B = gate_w; c.bias = gate_b; c.act = AZ_ACT_SIGMOID; c.C = gate;
+  if ((rc = gemm_f32(&c, s))) return rc;
+  c.B = upd_w1; c.bias = upd_b1; c.act = AZ_ACT_RELU; c.C = u1;
+  if ((rc = gemm_f32(&c, s))) return rc;
+  az_gemm_desc o = {};
+  o.M = D; o.N = F; o.K = F;
+  o.A = u1; o.lda = F; o.a_kmajor = 1;
+  o.B = upd_w2; o.ldb = F; o.b_kmajor = 1; o.bias = upd_b2;
+  o.R = x; o.ldr = F; o.G = gate; o.ldg = F;
+  o.C2 = u; o.ldc2 = F;  // pre-gate update, kept for the backward pass
+  o.C = x_out; o.ldc = F; o.c_rows = (D == V) ? nullptr : dst_rows;
+  o.ws = split; o.ws_bytes = split_bytes;
+  return gemm_f32(&o, s);
+}
+
 }  // namespace az
 
 using namespace az;
@@ -573,27 +605,41 @@ extern "C" int az_gnn_layer_fwd(const az_graph* g, const float* x, int F, int H,
       return rc;
     if ((rc = aggregate(g, x, F, F, L.alpha, L.agg, F, s))) return rc;
   }
-  // 4. gate = sigmoid(Wg [x_d; agg_d] + bg), u1 = relu(Wu1 [x_d; agg_d] + bu1)
-  az_gemm_desc c = {};
-  c.M = g->D; c.N = F; c.K = 2 * F;
-  c.A = x; c.lda = F; c.a_kmajor = 1; c.A2 = L.agg; c.lda2 = F; c.K0 = F;
-  c.a_rows = (g->D == g->V) ? nullptr : g->dst_rows;
-  c.b_kmajor = 1; c.ldb = 2 * F; c.ldc = F;
-  c.ws = L.split; c.ws_bytes = kSplitWsBytes;
-  c.B = w->gate_w; c.bias = w->gate_b; c.act = AZ_ACT_SIGMOID; c.C = L.gate;
-  if ((rc = gemm_f32(&c, s))) return rc;
-  c.B = w->upd_w1; c.bias = w->upd_b1; c.act = AZ_ACT_RELU; c.C = L.u1;
-  if ((rc = gemm_f32(&c, s))) return rc;
-  // 5. x_out[d] = x[d] + gate * (Wu2 u1 + bu2)
-  az_gemm_desc o = {};
-  o.M = g->D; o.N = F; o.K = F;
-  o.A = L.u1; o.lda = F; o.a_kmajor = 1;
-  o.B = w->upd_w2; o.ldb = F; o.b_kmajor = 1; o.bias = w->upd_b2;
-  o.R = x; o.ldr = F; o.G = L.gate; o.ldg = F;
-  o.C2 = L.u; o.ldc2 = F;  // pre-gate update, kept for the backward pass
-  o.C = x_out; o.ldc = F; o.c_rows = (g->D == g->V) ? nullptr : g->dst_rows;
-  o.ws = L.split; o.ws_bytes = kSplitWsBytes;
-  return gemm_f32(&o, s);
+  // 4.-5. the gated node update of the D destinations
+  return node_update(x, L.agg, g->V, F, g->D, g->dst_rows, w->gate_w, w->gate_b, w->upd_w1,
+                     w->upd_b1, w->upd_w2, w->upd_b2, x_out, L.gate, L.u1, L.u, L.split,
+                     kSplitWsBytes, s);
+}
+
+extern "C" size_t az_gnn_node_update_ws_bytes(int D, int F) {
+  (void)D;
+  (void)F;
+  return kSplitWsBytes;
+}
+
+extern "C" int az_gnn_node_update_fwd(const float* x, const float* agg, int V, int F, int D,
+                                      const int* dst_rows, const float* gate_w,
+                                      const float* gate_b, const float* upd_w1,
+                                      const float* upd_b1, const float* upd_w2,
+                                      const float* upd_b2, float* x_out, float* save, void* ws,
+                                      size_t ws_bytes, void* stream) {
+  AZ_REQUIRE(V >= 0 && D >= 0 && D <= V && F > 0 && F % 16 == 0, AZ_EINVAL,
+             "az_gnn_node_update_fwd: V=%d D=%d F=%d (D <= V, F %% 16)", V, D, F);
+  if (V == 0) return AZ_OK;
+  AZ_REQUIRE(x && agg && x_out && save && ws && x != x_out && (D == V || dst_rows), AZ_EINVAL,
+             "az_gnn_node_update_fwd: bad pointers");
+  AZ_REQUIRE(gate_w && gate_b && upd_w1 && upd_b1 && upd_w2 && upd_b2, AZ_EINVAL,
+             "az_gnn_node_update_fwd: null weight");
+  AZ_REQUIRE(ws_bytes >= az_gnn_node_update_ws_bytes(D, F), AZ_EINVAL,
+             "az_gnn_node_update_fwd: workspace too small");
+  hipStream_t s = as_stream(stream);
+  if (D < V &&
+      hipMemcpyAsync(x_out, x, (size_t)V * F * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return check_launch("hipMemcpyAsync");
+  if (D == 0) return AZ_OK;
+  const size_t DF = (size_t)D * F;
+  return node_update(x, agg, V, F, D, dst_rows, gate_w, gate_b, upd_w1, upd_b1, upd_w2, upd_b2,
+                     x_out, save, save + DF, save + 2 * DF, ws, ws_bytes, s);
 }
 
 extern "C" size_t az_gnn_layer_infer_ws_bytes(const az_graph* g, int F, int H) {

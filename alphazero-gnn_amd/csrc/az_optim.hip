@@ -106,3 +106,9 @@ extern "C" int az_adam_f32(float* p, const float* g, float* m, float* v, int64_t
   }
   return check_launch("adam_kernel");
 }
+
+// SURVEY.md §8b's name for the optimizer entry point: the same arguments, the same kernel.
+extern "C" int az_adam_step(float* p, const float* g, float* m, float* v, int64_t n, double lr,
+                            double beta1, double beta2, double eps, int step, void* stream) {
+  return az_adam_f32(p, g, m, v, n, lr, beta1, beta2, eps, step, stream);
+}

@@ -306,6 +306,24 @@ int az_gnn_source_proj_fwd(const az_graph* g, const float* x, int F, int H,
 int az_gnn_layer_fused_fwd(const az_graph* g, const float* x, const float* Ps, int F, int H,
                            const az_gnn_layer_w* w, float* x_out, void* stream);
 
+/* GNNLayer's gated node update on its own (gnn_utils.py:18-28 gate / update_net, :67-74), for a
+ * caller that computes the attention and the aggregation itself (SURVEY §8b
+ * az_gnn_node_update_fwd).  The destinations are dst_rows[0..D) -- the rows the reference's
+ * destination mask selects; D == V with dst_rows NULL means every row:
+ *   c = [x_d ; agg_d],  gate = sigmoid(Wg c + bg),  u1 = relu(Wu1 c + bu1),  u = Wu2 u1 + bu2,
+ *   x_out[d] = x[d] + gate * u,  x_out[v] = x[v] on every other row.
+ * x, agg, x_out: [V][F] (agg read on the destination rows only); x_out may not alias x;
+ * F % 16 == 0.  gate_w / upd_w1: [F][2F], upd_w2: [F][F] (nn.Linear layout).
+ * save: [3][D][F] written (gate, u1, u), read by az_gnn_node_update_bwd.
+ * ws >= az_gnn_node_update_ws_bytes(D, F).  The same GEMMs, in the same order, as the update
+ * inside az_gnn_layer_fwd. */
+size_t az_gnn_node_update_ws_bytes(int D, int F);
+int az_gnn_node_update_fwd(const float* x, const float* agg, int V, int F, int D,
+                           const int* dst_rows, const float* gate_w, const float* gate_b,
+                           const float* upd_w1, const float* upd_b1, const float* upd_w2,
+                           const float* upd_b2, float* x_out, float* save, void* ws,
+                           size_t ws_bytes, void* stream);
+
 /* output_transform, gnn_utils.py:101-105,115: y = W2 relu(W0 x + b0) + b2 on M rows.
  * hidden: [M][F] scratch (kept for the backward pass); ws: optional split-K workspace. */
 int az_mlp2_fwd(const float* x, int M, int F, const float* w0, const float* b0,
@@ -359,6 +377,18 @@ size_t az_gnn_layer_bwd_ws_bytes(int V, int E, int D, int F, int H);
 int az_gnn_layer_bwd(const az_graph* g, const float* x, int F, int H, const az_gnn_layer_w* w,
                      const void* fwd_ws, const float* dout, float* dx,
                      const az_gnn_layer_grads* gr, void* ws, size_t ws_bytes, void* stream);
+/* az_gnn_node_update_fwd's backward: from dout [V][F] and the forward's `save`:
+ *   dx [V][F]   = dout on every row, + d/dx_d of the update on the destination rows;
+ *   dagg [V][F] = d/dagg_d on the destination rows (other rows are not written);
+ * and the six parameter gradients (written, same layout as the weights).
+ * ws >= az_gnn_node_update_bwd_ws_bytes(D, F). */
+size_t az_gnn_node_update_bwd_ws_bytes(int D, int F);
+int az_gnn_node_update_bwd(const float* x, const float* agg, int V, int F, int D,
+                           const int* dst_rows, const float* gate_w, const float* upd_w1,
+                           const float* upd_w2, const float* save, const float* dout, float* dx,
+                           float* dagg, float* d_gate_w, float* d_gate_b, float* d_upd_w1,
+                           float* d_upd_b1, float* d_upd_w2, float* d_upd_b2, void* ws,
+                           size_t ws_bytes, void* stream);
 /* output_transform backward (gnn_utils.py:101-105): dW2, db2, dW0, db0, dh (scratch [M][F])
  * and dx (nullable).  ws >= az_colsum_ws_bytes(M, F) (+ split-K room). */
 int az_mlp2_bwd(const float* x, int M, int F, const float* w0, const float* w2,
@@ -373,6 +403,9 @@ int az_mlp2_bwd(const float* x, int M, int F, const float* w0, const float* w2,
  * --------------------------------------------------------------------------------- */
 int az_adam_f32(float* p, const float* g, float* m, float* v, int64_t n,
                 double lr, double beta1, double beta2, double eps, int step, void* stream);
+/* The same call under SURVEY §8b's name (reference: torch.optim.Adam.step, Connect4GNN.py:187-197). */
+int az_adam_step(float* p, const float* g, float* m, float* v, int64_t n,
+                 double lr, double beta1, double beta2, double eps, int step, void* stream);
 
 /* Parameters changed: every cached per-row weight scale and fp16 weight plane of the fp16 GEMM
  * form (az_gemm_f32's large K-major GEMMs on registered weights, below) is recomputed before its

@@ -376,3 +376,66 @@ def test_report_margins():
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "grad_round_margins.json"), "w") as f:
             json.dump(dict(sorted(MARGINS.items(), key=lambda kv: -kv[1])), f, indent=1)
+
+
+@pytest.mark.parametrize("V,F,D", [(40, 3136, 1), (500, 64, 350), (256, 64, 256)])
+def test_node_update_alone_fwd_bwd(lib, V, F, D):
+    """az_gnn_node_update_fwd / _bwd, the gated update of GNNLayer alone
+    (gnn_utils.py:18-28,67-74) for a caller that keeps its own attention and aggregation:
+    forward against oracle.nets.node_update (float64) at 1e-5 on the destination rows and
+    bit-equal to x elsewhere; dx, dagg and the six parameter gradients against float64 autograd
+    (check_grad's criterion).  (40, 3136, 1) is the reference's star shape (row 0 the only
+    destination), the others a sparse and a full destination set."""
+    import torch.nn.functional as Fn
+    from azhip import ops
+    from oracle import nets as O
+    rng = np.random.default_rng(V + F + D)
+    rows = np.sort(rng.choice(V, D, replace=False)).astype(np.int32) if D < V else None
+    x0 = rng.uniform(-1, 1, (V, F)).astype(np.float32)
+    a0 = rng.uniform(-1, 1, (V, F)).astype(np.float32)
+    dout = rng.standard_normal((V, F)).astype(np.float32)
+    shapes = {"gate.0.weight": (F, 2 * F), "gate.0.bias": (F,), "update_net.0.weight": (F, 2 * F),
+              "update_net.0.bias": (F,), "update_net.2.weight": (F, F), "update_net.2.bias": (F,)}
+    W = {k: (rng.uniform(-1, 1, s) / np.sqrt(s[-1] if len(s) > 1 else F)).astype(np.float32)
+         for k, s in shapes.items()}
+    Wd = {k: cu(v) for k, v in W.items()}
+    rd = None if rows is None else cu(rows)
+    x, agg = cu(x0), cu(a0)
+    out, save = ops.gnn_node_update(x, agg, Wd, dst_rows=rd)
+    grads = {k: torch.empty_like(v) for k, v in Wd.items()}
+    dx, dagg = ops.gnn_node_update_bwd(x, agg, Wd, save, cu(dout), grads, dst_rows=rd)
+    torch.cuda.synchronize()
+    sel = np.arange(V) if rows is None else rows
+    L = {k: v.astype(np.float64) for k, v in W.items()}
+    ref = O.node_update(x0[sel].astype(np.float64), a0[sel].astype(np.float64), L)
+    np.testing.assert_allclose(out.cpu().numpy()[sel], ref, atol=1e-5, rtol=0)
+    others = np.setdiff1d(np.arange(V), sel)
+    assert torch.equal(out[cu(others.astype(np.int64))], x[cu(others.astype(np.int64))])
+
+    idx = torch.from_numpy(sel.astype(np.int64))
+
+    def run(P, dtype, xt=None, at=None):
+        xt = torch.from_numpy(x0).to(dtype) if xt is None else xt
+        at = torch.from_numpy(a0).to(dtype) if at is None else at
+        c = torch.cat([xt[idx], at[idx]], 1)
+        g = torch.sigmoid(Fn.linear(c, P["gate.0.weight"], P["gate.0.bias"]))
+        u = torch.relu(Fn.linear(c, P["update_net.0.weight"], P["update_net.0.bias"]))
+        u = Fn.linear(u, P["update_net.2.weight"], P["update_net.2.bias"])
+        o = xt.index_add(0, idx, g * u)
+        return (o * torch.from_numpy(dout).to(dtype)).sum()
+
+    def ref_grads(dtype):
+        P = {k: torch.from_numpy(v).to(dtype).requires_grad_(True) for k, v in W.items()}
+        xt = torch.from_numpy(x0).to(dtype).requires_grad_(True)
+        at = torch.from_numpy(a0).to(dtype).requires_grad_(True)
+        run(P, dtype, xt, at).backward()
+        return {k: v.grad.numpy() for k, v in P.items()}, xt.grad.numpy(), at.grad.numpy()
+    g64, dx64, da64 = ref_grads(torch.float64)
+    g32, dx32, da32 = ref_grads(torch.float32)
+    S = abs_contributions(lambda P: run(P, torch.float64),
+                          {k: torch.from_numpy(v).double().requires_grad_(True)
+                           for k, v in W.items()})
+    check_grad(f"node_update/{V}x{F}/dx", dx.cpu().numpy(), dx64, dx32)
+    check_grad(f"node_update/{V}x{F}/dagg", dagg.cpu().numpy(), da64, da32)
+    for k in W:
+        check_grad(f"node_update/{V}x{F}/{k}", grads[k].cpu().numpy(), g64[k], g32[k], S[k])
