@@ -68,7 +68,7 @@ __device__ __forceinline__ void heads_row_block(const float* xr, const float* yr
       for (int a = 0; a < AMAX; ++a)
         pv[a] = fmaf(x[3], w[j][a][3], fmaf(x[2], w[j][a][2], fmaf(x[1], w[j][a][1], x[0] * w[j][a][0])));
       const float ps = wave_multi_sum<AMAX>(pv);
-      const float vs = wave_sum(fmaf(y[3], w[j][AMAX][3], fmaf(y[2], w[j][AMAX][2],
+      const float vs = wave_sum_x(fmaf(y[3], w[j][AMAX][3], fmaf(y[2], w[j][AMAX][2],
                                 fmaf(y[1], w[j][AMAX][1], y[0] * w[j][AMAX][0]))));
       const int a = lane >> (6 - LOGV);
       if ((lane & ((1 << (6 - LOGV)) - 1)) == 0 && a < A) part[c * PW + a] = ps;
@@ -137,7 +137,7 @@ __device__ __forceinline__ void heads_chunk_part(const float* xr, const float* y
   for (int a = 0; a < AMAX; ++a)
     pv[a] = fmaf(x[3], w[a][3], fmaf(x[2], w[a][2], fmaf(x[1], w[a][1], x[0] * w[a][0])));
   const float ps = wave_multi_sum<AMAX>(pv);
-  const float vs = wave_sum(fmaf(y[3], w[AMAX][3], fmaf(y[2], w[AMAX][2],
+  const float vs = wave_sum_x(fmaf(y[3], w[AMAX][3], fmaf(y[2], w[AMAX][2],
                             fmaf(y[1], w[AMAX][1], y[0] * w[AMAX][0]))));
   const int a = lane >> (6 - LOGV);
   if constexpr (SC1) {

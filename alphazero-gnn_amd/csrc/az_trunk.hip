@@ -72,34 +72,52 @@ __device__ __forceinline__ void trunk_rows_heads(const float* ob, int nb, int b0
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int A = hd.A;
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  for (int c = wave; c < NCH; c += 8) {
+  // Wave w takes chunks w and w + 8 (13 chunks, 8 waves), both chunks' weight loads issued up
+  // front.  The NB boards of a chunk are formed and reduced with no control flow between them
+  // (rows past nb use zeros and are not stored), so their exchange chains overlap instead of
+  // running board after board.  Each (row, chunk) partial is still the same fma chain and the
+  // same wave_multi_sum / wave sum, so the bits are az_heads_fwd's.
+  static_assert(NCH <= 16, "two chunks per wave");
+  auto load_w = [&](int c, f32x4 (&w)[AMAX + 1], bool& kin, int& kc) {
     const int k = c * HEADS_KC + lane * 4;
-    const bool kin = k < K;
-    const int kc = kin ? k : 0;
-    f32x4 w[AMAX + 1];
+    kin = k < K;
+    kc = kin ? k : 0;
 #pragma unroll
     for (int a = 0; a < AMAX; ++a)
       w[a] = *reinterpret_cast<const f32x4*>(hd.wp + (size_t)min(a, A - 1) * K + kc);
     w[AMAX] = *reinterpret_cast<const f32x4*>(hd.wv + kc);
+  };
+  auto chunk = [&](int c, f32x4 (&w)[AMAX + 1], bool kin, int kc) {
 #pragma unroll
     for (int a = 0; a < AMAX; ++a) w[a] = (a < A && kin) ? w[a] : z;
     w[AMAX] = kin ? w[AMAX] : z;
+    float ps[NB], vs[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      if (b >= nb) break;
-      const f32x4 x = kin ? *reinterpret_cast<const f32x4*>(ob + b * K + kc) : z;
+      const f32x4 x = kin && b < nb ? *reinterpret_cast<const f32x4*>(ob + b * K + kc) : z;
       float pv[AMAX];
 #pragma unroll
       for (int a = 0; a < AMAX; ++a)
         pv[a] = fmaf(x[3], w[a][3], fmaf(x[2], w[a][2], fmaf(x[1], w[a][1], x[0] * w[a][0])));
-      const float ps = wave_multi_sum<AMAX>(pv);
-      const float vs = wave_sum(
+      ps[b] = wave_multi_sum<AMAX>(pv);
+      vs[b] = wave_sum_x(
           fmaf(x[3], w[AMAX][3], fmaf(x[2], w[AMAX][2], fmaf(x[1], w[AMAX][1], x[0] * w[AMAX][0]))));
-      const int a = lane >> 3;
-      if ((lane & 7) == 0 && a < A) part[b][c][a] = ps;
-      if (lane == 0) part[b][c][A] = vs;
     }
-  }
+    const int a = lane >> 3;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (b < nb && (lane & 7) == 0 && a < A) part[b][c][a] = ps[b];
+      if (b < nb && lane == 0) part[b][c][A] = vs[b];
+    }
+  };
+  f32x4 w0[AMAX + 1], w1[AMAX + 1];
+  bool kin0, kin1 = false;
+  int kc0, kc1 = 0;
+  const bool two = wave + 8 < NCH;
+  load_w(wave, w0, kin0, kc0);
+  if (two) load_w(wave + 8, w1, kin1, kc1);
+  chunk(wave, w0, kin0, kc0);
+  if (two) chunk(wave + 8, w1, kin1, kc1);
   __syncthreads();
   if (tid < NB * PW) {
     const int b = tid / PW, a = tid % PW;
@@ -538,7 +556,7 @@ __global__ __launch_bounds__(256) void heads_partial_kernel(
     for (int a = 0; a < AMAX; ++a)
       pv[a] = fmaf(x[3], w[a][3], fmaf(x[2], w[a][2], fmaf(x[1], w[a][1], x[0] * w[a][0])));
     const float ps = wave_multi_sum<AMAX>(pv);        // policy logit (lane >> (6-LOGV))
-    const float vs = wave_sum(
+    const float vs = wave_sum_x(
         fmaf(y[3], w[AMAX][3], fmaf(y[2], w[AMAX][2], fmaf(y[1], w[AMAX][1], y[0] * w[AMAX][0]))));
     const int a = lane >> (6 - LOGV);
     if ((lane & ((1 << (6 - LOGV)) - 1)) == 0 && a < A) out[a] = ps;
@@ -606,7 +624,7 @@ __global__ __launch_bounds__(256) void splitk_heads_partial_kernel(
     for (int a = 0; a < AMAX; ++a)
       pv[a] = fmaf(x[3], w[a][3], fmaf(x[2], w[a][2], fmaf(x[1], w[a][1], x[0] * w[a][0])));
     const float ps = wave_multi_sum<AMAX>(pv);
-    const float vs = wave_sum(
+    const float vs = wave_sum_x(
         fmaf(x[3], w[AMAX][3], fmaf(x[2], w[AMAX][2], fmaf(x[1], w[AMAX][1], x[0] * w[AMAX][0]))));
     const int a = lane >> (6 - LOGV);
     if ((lane & ((1 << (6 - LOGV)) - 1)) == 0 && a < A) out[a] = ps;
@@ -787,7 +805,7 @@ __device__ __forceinline__ void heads_rowsw_body(int B, int K, const float* __re
     for (int a = 0; a < AMAX; ++a)
       pv[a] = fmaf(x[3], w[a][3], fmaf(x[2], w[a][2], fmaf(x[1], w[a][1], x[0] * w[a][0])));
     const float ps = wave_multi_sum<AMAX>(pv);
-    const float vs = wave_sum(
+    const float vs = wave_sum_x(
         fmaf(y[3], w[AMAX][3], fmaf(y[2], w[AMAX][2], fmaf(y[1], w[AMAX][1], y[0] * w[AMAX][0]))));
     const int a = lane >> (6 - LOGV);
     if ((lane & ((1 << (6 - LOGV)) - 1)) == 0 && a < A) part[i][c][a] = ps;
