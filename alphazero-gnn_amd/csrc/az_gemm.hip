@@ -1629,6 +1629,13 @@ __host__ __device__ __forceinline__ int csk_block_of(int u, int b, int W) {
   return ((u + 1) * b - 1) / W;
 }
 
+template <int BM, int BN, int WGM, int WGN, bool H3 = false, int NBUF = 2>
+constexpr int p3_smem_bytes() {
+  constexpr int NW = WGM * WGN, WM = BM / WGM;
+  constexpr int BUF = (H3 ? 2 : 3) * (BM + BN) * 64, STAGE = NW * WM * 36 * 4;
+  return NBUF * BUF > STAGE ? NBUF * BUF : STAGE;
+}
+
 // gemm_p3_body (below): the tile on operands already split into planes, LDS-DMA only
 template <int BM, int BN, int WGM, int WGN, bool H3 = false, bool FLEX = false, int NBUF = 2,
           int ABL = 0, bool HEADS = false>
@@ -1638,11 +1645,15 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
 // P2: the fp16 form on pre-split planes (p.apl: A's two planes from h3_split_rows_kernel, p.bpl:
 // W's, cached per weight generation), every stage global -> LDS by LDS-DMA; same products in the
 // same order as the in-tile split, so the same bits.
-template <bool MASK, bool H3, bool P2 = false, bool HEADS = false>
+// RING (P2 only): the pre-split tile's LDS-DMA ring depth, 3 in the product (two stages in
+// flight: the whole-line stage fill then takes 0.60 us per stage against the MFMA's ~0.73)
+template <bool MASK, bool H3, bool P2 = false, bool HEADS = false, int RING = 3>
 __global__ __launch_bounds__(512) void gemm_x3_csk(GemmArgs p, CskPlan q) {
   static_assert(!P2 || (H3 && !MASK), "P2: the fp16 form on whole 32-k tiles");
   static_assert(!HEADS || (H3 && !MASK), "HEADS: the fp16 form on whole 32-k tiles");
-  __shared__ __attribute__((aligned(1024))) char smem[x3_smem_bytes<256, 128, 4, 2, 32, H3 ? 2 : 3>()];
+  constexpr int SMEM = P2 ? p3_smem_bytes<256, 128, 4, 2, true, RING>()
+                          : x3_smem_bytes<256, 128, 4, 2, 32, H3 ? 2 : 3>();
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   const int L = xcd_swizzle(blockIdx.x, q.B);
   int r, b, am, an, mt0, nt0, bma;
   if (L < q.Cf * q.bf) {                  // r-major, cycle fastest: in-phase blocks adjacent
@@ -1684,8 +1695,8 @@ __global__ __launch_bounds__(512) void gemm_x3_csk(GemmArgs p, CskPlan q) {
     int mt_i = mt0 + (f - fn * am), bma_i = bma;   // opaque per segment: keeps the body's
     asm volatile("" : "+s"(mt_i), "+s"(bma_i));    // address setup in the loop (hoisted, it spills)
     if constexpr (P2)
-      gemm_p3_body<256, 128, 4, 2, true, true, 2, 0, HEADS>(g, smem, mt_i, nt0 + fn, sp, 32 * k0,
-                                                           min(p.K, 32 * k1), bma_i);
+      gemm_p3_body<256, 128, 4, 2, true, true, RING, 0, HEADS>(g, smem, mt_i, nt0 + fn, sp,
+                                                              32 * k0, min(p.K, 32 * k1), bma_i);
     else
       gemm_x3_body<256, 128, 4, 2, MASK, 0, false, 32, true, H3, HEADS>(
           g, smem, mt_i, nt0 + fn, sp, 32 * k0, min(p.K, 32 * k1), bma_i);
@@ -1869,25 +1880,17 @@ static bool csk_plan_cached(int M, int N, int K, int cus, double miss_cost, CskP
   return ok;
 }
 
-// gemm_x3 on operands that are ALREADY split ("p3"): A as three bf16 planes [3][M][K] (p.apl,
-// plane stride p.apl_plane) and W as three planes [3][N][K] (p.bpl, p.bpl_plane), row stride K,
-// K % 32 == 0.  Nothing is converted in the tile: each 32-k stage (three planes of BM + BN rows
-// x 64 B = 72 KB for 256 x 128) goes global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KB per
-// wave-instruction, no VGPR round trip, no VALU, no ds_write), double-buffered, one raw barrier
-// per stage: stage kt + 1 is issued right after the barrier that retires stage kt - 1's reads
-// and has the whole of stage kt's MFMAs to land.  The LDS image is gemm_x3's (plane-major,
-// [row][32 bf16], 16-B chunk c stored at c ^ ((row >> 2) & 3)): the swizzle is applied on the
-// global address, since a DMA's LDS destination is lane-linear.  Same products in the same
-// order as gemm_x3, so the same bits for the same split-K partition.
-// H3 (tile 16 of the tuning build): the fp16 form on pre-split planes -- two fp16 planes of the
-// row-scaled operands (h3_split_kernel), three products per step, accumulators unscaled by
-// 1 / (sa sw) before the epilogue.
-template <int BM, int BN, int WGM, int WGN, bool H3 = false, int NBUF = 2>
-constexpr int p3_smem_bytes() {
-  constexpr int NW = WGM * WGN, WM = BM / WGM;
-  constexpr int BUF = (H3 ? 2 : 3) * (BM + BN) * 64, STAGE = NW * WM * 36 * 4;
-  return NBUF * BUF > STAGE ? NBUF * BUF : STAGE;
-}
+// gemm_x3's fp16 form on operands that are ALREADY split ("p3", the product's P2 GEMM): A's and
+// W's row-scaled values as two fp16 planes each in the p2_chunk layout of az_x3.h (A from
+// h3_split_rows_kernel / the trunk / the fused split-K reduce, W cached per weight generation),
+// K % 32 == 0.  Nothing is converted in the tile: each 32-k stage ((BM + BN) rows x 128 B = 48 KB
+// for 256 x 128) goes global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KB = 8 whole 128-B
+// lines per wave-instruction, no VGPR round trip, no VALU, no ds_write), in a ring of NBUF
+// stages with one raw barrier per stage.  The LDS image is [row][8 units of 16 B], unit u stored
+// at slot u ^ ((row >> 1) & 7) (the swizzle applied on the global address, since a DMA's LDS
+// destination is lane-linear).  Three fp16 products per step (ah bl, al bh, ah bh), the
+// accumulators unscaled by 1 / (sa sw) before the epilogue: the same products in the same order
+// as gemm_x3's in-tile fp16 split, so the same bits for the same split-K partition.
 
 // FLEX (the cycled stream-K tail): bma = 256 (256 x 128 tile) or 128 (128 x 256), as gemm_x3_body.
 // NBUF = 3: a three-stage ring (stage kt + 2 issued while stage kt computes), one barrier per
@@ -1899,15 +1902,16 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
                                              int sp, int kbeg, int kend, int bma) {
   static_assert(NBUF == 2 || NBUF == 3, "p3 ring: 2 or 3 stages");
   static_assert(!FLEX || (BM == 256 && BN == 128 && WGM == 4 && WGN == 2), "FLEX: 256 x 128");
-  constexpr int PL = H3 ? 2 : 3;
+  static_assert(H3, "p3: the fp16 form's two planes (p2_chunk layout)");
+  constexpr int PL = 2;
   constexpr int BK = 32;
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TI = WM / 32, TJ = WN / 32;
   constexpr int ROWS = BM + BN;
-  constexpr int PLANE = ROWS * 64, BUF = PL * PLANE;
-  constexpr int PIECES = PL * ROWS / 16;           // 1-KB DMA pieces per stage
-  static_assert(ROWS % 16 == 0 && PIECES % NW == 0 && TI >= 1 && TJ >= 1, "bad p3 tile");
+  constexpr int BUF = ROWS * 128;                  // [ROWS][2 planes x 32 k]: 128 B per row
+  constexpr int PIECES = ROWS / 8;                 // 1-KB DMA pieces per stage, 8 rows each
+  static_assert(ROWS % 8 == 0 && PIECES % NW == 0 && TI >= 1 && TJ >= 1, "bad p3 tile");
   constexpr int PPW = PIECES / NW;
   const int tbm = FLEX ? bma : BM, tbn = FLEX ? BM + BN - bma : BN;
   const int wgn = FLEX ? tbn / WN : WGN;
@@ -1915,28 +1919,30 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / wgn, wn = wave % wgn;
 
-  // piece q * NW + wave covers image rows 16 piece .. + 15 (plane-major [3][ROWS]); lane l lands
-  // at byte 16 l of it: row 16 piece + (l >> 2), chunk slot l & 3 = logical chunk (l & 3) ^ key
+  // piece q * NW + wave covers image rows 8 piece .. + 7, each row one whole 128-B line of the
+  // p2_chunk layout (8 units of 16 B: plane 0's four k chunks, then plane 1's); lane l lands at
+  // byte 16 l of the piece: row 8 piece + (l >> 3), unit slot l & 7 = logical unit
+  // (l & 7) ^ key(row), key = (row >> 1) & 7 -- any 16 rows r..r+15 (r % 16 == 0) then put one
+  // unit on 16 distinct 16-B slots of the 256-B bank row, so the fragment reads are conflict-free
   const unsigned short* src[PPW];
 #pragma unroll
   for (int q = 0; q < PPW; ++q) {
-    const int R = (q * NW + wave) * 16 + (lane >> 2);
-    const int pl = R / ROWS, r = R % ROWS;
-    const int c = (lane & 3) ^ ((r >> 2) & 3);
+    const int r = (q * NW + wave) * 8 + (lane >> 3);
+    const int u = (lane & 7) ^ ((r >> 1) & 7);
     if (r < tbm) {
       const int gr = min(m0 + r, p.M - 1);
-      src[q] = p.apl + pl * p.apl_plane + (size_t)gr * p.K + 8 * c;
+      src[q] = p.apl + (size_t)gr * 2 * p.K + 8 * u;
     } else {
       const int gr = min(n0 + r - tbm, p.N - 1);
-      src[q] = p.bpl + pl * p.bpl_plane + (size_t)gr * p.K + 8 * c;
+      src[q] = p.bpl + (size_t)gr * 2 * p.K + 8 * u;
     }
   }
-  auto issue = [&](int buf, int k0) {
+  auto issue = [&](int buf, int k0) {    // k0 % 32 == 0: step k0 / 32 starts at element 2 k0
     if constexpr ((ABL & 4) != 0) return;
 #pragma unroll
     for (int q = 0; q < PPW; ++q)
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src[q] + k0),
+          (const __attribute__((address_space(1))) void*)(src[q] + 2 * k0),
           (__attribute__((address_space(3))) void*)(smem + buf * BUF + (q * NW + wave) * 1024),
           16, 0, 0);
   };
@@ -1952,27 +1958,27 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
     const int row = wm * WM + i * 32 + (lane & 31);
-    aoff[i] = row * 64;
-    akey[i] = (row >> 2) & 3;
+    aoff[i] = row * 128;
+    akey[i] = (row >> 1) & 7;
   }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int row = tbm + wn * WN + j * 32 + (lane & 31);
-    boff[j] = row * 64;
-    bkey[j] = (row >> 2) & 3;
+    boff[j] = row * 128;
+    bkey[j] = (row >> 1) & 7;
   }
   const int hk = lane >> 5;
   struct Frags { bf16x8 a[PL][TI], b[PL][TJ]; };
   auto read = [&](Frags& f, const char* S, int s) {
-    const int c = 2 * s + hk;
+    const int c = 2 * s + hk;          // k chunk of this half of the wave; unit 4 pl + c
 #pragma unroll
     for (int pl = 0; pl < PL; ++pl) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
-        f.a[pl][i] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + aoff[i] + ((c ^ akey[i]) << 4));
+        f.a[pl][i] = *reinterpret_cast<const bf16x8*>(S + aoff[i] + (((4 * pl + c) ^ akey[i]) << 4));
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
-        f.b[pl][j] = *reinterpret_cast<const bf16x8*>(S + pl * PLANE + boff[j] + ((c ^ bkey[j]) << 4));
+        f.b[pl][j] = *reinterpret_cast<const bf16x8*>(S + boff[j] + (((4 * pl + c) ^ bkey[j]) << 4));
     }
   };
   auto mfma6 = [&](const Frags& f, int i, int j) {
@@ -2081,33 +2087,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3(GemmArgs p) {
   const int kbeg = sp * p.kc, kend = min(p.K, kbeg + p.kc);
   gemm_p3_body<BM, BN, WGM, WGN, H3, false, NBUF, ABL, HEADS>(p, smem, mt, nt, sp, kbeg, kend,
                                                               BM);
-}
-
-// gemm_p3 in stream-K form (see gemm_x3_sk), pieces summed by streamk_fixup4_kernel
-template <int BM, int BN, int WGM, int WGN>
-__global__ __launch_bounds__(64 * WGM * WGN) void gemm_p3_sk(GemmArgs p, SkPlan sq) {
-  __shared__ __attribute__((aligned(1024))) char smem[p3_smem_bytes<BM, BN, WGM, WGN>()];
-  const int b = xcd_swizzle(blockIdx.x, sq.B);
-  const int mt_n = sq.mt_n, KT = sq.KT;
-  long i0 = sk_first(sq, b);
-  const long i1 = b + 1 < sq.B ? sk_first(sq, b + 1) : (long)mt_n * ((p.N + BN - 1) / BN) * KT;
-  while (i0 < i1) {
-    const int t = (int)(i0 / KT);
-    const int k0 = (int)(i0 - (long)t * KT);
-    const int k1 = (int)min((long)KT, k0 + (i1 - i0));
-    GemmArgs q = p;
-    int sp = 0;
-    if (k0 == 0 && k1 == KT) {
-      q.splits = 1;
-    } else {
-      q.splits = 2;
-      sp = b - sk_block(sq, t, 0);
-    }
-    gemm_p3_body<BM, BN, WGM, WGN, false, false>(q, smem, t % mt_n, t / mt_n, sp, 32 * k0,
-                                                  min(p.K, 32 * k1), BM);
-    i0 += k1 - k0;
-    if (i0 < i1) __syncthreads();
-  }
 }
 
 // gemm_x3 as a two-group ping-pong ("x3pp").  The timing ablations of gemm_x3 (tools/gemm_sweep.py
@@ -2493,22 +2472,6 @@ __global__ __launch_bounds__(256) void x3_split_kernel(const float* __restrict__
   for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(d + pl * plane) = o[pl];
 }
 
-// the fp16 form's two planes of a row-scaled operand (sc[r] = the row's power of two)
-__global__ __launch_bounds__(256) void h3_split_kernel(const float* __restrict__ A, int lda, int M,
-                                                       int K, const float* __restrict__ sc,
-                                                       unsigned short* __restrict__ out,
-                                                       size_t plane) {
-  const long idx = blockIdx.x * 256L + threadIdx.x;
-  const int segs = K >> 3;
-  if (idx >= (long)M * segs) return;
-  const int r = (int)(idx / segs), c = (int)(idx % segs);
-  const float* s = A + (size_t)r * lda + c * 8;
-  u32x4 o[2];
-  split2s(*reinterpret_cast<const f32x4*>(s), *reinterpret_cast<const f32x4*>(s + 4), sc[r], o);
-  unsigned short* d = out + (size_t)r * K + c * 8;
-#pragma unroll
-  for (int pl = 0; pl < 2; ++pl) *reinterpret_cast<u32x4*>(d + pl * plane) = o[pl];
-}
 #endif
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p) {
@@ -3595,13 +3558,13 @@ __global__ __launch_bounds__(256) void row_scale_kernel(const float* __restrict_
 }
 
 // A row's power-of-two scale (as row_scale_kernel: sc[r] = s, sc[rows + r] = 1 / s) AND its two fp16
-// planes (split2s of x s: plane 0 at out + r * cols, plane 1 at out + plane + r * cols), one
-// 256-thread block per row, the row read once when cols <= 4096 (8-float chunks in registers):
-// the P2 GEMM's operands.  cols % 8 == 0 and 16-B aligned rows (the caller checks).
+// planes (split2s of x s, in the p2_chunk layout of az_x3.h), one 256-thread block per row, the
+// row read once when cols <= 4096 (8-float chunks in registers): the P2 GEMM's operands.
+// cols % 32 == 0 and 16-B aligned rows (the caller checks).
 __global__ __launch_bounds__(256) void h3_split_rows_kernel(const float* __restrict__ X, int rows,
                                                             int cols, int ld, int T,
                                                             unsigned short* __restrict__ out,
-                                                            size_t plane, float* __restrict__ sc) {
+                                                            float* __restrict__ sc) {
   __shared__ float wm[4];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   if (r >= rows) return;
@@ -3640,12 +3603,11 @@ __global__ __launch_bounds__(256) void h3_split_rows_kernel(const float* __restr
     sc[r] = s;
     sc[rows + r] = ldexpf(1.f, -e);
   }
-  unsigned short* d = out + (size_t)r * cols;
   auto put = [&](int ch, const f32x4& a, const f32x4& b) {
     u32x4 o[2];
     split2s(a, b, s, o);
-    *reinterpret_cast<u32x4*>(d + 8 * ch) = o[0];
-    *reinterpret_cast<u32x4*>(d + plane + 8 * ch) = o[1];
+    *reinterpret_cast<u32x4*>(out + p2_chunk(r, ch, 0, cols)) = o[0];
+    *reinterpret_cast<u32x4*>(out + p2_chunk(r, ch, 1, cols)) = o[1];
   };
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -3659,8 +3621,8 @@ __global__ __launch_bounds__(256) void h3_split_rows_kernel(const float* __restr
 // 8-column chunks are summed over the S slabs in slab order from 0.f, then bias and activation
 // -- splitk_reduce4_kernel's arithmetic, so C's bits are unchanged -- and stored; the row's max
 // |C| (one block reduction) gives the scale, and the chunks, still in registers, leave as the two
-// fp16 planes + scales h3_split_rows_kernel would make of C (out [2][M][N], sc [2][M]).  N % 8
-// == 0, N <= 4096, bias / activation epilogue only, 16-B aligned rows (splitk_reduce_split).
+// fp16 planes + scales h3_split_rows_kernel would make of C (out: the p2_chunk layout, sc [2][M]).
+// N % 32 == 0, N <= 4096, bias / activation epilogue only, 16-B aligned rows (splitk_reduce_split).
 template <int S>
 __global__ __launch_bounds__(256) void splitk_reduce_split_kernel(GemmArgs p,
                                                                   unsigned short* __restrict__ out,
@@ -3719,15 +3681,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_split_kernel(GemmArgs p,
     sc[r] = s;
     sc[p.M + r] = inv;
   }
-  unsigned short* d = out + (size_t)r * p.N;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int ch = tid + 256 * u;
     if (ch < nch) {
       u32x4 o[2];
       split2s(v[u][0], v[u][1], s, o);
-      *reinterpret_cast<u32x4*>(d + 8 * ch) = o[0];
-      *reinterpret_cast<u32x4*>(d + plane + 8 * ch) = o[1];
+      *reinterpret_cast<u32x4*>(out + p2_chunk(r, ch, 0, p.N)) = o[0];
+      *reinterpret_cast<u32x4*>(out + p2_chunk(r, ch, 1, p.N)) = o[1];
     }
   }
 }
@@ -3883,7 +3844,7 @@ static const unsigned short* w_planes(const float* w, int n, int k, int ld, hipS
   }
   const int nxt = e->pcur ^ 1;
   hipLaunchKernelGGL(h3_split_rows_kernel, dim3(n), dim3(256), 0, s, w, n, k, ld, H3_TW,
-                     e->planes[nxt], (size_t)n * k, e->pbuf[nxt]);
+                     e->planes[nxt], e->pbuf[nxt]);
   if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
   e->pcur = nxt;
   e->pgen = gen;
@@ -4093,7 +4054,7 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
       a.sa = pre->sc;
     } else {
       hipLaunchKernelGGL(h3_split_rows_kernel, dim3(a.M), dim3(256), 0, s, a.A, a.M, a.K, a.lda,
-                         H3_TA, apl_buf, (size_t)a.M * a.K, sa_buf);
+                         H3_TA, apl_buf, sa_buf);
       a.apl = apl_buf;
       a.sa = sa_buf;
     }
@@ -4183,6 +4144,12 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
       ok = csk_plan_cached(a.M, a.N, a.K, cus, CSK_MISS_COST, cq);
 #endif
       const int mp = use_csk && ok ? csk_max_pieces(cq) : 0;
+#ifdef AZ_TUNING
+      static const char* env_cring = tuning_env("AZ_P3_RING");
+      const int csk_ring = env_cring ? atoi(env_cring) : 3;
+#else
+      constexpr int csk_ring = 3;
+#endif
       // the finalize gives each lane one whole 64-column block of a row: N % 64 == 0, N <= 4,096
       if (use_csk && ok && a.he.part && whole && (p2 || h3) && a.N % 64 == 0 && a.N <= 64 * 64 &&
           (size_t)a.M * (a.N / 64) * mp * HEADS_TILE_SLOTS * 4 * 2 <= ws_bytes &&
@@ -4191,7 +4158,9 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
         if (p2) p2 = p2_prep();
         if (!p2) h3 = h3_scales();
         a.he.mp = mp;
-        if (p2) hipLaunchKernelGGL((gemm_x3_csk<false, true, true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        if (p2 && csk_ring == 2)
+          hipLaunchKernelGGL((gemm_x3_csk<false, true, true, true, 2>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        else if (p2) hipLaunchKernelGGL((gemm_x3_csk<false, true, true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
         else hipLaunchKernelGGL((gemm_x3_csk<false, true, false, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
         const int P = (a.N / 64) * mp;
         hipLaunchKernelGGL(heads_tiles_finalize_kernel<true>, dim3((a.M + 3) / 4), dim3(256),
@@ -4204,7 +4173,9 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
       if (use_csk && ok && mp * (size_t)a.M * a.N * 4 <= ws_bytes) {
         if (p2) p2 = p2_prep();
         if (!p2 && h3) h3 = h3_scales();
-        if (p2) hipLaunchKernelGGL((gemm_x3_csk<false, true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        if (p2 && csk_ring == 2)
+          hipLaunchKernelGGL((gemm_x3_csk<false, true, true, false, 2>), dim3(cq.B), dim3(512), 0, s, a, cq);
+        else if (p2) hipLaunchKernelGGL((gemm_x3_csk<false, true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
         else if (h3 && whole) hipLaunchKernelGGL((gemm_x3_csk<false, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
         else if (h3) hipLaunchKernelGGL((gemm_x3_csk<true, true>), dim3(cq.B), dim3(512), 0, s, a, cq);
         else if (whole) hipLaunchKernelGGL((gemm_x3_csk<false, false>), dim3(cq.B), dim3(512), 0, s, a, cq);
@@ -4248,97 +4219,6 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
     hipLaunchKernelGGL((gemm_x3<256, 128, 4, 2, false, 0, true>), grid, dim3(512), 0, s, a);
     return true;
   }
-  // tile 15: gemm_p3 -- both operands split into planes first (x3_split_kernel into buffers of
-  // this build); AZ_P3_REUSE=1 splits only on the first call (a probe with fixed operands then
-  // times the tile kernel alone); AZ_P3_SK=1 the stream-K grid
-  if (tile == 15 && whole && a.lda == a.K && a.ldb == a.K) {
-    static unsigned short* pbuf = nullptr;
-    static size_t pcap = 0;
-    static const float *lastA = nullptr, *lastB = nullptr;
-    static const bool reuse = tuning_env("AZ_P3_REUSE") != nullptr;
-    static const bool sk = tuning_env("AZ_P3_SK") != nullptr;
-    const size_t need = (size_t)3 * ((size_t)a.M + a.N) * a.K;
-    if (need > pcap) {
-      if (pbuf) (void)hipFree(pbuf);
-      if (hipMalloc(&pbuf, need * 2) != hipSuccess) return false;
-      pcap = need;
-      lastA = lastB = nullptr;
-    }
-    a.apl = pbuf;
-    a.apl_plane = (size_t)a.M * a.K;
-    a.bpl = pbuf + 3 * a.apl_plane;
-    a.bpl_plane = (size_t)a.N * a.K;
-    if (!reuse || lastA != a.A || lastB != a.B) {
-      const long sa = (long)a.M * (a.K / 8), sb = (long)a.N * (a.K / 8);
-      hipLaunchKernelGGL(x3_split_kernel, dim3((unsigned)((sa + 255) / 256)), dim3(256), 0, s,
-                         a.A, a.lda, a.M, a.K, pbuf, a.apl_plane);
-      hipLaunchKernelGGL(x3_split_kernel, dim3((unsigned)((sb + 255) / 256)), dim3(256), 0, s,
-                         a.B, a.ldb, a.N, a.K, const_cast<unsigned short*>(a.bpl), a.bpl_plane);
-      lastA = a.A;
-      lastB = a.B;
-    }
-    const int KT = a.K / 32;
-    const long I = tiles * (long)KT;
-    const int B = (int)std::min<long>(256, I);
-    const SkPlan q = sk_plan(a.M, a.N, a.K, 256, 128, B, false);
-    if (sk && a.slab && a.vec_epi && I / B >= 1 &&
-        (size_t)sk_max_pieces(q, a.N, 128) * a.M * a.N * 4 <= ws_bytes) {
-      hipLaunchKernelGGL((gemm_p3_sk<256, 128, 4, 2>), dim3(B), dim3(512), 0, s, a, q);
-      const long n4 = (long)a.M * (a.N / 4);
-      hipLaunchKernelGGL(streamk_fixup4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                         a, 256, 128, q);
-      a.splits = 1;
-      return true;
-    }
-    hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2>), grid, dim3(512), 0, s, a);
-    return true;
-  }
-  // tile 16: the fp16 form on pre-split planes (row scales as the product computes them, both
-  // operands split by h3_split_kernel into this build's buffers; AZ_P3_REUSE=1 splits only on
-  // the first call, so a probe with fixed operands times the tile kernel alone)
-  if (tile == 16 && whole && a.lda == a.K && a.ldb == a.K && h3) {
-    static unsigned short* pbuf = nullptr;
-    static float* sbuf = nullptr;
-    static size_t pcap = 0, scap = 0;
-    static const float *lastA = nullptr, *lastB = nullptr;
-    static const bool reuse = tuning_env("AZ_P3_REUSE") != nullptr;
-    const size_t need = (size_t)2 * ((size_t)a.M + a.N) * a.K;
-    if (need > pcap) {
-      if (pbuf) (void)hipFree(pbuf);
-      if (hipMalloc(&pbuf, need * 2) != hipSuccess) return false;
-      pcap = need;
-      lastA = lastB = nullptr;
-    }
-    const size_t sneed = (size_t)2 * (a.M + a.N);
-    if (sneed > scap) {
-      if (sbuf) (void)hipFree(sbuf);
-      if (hipMalloc(&sbuf, sneed * 4) != hipSuccess) return false;
-      scap = sneed;
-      lastA = lastB = nullptr;
-    }
-    a.apl = pbuf;
-    a.apl_plane = (size_t)a.M * a.K;
-    a.bpl = pbuf + 2 * a.apl_plane;
-    a.bpl_plane = (size_t)a.N * a.K;
-    a.sa = sbuf;
-    a.sw = sbuf + 2 * a.M;
-    if (!reuse || lastA != a.A || lastB != a.B) {
-      hipLaunchKernelGGL(row_scale_kernel, dim3(a.M), dim3(256), 0, s, a.A, a.M, a.K, a.lda,
-                         H3_TA, sbuf);
-      hipLaunchKernelGGL(row_scale_kernel, dim3(a.N), dim3(256), 0, s, a.B, a.N, a.K, a.ldb,
-                         H3_TW, sbuf + 2 * a.M);
-      const long sa = (long)a.M * (a.K / 8), sb = (long)a.N * (a.K / 8);
-      hipLaunchKernelGGL(h3_split_kernel, dim3((unsigned)((sa + 255) / 256)), dim3(256), 0, s,
-                         a.A, a.lda, a.M, a.K, sbuf, pbuf, a.apl_plane);
-      hipLaunchKernelGGL(h3_split_kernel, dim3((unsigned)((sb + 255) / 256)), dim3(256), 0, s,
-                         a.B, a.ldb, a.N, a.K, sbuf + 2 * a.M, const_cast<unsigned short*>(a.bpl),
-                         a.bpl_plane);
-      lastA = a.A;
-      lastB = a.B;
-    }
-    hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true>), grid, dim3(512), 0, s, a);
-    return true;
-  }
 #endif
 #define AZ_X3(BM_, BN_, WM_, WN_)                                                              \
   if (whole) hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, false>), grid, dim3(64 * WM_ * WN_), \
@@ -4350,37 +4230,47 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
   else hipLaunchKernelGGL((gemm_x3<BM_, BN_, WM_, WN_, true, 0, false, 32, true>), grid,         \
                           dim3(64 * WM_ * WN_), 0, s, a);
   if (p2 && (tile == 1 || tile == 2) && p2_prep()) {
+    // the 256 x 128 tile's LDS-DMA ring: 3 stages (two in flight) in the product; the tuning
+    // build's AZ_P3_RING=2 keeps round 5's double buffer for A/B runs (same bits)
     static const char* env_ring = tuning_env("AZ_P3_RING");
-    const int ring = env_ring ? atoi(env_ring) : 2;
+    const int ring = env_ring ? atoi(env_ring) : 3;
     static const char* env_abl = tuning_env("AZ_P3_ABL");
     const int abl = env_abl ? atoi(env_abl) : 0;
-    if (tile == 1 && ring == 3)
-      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3>), grid, dim3(512), 0, s, a);
+    if (false) {
+    }
 #ifdef AZ_TUNING
     else if (tile == 1 && abl == 1)
-      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 1>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3, 1>), grid, dim3(512), 0, s, a);
     else if (tile == 1 && abl == 2)
-      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 2>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3, 2>), grid, dim3(512), 0, s, a);
     else if (tile == 1 && abl == 4)
-      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 4>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3, 4>), grid, dim3(512), 0, s, a);
     else if (tile == 1 && abl == 5)
-      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 5>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3, 5>), grid, dim3(512), 0, s, a);
     else if (tile == 1 && abl == 6)
-      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 6>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3, 6>), grid, dim3(512), 0, s, a);
     else if (tile == 1 && a.splits == 1 && tuning_env("AZ_P3_WIDE")) {
       // 256 x 256 tiles (waves 4 x 2 of 64 x 128): half the L2 misses per flop of 256 x 128
       const dim3 gw((unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256)));
       hipLaunchKernelGGL((gemm_p3<256, 256, 4, 2, true>), gw, dim3(512), 0, s, a);
     }
+    else if (tile == 1 && ring == 2) {
+      if (a.he.part) {
+        hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 0, true>), grid, dim3(512), 0, s, a);
+        launch_heads_finalize(a, s);
+      } else {
+        hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2>), grid, dim3(512), 0, s, a);
+      }
+    }
 #endif
     else if (a.he.part) {
       if (tile == 1)
-        hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 2, 0, true>), grid, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3, 0, true>), grid, dim3(512), 0, s, a);
       else
         hipLaunchKernelGGL((gemm_p3<128, 128, 2, 2, true, 2, 0, true>), grid, dim3(256), 0, s, a);
       launch_heads_finalize(a, s);
     }
-    else if (tile == 1) hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true>), grid, dim3(512), 0, s, a);
+    else if (tile == 1) hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3>), grid, dim3(512), 0, s, a);
     else hipLaunchKernelGGL((gemm_p3<128, 128, 2, 2, true>), grid, dim3(256), 0, s, a);
     return true;
   }
@@ -4609,7 +4499,7 @@ int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s) {
 // negative AZ_E* code.
 int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* planes, float* sc,
                         hipStream_t s) {
-  if (!(splits >= 2 && splits <= 8 && d->N % 8 == 0 && d->N <= 4096 && d->M > 0 && !d->C2 &&
+  if (!(splits >= 2 && splits <= 8 && d->N % 32 == 0 && d->N <= 4096 && d->M > 0 && !d->C2 &&
         !d->R && !d->G && !d->c_rows && d->beta == 0.f &&
         (d->act == AZ_ACT_NONE || d->act == AZ_ACT_RELU) && d->ldc % 4 == 0 && aligned16(d->C) &&
         (!d->bias || aligned16(d->bias)) && aligned16(d->ws) && planes && sc &&

@@ -160,7 +160,7 @@ __device__ __forceinline__ void trunk_rows_heads(const float* ob, int nb, int b0
 // 72 scattered 4-byte loads per lane in all 8 waves), and with NB <= 4 the feature rows are then
 // assembled in it (still there on return).
 // apl / asc (NB <= 4 only; may be null): the feature rows also leave as the P2 GEMM's A operand
-// for output_transform.0 (PreSplitA: two fp16 planes [2][B][3136] and scales [2][B], the bits
+// for output_transform.0 (PreSplitA: two fp16 planes in the p2_chunk layout and scales [2][B], the bits
 // h3_split_rows_kernel would make of feat), so that GEMM needs no split launch of its own.
 // REGW: w2f (non-null) is conv2's weights already in fragment order (az_gemm.hip conv2_frags,
 // cached per weight generation): each lane loads its 72 weights as 18 coalesced float4 loads,
@@ -409,7 +409,6 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
       for (int i = tid; i < nb * 784; i += 512) dst[i] = src[i];
       return;
     }
-    const size_t plane = (size_t)B * 3136;
     for (int ch = tid; ch < nb * 392; ch += 512) {     // 8-float chunks: fp32 row + two planes
       const int b = ch / 392, c = ch - b * 392;
       float mx = wmax[b][0];
@@ -422,9 +421,8 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
       dst[2 * ch + 1] = hi;
       u32x4 o[2];
       split2s(__builtin_bit_cast(f32x4, lo), __builtin_bit_cast(f32x4, hi), sc, o);
-      unsigned short* d = apl + (size_t)(b0 + b) * 3136 + 8 * c;
-      *reinterpret_cast<u32x4*>(d) = o[0];
-      *reinterpret_cast<u32x4*>(d + plane) = o[1];
+      *reinterpret_cast<u32x4*>(apl + p2_chunk(b0 + b, c, 0, 3136)) = o[0];
+      *reinterpret_cast<u32x4*>(apl + p2_chunk(b0 + b, c, 1, 3136)) = o[1];
       if (c == 0) {
         asc[b0 + b] = sc;
         asc[B + b0 + b] = inv;

@@ -136,10 +136,21 @@ __device__ __forceinline__ f32x16 mfma6_32x32x16(const bf16x8 (&a)[3], const bf1
 // cached between weight updates (az_gemm.hip) and stay safe while the weights grow up to 64x.
 constexpr int H3_TA = 14, H3_TW = 10;
 
+// The P2 GEMM's fp16 planes are stored row-interleaved per 32-k step, [rows][K / 32][2][32]:
+// one row's two planes for one k step form one 128-B line, so every LDS-DMA piece of a stage
+// (8 rows x 128 B) moves whole lines.  With the planes apart ([2][rows][K]) a piece was 16 rows
+// x 64 B, half of each line it touched: the stage fill alone took 0.93 us per 48-KB stage with
+// two stages in flight against 0.60 for whole lines, above the stage's ~0.73 us of MFMA
+// (profiles/r06/dma_pattern/).  Element offset of the 8-element chunk ch (k = 8 ch .. 8 ch + 7)
+// of row r, plane pl, in a matrix of K columns (K % 32 == 0).
+__host__ __device__ __forceinline__ size_t p2_chunk(size_t r, int ch, int pl, int K) {
+  return r * 2 * (size_t)K + (size_t)(ch >> 2) * 64 + pl * 32 + (ch & 3) * 8;
+}
+
 // An A operand already in the P2 GEMM's form, made by whoever produced A (the Connect4 trunk,
-// the fused split-K reduce of the GEMM before): planes = two fp16 planes [2][M][K] (split2s of
-// x * s), sc = [2][M] (s, then 1 / s) with s = h3_scale(max_k |x|, H3_TA) -- exactly what
-// h3_split_rows_kernel would write, so the GEMM's bits do not depend on who split A.
+// the fused split-K reduce of the GEMM before): planes = the two fp16 planes of x * s in the
+// p2_chunk layout (split2s), sc = [2][M] (s, then 1 / s) with s = h3_scale(max_k |x|, H3_TA) --
+// exactly what h3_split_rows_kernel would write, so the GEMM's bits do not depend on who split A.
 struct PreSplitA {
   const unsigned short* planes;
   const float* sc;

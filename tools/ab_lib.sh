@@ -12,7 +12,7 @@ objs=""
 for f in $B/*.hip; do
   o=$B/$(basename $f .hip).o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function \
-    -fno-gpu-rdc -c $f -o $o &
+    -fno-gpu-rdc -Xclang -target-feature -Xclang -packed-fp32-ops -c $f -o $o &
   objs="$objs $o"
 done
 wait
