@@ -1937,14 +1937,16 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
       src[q] = p.bpl + (size_t)gr * 2 * p.K + 8 * u;
     }
   }
-  auto issue = [&](int buf, int k0) {    // k0 % 32 == 0: step k0 / 32 starts at element 2 k0
+  auto issue_one = [&](int buf, int k0, int q) {   // k0 % 32 == 0: step k0 / 32 at element 2 k0
     if constexpr ((ABL & 4) != 0) return;
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(src[q] + 2 * k0),
+        (__attribute__((address_space(3))) void*)(smem + buf * BUF + (q * NW + wave) * 1024),
+        16, 0, 0);
+  };
+  auto issue = [&](int buf, int k0) {
 #pragma unroll
-    for (int q = 0; q < PPW; ++q)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src[q] + 2 * k0),
-          (__attribute__((address_space(3))) void*)(smem + buf * BUF + (q * NW + wave) * 1024),
-          16, 0, 0);
+    for (int q = 0; q < PPW; ++q) issue_one(buf, k0, q);
   };
 
   f32x16 acc[TI][TJ];
@@ -2016,10 +2018,13 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
     if (NBUF == 3 && kt + 1 < nk) wait_vm<PPW>();   // stage kt + 1's pieces may still fly
     else wait_vm<0>();     // this wave's pieces of stage kt have landed
     lds_barrier();         // ... everyone's; and every wave is done reading stage kt - 1
-    if (kt + NBUF - 1 < nk) {
-      const int nb = cur == 0 ? NBUF - 1 : cur - 1;  // (kt + NBUF - 1) % NBUF: stage kt - 1's
-      issue(nb, kbeg + (kt + NBUF - 1) * BK);
-    }
+    // stage kt + NBUF - 1 goes into stage kt - 1's buffer, free since the barrier.  Its pieces
+    // leave one by one between this stage's MFMA groups (piece q after group 2 NG q / PPW): all
+    // 48 of a CU's pieces issued together at the barrier kept both waves of every SIMD waiting
+    // for memory-issue room while their MFMA pipe idled
+    const bool more = kt + NBUF - 1 < nk;
+    const int nb = cur == 0 ? NBUF - 1 : cur - 1;   // (kt + NBUF - 1) % NBUF
+    const int kn = kbeg + (kt + NBUF - 1) * BK;
     const char* S = smem + cur * BUF;
     cur = cur + 1 == NBUF ? 0 : cur + 1;
     Frags f0, f1;
@@ -2033,6 +2038,13 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
         read(f1, S, 1);
         __builtin_amdgcn_sched_barrier(0);
       }
+#pragma unroll
+      for (int q = 0; q < PPW; ++q)
+        if (q * 2 * NG / PPW == g && more) {
+          __builtin_amdgcn_sched_barrier(0);
+          issue_one(nb, kn, q);
+          __builtin_amdgcn_sched_barrier(0);
+        }
     }
   }
   if constexpr (H3) {
