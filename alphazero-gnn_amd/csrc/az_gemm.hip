@@ -4261,9 +4261,15 @@ static bool launch_x3(GemmArgs& a, size_t ws_bytes, hipStream_t s, const PreSpli
       hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3, 5>), grid, dim3(512), 0, s, a);
     else if (tile == 1 && abl == 6)
       hipLaunchKernelGGL((gemm_p3<256, 128, 4, 2, true, 3, 6>), grid, dim3(512), 0, s, a);
-    else if (tile == 1 && a.splits == 1 && tuning_env("AZ_P3_WIDE")) {
-      // 256 x 256 tiles (waves 4 x 2 of 64 x 128): half the L2 misses per flop of 256 x 128
-      const dim3 gw((unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256)));
+    else if (tile == 1 && tuning_env("AZ_P3_WIDE")) {
+      // 256 x 256 tiles (waves 4 x 2 of 64 x 128): 2/3 of the 256 x 128 tile's DMA bytes per
+      // flop; AZ_P3_WIDE_SPLITS = its split-K (default: none)
+      static const char* env_ws = tuning_env("AZ_P3_WIDE_SPLITS");
+      int S = env_ws ? atoi(env_ws) : 1;
+      while (S > 1 && (!a.slab || (size_t)S * a.M * a.N * 4 > ws_bytes)) --S;
+      a.kc = S > 1 ? ((a.K + S - 1) / S + 31) / 32 * 32 : a.K;
+      a.splits = S > 1 ? (a.K + a.kc - 1) / a.kc : 1;
+      const dim3 gw((unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256) * a.splits));
       hipLaunchKernelGGL((gemm_p3<256, 256, 4, 2, true>), gw, dim3(512), 0, s, a);
     }
     else if (tile == 1 && ring == 2) {

@@ -472,7 +472,10 @@ def large_batch_leg(torch, ops, ev, device, B=65536, reps=5):
     torch.cuda.empty_cache()
     return {"batch": B, "ms_per_batch": round(ms, 3), "boards_per_s": round(B / (ms * 1e-3), 1),
             "gemm": x3_roofline("az_gemm_f32 output_transform.0 at M = %d" % B,
-                                2.0 * B * F * F, gemm_ms * 1e-3, products=gemm_products(B))}
+                                2.0 * B * F * F, gemm_ms * 1e-3,
+                                traffic=pmc_traffic("gemm_large") if B == 65536 else None,
+                                traffic_run=pmc_run("gemm_large") if B == 65536 else None,
+                                products=gemm_products(B))}
 
 
 def gemm_products(M, N=F, K=F):

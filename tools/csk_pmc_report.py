@@ -34,7 +34,7 @@ def main():
             for r in csv.DictReader(open(f)):
                 kt[r["Name"].split("(")[0]] = (float(r["AverageNs"]), int(r["Calls"]))
         fe, wr, tc, sq = (counters(d, s) for s in ("fetch", "write", "tcc", "sq"))
-        gemm = [k for k in fe if "gemm_x3" in k]
+        gemm = [k for k in fe if "gemm_x3" in k or "gemm_p3" in k]
         fix = [k for k in fe if "fixup" in k]
         if not gemm:
             continue
@@ -53,7 +53,7 @@ def main():
         h, m = mean(tc[g]["TCC_HIT_sum"]), mean(tc[g]["TCC_MISS_sum"])
         if h is not None and m:
             row["l2_hit"] = round(h / (h + m), 3)
-        ns = next((v[0] for k, v in kt.items() if "gemm_x3" in k), None)
+        ns = next((v[0] for k, v in kt.items() if "gemm_x3" in k or "gemm_p3" in k), None)
         fns = next((v[0] for k, v in kt.items() if "fixup" in k), None)
         row["kernel_us"] = round(ns / 1e3, 2) if ns else None
         row["fixup_us"] = round(fns / 1e3, 2) if fns else None
