@@ -1636,6 +1636,13 @@ constexpr int p3_smem_bytes() {
   return NBUF * BUF > STAGE ? NBUF * BUF : STAGE;
 }
 
+#ifdef AZ_P3_STAMPS
+// timing-experiment library only (tools/p3_stamp_probe.py): lane 0 of every wave of a gemm_p3
+// block records s_memrealtime (100 MHz) at fixed points -- [block][wave][72]: 0 body start,
+// 1 prologue issued, 2 + 2 kt before stage kt's wait, 3 + 2 kt after its barrier, 66 loop end,
+// 67 epilogue end, 68 / 69 s_memtime at start / end, 70 HW_ID, 71 XCC_ID
+__device__ unsigned long long* g_p3_stamps;
+#endif
 // gemm_p3_body (below): the tile on operands already split into planes, LDS-DMA only
 template <int BM, int BN, int WGM, int WGN, bool H3 = false, bool FLEX = false, int NBUF = 2,
           int ABL = 0, bool HEADS = false>
@@ -2011,13 +2018,33 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
   HeadsRegs<TJ> hregs;                 // HEADS: the heads' weights, loaded before the loop
   if constexpr (HEADS) heads_preload<TJ>(p, n0 + wn * WN, hregs);
   const int nk = (kend - kbeg) / BK;
+#ifdef AZ_P3_STAMPS
+  unsigned long long* const stp = (g_p3_stamps && !FLEX && lane == 0)
+                                      ? g_p3_stamps + ((size_t)blockIdx.x * NW + wave) * 72
+                                      : nullptr;
+  auto stamp = [&](int slot) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if (stp) stp[slot] = t;
+  };
+  if (stp) {
+    stp[68] = __builtin_amdgcn_s_memtime();
+    stp[70] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));
+    stp[71] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((32 - 1) << 11));
+  }
+  stamp(0);
+#else
+  auto stamp = [](int) {};
+#endif
   if (nk > 0) issue(0, kbeg);
   if (NBUF == 3 && nk > 1) issue(1, kbeg + BK);
+  stamp(1);
   int cur = 0;             // kt % NBUF
   for (int kt = 0; kt < nk; ++kt) {
+    if (kt < 32) stamp(2 + 2 * kt);
     if (NBUF == 3 && kt + 1 < nk) wait_vm<PPW>();   // stage kt + 1's pieces may still fly
     else wait_vm<0>();     // this wave's pieces of stage kt have landed
     lds_barrier();         // ... everyone's; and every wave is done reading stage kt - 1
+    if (kt < 32) stamp(3 + 2 * kt);
     // stage kt + NBUF - 1 goes into stage kt - 1's buffer, free since the barrier.  Its pieces
     // leave one by one between this stage's MFMA groups (piece q after group 2 NG q / PPW): all
     // 48 of a CU's pieces issued together at the barrier kept both waves of every SIMD waiting
@@ -2047,6 +2074,7 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
         }
     }
   }
+  stamp(66);
   if constexpr (H3) {
     float iw[TJ];
 #pragma unroll
@@ -2079,10 +2107,18 @@ __device__ __forceinline__ void gemm_p3_body(const GemmArgs& p, char* smem, int 
     float* f = reinterpret_cast<float*>(smem);
     heads_tile_epilogue<TI, TJ, WGM, WGN>(p, acc, hregs, m0 + wm * WM, n0 + wn * WN, nt, sp, wm,
                                           wn, f + wave * (WM * 36), f + NW * WM * 36);
+#ifdef AZ_P3_STAMPS
+    stamp(67);
+    if (stp) stp[69] = __builtin_amdgcn_s_memtime();
+#endif
     return;
   }
   tile_epilogue<32, TI, TJ>(p, acc, m0 + wm * WM, n0 + wn * WN, sp,
                             reinterpret_cast<float*>(smem) + wave * (WM * 36));
+#ifdef AZ_P3_STAMPS
+  stamp(67);
+  if (stp) stp[69] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 template <int BM, int BN, int WGM, int WGN, bool H3 = false, int NBUF = 2, int ABL = 0,
@@ -4537,6 +4573,14 @@ int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* plane
   const int rc = check_launch("splitk_reduce_split_kernel");
   return rc == AZ_OK ? 1 : rc;
 }
+
+#ifdef AZ_P3_STAMPS
+}  // namespace az
+extern "C" int az_debug_p3_stamps(void* buf) {   // timing-experiment library only
+  return hipMemcpyToSymbol(HIP_SYMBOL(az::g_p3_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+namespace az {
+#endif
 
 // Whether a GEMM with weight w (n x k, row stride ld) takes the P2 path's cached weight planes,
 // i.e. whether splitting its A ahead of the call (PreSplitA) can pay off.
