@@ -4582,6 +4582,25 @@ extern "C" int az_debug_p3_stamps(void* buf) {   // timing-experiment library on
 namespace az {
 #endif
 
+// Whether az_gemm_f32(d), given a PreSplitA of its A, takes the P2 tiles and so never reads
+// d->A: gemm_f32_partial's and launch_x3's conditions for that path (product dispatch: M > 64,
+// K-major 32-k operands, the workspace for the scales, registered W) and W's planes in the cache
+// (w_planes, which fills it now if needed: the later p2_prep of the same call then returns them)
+bool gemm_p2_certain(const az_gemm_desc* d, hipStream_t s) {
+  if (!(d->a_kmajor && d->b_kmajor && !d->A2 && !d->a_rows && !d->b_rows && d->M > 64 &&
+        d->K >= 1024 && d->N >= 256 && d->K % 32 == 0 && d->lda % 4 == 0 && d->ldb % 4 == 0 &&
+        aligned16(d->A) && aligned16(d->B) && d->ws && d->act != AZ_ACT_DRELU))
+    return false;
+  if (tuning_env("AZ_GEMM_X3") || tuning_env("AZ_GEMM_SPLITS") || tuning_env("AZ_GEMM_NOP2") ||
+      tuning_env("AZ_GEMM_PREC") || tuning_env("AZ_GEMM_KSLICE"))
+    return false;
+  const size_t sa_bytes = ((size_t)2 * (d->M + d->N) * sizeof(float) + 255) / 256 * 256;
+  if (d->ws_bytes < sa_bytes + 512) return false;
+  if (!weights_registered(d->B, d->N, d->K, d->ldb)) return false;
+  const float* sw = nullptr;
+  return w_planes(d->B, d->N, d->K, d->ldb, s, &sw) != nullptr;
+}
+
 // Whether a GEMM with weight w (n x k, row stride ld) takes the P2 path's cached weight planes,
 // i.e. whether splitting its A ahead of the call (PreSplitA) can pay off.
 bool gemm_p2_weights(const float* w, int n, int k, int ld) {

@@ -403,7 +403,8 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
 #pragma unroll
     for (int it = 0; it < NIT; ++it) c1_check(2, tid + 512 * it);     // the image at the end
 #endif
-    f32x4v* dst = reinterpret_cast<f32x4v*>(feat + (size_t)b0 * 3136);
+    // feat may be null when apl is not: the caller's GEMM then reads only the planes
+    f32x4v* dst = feat ? reinterpret_cast<f32x4v*>(feat + (size_t)b0 * 3136) : nullptr;
     const f32x4v* src = reinterpret_cast<const f32x4v*>(ob);
     if (!apl) {
       for (int i = tid; i < nb * 784; i += 512) dst[i] = src[i];
@@ -417,8 +418,10 @@ __device__ __forceinline__ void c4_trunk_tile(const int8_t* __restrict__ boards,
       float inv;
       const float sc = h3_scale(mx, H3_TA, &inv);
       const f32x4v lo = src[2 * ch], hi = src[2 * ch + 1];
-      dst[2 * ch] = lo;
-      dst[2 * ch + 1] = hi;
+      if (dst) {
+        dst[2 * ch] = lo;
+        dst[2 * ch + 1] = hi;
+      }
       u32x4 o[2];
       split2s(__builtin_bit_cast(f32x4, lo), __builtin_bit_cast(f32x4, hi), sc, o);
       *reinterpret_cast<u32x4*>(apl + p2_chunk(b0 + b, c, 0, 3136)) = o[0];
@@ -942,7 +945,7 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
                            const float* conv1_b, const float* conv2_w, const float* conv2_b,
                            float* feat, unsigned short* apl, float* asc, bool* split,
                            hipStream_t s, const TrunkHeads* heads = nullptr,
-                           bool* heads_done = nullptr) {
+                           bool* heads_done = nullptr, bool feat_optional = false) {
   static const char* env = tuning_env("AZ_TRUNK_NB");   // tuning experiments only
   // boards per block from a fitted time model (below; every NB is bit-identical); when the caller
   // wants output_transform.0's A pre-split (apl), NB > 4 pays the separate split pass (~3.8 ns
@@ -984,6 +987,9 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
   // the standard heads ride along when the rows are staged in LDS (the split-A kernel)
   const bool hk = sa && heads && heads->A >= 1 && heads->A <= 8;
   if (heads_done) *heads_done = hk;
+  // feat_optional: the caller's GEMM takes the pre-split operand for certain and nothing else
+  // reads feat unless the standard heads do -- the split-A kernel then skips the fp32 rows
+  float* const feat_sa = feat_optional && sa && (!heads || hk) ? nullptr : feat;
 #ifdef AZ_TUNING   // AZ_TRUNK_DYN_LDS=<bytes>: extra (unused) LDS per block, to limit residency
   static const char* env_dyn = tuning_env("AZ_TRUNK_DYN_LDS");
   const size_t dyn = env_dyn ? (size_t)atol(env_dyn) : 0;
@@ -993,10 +999,10 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
 #define AZ_TRUNK_RW(NB_, RW_)                                                                    \
   if (hk) hipLaunchKernelGGL((c4_trunk_split_a_kernel<NB_, true, RW_>),                          \
                              dim3((B + NB_ - 1) / NB_), dim3(512), dyn, s, boards, B, conv1_w,  \
-                             conv1_b, conv2_w, conv2_b, feat, apl, asc, w2f, *heads);            \
+                             conv1_b, conv2_w, conv2_b, feat_sa, apl, asc, w2f, *heads);         \
   else if (sa) hipLaunchKernelGGL((c4_trunk_split_a_kernel<NB_, false, RW_>),                    \
                                   dim3((B + NB_ - 1) / NB_), dim3(512), dyn, s, boards, B,      \
-                                  conv1_w, conv1_b, conv2_w, conv2_b, feat, apl, asc, w2f,      \
+                                  conv1_w, conv1_b, conv2_w, conv2_b, feat_sa, apl, asc, w2f,   \
                                   TrunkHeads{});                                                 \
   else hipLaunchKernelGGL((c4_trunk_kernel<NB_, RW_>), dim3((B + NB_ - 1) / NB_), dim3(512),    \
                           dyn, s, boards, B, conv1_w, conv1_b, conv2_w, conv2_b, feat, w2f);
@@ -1075,6 +1081,7 @@ int gemm_f32(const az_gemm_desc* d, hipStream_t s);
 int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out, const PreSplitA* pre,
                      const HeadsEpi* he = nullptr, bool* heads_done = nullptr);
 int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s);
+bool gemm_p2_certain(const az_gemm_desc* d, hipStream_t s);
 int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* planes, float* sc,
                         hipStream_t s);
 bool gemm_p2_weights(const float* w, int n, int k, int ld);
@@ -1480,13 +1487,28 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
     const TrunkHeads th{e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,
                         e->logp, pi, v};
     bool heads_done = false;
+    const bool want_th = v && e->logp && e->fc_policy_w && e->fc_policy_b && e->fc_value_w &&
+                         e->fc_value_b && !no_th && aligned16(e->fc_policy_w) &&
+                         aligned16(e->fc_value_w);
+    // e->feat stays unwritten when output_transform.0 certainly takes the trunk's pre-split
+    // operand (gemm_p2_certain on the descriptor transform_heads_impl builds below) and the
+    // standard heads, if wanted, come from the trunk's LDS rows
+    bool feat_opt = false;
+    static const bool keep_feat = tuning_env("AZ_EVAL_KEEP_FEAT") != nullptr;   // A/B experiments
+    if (R.planes && gv && e->ot0_w && e->ot0_b && e->hidden && (!v || want_th) && !keep_feat) {
+      const size_t part_bytes = align256(az_heads_ws_bytes(B, 3136, e->A > 0 ? e->A : 1));
+      az_gemm_desc d = {};
+      d.M = B; d.N = 3136; d.K = 3136;
+      d.A = e->feat; d.lda = 3136; d.a_kmajor = 1;
+      d.B = e->ot0_w; d.ldb = 3136; d.b_kmajor = 1; d.bias = e->ot0_b; d.act = AZ_ACT_RELU;
+      d.C = e->hidden; d.ldc = 3136;
+      d.ws = static_cast<char*>(e->ws) + part_bytes;
+      d.ws_bytes = e->ws_bytes > part_bytes + R.bytes ? e->ws_bytes - part_bytes - R.bytes : 0;
+      feat_opt = gemm_p2_certain(&d, as_stream(stream));
+    }
     rc = c4_trunk_launch(boards, B, e->conv1_w, e->conv1_b, e->conv2_w, e->conv2_b, e->feat,
-                         R.planes, R.sc, &split, as_stream(stream),
-                         v && e->logp && e->fc_policy_w && e->fc_policy_b && e->fc_value_w &&
-                                 e->fc_value_b && !no_th && aligned16(e->fc_policy_w) &&
-                                 aligned16(e->fc_value_w)
-                             ? &th : nullptr,
-                         &heads_done);
+                         R.planes, R.sc, &split, as_stream(stream), want_th ? &th : nullptr,
+                         &heads_done, feat_opt);
     if (!rc && v && !heads_done)
       rc = az_heads_fwd(e->feat, 3136, e->feat, 3136, B, 3136, e->fc_policy_w, e->fc_policy_b,
                         e->A, e->fc_value_w, e->fc_value_b, e->logp, pi, v, e->ws, e->ws_bytes,
