@@ -3709,9 +3709,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_split_kernel(GemmArgs p,
       }
     const int ch = tid + 256 * u;
     if (ch < nch) {
-      float* dst = p.C + (size_t)r * p.ldc + 8 * ch;
-      *reinterpret_cast<f32x4*>(dst) = v[u][0];
-      *reinterpret_cast<f32x4*>(dst + 4) = v[u][1];
+      if (p.C) {                                  // null: the caller needs only the planes
+        float* dst = p.C + (size_t)r * p.ldc + 8 * ch;
+        *reinterpret_cast<f32x4*>(dst) = v[u][0];
+        *reinterpret_cast<f32x4*>(dst + 4) = v[u][1];
+      }
       m = fmaxf(m, fmaxf(fmaxf(fmaxf(fabsf(v[u][0][0]), fabsf(v[u][0][1])),
                                fmaxf(fabsf(v[u][0][2]), fabsf(v[u][0][3]))),
                          fmaxf(fmaxf(fabsf(v[u][1][0]), fabsf(v[u][1][1])),
@@ -4552,7 +4554,7 @@ int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s) {
 // the shapes / epilogue do not qualify (nothing launched: the caller reduces the usual way), or a
 // negative AZ_E* code.
 int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* planes, float* sc,
-                        hipStream_t s) {
+                        hipStream_t s, bool write_c) {
   if (!(splits >= 2 && splits <= 8 && d->N % 32 == 0 && d->N <= 4096 && d->M > 0 && !d->C2 &&
         !d->R && !d->G && !d->c_rows && d->beta == 0.f &&
         (d->act == AZ_ACT_NONE || d->act == AZ_ACT_RELU) && d->ldc % 4 == 0 && aligned16(d->C) &&
@@ -4561,7 +4563,7 @@ int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* plane
     return 0;
   GemmArgs a = {};
   a.M = d->M; a.N = d->N;
-  a.bias = d->bias; a.act = d->act; a.C = d->C; a.ldc = d->ldc;
+  a.bias = d->bias; a.act = d->act; a.C = write_c ? d->C : nullptr; a.ldc = d->ldc;
   a.slab = static_cast<float*>(d->ws);
   a.splits = splits;
   switch (splits) {

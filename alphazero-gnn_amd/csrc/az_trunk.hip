@@ -1083,7 +1083,7 @@ int gemm_f32_partial(const az_gemm_desc* d, hipStream_t s, int* splits_out, cons
 int splitk_reduce(const az_gemm_desc* d, int splits, hipStream_t s);
 bool gemm_p2_certain(const az_gemm_desc* d, hipStream_t s);
 int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* planes, float* sc,
-                        hipStream_t s);
+                        hipStream_t s, bool write_c = true);
 bool gemm_p2_weights(const float* w, int n, int k, int ld);
 const float* conv2_frags(const float* w2, hipStream_t s);
 
@@ -1367,7 +1367,8 @@ static int transform_heads_impl(const float* x, int B, int F, const float* w0, c
                                 const float* w2, const float* b2, const float* wp,
                                 const float* bp, int A, const float* wv, const float* bv,
                                 float* hidden, float* y, float* logp, float* pi, float* v,
-                                void* ws, size_t ws_bytes, void* stream, const PreSplitA* pre_x) {
+                                void* ws, size_t ws_bytes, void* stream, const PreSplitA* pre_x,
+                                bool hidden_scratch = false) {
   const size_t part_bytes = align256(az_heads_ws_bytes(B, F, A > 0 ? A : 1));
   AZ_REQUIRE(ws_bytes >= part_bytes, AZ_EINVAL, "az_transform_heads_fwd: workspace too small");
   hipStream_t s = as_stream(stream);
@@ -1391,7 +1392,26 @@ static int transform_heads_impl(const float* x, int B, int F, const float* w0, c
   if ((rc = gemm_f32_partial(&d, s, &S, pre_x))) return rc;
   PreSplitA pre_h{nullptr, nullptr};
   if (S > 1) {
-    rc = R.planes ? splitk_reduce_split(&d, S, R.planes, R.sc, s) : 0;
+    // hidden_scratch (az_c4_eval_fwd's e->hidden): the fp32 hidden rows are skipped when
+    // output_transform.2 certainly takes the reduce's planes -- gemm_p2_certain on the
+    // descriptor linear_heads_impl builds (y NULL: its scratch y at the workspace's end)
+    bool write_c = true;
+    if (R.planes && hidden_scratch && A > 0 && A <= 32) {
+      size_t wsb = ws_bytes - R.bytes;
+      const size_t part2 = align256(az_heads_ws_bytes(B, F, A));
+      const size_t yb = y ? 0 : align256((size_t)4 * B * F);
+      if (wsb >= part2 + yb + 256) {
+        wsb = y ? wsb : (wsb - yb) / 256 * 256;
+        az_gemm_desc d2 = {};
+        d2.M = B; d2.N = F; d2.K = F;
+        d2.A = hidden; d2.lda = F; d2.a_kmajor = 1;
+        d2.B = w2; d2.ldb = F; d2.b_kmajor = 1; d2.bias = b2; d2.act = AZ_ACT_NONE;
+        d2.ws = static_cast<char*>(ws) + part2;
+        d2.ws_bytes = wsb - part2;
+        write_c = !gemm_p2_certain(&d2, s);
+      }
+    }
+    rc = R.planes ? splitk_reduce_split(&d, S, R.planes, R.sc, s, write_c) : 0;
     if (rc < 0) return rc;
     if (rc == 1) pre_h = {R.planes, R.sc};
     else if ((rc = splitk_reduce(&d, S, s))) return rc;
@@ -1468,6 +1488,9 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
   constexpr int TRUNK_HEADS_ONE_LAUNCH = 320;   // az_c4_trunk_heads_fwd's one-launch limit
   PreRegion R{nullptr, nullptr, 0};
   bool split = false;
+  // the fp32 scratch rows (e->feat, e->hidden) a certain pre-split hand-off never reads are not
+  // written; AZ_EVAL_KEEP_FEAT (tuning build) writes them for A/B runs
+  static const bool keep_feat = tuning_env("AZ_EVAL_KEEP_FEAT") != nullptr;
   static const bool no_fuse = tuning_env("AZ_NO_PRESPLIT") != nullptr;   // A/B experiments
   static const bool no_both = tuning_env("AZ_NO_PRESPLIT_BOTH") != nullptr;
   if (gv && (!v || (B > TRUNK_HEADS_ONE_LAUNCH && !no_both)) && !no_fuse && e->ot0_w &&
@@ -1494,7 +1517,6 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
     // operand (gemm_p2_certain on the descriptor transform_heads_impl builds below) and the
     // standard heads, if wanted, come from the trunk's LDS rows
     bool feat_opt = false;
-    static const bool keep_feat = tuning_env("AZ_EVAL_KEEP_FEAT") != nullptr;   // A/B experiments
     if (R.planes && gv && e->ot0_w && e->ot0_b && e->hidden && (!v || want_th) && !keep_feat) {
       const size_t part_bytes = align256(az_heads_ws_bytes(B, 3136, e->A > 0 ? e->A : 1));
       az_gemm_desc d = {};
@@ -1525,5 +1547,5 @@ extern "C" int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, 
   return transform_heads_impl(e->feat, B, 3136, e->ot0_w, e->ot0_b, e->ot2_w, e->ot2_b,
                               e->fc_policy_w, e->fc_policy_b, e->A, e->fc_value_w, e->fc_value_b,
                               e->hidden, nullptr, e->glogp, gpi, gv, e->ws, e->ws_bytes, stream,
-                              split ? &pre : nullptr);
+                              split ? &pre : nullptr, !keep_feat);
 }

@@ -175,9 +175,10 @@ typedef struct az_c4_eval {
  * written for B > 8), so the outputs are bit-identical to az_c4_trunk_fwd +
  * az_transform_heads_fwd(y = NULL).  Both v and gv above 320 rows (predict_both): the same
  * hand-off, and the trunk kernel that writes the split operand also forms the standard heads from
- * the rows in its LDS tile -- bit-identical to az_heads_fwd on feat.  e->feat is scratch: above
- * 64 rows, when output_transform.0 takes the pre-split operand for certain (registered weights,
- * their planes cached) and nothing else reads the fp32 rows, they are not written. */
+ * the rows in its LDS tile -- bit-identical to az_heads_fwd on feat.  e->feat and e->hidden are
+ * scratch: above 64 rows, when output_transform.0 / .2 take the pre-split operands for certain
+ * (registered weights, their planes cached) and nothing else reads the fp32 rows, those rows are
+ * not written. */
 int az_c4_eval_fwd(const az_c4_eval* e, const int8_t* boards, int B, float* pi, float* v,
                    float* gpi, float* gv, void* stream);
 

@@ -38,17 +38,17 @@ def test_c4_gnn_eval_equals_unfused_calls(ev, B):
     Wn, Gn = ev.nnet.params, ev.gnn.params
     rng = np.random.default_rng(B)
     boards = torch.from_numpy(rng.integers(-1, 2, size=(B, 7, 7)).astype(np.int8)).cuda()
-    # above 64 rows output_transform.0 takes the trunk's pre-split operand for certain and the
-    # fp32 feature rows are not written (az_hip.h az_c4_eval_fwd): NaN there would reach the
+    # above 64 rows output_transform.0 / .2 take the pre-split operands for certain and the fp32
+    # feature / hidden rows are not written (az_hip.h az_c4_eval_fwd): NaN there would reach the
     # outputs if anything still read them
     feat = torch.full((B, 3136), float("nan"), device="cuda")
-    hidden = torch.empty((B, 3136), device="cuda")
+    hidden = torch.full((B, 3136), float("nan"), device="cuda")
     logp, pi, v = ops.c4_gnn_eval(boards, Wn, Gn, feat=feat, hidden=hidden)
     feat_u, h_u, logp_u, pi_u, v_u = _unfused(ops, boards, Wn, Gn)
     _, pi_e, v_e = ev.evaluate(boards, gnn=True)
     torch.cuda.synchronize()
     assert torch.equal(feat, feat_u) or (B > 64 and bool(torch.isnan(feat).all()))
-    assert torch.equal(hidden, h_u)
+    assert torch.equal(hidden, h_u) or (B > 64 and bool(torch.isnan(hidden).all()))
     assert torch.equal(logp, logp_u) and torch.equal(pi, pi_u) and torch.equal(v, v_u)
     assert torch.equal(pi, pi_e) and torch.equal(v, v_e)
 
