@@ -38,6 +38,9 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 TOL = 1e-5
+# L1 trajectory error / the reference's L1 travel: measured 0.020 overall (max tensor 0.084,
+# conv2.bias) at lr 0.001 and 0 at lr 0.01 (profiles/r06/traj/); a wrong gradient gives ~1
+TRAJ_BOUND, TRAJ_BOUND_TENSOR = 0.1, 0.25
 RUNS = ("c4_gnn_trained_lr001.npz", "c4_gnn_trained_lr01.npz")
 
 
@@ -100,6 +103,32 @@ def test_trained_weights_follow_reference_training(trained):
     report(f"trained_{t.tag}/weights_vs_reference_training", per_tensor=per)
     bad = {k: v for k, v in per.items() if v["max_abs"] > v["tol"]}
     assert not bad, bad
+
+
+def test_trained_cnn_follows_reference_trajectory(trained):
+    """The same comparison relative to how far training moved the weights (VERDICT r05 weak #7:
+    the per-tensor envelope above allows up to 0.19 where |w| <= 0.24).  For the CNN, held in
+    full: the L1 distance to the reference's trained weights over the L1 distance the reference
+    itself travelled from the common start, per tensor and over all tensors.  A near-zero
+    gradient's Adam step (lr / eps at g = 0) scatters single weights by ~lr, which the L1 ratio
+    averages out; a wrong gradient moves whole tensors elsewhere and shows up here as a ratio
+    near 1 or above."""
+    t, zz = trained, trained.zz
+    W0 = split_weights(golden("c4_net.npz"), "w/")
+    per, num, den = {}, 0.0, 0.0
+    for k, a in t.W.items():
+        ref = zz["w/" + k]
+        w0 = W0[k].numpy() if hasattr(W0[k], "numpy") else np.asarray(W0[k])
+        d = float(np.abs(ref - w0).sum())
+        e = float(np.abs(a - ref).sum())
+        per[k] = {"l1_err": e, "l1_travel": d, "ratio": e / max(d, 1e-30)}
+        num += e
+        den += d
+    total = num / den
+    report(f"trained_{t.tag}/cnn_trajectory_vs_reference", total_ratio=total, per_tensor=per,
+           bound=TRAJ_BOUND, bound_tensor=TRAJ_BOUND_TENSOR)
+    assert total <= TRAJ_BOUND, (total, per)
+    assert all(v["ratio"] <= TRAJ_BOUND_TENSOR for v in per.values()), per
 
 
 def _check(t, name, lp, pi, v, rows):
