@@ -105,6 +105,12 @@ def test_trained_weights_follow_reference_training(trained):
     assert not bad, bad
 
 
+def c4_gnn_weights_np(t):
+    from azhip.weights import gnn_spec, synthetic_state_dict
+    from conftest import golden as _g
+    return synthetic_state_dict(gnn_spec(3136, 2), int(_g("c4_gnn.npz")["seed"]))
+
+
 def test_trained_cnn_follows_reference_trajectory(trained):
     """The same comparison relative to how far training moved the weights (VERDICT r05 weak #7:
     the per-tensor envelope above allows up to 0.19 where |w| <= 0.24).  For the CNN, held in
@@ -125,6 +131,23 @@ def test_trained_cnn_follows_reference_trajectory(trained):
         num += e
         den += d
     total = num / den
+    # the GNN by the fixture's spot values: reported, not held -- the reference's own 3- vs
+    # 8-thread runs already spread these tensors by up to 0.15 at lr 0.01 (|w| <= 0.12) and 0.04
+    # at lr 0.001 (envmax/g/...), Adam's lr / eps response to near-zero gradients; measured
+    # ratios 0.34 (lr 0.001) / 0.40 (lr 0.01), profiles/r06/traj/
+    G0 = c4_gnn_weights_np(t)
+    gper, gnum, gden = {}, 0.0, 0.0
+    for k, a in t.w.gnn.params.cpu_state_dict().items():
+        idx = zz["gidx/" + k]
+        ref = zz["gval/" + k]
+        w0 = G0[k].ravel()[idx]
+        d = float(np.abs(ref - w0).sum())
+        e = float(np.abs(a.numpy().ravel()[idx] - ref).sum())
+        gper[k] = {"l1_err": e, "l1_travel": d, "ratio": e / max(d, 1e-30)}
+        gnum += e
+        gden += d
+    report(f"trained_{t.tag}/gnn_spot_trajectory_vs_reference", total_ratio=gnum / max(gden, 1e-30),
+           per_tensor=gper)
     report(f"trained_{t.tag}/cnn_trajectory_vs_reference", total_ratio=total, per_tensor=per,
            bound=TRAJ_BOUND, bound_tensor=TRAJ_BOUND_TENSOR)
     assert total <= TRAJ_BOUND, (total, per)
