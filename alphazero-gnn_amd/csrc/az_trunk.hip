@@ -981,6 +981,11 @@ static int c4_trunk_launch(const int8_t* boards, int B, const float* conv1_w,
       if (nb == 1 || t < best) best = t, nbk = nb;
     }
   }
+  // the split-A form without heads (the batched predict_with_gnn) above one round of 256 blocks
+  // and up to two blocks per CU: one board per block measured 1.3 us faster per B = 512 step
+  // than the model's NB = 2 (97.5 vs 98.8 us, tools/gpu_r06_nb_sweep.sh; the kernels alone are
+  // within 0.3 us: profiles/r06/trunk_nb/)
+  if (regw && apl && asc && !heads && B > cus && B <= 2 * cus) nbk = 1;
   if (env) nbk = atoi(env);
   const bool sa = apl && asc && nbk >= 1 && nbk <= 4;
   if (split) *split = sa;
