@@ -3919,7 +3919,7 @@ __global__ __launch_bounds__(256) void heads_tiles_finalize_kernel(HeadsEpi he, 
                                                                    int P, CskPlan q) {
   constexpr int HS = HEADS_TILE_SLOTS;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   // one row per wave
   const float* src = he.part + (size_t)min(row, M - 1) * P * HS;
   float s[16];
 #pragma unroll
@@ -4054,8 +4054,11 @@ const float* conv2_frags(const float* w2, hipStream_t s) {
 // the split-K HEADS tiles' finalize (P = 128-column tiles x k splits)
 static void launch_heads_finalize(GemmArgs& a, hipStream_t s) {
   const int P = (a.N + 127) / 128 * a.splits;
-  hipLaunchKernelGGL(heads_tiles_finalize_kernel<false>, dim3((a.M + 3) / 4), dim3(256), 0, s,
-                     a.he, a.M, a.N, P, CskPlan{});
+  // one wave (one row) per block: the M = 512 rows over every CU rather than 128 of them
+  // (6.01 -> 5.11 us per launch, profiles/r06/finalize_ab); staging the row's slots through
+  // LDS by coalesced loads first, as the stream-K form does, measured 6.57 us
+  hipLaunchKernelGGL(heads_tiles_finalize_kernel<false>, dim3(a.M), dim3(64), 0, s, a.he, a.M,
+                     a.N, P, CskPlan{});
   a.heads_done = 1;
 }
 
