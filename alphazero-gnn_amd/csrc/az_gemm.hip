@@ -3665,26 +3665,27 @@ __global__ __launch_bounds__(256) void h3_split_rows_kernel(const float* __restr
 }
 
 // The split-K reduce of a GEMM whose C is the next GEMM's A, fused with that GEMM's A split (the
-// output_transform.0 -> .2 hand-off, gnn_utils.py:115): one 256-thread block per row; each lane's
-// 8-column chunks are summed over the S slabs in slab order from 0.f, then bias and activation
+// output_transform.0 -> .2 hand-off, gnn_utils.py:115): one block per row; each lane's
+// 8-column chunk(s) are summed over the S slabs in slab order from 0.f, then bias and activation
 // -- splitk_reduce4_kernel's arithmetic, so C's bits are unchanged -- and stored; the row's max
 // |C| (one block reduction) gives the scale, and the chunks, still in registers, leave as the two
 // fp16 planes + scales h3_split_rows_kernel would make of C (out: the p2_chunk layout, sc [2][M]).
 // N % 32 == 0, N <= 4096, bias / activation epilogue only, 16-B aligned rows (splitk_reduce_split).
-template <int S>
-__global__ __launch_bounds__(256) void splitk_reduce_split_kernel(GemmArgs p,
+template <int S, int U>
+__global__ __launch_bounds__(512) void splitk_reduce_split_kernel(GemmArgs p,
                                                                   unsigned short* __restrict__ out,
                                                                   float* __restrict__ sc) {
-  __shared__ float wm[4];
+  __shared__ float wm[8];
+  const int T = blockDim.x;          // U chunks per thread, stride T
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int nch = p.N >> 3;
   const size_t plane = (size_t)p.M * p.N;
   const float* sl = p.slab + (size_t)r * p.N;
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  f32x4 x[2][S][2], bb[2][2];
+  f32x4 x[U][S][2], bb[U][2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {               // every load issued before the first add
-    const int c = 8 * min(tid + 256 * u, nch - 1);
+  for (int u = 0; u < U; ++u) {               // every load issued before the first add
+    const int c = 8 * min(tid + T * u, nch - 1);
 #pragma unroll
     for (int q = 0; q < S; ++q) {
       x[u][q][0] = *reinterpret_cast<const f32x4*>(sl + q * plane + c);
@@ -3693,10 +3694,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_split_kernel(GemmArgs p,
     bb[u][0] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + c) : z;
     bb[u][1] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + c + 4) : z;
   }
-  f32x4 v[2][2];
+  f32x4 v[U][2];
   float m = 0.f;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < U; ++u) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -3707,7 +3708,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_split_kernel(GemmArgs p,
         if (p.bias) t += bb[u][h][e];
         v[u][h][e] = apply_act(t, p.act);
       }
-    const int ch = tid + 256 * u;
+    const int ch = tid + T * u;
     if (ch < nch) {
       if (p.C) {                                  // null: the caller needs only the planes
         float* dst = p.C + (size_t)r * p.ldc + 8 * ch;
@@ -3724,7 +3725,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_split_kernel(GemmArgs p,
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if (lane == 0) wm[tid >> 6] = m;
   __syncthreads();
-  m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+  m = wm[0];
+  for (int w = 1; w < (T >> 6); ++w) m = fmaxf(m, wm[w]);
   float inv;
   const float s = h3_scale(m, H3_TA, &inv);
   if (tid == 0) {
@@ -3732,8 +3734,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_split_kernel(GemmArgs p,
     sc[p.M + r] = inv;
   }
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int ch = tid + 256 * u;
+  for (int u = 0; u < U; ++u) {
+    const int ch = tid + T * u;
     if (ch < nch) {
       u32x4 o[2];
       split2s(v[u][0], v[u][1], s, o);
@@ -4569,8 +4571,11 @@ int splitk_reduce_split(const az_gemm_desc* d, int splits, unsigned short* plane
   a.bias = d->bias; a.act = d->act; a.C = write_c ? d->C : nullptr; a.ldc = d->ldc;
   a.slab = static_cast<float*>(d->ws);
   a.splits = splits;
+  // one 8-column chunk per thread (N = 3,136: 7 waves; 8.5 -> 8.35 us per M = 512 launch against
+  // two chunks on 4 waves, profiles/r06/reduce_ab)
+  const int T = (d->N / 8 + 63) / 64 * 64;
   switch (splits) {
-#define AZ_RS(SS) case SS: hipLaunchKernelGGL(splitk_reduce_split_kernel<SS>, dim3(a.M), dim3(256), \
+#define AZ_RS(SS) case SS: hipLaunchKernelGGL((splitk_reduce_split_kernel<SS, 1>), dim3(a.M), dim3(T), \
                                              0, s, a, planes, sc); break;
     AZ_RS(2) AZ_RS(3) AZ_RS(4) AZ_RS(5) AZ_RS(6) AZ_RS(7) default: AZ_RS(8)
 #undef AZ_RS
